@@ -1,0 +1,144 @@
+/*
+ * maxcover.h — C-ABI of libmaxcover, the MI355X (gfx950) implementation of the
+ * MADS area-coverage objective of Gabisanth/MaximumAreaCoverageOptimization.jl.
+ *
+ * Plain C, no C++ exceptions cross it, no torch types: it is what a Julia
+ * `ccall`, a Python `ctypes` stub or any other FFI binds.
+ *
+ * Reference seam this replaces (paths relative to the reference repo root):
+ *   - AreaCoverageCalculation.calculateArea(circles, points)
+ *         src/AreaCoverageCalculation.jl:63-110 (live loop :67-78)
+ *   - the AreaMaxObjective closure built by TDM_STATIC_opt.createObjective
+ *         src/TDM_STATIC_opt.jl:82-100 (penalty :89-97)
+ *   - the extreme constraint cons3 built by create_cons3
+ *         src/TDM_Constraints.jl:54-75
+ *   - CellFunctions.rmvCoveredPOI (order-preserving deletion)
+ *         src/CellFunctions.jl:81-108 (predicate :90, deleteat! :101)
+ *   - DirectSearch's poll step (evaluate every trial point, keep the best)
+ *         called at src/TDM_STATIC_opt.jl:162 (third-party, not vendored)
+ *
+ * Semantics kept bit-for-bit:
+ *   covered(p) = exists c: sqrt((px-cx)^2 + (py-cy)^2) < r_c     (fp64, ^2 = x*x, no FMA,
+ *                                                                 correctly rounded sqrt, strict <)
+ *   area       = sum of w_p over covered p, w = record column 4   (duplicates counted per entry)
+ *   objective  = -area + 1e5 * sum_i |x[2N+i] - r_max[i]|        (sequential sum over i)
+ * Candidates use the reference layout [x_1..x_N; y_1..y_N; r_1..r_N] (3N doubles).
+ *
+ * Ownership: host arrays are borrowed read-only for the duration of a call; the library
+ * copies what it keeps into device buffers it owns. Outputs are written before return
+ * (synchronous API) except for the *_dev entry points, which are stream-ordered.
+ * Threading: mac_area_* / mac_objective_* / mac_poll_* may be called concurrently on one
+ * context from several host threads (DirectSearch SetMaxEvals, src/TDM_STATIC_opt.jl:129);
+ * mac_set_points_* / mac_remove_covered_* must not overlap evaluations (points only
+ * change between MADS calls, src/FullSimulation.jl:50-61).
+ */
+#ifndef MAXCOVER_H
+#define MAXCOVER_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes --------------------------------------------------------------- */
+#define MAC_OK            0
+#define MAC_E_INVAL       1  /* null pointer / negative size / bad option                    */
+#define MAC_E_SIZE        2  /* three_n % 3 != 0: the reference's Int(length/3) InexactError,
+                                src/AreaCoverageCalculation.jl:65                            */
+#define MAC_E_NOPOINTS    3  /* no point list set on the context                             */
+#define MAC_E_HIP         4  /* a HIP runtime call failed (see mac_last_error)               */
+#define MAC_E_NOMEM       5  /* device allocation failed                                     */
+#define MAC_E_LOSSY       6  /* f32 storage requested but a coordinate/weight is not exact   */
+#define MAC_E_NODEVICE    7  /* no HIP device / bad device index                             */
+
+/* ---- options (mac_set_option) --------------------------------------------------- */
+#define MAC_OPT_ALGO         1  /* MAC_ALGO_AUTO (default) | MAC_ALGO_SCAN | MAC_ALGO_TILED     */
+#define MAC_OPT_STORAGE      2  /* MAC_STORE_F64 (default) | MAC_STORE_F32 (lossless coords)   */
+#define MAC_OPT_TILE_POINTS  3  /* target points per spatial tile (default 4), set before points */
+
+#define MAC_ALGO_AUTO   0
+#define MAC_ALGO_SCAN   1  /* streaming brute-force scan: every point against every disk     */
+#define MAC_ALGO_TILED  2  /* disk-major walk over the tile-binned point list (exact culling) */
+
+#define MAC_STORE_F64   0
+#define MAC_STORE_F32   1
+
+typedef struct mac_ctx mac_ctx;
+
+/* Thread-local message for the last non-zero status returned on this thread. */
+const char* mac_last_error(void);
+/* Library version string, e.g. "maxcover 0.1.0 gfx950". */
+const char* mac_version(void);
+
+int32_t mac_device_count(int32_t* count_out);
+int32_t mac_ctx_create(mac_ctx** out, int32_t device);
+void    mac_ctx_destroy(mac_ctx* ctx);
+int32_t mac_set_option(mac_ctx* ctx, int32_t option, int64_t value);
+
+/* ---- point list (per MPC step) -------------------------------------------------- */
+/* SoA host arrays, M entries each; weight w = the reference's column 4 ("importance"). */
+int32_t mac_set_points_f64(mac_ctx* ctx, const double* x, const double* y, const double* w,
+                           int64_t M);
+/* Reference records: M rows of `stride` doubles, [x, y, area, importance, covered, ...];
+ * x = col 1, y = col 2, weight = col 4 (src/AreaCoverageCalculation.jl:16,72). stride >= 4. */
+int32_t mac_set_points_records_f64(mac_ctx* ctx, const double* rec, int64_t M, int64_t stride);
+/* Same, from device-resident SoA arrays (borrowed for the call, copied). */
+int32_t mac_set_points_dev_f64(mac_ctx* ctx, const double* d_x, const double* d_y,
+                               const double* d_w, int64_t M);
+int32_t mac_num_points(mac_ctx* ctx, int64_t* M_out);
+/* Copy the current list (original order) back to host SoA arrays (each M_out entries). */
+int32_t mac_get_points_f64(mac_ctx* ctx, double* x, double* y, double* w);
+
+/* rmvCoveredPOI (src/CellFunctions.jl:81-108): delete, in place and order-preserving, every
+ * entry covered by `circles` ([x;y;r], three_n doubles). kept_idx (nullable, capacity M)
+ * receives the 0-based original indices of the kept entries; *M_out the new length. */
+int32_t mac_remove_covered_f64(mac_ctx* ctx, const double* circles, int64_t three_n,
+                               int64_t* kept_idx, int64_t* M_out);
+/* Covered flags for the current list (original order), one byte per entry. */
+int32_t mac_covered_flags_f64(mac_ctx* ctx, const double* circles, int64_t three_n,
+                              uint8_t* flags_out);
+
+/* ---- objective ------------------------------------------------------------------ */
+/* calculateArea(circles, points): one candidate. */
+int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, double* area_out);
+/* K candidates, column-major 3N x K (each candidate contiguous, as a Julia Matrix(3N,K)). */
+int32_t mac_area_batch_f64(mac_ctx* ctx, const double* cands, int64_t three_n, int64_t K,
+                           double* area_out);
+/* AreaMaxObjective for K candidates: obj_k = -area_k + penalty * sum_i |x[2N+i] - r_max[i]|
+ * (penalty = 1e5 in the reference). r_max: N doubles. */
+int32_t mac_objective_batch_f64(mac_ctx* ctx, const double* cands, int64_t three_n, int64_t K,
+                                const double* r_max, double penalty, double* obj_out);
+
+/* Poll step: evaluate K candidates, reject those failing cons3 (3-D displacement from
+ * `prev` [x;y;r] > d_lim[i], z = R / tan_half_fov; src/TDM_Constraints.jl:54-75) when prev
+ * is non-null, and return the lowest-index minimiser (ties -> lowest index, the order a
+ * sequential poll keeps its first best). best_idx = -1 when no candidate is feasible.
+ * obj_out (nullable, K doubles) receives every objective (+inf for infeasible). */
+int32_t mac_poll_best_f64(mac_ctx* ctx, const double* cands, int64_t three_n, int64_t K,
+                          const double* r_max, double penalty,
+                          const double* prev, const double* d_lim, double tan_half_fov,
+                          double* obj_out, double* best_obj, int64_t* best_idx);
+
+/* ---- device-pointer, stream-ordered variants (inputs already resident in HBM) ----- */
+/* d_cands: 3N x K column-major on the context's device; d_area: K doubles. `stream` is a
+ * hipStream_t (NULL = the context's own stream). Returns after enqueueing. */
+int32_t mac_area_batch_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three_n, int64_t K,
+                               double* d_area, void* stream);
+/* Device poll: d_best receives {best_obj (double), best_idx (int64 stored as double bits)}
+ * as 16 bytes; d_obj (nullable) K objectives. d_prev/d_dlim nullable (no cons3). */
+int32_t mac_poll_best_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three_n, int64_t K,
+                              const double* d_rmax, double penalty,
+                              const double* d_prev, const double* d_dlim, double tan_half_fov,
+                              int64_t idx_base, double* d_obj, void* d_best, void* stream);
+
+/* ---- exact predicate helpers (host) --------------------------------------------- */
+/* Largest double T with: for every double a >= 0, (sqrt(a) < r) <=> (a <= T), where sqrt is
+ * the correctly rounded fp64 sqrt. -1.0 when nothing can be covered (r <= 0 or NaN). */
+double mac_cover_threshold(double r);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MAXCOVER_H */

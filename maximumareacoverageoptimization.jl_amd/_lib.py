@@ -1,0 +1,324 @@
+"""ctypes binding of libmaxcover.so (include/maxcover.h).
+
+This is the Python stand-in for the Julia ``ccall`` shim (julia/MaxCoverAMD.jl): same entry
+points, same array layouts, same error behaviour. There is no CPU fallback: if the shared
+library is missing or cannot be loaded, every entry point raises ``MaxCoverError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmaxcover.so")
+
+MAC_OK = 0
+MAC_E_INVAL = 1
+MAC_E_SIZE = 2
+MAC_E_NOPOINTS = 3
+MAC_E_HIP = 4
+MAC_E_NOMEM = 5
+MAC_E_LOSSY = 6
+MAC_E_NODEVICE = 7
+
+MAC_OPT_ALGO = 1
+MAC_OPT_STORAGE = 2
+MAC_OPT_TILE_POINTS = 3
+MAC_ALGO_AUTO = 0
+MAC_ALGO_SCAN = 1
+MAC_ALGO_TILED = 2
+MAC_STORE_F64 = 0
+MAC_STORE_F32 = 1
+
+ALGOS = {"auto": MAC_ALGO_AUTO, "scan": MAC_ALGO_SCAN, "tiled": MAC_ALGO_TILED}
+
+# Every symbol include/maxcover.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "mac_last_error", "mac_version", "mac_device_count", "mac_ctx_create", "mac_ctx_destroy",
+    "mac_set_option", "mac_set_points_f64", "mac_set_points_records_f64",
+    "mac_set_points_dev_f64", "mac_num_points", "mac_get_points_f64",
+    "mac_remove_covered_f64", "mac_covered_flags_f64", "mac_area_f64", "mac_area_batch_f64",
+    "mac_objective_batch_f64", "mac_poll_best_f64", "mac_area_batch_dev_f64",
+    "mac_poll_best_dev_f64", "mac_cover_threshold",
+)
+
+
+class MaxCoverError(RuntimeError):
+    """Non-zero status from libmaxcover (message from mac_last_error)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libmaxcover error {code}: {msg}")
+        self.code = code
+
+
+class InexactError(MaxCoverError, ValueError):
+    """Julia's InexactError from Int(length(circles)/3) (src/AreaCoverageCalculation.jl:65)."""
+
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def _declare(L: ctypes.CDLL) -> None:
+    sig = {
+        "mac_last_error": ([], ctypes.c_char_p),
+        "mac_version": ([], ctypes.c_char_p),
+        "mac_device_count": ([ctypes.POINTER(_i32)], _i32),
+        "mac_ctx_create": ([ctypes.POINTER(_vp), _i32], _i32),
+        "mac_ctx_destroy": ([_vp], None),
+        "mac_set_option": ([_vp, _i32, _i64], _i32),
+        "mac_set_points_f64": ([_vp, _dp, _dp, _dp, _i64], _i32),
+        "mac_set_points_records_f64": ([_vp, _dp, _i64, _i64], _i32),
+        "mac_set_points_dev_f64": ([_vp, _vp, _vp, _vp, _i64], _i32),
+        "mac_num_points": ([_vp, _i64p], _i32),
+        "mac_get_points_f64": ([_vp, _dp, _dp, _dp], _i32),
+        "mac_remove_covered_f64": ([_vp, _dp, _i64, _i64p, _i64p], _i32),
+        "mac_covered_flags_f64": ([_vp, _dp, _i64, _u8p], _i32),
+        "mac_area_f64": ([_vp, _dp, _i64, _dp], _i32),
+        "mac_area_batch_f64": ([_vp, _dp, _i64, _i64, _dp], _i32),
+        "mac_objective_batch_f64": ([_vp, _dp, _i64, _i64, _dp, ctypes.c_double, _dp], _i32),
+        "mac_poll_best_f64": ([_vp, _dp, _i64, _i64, _dp, ctypes.c_double, _dp, _dp,
+                               ctypes.c_double, _dp, _dp, _i64p], _i32),
+        "mac_area_batch_dev_f64": ([_vp, _vp, _i64, _i64, _vp, _vp], _i32),
+        "mac_poll_best_dev_f64": ([_vp, _vp, _i64, _i64, _vp, ctypes.c_double, _vp, _vp,
+                                   ctypes.c_double, _i64, _vp, _vp, _vp], _i32),
+        "mac_cover_threshold": ([ctypes.c_double], ctypes.c_double),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+
+
+def load_library(path: str | None = None) -> ctypes.CDLL:
+    """Load libmaxcover.so (raises MaxCoverError if absent: there is no fallback path)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise MaxCoverError(MAC_E_HIP, f"{p} not built (run __graft_entry__.build())")
+        try:
+            L = ctypes.CDLL(p)
+        except OSError as e:  # pragma: no cover - depends on the host
+            raise MaxCoverError(MAC_E_HIP, f"cannot load {p}: {e}") from e
+        _declare(L)
+        if path is None:
+            _lib = L
+        return L
+
+
+def _check(rc: int) -> None:
+    if rc != MAC_OK:
+        msg = load_library().mac_last_error().decode(errors="replace")
+        if rc == MAC_E_SIZE:
+            raise InexactError(rc, msg)
+        raise MaxCoverError(rc, msg)
+
+
+def version() -> str:
+    return load_library().mac_version().decode()
+
+
+def device_count() -> int:
+    n = _i32()
+    _check(load_library().mac_device_count(ctypes.byref(n)))
+    return int(n.value)
+
+
+def cover_threshold(r: float) -> float:
+    return float(load_library().mac_cover_threshold(float(r)))
+
+
+def _f64(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(_dp)
+
+
+def _devptr(t) -> int:
+    """Device address of a torch tensor / int / None."""
+    if t is None:
+        return 0
+    if isinstance(t, int):
+        return t
+    return int(t.data_ptr())
+
+
+class Context:
+    """One libmaxcover context = one GPU + one device-resident fire-point list."""
+
+    def __init__(self, device: int = 0, algo: str = "auto", tile_points: int | None = None):
+        L = load_library()
+        h = _vp()
+        _check(L.mac_ctx_create(ctypes.byref(h), int(device)))
+        self._h = h
+        self.device = int(device)
+        self._L = L
+        self.set_algo(algo)
+        if tile_points is not None:
+            self.set_option(MAC_OPT_TILE_POINTS, int(tile_points))
+
+    # -- lifetime
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.mac_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- options
+    def set_option(self, option: int, value: int) -> None:
+        _check(self._L.mac_set_option(self._h, int(option), int(value)))
+
+    def set_algo(self, algo: str) -> None:
+        if algo not in ALGOS:
+            raise ValueError(f"algo must be one of {sorted(ALGOS)}")
+        self.set_option(MAC_OPT_ALGO, ALGOS[algo])
+
+    # -- point list
+    def set_points(self, x, y, w) -> None:
+        x, y, w = _f64(x), _f64(y), _f64(w)
+        if not (x.shape == y.shape == w.shape) or x.ndim != 1:
+            raise ValueError("x, y, w must be 1-D arrays of equal length")
+        _check(self._L.mac_set_points_f64(self._h, _ptr(x), _ptr(y), _ptr(w), x.size))
+
+    def set_points_records(self, rec) -> None:
+        r = _f64(rec)
+        if r.ndim == 1:
+            r = r.reshape(-1, 5)
+        if r.ndim != 2 or (r.shape[0] and r.shape[1] < 4):
+            raise ValueError("records must be M x >=4 ([x, y, area, importance, covered])")
+        _check(self._L.mac_set_points_records_f64(self._h, _ptr(r), r.shape[0],
+                                                  r.shape[1] if r.shape[0] else 5))
+
+    def set_points_device(self, x, y, w, M: int | None = None) -> None:
+        """x, y, w: torch float64 tensors on this context's device (copied)."""
+        n = int(M if M is not None else x.numel())
+        _check(self._L.mac_set_points_dev_f64(self._h, _devptr(x), _devptr(y), _devptr(w), n))
+
+    @property
+    def num_points(self) -> int:
+        m = _i64()
+        _check(self._L.mac_num_points(self._h, ctypes.byref(m)))
+        return int(m.value)
+
+    def get_points(self):
+        M = self.num_points
+        x = np.empty(M)
+        y = np.empty(M)
+        w = np.empty(M)
+        _check(self._L.mac_get_points_f64(self._h, _ptr(x), _ptr(y), _ptr(w)))
+        return x, y, w
+
+    def covered_flags(self, circles) -> np.ndarray:
+        c = _f64(circles)
+        out = np.zeros(max(self.num_points, 1), dtype=np.uint8)
+        _check(self._L.mac_covered_flags_f64(self._h, _ptr(c), c.size,
+                                             out.ctypes.data_as(_u8p)))
+        return out[: self.num_points].astype(bool)
+
+    def remove_covered(self, circles) -> np.ndarray:
+        """rmvCoveredPOI on the device list; returns the kept original indices (list order)."""
+        c = _f64(circles)
+        M = self.num_points
+        kept = np.zeros(max(M, 1), dtype=np.int64)
+        m = _i64()
+        _check(self._L.mac_remove_covered_f64(self._h, _ptr(c), c.size,
+                                              kept.ctypes.data_as(_i64p), ctypes.byref(m)))
+        return kept[: m.value].copy()
+
+    # -- objective
+    def area(self, circles) -> float:
+        c = _f64(circles)
+        out = ctypes.c_double()
+        _check(self._L.mac_area_f64(self._h, _ptr(c), c.size, ctypes.byref(out)))
+        return out.value
+
+    def area_batch(self, cands) -> np.ndarray:
+        """cands: K x 3N (row k = candidate k, i.e. the 3N x K column-major matrix)."""
+        c = _f64(cands)
+        if c.ndim != 2:
+            raise ValueError("cands must be K x 3N")
+        K, three_n = c.shape
+        out = np.empty(K)
+        _check(self._L.mac_area_batch_f64(self._h, _ptr(c), three_n, K, _ptr(out)))
+        return out
+
+    def objective_batch(self, cands, r_max, penalty: float = 1e5) -> np.ndarray:
+        c = _f64(cands)
+        K, three_n = c.shape
+        rm = _f64(r_max)
+        out = np.empty(K)
+        _check(self._L.mac_objective_batch_f64(self._h, _ptr(c), three_n, K, _ptr(rm),
+                                               float(penalty), _ptr(out)))
+        return out
+
+    def poll_best(self, cands, r_max, penalty: float = 1e5, prev=None, d_lim=None,
+                  tan_half_fov: float = 1.0, want_all: bool = False):
+        """Returns (best_obj, best_idx[, objectives]); best_idx = -1 if none feasible."""
+        c = _f64(cands)
+        K, three_n = c.shape
+        rm = _f64(r_max)
+        pv = _f64(prev) if prev is not None else None
+        dl = _f64(d_lim) if d_lim is not None else None
+        objs = np.empty(K) if want_all else None
+        bo = ctypes.c_double()
+        bi = _i64()
+        _check(self._L.mac_poll_best_f64(
+            self._h, _ptr(c), three_n, K, _ptr(rm), float(penalty),
+            _ptr(pv) if pv is not None else None, _ptr(dl) if dl is not None else None,
+            float(tan_half_fov), _ptr(objs) if objs is not None else None,
+            ctypes.byref(bo), ctypes.byref(bi)))
+        if want_all:
+            return bo.value, int(bi.value), objs
+        return bo.value, int(bi.value)
+
+    # -- device-resident, stream-ordered
+    def area_batch_dev(self, d_cands, three_n: int, K: int, d_area, stream=None) -> None:
+        _check(self._L.mac_area_batch_dev_f64(self._h, _devptr(d_cands), int(three_n), int(K),
+                                              _devptr(d_area), _devptr(stream)))
+
+    def poll_best_dev(self, d_cands, three_n: int, K: int, d_rmax, d_best, penalty: float = 1e5,
+                      d_prev=None, d_dlim=None, tan_half_fov: float = 1.0, idx_base: int = 0,
+                      d_obj=None, stream=None) -> None:
+        _check(self._L.mac_poll_best_dev_f64(
+            self._h, _devptr(d_cands), int(three_n), int(K), _devptr(d_rmax), float(penalty),
+            _devptr(d_prev), _devptr(d_dlim), float(tan_half_fov), int(idx_base),
+            _devptr(d_obj), _devptr(d_best), _devptr(stream)))
+
+
+_default_ctx = None
+_default_lock = threading.Lock()
+
+
+def default_context() -> Context:
+    """Process-wide context on LOCAL_RANK's GPU (device 0 by default)."""
+    global _default_ctx
+    with _default_lock:
+        if _default_ctx is None:
+            _default_ctx = Context(int(os.environ.get("LOCAL_RANK", "0")))
+        return _default_ctx

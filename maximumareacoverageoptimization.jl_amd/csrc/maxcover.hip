@@ -1,0 +1,819 @@
+// maxcover.hip — libmaxcover: context, device-resident point list, and the C-ABI declared in
+// include/maxcover.h. gfx950 only (hipcc --offload-arch=gfx950).
+//
+// Reference seam: src/TDM_STATIC_opt.jl:82-100 (AreaMaxObjective / createObjective) and
+// src/AreaCoverageCalculation.jl:63-110 (calculateArea). See DESIGN.md.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+#include "maxcover.h"
+
+#pragma clang fp contract(off)
+
+using namespace mac;
+
+// ------------------------------------------------------------------ errors
+
+static thread_local std::string g_last_error;
+
+static int32_t fail(int32_t code, const std::string& msg)
+{
+    g_last_error = msg;
+    return code;
+}
+
+struct HipError {
+    hipError_t e;
+    const char* what;
+    int line;
+};
+
+#define HCK(expr)                                              \
+    do {                                                       \
+        hipError_t _e = (expr);                                \
+        if (_e != hipSuccess) throw HipError{_e, #expr, __LINE__}; \
+    } while (0)
+
+#define ABI_BEGIN try {
+#define ABI_END                                                                               \
+    }                                                                                         \
+    catch (const HipError& he) {                                                              \
+        char buf[512];                                                                        \
+        snprintf(buf, sizeof buf, "HIP error %d (%s) at maxcover.hip:%d in %s", (int)he.e,     \
+                 hipGetErrorString(he.e), he.line, he.what);                                  \
+        return fail(he.e == hipErrorOutOfMemory ? MAC_E_NOMEM : MAC_E_HIP, buf);              \
+    }                                                                                         \
+    catch (const std::bad_alloc&) {                                                           \
+        return fail(MAC_E_NOMEM, "host allocation failed");                                   \
+    }                                                                                         \
+    catch (...) {                                                                             \
+        return fail(MAC_E_HIP, "unexpected exception");                                       \
+    }
+
+// ------------------------------------------------------------------ device buffers
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    void reserve(size_t bytes)
+    {
+        if (bytes <= cap) return;
+        if (p) HCK(hipFree(p));
+        p = nullptr;
+        cap = 0;
+        size_t b = bytes < 256 ? 256 : bytes;
+        b = (b + 255) & ~(size_t)255;
+        HCK(hipMalloc(&p, b));
+        cap = b;
+    }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T* as() const { return (T*)p; }
+};
+
+// Per-call scratch + stream ("lane"); lanes are pooled so concurrent host threads each get one.
+struct Lane {
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim;
+    std::vector<double> h_dlim;
+};
+
+struct mac_ctx {
+    int device = 0;
+    int cus = 256;
+    std::mutex mu;
+    std::vector<Lane*> lanes_free;
+    std::vector<Lane*> lanes_all;
+    hipStream_t setup_stream = nullptr;
+
+    int algo = MAC_ALGO_AUTO;
+    int storage = MAC_STORE_F64;
+    int tile_ppt = 4;
+
+    int64_t M = 0;
+    bool has_points = false;
+    // original (list) order
+    DevBuf x, y, w;
+    // tile-sorted order
+    DevBuf xys, ws, perm, off;
+    Grid grid{};
+    int64_t nTiles = 1;
+    // setup scratch
+    DevBuf keys_in, keys_out, idx_in, tmp, bbox, flags_s, flags_o, keep, sel_count, cx, cy, cw,
+        cidx, circ, cdisk;
+};
+
+static void set_device(mac_ctx* ctx) { HCK(hipSetDevice(ctx->device)); }
+
+static Lane* acquire_lane(mac_ctx* ctx)
+{
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        for (size_t i = 0; i < ctx->lanes_free.size(); ++i) {
+            Lane* l = ctx->lanes_free[i];
+            if (hipEventQuery(l->done) == hipSuccess) {
+                ctx->lanes_free.erase(ctx->lanes_free.begin() + (long)i);
+                return l;
+            }
+        }
+    }
+    Lane* l = new Lane();
+    HCK(hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking));
+    HCK(hipEventCreateWithFlags(&l->done, hipEventDisableTiming));
+    HCK(hipEventRecord(l->done, l->stream));
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->lanes_all.push_back(l);
+    return l;
+}
+
+static void release_lane(mac_ctx* ctx, Lane* l, hipStream_t used)
+{
+    (void)hipEventRecord(l->done, used);
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->lanes_free.push_back(l);
+}
+
+struct LaneGuard {
+    mac_ctx* ctx;
+    Lane* lane;
+    hipStream_t used;
+    LaneGuard(mac_ctx* c) : ctx(c), lane(acquire_lane(c)), used(lane->stream) {}
+    ~LaneGuard() { release_lane(ctx, lane, used); }
+};
+
+static inline unsigned grid1d(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
+
+// ------------------------------------------------------------------ point list set-up
+
+static Grid choose_grid(double xmn, double xmx, double ymn, double ymx, int64_t M, int ppt)
+{
+    Grid g{};
+    if (!(xmn <= xmx) || !(ymn <= ymx) || M <= 0) {  // no finite point
+        g.gx0 = 0.0;
+        g.gy0 = 0.0;
+        g.S = 1.0;
+        g.invS = 1.0;
+        g.nTx = 1;
+        g.nTy = 1;
+        return g;
+    }
+    const double W = xmx - xmn, H = ymx - ymn;
+    double S;
+    if (W > 0 && H > 0)
+        S = std::sqrt(W * H * (double)ppt / (double)M);
+    else if (W > 0 || H > 0)
+        S = std::max(W, H) * (double)ppt / (double)M;
+    else
+        S = 1.0;
+    if (!(S > 0) || !std::isfinite(S)) S = 1.0;
+    // cap the tile count (int32 keys, offsets memory): at most max(4M, 2^20) tiles, 2^28 total
+    const double cap = std::min(268435456.0, std::max(4.0 * (double)M, 1048576.0));
+    for (int it = 0; it < 64; ++it) {
+        const double nx = std::floor(W / S) + 1.0, ny = std::floor(H / S) + 1.0;
+        if (nx * ny <= cap && nx < 1e8 && ny < 1e8) break;
+        S *= 1.5;
+    }
+    {   // still too many tiles (e.g. a bbox of 1e300 m): at most 1024 x 1024
+        const double nx = std::floor(W / S) + 1.0, ny = std::floor(H / S) + 1.0;
+        if (!(nx * ny <= cap) || !(nx < 1e8) || !(ny < 1e8)) S = std::max(W, H) / 1000.0;
+        if (!(S > 0) || !std::isfinite(S)) S = kDblMax;
+    }
+    g.gx0 = xmn;
+    g.gy0 = ymn;
+    g.S = S;
+    g.invS = 1.0 / S;
+    g.nTx = (int)std::min(std::floor(W * g.invS) + 1.0, 1e8);
+    g.nTy = (int)std::min(std::floor(H * g.invS) + 1.0, 1e8);
+    if (g.nTx < 1) g.nTx = 1;
+    if (g.nTy < 1) g.nTy = 1;
+    return g;
+}
+
+// Build the tile-sorted copy (xys, ws, perm, off) from ctx->x/y/w (list order), on `s`.
+static void build_index(mac_ctx* ctx, hipStream_t s)
+{
+    const int64_t M = ctx->M;
+    // bbox
+    const int nb = (int)std::min<int64_t>(std::max<int64_t>(grid1d(M, kBlock), 1), 1024);
+    ctx->bbox.reserve(sizeof(double4) * nb);
+    hipLaunchKernelGGL(bbox_kernel, dim3(nb), dim3(kBlock), 0, s, ctx->x.as<double>(),
+                       ctx->y.as<double>(), M, ctx->bbox.as<double4>());
+    HCK(hipGetLastError());
+    std::vector<double4> hb(nb);
+    HCK(hipMemcpyAsync(hb.data(), ctx->bbox.p, sizeof(double4) * nb, hipMemcpyDeviceToHost, s));
+    HCK(hipStreamSynchronize(s));
+    double xmn = INFINITY, xmx = -INFINITY, ymn = INFINITY, ymx = -INFINITY;
+    for (auto& b : hb) {
+        xmn = std::min(xmn, b.x);
+        xmx = std::max(xmx, b.y);
+        ymn = std::min(ymn, b.z);
+        ymx = std::max(ymx, b.w);
+    }
+    ctx->grid = choose_grid(xmn, xmx, ymn, ymx, M, ctx->tile_ppt);
+    ctx->nTiles = (int64_t)ctx->grid.nTx * ctx->grid.nTy;
+
+    ctx->xys.reserve(sizeof(double2) * std::max<int64_t>(M, 1));
+    ctx->ws.reserve(sizeof(double) * std::max<int64_t>(M, 1));
+    ctx->perm.reserve(sizeof(uint32_t) * std::max<int64_t>(M, 1));
+    ctx->off.reserve(sizeof(int32_t) * (ctx->nTiles + 1));
+    if (M > 0) {
+        ctx->keys_in.reserve(sizeof(uint32_t) * M);
+        ctx->keys_out.reserve(sizeof(uint32_t) * M);
+        ctx->idx_in.reserve(sizeof(uint32_t) * M);
+        hipLaunchKernelGGL(tile_key_kernel, dim3(grid1d(M, 256)), dim3(256), 0, s,
+                           ctx->x.as<double>(), ctx->y.as<double>(), M, ctx->grid,
+                           ctx->keys_in.as<uint32_t>(), ctx->idx_in.as<uint32_t>());
+        HCK(hipGetLastError());
+        int end_bit = 1;
+        while (end_bit < 32 && ((uint64_t)1 << end_bit) < (uint64_t)ctx->nTiles) ++end_bit;
+        size_t tb = 0;
+        HCK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ctx->keys_in.as<uint32_t>(),
+                                               ctx->keys_out.as<uint32_t>(),
+                                               ctx->idx_in.as<uint32_t>(), ctx->perm.as<uint32_t>(),
+                                               (int)M, 0, end_bit, s));
+        ctx->tmp.reserve(tb);
+        HCK(hipcub::DeviceRadixSort::SortPairs(ctx->tmp.p, tb, ctx->keys_in.as<uint32_t>(),
+                                               ctx->keys_out.as<uint32_t>(),
+                                               ctx->idx_in.as<uint32_t>(), ctx->perm.as<uint32_t>(),
+                                               (int)M, 0, end_bit, s));
+        hipLaunchKernelGGL(gather_sorted_kernel, dim3(grid1d(M, 256)), dim3(256), 0, s,
+                           ctx->x.as<double>(), ctx->y.as<double>(), ctx->w.as<double>(),
+                           ctx->perm.as<uint32_t>(), M, ctx->xys.as<double2>(), ctx->ws.as<double>());
+        HCK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(tile_offsets_kernel, dim3(grid1d(ctx->nTiles + 1, 256)), dim3(256), 0, s,
+                       ctx->keys_out.as<uint32_t>(), M, ctx->nTiles, ctx->off.as<int32_t>());
+    HCK(hipGetLastError());
+    HCK(hipStreamSynchronize(s));
+    ctx->has_points = true;
+}
+
+static int32_t check_M(int64_t M)
+{
+    if (M < 0) return fail(MAC_E_INVAL, "M < 0");
+    if (M >= ((int64_t)1 << 31) - 1) return fail(MAC_E_INVAL, "M must be < 2^31-1");
+    return MAC_OK;
+}
+
+// ------------------------------------------------------------------ evaluation core
+
+static bool use_tiled(mac_ctx* ctx, int N, const double* h_cands, int64_t three_n)
+{
+    if (N <= 0 || N > 2048) return false;
+    if (ctx->algo == MAC_ALGO_SCAN) return false;
+    if (ctx->algo == MAC_ALGO_TILED) return true;
+    if (!h_cands) return true;
+    // AUTO with host candidates: compare the tiled walk's point visits for candidate 0 with
+    // the scan's M (both per disk); prefer the scan when disks span most of the list.
+    const Grid& g = ctx->grid;
+    double visits = 0.0;
+    for (int i = 0; i < N; ++i) {
+        int x0, x1, y0, y1;
+        const double r = h_cands[2 * N + i];
+        if (!tile_span(h_cands[i], r, g.gx0, g.invS, g.nTx, x0, x1)) continue;
+        if (!tile_span(h_cands[N + i], r, g.gy0, g.invS, g.nTy, y0, y1)) continue;
+        visits += (double)(x1 - x0 + 1) * (double)(y1 - y0 + 1);
+    }
+    visits *= (double)ctx->M / (double)std::max<int64_t>(ctx->nTiles, 1);
+    (void)three_n;
+    return visits < 0.5 * (double)ctx->M * (double)N;
+}
+
+// Enqueue disk prep + coverage + finalize (+ argmin) on stream s. All pointers device.
+// area_out/obj_out may be null; best may be null.
+static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_cands, int N,
+                         int K, bool tiled, const double* d_rmax, double penalty,
+                         const double* d_prev, const double* d_dlimT, double tan_half_fov,
+                         double* d_area, double* d_obj, double* d_best, int64_t idx_base)
+{
+    const int ldc = 3 * N;
+    L->disks.reserve(sizeof(DiskRec) * (size_t)std::max<int64_t>((int64_t)N * K, 1));
+    hipLaunchKernelGGL(disk_prep_kernel, dim3(grid1d((int64_t)N * K, 256)), dim3(256), 0, s,
+                       d_cands, N, ldc, K, L->disks.as<DiskRec>());
+    HCK(hipGetLastError());
+    const int64_t M = ctx->M;
+    int G;
+    if (tiled) {
+        // enough workgroups to fill the chip; each slice keeps >= 1 disk per wave
+        const int target = 8 * ctx->cus;
+        G = (int)std::max<int64_t>(1, std::min<int64_t>((target + K - 1) / K,
+                                                        std::max(1, N / kWavesPerBlock)));
+        L->partial.reserve(sizeof(double) * (size_t)K * G);
+        const size_t lds = tiled_lds_bytes(N);
+        hipLaunchKernelGGL(coverage_tiled_kernel, dim3((unsigned)((int64_t)K * G)), dim3(kBlock),
+                           lds, s, ctx->xys.as<double2>(), ctx->ws.as<double>(),
+                           ctx->off.as<int32_t>(), ctx->grid, L->disks.as<DiskRec>(), N, K, G,
+                           L->partial.as<double>());
+        HCK(hipGetLastError());
+    } else {
+        constexpr int KB = 4, PPT = 4;
+        const int64_t per_pass = (int64_t)kBlock * PPT;
+        int64_t nblk = std::max<int64_t>(1, (M + per_pass - 1) / per_pass);
+        const int kgroups = (K + KB - 1) / KB;
+        const int64_t want = std::max<int64_t>(1, (int64_t)(8 * ctx->cus) / kgroups);
+        nblk = std::min(nblk, std::max<int64_t>(want, 1));
+        int64_t chunk = (M + nblk - 1) / nblk;
+        chunk = ((chunk + per_pass - 1) / per_pass) * per_pass;
+        if (chunk == 0) chunk = per_pass;
+        nblk = std::max<int64_t>(1, (M + chunk - 1) / chunk);
+        G = (int)nblk;
+        L->partial.reserve(sizeof(double) * (size_t)K * G);
+        hipLaunchKernelGGL((coverage_scan_kernel<KB, PPT>), dim3((unsigned)nblk, (unsigned)kgroups),
+                           dim3(kBlock), 0, s, ctx->xys.as<double2>(), ctx->ws.as<double>(), M,
+                           L->disks.as<DiskRec>(), N, K, chunk, (int)nblk, L->partial.as<double>());
+        HCK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(finalize_kernel, dim3(grid1d(K, 256)), dim3(256), 0, s,
+                       L->partial.as<double>(), G, K, d_cands, N, ldc, d_rmax, penalty, d_prev,
+                       d_dlimT, tan_half_fov, d_area, d_obj);
+    HCK(hipGetLastError());
+    if (d_best) {
+        hipLaunchKernelGGL(argmin_kernel, dim3(1), dim3(kBlock), 0, s, d_obj, K, idx_base, d_best);
+        HCK(hipGetLastError());
+    }
+}
+
+static double dlim_threshold(double d) { return mac::dlim_threshold(d); }
+
+static int32_t check_common(mac_ctx* ctx, int64_t three_n, int64_t K)
+{
+    if (!ctx) return fail(MAC_E_INVAL, "null context");
+    if (three_n < 0 || K < 0) return fail(MAC_E_INVAL, "negative size");
+    if (three_n % 3 != 0)
+        return fail(MAC_E_SIZE, "InexactError: Int64(" + std::to_string(three_n) + "/3)");
+    if (!ctx->has_points) return fail(MAC_E_NOPOINTS, "no point list set");
+    if (three_n / 3 > 65535) return fail(MAC_E_INVAL, "N > 65535 UAVs");
+    if (K > (int64_t)1 << 30) return fail(MAC_E_INVAL, "K too large");
+    return MAC_OK;
+}
+
+// Host-pointer batch: upload, evaluate, download.
+static int32_t host_eval(mac_ctx* ctx, const double* cands, int64_t three_n, int64_t K,
+                         const double* r_max, double penalty, const double* prev,
+                         const double* d_lim, double tan_half_fov, double* area_out,
+                         double* obj_out, double* best_obj, int64_t* best_idx)
+{
+    int32_t rc = check_common(ctx, three_n, K);
+    if (rc) return rc;
+    if (K == 0) {
+        if (best_idx) *best_idx = -1;
+        if (best_obj) *best_obj = INFINITY;
+        return MAC_OK;
+    }
+    if (!cands) return fail(MAC_E_INVAL, "null candidates");
+    const int N = (int)(three_n / 3);
+    set_device(ctx);
+    LaneGuard lg(ctx);
+    Lane* L = lg.lane;
+    hipStream_t s = L->stream;
+    L->cands.reserve(sizeof(double) * (size_t)std::max<int64_t>(three_n * K, 1));
+    L->area.reserve(sizeof(double) * K);
+    L->obj.reserve(sizeof(double) * K);
+    L->best.reserve(16);
+    if (three_n * K > 0)
+        HCK(hipMemcpyAsync(L->cands.p, cands, sizeof(double) * three_n * K, hipMemcpyHostToDevice,
+                           s));
+    const bool want_obj = obj_out || best_obj || best_idx;
+    double* d_rmax = nullptr;
+    if (want_obj && r_max && N > 0) {
+        L->rmax.reserve(sizeof(double) * N);
+        HCK(hipMemcpyAsync(L->rmax.p, r_max, sizeof(double) * N, hipMemcpyHostToDevice, s));
+        d_rmax = L->rmax.as<double>();
+    }
+    double* d_prev = nullptr;
+    double* d_dlimT = nullptr;
+    if (want_obj && prev && N > 0) {
+        if (!d_lim) return fail(MAC_E_INVAL, "prev given without d_lim");
+        L->prev.reserve(sizeof(double) * three_n);
+        L->dlim.reserve(sizeof(double) * N);
+        L->h_dlim.resize(N);
+        for (int i = 0; i < N; ++i) L->h_dlim[i] = dlim_threshold(d_lim[i]);
+        HCK(hipMemcpyAsync(L->prev.p, prev, sizeof(double) * three_n, hipMemcpyHostToDevice, s));
+        HCK(hipMemcpyAsync(L->dlim.p, L->h_dlim.data(), sizeof(double) * N, hipMemcpyHostToDevice,
+                           s));
+        d_prev = L->prev.as<double>();
+        d_dlimT = L->dlim.as<double>();
+    }
+    const bool tiled = use_tiled(ctx, N, cands, three_n);
+    enqueue_eval(ctx, L, s, L->cands.as<double>(), N, (int)K, tiled, d_rmax, penalty, d_prev,
+                 d_dlimT, tan_half_fov, L->area.as<double>(), want_obj ? L->obj.as<double>() : nullptr,
+                 (best_obj || best_idx) ? L->best.as<double>() : nullptr, 0);
+    if (area_out)
+        HCK(hipMemcpyAsync(area_out, L->area.p, sizeof(double) * K, hipMemcpyDeviceToHost, s));
+    if (obj_out)
+        HCK(hipMemcpyAsync(obj_out, L->obj.p, sizeof(double) * K, hipMemcpyDeviceToHost, s));
+    double hb[2] = {0, 0};
+    if (best_obj || best_idx)
+        HCK(hipMemcpyAsync(hb, L->best.p, 16, hipMemcpyDeviceToHost, s));
+    HCK(hipStreamSynchronize(s));
+    if (best_obj) *best_obj = hb[0];
+    if (best_idx) *best_idx = __builtin_bit_cast(int64_t, hb[1]);
+    return MAC_OK;
+}
+
+// ------------------------------------------------------------------ C-ABI
+
+extern "C" {
+
+const char* mac_last_error(void) { return g_last_error.c_str(); }
+
+const char* mac_version(void) { return "maxcover 0.1.0 gfx950"; }
+
+double mac_cover_threshold(double r) { return cover_threshold(r); }
+
+int32_t mac_device_count(int32_t* count_out)
+{
+    ABI_BEGIN
+    if (!count_out) return fail(MAC_E_INVAL, "null count_out");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *count_out = n;
+    return MAC_OK;
+    ABI_END
+}
+
+int32_t mac_ctx_create(mac_ctx** out, int32_t device)
+{
+    ABI_BEGIN
+    if (!out) return fail(MAC_E_INVAL, "null out");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return fail(MAC_E_NODEVICE, "no HIP device visible");
+    if (device < 0 || device >= n) return fail(MAC_E_NODEVICE, "device index out of range");
+    HCK(hipSetDevice(device));
+    mac_ctx* ctx = new mac_ctx();
+    ctx->device = device;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        ctx->cus = prop.multiProcessorCount;
+    HCK(hipStreamCreateWithFlags(&ctx->setup_stream, hipStreamNonBlocking));
+    *out = ctx;
+    return MAC_OK;
+    ABI_END
+}
+
+void mac_ctx_destroy(mac_ctx* ctx)
+{
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipDeviceSynchronize();
+    for (Lane* l : ctx->lanes_all) {
+        for (DevBuf* b : {&l->cands, &l->disks, &l->partial, &l->area, &l->obj, &l->best,
+                          &l->rmax, &l->prev, &l->dlim})
+            b->release();
+        if (l->done) (void)hipEventDestroy(l->done);
+        if (l->stream) (void)hipStreamDestroy(l->stream);
+        delete l;
+    }
+    for (DevBuf* b : {&ctx->x, &ctx->y, &ctx->w, &ctx->xys, &ctx->ws, &ctx->perm, &ctx->off,
+                      &ctx->keys_in, &ctx->keys_out, &ctx->idx_in, &ctx->tmp, &ctx->bbox,
+                      &ctx->flags_s, &ctx->flags_o, &ctx->keep, &ctx->sel_count, &ctx->cx,
+                      &ctx->cy, &ctx->cw, &ctx->cidx, &ctx->circ, &ctx->cdisk})
+        b->release();
+    if (ctx->setup_stream) (void)hipStreamDestroy(ctx->setup_stream);
+    delete ctx;
+}
+
+int32_t mac_set_option(mac_ctx* ctx, int32_t option, int64_t value)
+{
+    if (!ctx) return fail(MAC_E_INVAL, "null context");
+    switch (option) {
+    case MAC_OPT_ALGO:
+        if (value < MAC_ALGO_AUTO || value > MAC_ALGO_TILED) return fail(MAC_E_INVAL, "bad algo");
+        ctx->algo = (int)value;
+        return MAC_OK;
+    case MAC_OPT_STORAGE:
+        if (value != MAC_STORE_F64 && value != MAC_STORE_F32)
+            return fail(MAC_E_INVAL, "bad storage");
+        if (value == MAC_STORE_F32) return fail(MAC_E_INVAL, "f32 storage not available yet");
+        ctx->storage = (int)value;
+        return MAC_OK;
+    case MAC_OPT_TILE_POINTS:
+        if (value < 1 || value > 4096) return fail(MAC_E_INVAL, "tile points out of range");
+        ctx->tile_ppt = (int)value;
+        return MAC_OK;
+    default:
+        return fail(MAC_E_INVAL, "unknown option");
+    }
+}
+
+static int32_t set_points_common(mac_ctx* ctx, int64_t M)
+{
+    if (!ctx) return fail(MAC_E_INVAL, "null context");
+    int32_t rc = check_M(M);
+    if (rc) return rc;
+    set_device(ctx);
+    HCK(hipDeviceSynchronize());  // no evaluation may overlap a point-list change
+    ctx->M = M;
+    ctx->has_points = false;
+    const size_t b = sizeof(double) * (size_t)std::max<int64_t>(M, 1);
+    ctx->x.reserve(b);
+    ctx->y.reserve(b);
+    ctx->w.reserve(b);
+    return MAC_OK;
+}
+
+int32_t mac_set_points_f64(mac_ctx* ctx, const double* x, const double* y, const double* w,
+                           int64_t M)
+{
+    ABI_BEGIN
+    if (M > 0 && (!x || !y || !w)) return fail(MAC_E_INVAL, "null point array");
+    int32_t rc = set_points_common(ctx, M);
+    if (rc) return rc;
+    hipStream_t s = ctx->setup_stream;
+    if (M > 0) {
+        HCK(hipMemcpyAsync(ctx->x.p, x, sizeof(double) * M, hipMemcpyHostToDevice, s));
+        HCK(hipMemcpyAsync(ctx->y.p, y, sizeof(double) * M, hipMemcpyHostToDevice, s));
+        HCK(hipMemcpyAsync(ctx->w.p, w, sizeof(double) * M, hipMemcpyHostToDevice, s));
+    }
+    build_index(ctx, s);
+    return MAC_OK;
+    ABI_END
+}
+
+int32_t mac_set_points_records_f64(mac_ctx* ctx, const double* rec, int64_t M, int64_t stride)
+{
+    ABI_BEGIN
+    if (M > 0 && !rec) return fail(MAC_E_INVAL, "null records");
+    if (stride < 4) return fail(MAC_E_INVAL, "record stride < 4");
+    std::vector<double> hx(std::max<int64_t>(M, 0)), hy(hx.size()), hw(hx.size());
+    for (int64_t i = 0; i < M; ++i) {
+        hx[i] = rec[i * stride + 0];
+        hy[i] = rec[i * stride + 1];
+        hw[i] = rec[i * stride + 3];  // column 4, src/AreaCoverageCalculation.jl:72
+    }
+    return mac_set_points_f64(ctx, hx.data(), hy.data(), hw.data(), M);
+    ABI_END
+}
+
+int32_t mac_set_points_dev_f64(mac_ctx* ctx, const double* d_x, const double* d_y,
+                               const double* d_w, int64_t M)
+{
+    ABI_BEGIN
+    if (M > 0 && (!d_x || !d_y || !d_w)) return fail(MAC_E_INVAL, "null point array");
+    int32_t rc = set_points_common(ctx, M);
+    if (rc) return rc;
+    hipStream_t s = ctx->setup_stream;
+    if (M > 0) {
+        HCK(hipMemcpyAsync(ctx->x.p, d_x, sizeof(double) * M, hipMemcpyDeviceToDevice, s));
+        HCK(hipMemcpyAsync(ctx->y.p, d_y, sizeof(double) * M, hipMemcpyDeviceToDevice, s));
+        HCK(hipMemcpyAsync(ctx->w.p, d_w, sizeof(double) * M, hipMemcpyDeviceToDevice, s));
+    }
+    build_index(ctx, s);
+    return MAC_OK;
+    ABI_END
+}
+
+int32_t mac_num_points(mac_ctx* ctx, int64_t* M_out)
+{
+    if (!ctx || !M_out) return fail(MAC_E_INVAL, "null argument");
+    *M_out = ctx->has_points ? ctx->M : 0;
+    return MAC_OK;
+}
+
+int32_t mac_get_points_f64(mac_ctx* ctx, double* x, double* y, double* w)
+{
+    ABI_BEGIN
+    if (!ctx) return fail(MAC_E_INVAL, "null context");
+    if (!ctx->has_points) return fail(MAC_E_NOPOINTS, "no point list set");
+    set_device(ctx);
+    hipStream_t s = ctx->setup_stream;
+    const size_t b = sizeof(double) * ctx->M;
+    if (ctx->M > 0) {
+        if (x) HCK(hipMemcpyAsync(x, ctx->x.p, b, hipMemcpyDeviceToHost, s));
+        if (y) HCK(hipMemcpyAsync(y, ctx->y.p, b, hipMemcpyDeviceToHost, s));
+        if (w) HCK(hipMemcpyAsync(w, ctx->w.p, b, hipMemcpyDeviceToHost, s));
+    }
+    HCK(hipStreamSynchronize(s));
+    return MAC_OK;
+    ABI_END
+}
+
+// covered flags (list order) into ctx->flags_o for one candidate; returns on stream s.
+static void compute_flags(mac_ctx* ctx, hipStream_t s, const double* circles, int N)
+{
+    const int64_t M = ctx->M;
+    ctx->flags_s.reserve(std::max<int64_t>(M, 1));
+    ctx->flags_o.reserve(std::max<int64_t>(M, 1));
+    ctx->circ.reserve(sizeof(double) * std::max(3 * N, 1));
+    ctx->cdisk.reserve(sizeof(DiskRec) * std::max(N, 1));
+    if (M == 0) return;
+    HCK(hipMemsetAsync(ctx->flags_s.p, 0, M, s));
+    if (N > 0) {
+        HCK(hipMemcpyAsync(ctx->circ.p, circles, sizeof(double) * 3 * N, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(disk_prep_kernel, dim3(grid1d(N, 256)), dim3(256), 0, s,
+                           ctx->circ.as<double>(), N, 3 * N, 1, ctx->cdisk.as<DiskRec>());
+        HCK(hipGetLastError());
+        const unsigned nb = (unsigned)std::max(1, std::min((N + kWavesPerBlock - 1) / kWavesPerBlock,
+                                                           8 * ctx->cus));
+        hipLaunchKernelGGL(covered_flags_tiled_kernel, dim3(nb), dim3(kBlock), 0, s,
+                           ctx->xys.as<double2>(), ctx->off.as<int32_t>(), ctx->grid,
+                           ctx->cdisk.as<DiskRec>(), N, ctx->flags_s.as<uint8_t>());
+        HCK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(scatter_flags_kernel, dim3(grid1d(M, 256)), dim3(256), 0, s,
+                       ctx->flags_s.as<uint8_t>(), ctx->perm.as<uint32_t>(), M,
+                       ctx->flags_o.as<uint8_t>());
+    HCK(hipGetLastError());
+}
+
+int32_t mac_covered_flags_f64(mac_ctx* ctx, const double* circles, int64_t three_n,
+                              uint8_t* flags_out)
+{
+    ABI_BEGIN
+    int32_t rc = check_common(ctx, three_n, 0);
+    if (rc) return rc;
+    if (three_n > 0 && !circles) return fail(MAC_E_INVAL, "null circles");
+    set_device(ctx);
+    hipStream_t s = ctx->setup_stream;
+    HCK(hipDeviceSynchronize());
+    compute_flags(ctx, s, circles, (int)(three_n / 3));
+    if (ctx->M > 0 && flags_out)
+        HCK(hipMemcpyAsync(flags_out, ctx->flags_o.p, ctx->M, hipMemcpyDeviceToHost, s));
+    HCK(hipStreamSynchronize(s));
+    return MAC_OK;
+    ABI_END
+}
+
+int32_t mac_remove_covered_f64(mac_ctx* ctx, const double* circles, int64_t three_n,
+                               int64_t* kept_idx, int64_t* M_out)
+{
+    ABI_BEGIN
+    int32_t rc = check_common(ctx, three_n, 0);
+    if (rc) return rc;
+    if (three_n > 0 && !circles) return fail(MAC_E_INVAL, "null circles");
+    set_device(ctx);
+    hipStream_t s = ctx->setup_stream;
+    HCK(hipDeviceSynchronize());
+    const int64_t M = ctx->M;
+    compute_flags(ctx, s, circles, (int)(three_n / 3));
+    int64_t kept = M;
+    if (M > 0) {
+        ctx->keep.reserve(M);
+        hipLaunchKernelGGL(invert_flags_kernel, dim3(grid1d(M, 256)), dim3(256), 0, s,
+                           ctx->flags_o.as<uint8_t>(), M, ctx->keep.as<uint8_t>());
+        HCK(hipGetLastError());
+        ctx->sel_count.reserve(sizeof(int64_t) * 4);
+        const size_t b = sizeof(double) * M;
+        ctx->cx.reserve(b);
+        ctx->cy.reserve(b);
+        ctx->cw.reserve(b);
+        ctx->cidx.reserve(sizeof(int64_t) * M);
+        size_t tb = 0, tb2 = 0;
+        HCK(hipcub::DeviceSelect::Flagged(nullptr, tb, ctx->x.as<double>(), ctx->keep.as<uint8_t>(),
+                                          ctx->cx.as<double>(), ctx->sel_count.as<int64_t>(), M, s));
+        hipcub::CountingInputIterator<int64_t> it(0);
+        HCK(hipcub::DeviceSelect::Flagged(nullptr, tb2, it, ctx->keep.as<uint8_t>(),
+                                          ctx->cidx.as<int64_t>(), ctx->sel_count.as<int64_t>(), M,
+                                          s));
+        ctx->tmp.reserve(std::max(tb, tb2));
+        HCK(hipcub::DeviceSelect::Flagged(ctx->tmp.p, tb, ctx->x.as<double>(), ctx->keep.as<uint8_t>(),
+                                          ctx->cx.as<double>(), ctx->sel_count.as<int64_t>(), M, s));
+        HCK(hipcub::DeviceSelect::Flagged(ctx->tmp.p, tb, ctx->y.as<double>(), ctx->keep.as<uint8_t>(),
+                                          ctx->cy.as<double>(), ctx->sel_count.as<int64_t>(), M, s));
+        HCK(hipcub::DeviceSelect::Flagged(ctx->tmp.p, tb, ctx->w.as<double>(), ctx->keep.as<uint8_t>(),
+                                          ctx->cw.as<double>(), ctx->sel_count.as<int64_t>(), M, s));
+        HCK(hipcub::DeviceSelect::Flagged(ctx->tmp.p, tb2, it, ctx->keep.as<uint8_t>(),
+                                          ctx->cidx.as<int64_t>(), ctx->sel_count.as<int64_t>(), M,
+                                          s));
+        HCK(hipMemcpyAsync(&kept, ctx->sel_count.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HCK(hipStreamSynchronize(s));
+        std::swap(ctx->x, ctx->cx);
+        std::swap(ctx->y, ctx->cy);
+        std::swap(ctx->w, ctx->cw);
+        if (kept_idx && kept > 0)
+            HCK(hipMemcpyAsync(kept_idx, ctx->cidx.p, sizeof(int64_t) * kept, hipMemcpyDeviceToHost,
+                               s));
+        ctx->M = kept;
+        build_index(ctx, s);
+    }
+    if (M_out) *M_out = kept;
+    return MAC_OK;
+    ABI_END
+}
+
+int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, double* area_out)
+{
+    ABI_BEGIN
+    if (!area_out) return fail(MAC_E_INVAL, "null area_out");
+    return host_eval(ctx, circles, three_n, 1, nullptr, 0.0, nullptr, nullptr, 1.0, area_out,
+                     nullptr, nullptr, nullptr);
+    ABI_END
+}
+
+int32_t mac_area_batch_f64(mac_ctx* ctx, const double* cands, int64_t three_n, int64_t K,
+                           double* area_out)
+{
+    ABI_BEGIN
+    if (!area_out && K > 0) return fail(MAC_E_INVAL, "null area_out");
+    return host_eval(ctx, cands, three_n, K, nullptr, 0.0, nullptr, nullptr, 1.0, area_out,
+                     nullptr, nullptr, nullptr);
+    ABI_END
+}
+
+int32_t mac_objective_batch_f64(mac_ctx* ctx, const double* cands, int64_t three_n, int64_t K,
+                                const double* r_max, double penalty, double* obj_out)
+{
+    ABI_BEGIN
+    if (!obj_out && K > 0) return fail(MAC_E_INVAL, "null obj_out");
+    if (!r_max && three_n > 0) return fail(MAC_E_INVAL, "null r_max");
+    return host_eval(ctx, cands, three_n, K, r_max, penalty, nullptr, nullptr, 1.0, nullptr,
+                     obj_out, nullptr, nullptr);
+    ABI_END
+}
+
+int32_t mac_poll_best_f64(mac_ctx* ctx, const double* cands, int64_t three_n, int64_t K,
+                          const double* r_max, double penalty, const double* prev,
+                          const double* d_lim, double tan_half_fov, double* obj_out,
+                          double* best_obj, int64_t* best_idx)
+{
+    ABI_BEGIN
+    if (!best_obj || !best_idx) return fail(MAC_E_INVAL, "null best output");
+    if (!r_max && three_n > 0) return fail(MAC_E_INVAL, "null r_max");
+    return host_eval(ctx, cands, three_n, K, r_max, penalty, prev, d_lim, tan_half_fov, nullptr,
+                     obj_out, best_obj, best_idx);
+    ABI_END
+}
+
+int32_t mac_area_batch_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three_n, int64_t K,
+                               double* d_area, void* stream)
+{
+    ABI_BEGIN
+    int32_t rc = check_common(ctx, three_n, K);
+    if (rc) return rc;
+    if (K == 0) return MAC_OK;
+    if (!d_cands || !d_area) return fail(MAC_E_INVAL, "null device pointer");
+    set_device(ctx);
+    LaneGuard lg(ctx);
+    hipStream_t s = stream ? (hipStream_t)stream : lg.lane->stream;
+    lg.used = s;
+    const int N = (int)(three_n / 3);
+    enqueue_eval(ctx, lg.lane, s, d_cands, N, (int)K, use_tiled(ctx, N, nullptr, three_n), nullptr,
+                 0.0, nullptr, nullptr, 1.0, d_area, nullptr, nullptr, 0);
+    return MAC_OK;
+    ABI_END
+}
+
+int32_t mac_poll_best_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three_n, int64_t K,
+                              const double* d_rmax, double penalty, const double* d_prev,
+                              const double* d_dlim, double tan_half_fov, int64_t idx_base,
+                              double* d_obj, void* d_best, void* stream)
+{
+    ABI_BEGIN
+    int32_t rc = check_common(ctx, three_n, K);
+    if (rc) return rc;
+    if (!d_best) return fail(MAC_E_INVAL, "null d_best");
+    if (K > 0 && !d_cands) return fail(MAC_E_INVAL, "null d_cands");
+    set_device(ctx);
+    LaneGuard lg(ctx);
+    Lane* L = lg.lane;
+    hipStream_t s = stream ? (hipStream_t)stream : L->stream;
+    lg.used = s;
+    const int N = (int)(three_n / 3);
+    if (K == 0) {
+        double hb[2] = {INFINITY, __builtin_bit_cast(double, (int64_t)-1)};
+        L->best.reserve(16);
+        HCK(hipMemcpyAsync(d_best, hb, 16, hipMemcpyHostToDevice, s));
+        HCK(hipStreamSynchronize(s));
+        return MAC_OK;
+    }
+    double* d_dlimT = nullptr;
+    if (d_prev) {
+        if (!d_dlim) return fail(MAC_E_INVAL, "d_prev given without d_dlim");
+        L->dlim.reserve(sizeof(double) * std::max(N, 1));
+        hipLaunchKernelGGL(dlim_threshold_kernel, dim3(grid1d(std::max(N, 1), 256)), dim3(256), 0,
+                           s, d_dlim, N, L->dlim.as<double>());
+        HCK(hipGetLastError());
+        d_dlimT = L->dlim.as<double>();
+    }
+    double* d_o = d_obj;
+    if (!d_o) {
+        L->obj.reserve(sizeof(double) * K);
+        d_o = L->obj.as<double>();
+    }
+    enqueue_eval(ctx, L, s, d_cands, N, (int)K, use_tiled(ctx, N, nullptr, three_n), d_rmax,
+                 penalty, d_prev, d_dlimT, tan_half_fov, nullptr, d_o, (double*)d_best, idx_base);
+    return MAC_OK;
+    ABI_END
+}
+
+}  // extern "C"

@@ -1,0 +1,58 @@
+"""Multi-GPU poll: candidate sharding + one 16-byte-per-rank all-gather of the local best.
+
+One process per GPU (torch.distributed; backend "nccl" is RCCL on ROCm, over xGMI). Every rank
+holds a full replica of the point list (403 MB at 16M fp64 entries, against 288 GB of HBM) and
+evaluates the contiguous candidate slice [floor(rK/P), floor((r+1)K/P)). Its libmaxcover poll
+writes {best objective (f64), best global index (i64 bits)} into a 16-byte device buffer; one
+all_gather of those 16 B per rank (latency-bound, tens of microseconds) is the only data-path
+collective, after which every rank takes the lexicographic minimum (objective, index): the
+lowest index wins ties, the order in which a sequential poll keeps its first best.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def shard_range(K: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous slice of the K candidates owned by `rank` (balanced to within one)."""
+    if world <= 0 or not (0 <= rank < world):
+        raise ValueError("bad rank/world")
+    return (rank * K) // world, ((rank + 1) * K) // world
+
+
+def reduce_best(objs: np.ndarray, idxs: np.ndarray) -> tuple[float, int]:
+    """Lexicographic min over per-rank (objective, index); index -1 = rank had no candidate."""
+    best_o, best_i = np.inf, -1
+    for o, i in zip(np.asarray(objs, dtype=np.float64), np.asarray(idxs, dtype=np.int64)):
+        if i < 0 or not (o < np.inf or o == -np.inf) or o != o:
+            continue
+        if best_i < 0 or o < best_o or (o == best_o and i < best_i):
+            best_o, best_i = float(o), int(i)
+    return best_o, best_i
+
+
+def gather_best(best16, group=None):
+    """all_gather of the 16-byte {obj f64, idx i64} record; returns (obj, idx) lexicographic min.
+
+    ``best16``: torch tensor of 2 float64 (the poll's d_best; the index is stored as raw int64
+    bits). Works on any backend: RCCL for device tensors, gloo for CPU tensors."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    out = [torch.empty_like(best16) for _ in range(world)]
+    dist.all_gather(out, best16, group=group)
+    stacked = torch.stack(out).cpu()
+    objs = stacked[:, 0].numpy().copy()
+    idxs = stacked.view(torch.int64)[:, 1].numpy().copy()
+    return reduce_best(objs, idxs)
+
+
+def pack_best(obj: float, idx: int, device="cpu"):
+    """Host-side constructor of the 16-byte record (for tests and CPU ranks)."""
+    import torch
+
+    t = torch.empty(2, dtype=torch.float64, device=device)
+    t[0] = float(obj)
+    t.view(torch.int64)[1] = int(idx)
+    return t

@@ -1,0 +1,326 @@
+"""GPU parity: libmaxcover (HIP, gfx950) against the oracle, through the C-ABI.
+
+Bar: bit-exact coverage decisions everywhere, and bit-exact areas/objectives whenever the
+partial sums are exact (every reference input: weight 25.0 on every entry). For arbitrary real
+weights the library sums in a fixed tile order instead of list order; the covered SET is still
+checked exactly (mac_covered_flags_f64) and the area within rtol 1e-12 (north star: 1e-9 rel).
+"""
+import hashlib
+import math
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ALGOS = ("tiled", "scan")
+TAN50 = math.tan(100 / 180 * math.pi / 2)
+
+
+def recs(x, y, w):
+    return np.stack([x, y, w * 2, w, np.zeros_like(x)], axis=1)
+
+
+def both(ctx, fn):
+    out = {}
+    for a in ALGOS:
+        ctx.set_algo(a)
+        out[a] = fn()
+    ctx.set_algo("auto")
+    return out
+
+
+# ---------------------------------------------------------------------------- golden vectors
+
+def test_golden_static_grid(ctx, pkg, golden, orc):
+    poi = pkg.AreaCoverageCalculation.createPOI(5.0, 5.0, 100.0, 100.0)
+    ctx.set_points_records(poi)
+    for a, got in both(ctx, lambda: ctx.area_batch(golden["A_cands"])).items():
+        assert np.array_equal(got, golden["A_area"]), a
+    for a, got in both(ctx, lambda: ctx.objective_batch(golden["A_cands"], golden["A_rmax"])).items():
+        assert np.array_equal(got, golden["A_obj"]), a
+    # poll with cons3 on the device == oracle's extreme barrier + argmin
+    bo, bi, objs = ctx.poll_best(golden["A_cands"], golden["A_rmax"], 1e5, prev=golden["A_prev"],
+                                 d_lim=golden["A_dlim"], tan_half_fov=float(golden["A_tan"][0]),
+                                 want_all=True)
+    feas = golden["A_cons3"].astype(bool)
+    want = np.where(feas, golden["A_obj"], np.inf)
+    assert np.array_equal(objs, want)
+    k = int(np.argmin(want))
+    assert bi == k and bo == want[k]
+
+
+def test_golden_firepoints(ctx, golden, firepoints):
+    fp10 = np.concatenate(firepoints[:10])
+    fpall = np.concatenate(firepoints)
+    for rec, key in ((fp10, "B_area10"), (fpall, "B_area_all")):
+        ctx.set_points_records(rec)
+        for a, got in both(ctx, lambda: ctx.area_batch(golden["B_cands"])).items():
+            assert np.array_equal(got, golden[key]), (a, key)
+
+
+def test_golden_removal(ctx, pkg, golden, firepoints):
+    poi = pkg.AreaCoverageCalculation.createPOI(5.0, 5.0, 100.0, 100.0)
+    ctx.set_points_records(poi)
+    kept = ctx.remove_covered(golden["A_rmv_cand"])
+    assert np.array_equal(kept, golden["A_rmv_kept"])
+    assert ctx.num_points == kept.size
+    x, y, w = ctx.get_points()
+    assert np.array_equal(x, poi[kept, 0]) and np.array_equal(y, poi[kept, 1])
+    fpall = np.concatenate(firepoints)
+    ctx.set_points_records(fpall)
+    assert np.array_equal(ctx.remove_covered(golden["B_rmv_cand"]), golden["B_rmv_kept"])
+
+
+def test_golden_synthetic_real_weights(ctx, pkg, golden, orc):
+    wl = pkg.workloads
+    rngC = wl.SplitMix64(303)
+    M = 20000
+    xc = rngC.uniform(M) * 400.0 - 50.0
+    yc = rngC.uniform(M) * 300.0 + 10.0
+    wc = rngC.uniform(M) * 10.0 + 0.5
+    xc, yc, wc = wl.shuffled_with_duplicates(xc, yc, wc, rngC, 0.05)
+    h = hashlib.sha256()
+    for a in (xc, yc, wc):
+        h.update(np.ascontiguousarray(a).tobytes())
+    assert h.hexdigest() == str(golden["C_sha"][0]), "generator drifted from the fixture"
+    ctx.set_points(xc, yc, wc)
+    for a, got in both(ctx, lambda: ctx.area_batch(golden["C_cands"])).items():
+        np.testing.assert_allclose(got, golden["C_area"], rtol=1e-12, atol=0, err_msg=a)
+    for c in golden["C_cands"]:
+        assert np.array_equal(ctx.covered_flags(c), orc.np_covered(c, xc, yc))
+
+
+def test_golden_lattice_kats(ctx, pkg, golden):
+    x, y, w = pkg.workloads.grid_points(64)
+    ctx.set_points(x, y, w)
+    for k, c in enumerate(golden["D_cands"]):
+        cc = c[: 3 * int(golden["D_N"][k])]
+        for a, got in both(ctx, lambda: ctx.area(cc)).items():
+            assert got == 25.0 * golden["D_count"][k], (a, k)
+
+
+# ---------------------------------------------------------------------------- edge cases
+
+def test_empty_and_size_errors(ctx, pkg):
+    ctx.set_points(np.zeros(0), np.zeros(0), np.zeros(0))
+    for a in ALGOS:
+        ctx.set_algo(a)
+        assert ctx.area(np.array([1.0, 2.0, 3.0])) == 0.0
+        assert np.array_equal(ctx.area_batch(np.zeros((3, 6))), np.zeros(3))
+    ctx.set_algo("auto")
+    assert ctx.remove_covered(np.array([0.0, 0.0, 10.0])).size == 0
+    x, y, w = pkg.workloads.grid_points(10)
+    ctx.set_points(x, y, w)
+    assert ctx.area(np.zeros(0)) == 0.0          # no UAV: nothing covered
+    with pytest.raises(pkg.InexactError):
+        ctx.area(np.zeros(4))                   # Int(4/3): InexactError
+    assert ctx.area_batch(np.zeros((0, 6))).size == 0
+
+
+def test_special_values(ctx, orc):
+    x = np.array([0.0, 1.0, np.nan, np.inf, -np.inf, 2.0, 2.0, 1e300, -3.0, 0.5])
+    y = np.array([0.0, 1.0, 1.0, 0.0, 5.0, np.nan, 2.0, 0.0, -3.0, 0.25])
+    w = np.array([1.0, 2.0, 4.0, 8.0, 16.0, 32.0, 64.0, 128.0, 256.0, 512.0])
+    ctx.set_points(x, y, w)
+    rec = recs(x, y, w)
+    cases = [
+        [0.0, 0.0, 1.5],                       # plain
+        [0.0, 0.0, math.sqrt(2.0)],            # point (1,1) exactly on the boundary
+        [0.0, 0.0, np.inf],                    # infinite radius: every finite point
+        [0.0, 0.0, 0.0], [0.0, 0.0, -1.0],     # covers nothing
+        [np.nan, 0.0, 5.0], [0.0, 0.0, np.nan],
+        [np.inf, 0.0, 5.0],
+        [1.0, 1.0, 1e308],                     # huge finite radius
+        [0.0, 1.0, 0.0, 1.0, 1.0, 1.0],        # two disks, overlapping
+        [0.0, 0.0, 0.0, 0.0, 2.0, 2.0],        # identical disks
+        [0.5, -3.0, 0.25, -3.0, 5e-324, 1e-300],
+    ]
+    for c in cases:
+        c = np.array(c, dtype=float)
+        want = orc.ref_area(c, rec)
+        for a, got in both(ctx, lambda: ctx.area(c)).items():
+            assert got == want, (a, c, got, want)
+        assert np.array_equal(ctx.covered_flags(c), orc.np_covered(c, x, y)), c
+
+
+def test_degenerate_point_sets(ctx, orc):
+    rng = np.random.default_rng(9)
+    sets = [
+        (np.full(500, 3.0), np.full(500, 4.0)),                    # all entries identical
+        (np.linspace(0, 100, 700), np.full(700, 7.0)),             # collinear (H = 0)
+        (np.full(300, -2.0), np.linspace(-50, 50, 300)),           # collinear (W = 0)
+        (np.array([1.0]), np.array([1.0])),                        # single entry
+        (rng.normal(0, 1e6, 2000), rng.normal(0, 1e-3, 2000)),     # extreme aspect ratio
+    ]
+    for x, y in sets:
+        w = np.full(x.size, 25.0)
+        ctx.set_points(x, y, w)
+        rec = recs(x, y, w)
+        for _ in range(5):
+            N = int(rng.integers(1, 6))
+            c = np.concatenate([rng.choice(x, N) + rng.normal(0, 2, N),
+                                rng.choice(y, N) + rng.normal(0, 2, N), rng.uniform(0, 20, N)])
+            want = orc.ref_area(c, rec)
+            for a, got in both(ctx, lambda: ctx.area(c)).items():
+                assert got == want, (a, c)
+
+
+# ---------------------------------------------------------------------------- fuzz
+
+@pytest.mark.parametrize("seed", range(12))
+def test_fuzz_vs_oracle(ctx, pkg, orc, seed):
+    wl = pkg.workloads
+    rng = wl.SplitMix64(1000 + seed)
+    lattice = seed % 2 == 0
+    if lattice:
+        G = int(rng.integers(8, 120, 1)[0])
+        x, y, w = wl.grid_points(G)
+        x, y, w = wl.shuffled_with_duplicates(x, y, w, rng, 0.05)
+    else:
+        M = int(rng.integers(1, 30000, 1)[0])
+        x = rng.uniform(M) * 500 - 100
+        y = rng.uniform(M) * 300
+        w = np.full(M, 25.0)
+    ctx.set_points(x, y, w)
+    rec = recs(x, y, w)
+    N = int(rng.integers(1, 300, 1)[0])
+    span = float(np.nanmax(x) - np.nanmin(x)) + 10
+    x0 = np.concatenate([np.round(rng.uniform(N) * span), np.round(rng.uniform(N) * 300),
+                         np.round(rng.uniform(N) * 40)])
+    K = int(rng.integers(1, 40, 1)[0])
+    C = np.concatenate([x0[None, :], wl.poll_candidates(x0, rng, ell=2)[: K - 1]], axis=0)
+    want = orc.PointerList(rec).area_batch(C)
+    for a, got in both(ctx, lambda: ctx.area_batch(C)).items():
+        assert np.array_equal(got, want), (a, seed, np.flatnonzero(got != want)[:5])
+
+
+def test_many_uavs_falls_back_to_scan(ctx, pkg, orc):
+    wl = pkg.workloads
+    rng = wl.SplitMix64(55)
+    x, y, w = wl.grid_points(60)
+    ctx.set_points(x, y, w)
+    N = 2100   # above the tiled kernel's LDS limit
+    c = np.concatenate([rng.uniform(N) * 300, rng.uniform(N) * 300, rng.uniform(N) * 3])
+    for a, got in both(ctx, lambda: ctx.area(c)).items():
+        assert got == orc.ref_area(c, recs(x, y, w)), a
+
+
+def test_determinism_and_slicing(ctx, pkg):
+    """Same inputs -> bit-identical results; the multi-workgroup-per-candidate path (small K)
+    equals the one-workgroup path (large K)."""
+    wl = pkg.workloads
+    rng = wl.SplitMix64(8)
+    x, y, w = wl.grid_points(300)
+    ctx.set_points(x, y, w)
+    x0 = wl.clustered_disks(64, 300, rng)
+    C = wl.poll_candidates(x0, rng)
+    ctx.set_algo("tiled")
+    a1 = ctx.area_batch(C)
+    a2 = ctx.area_batch(C)
+    singles = np.array([ctx.area(c) for c in C[:20]])
+    ctx.set_algo("auto")
+    assert np.array_equal(a1, a2)
+    assert np.array_equal(a1[:20], singles)
+
+
+def test_concurrent_host_threads(ctx, pkg):
+    wl = pkg.workloads
+    rng = wl.SplitMix64(21)
+    x, y, w = wl.grid_points(200)
+    ctx.set_points(x, y, w)
+    x0 = wl.uniform_disks(20, 200, rng)
+    C = wl.poll_candidates(x0, rng)
+    want = ctx.area_batch(C)
+    res = {}
+
+    def run(t):
+        res[t] = [ctx.area_batch(C[t::4]) for _ in range(5)]
+
+    th = [threading.Thread(target=run, args=(t,)) for t in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for t in range(4):
+        for r in res[t]:
+            assert np.array_equal(r, want[t::4])
+
+
+# ---------------------------------------------------------------------------- device API
+
+def test_device_pointer_api(ctx, pkg, orc):
+    import torch
+    wl = pkg.workloads
+    rng = wl.SplitMix64(31)
+    x, y, w = wl.grid_points(150)
+    dev = torch.device("cuda", ctx.device)
+    tx, ty, tw = (torch.from_numpy(a).to(dev) for a in (x, y, w))
+    ctx.set_points_device(tx, ty, tw)
+    x0 = wl.uniform_disks(10, 150, rng)
+    C = wl.poll_candidates(x0, rng)
+    rmax = np.full(10, 36.0)
+    tC = torch.from_numpy(C).to(dev)
+    tA = torch.empty(C.shape[0], dtype=torch.float64, device=dev)
+    s = torch.cuda.current_stream(dev)
+    ctx.area_batch_dev(tC, C.shape[1], C.shape[0], tA, stream=s.cuda_stream)
+    tR = torch.from_numpy(rmax).to(dev)
+    tB = torch.empty(2, dtype=torch.float64, device=dev)
+    tO = torch.empty(C.shape[0], dtype=torch.float64, device=dev)
+    ctx.poll_best_dev(tC, C.shape[1], C.shape[0], tR, tB, idx_base=100, d_obj=tO,
+                      stream=s.cuda_stream)
+    torch.cuda.synchronize(dev)
+    rec = recs(x, y, w)
+    want = orc.PointerList(rec).area_batch(C)
+    assert np.array_equal(tA.cpu().numpy(), want)
+    wobj = np.array([orc.ref_objective(c, rec, rmax) for c in C])
+    assert np.array_equal(tO.cpu().numpy(), wobj)
+    b = tB.cpu()
+    assert b[0].item() == wobj.min() and b.view(torch.int64)[1].item() == 100 + int(np.argmin(wobj))
+
+
+# ---------------------------------------------------------------------------- full size
+
+def test_config2_full_size(ctx, pkg, orc):
+    """32 UAVs x 1,048,576 cells fp64: both kernels == the C oracle == integer lattice count."""
+    x, y, w, C, rmax = pkg.workloads.make_config(2)
+    ctx.set_points(x, y, w)
+    want = orc.PointerList(recs(x, y, w)).area_batch(C)
+    assert want[0] == 25.0 * orc.lattice_count_fast(C[0].astype(np.int64), 1024)
+    for a, got in both(ctx, lambda: ctx.area_batch(C)).items():
+        assert np.array_equal(got, want), a
+    kept = ctx.remove_covered(C[0])
+    assert np.array_equal(kept, orc.ref_remove_covered(C[0], recs(x, y, w)))
+
+
+def test_config3_full_poll(ctx, pkg, orc):
+    """128 UAVs x 4M cells, K=769: tiled == scan on every candidate; lattice KAT on a sample."""
+    x, y, w, C, rmax = pkg.workloads.make_config(3)
+    ctx.set_points(x, y, w)
+    r = both(ctx, lambda: ctx.area_batch(C))
+    assert np.array_equal(r["tiled"], r["scan"])
+    for k in range(0, C.shape[0], 97):
+        assert r["tiled"][k] == 25.0 * orc.lattice_count_fast(C[k].astype(np.int64), 2048), k
+    ctx.set_algo("tiled")
+    bo, bi, objs = ctx.poll_best(C, rmax, want_all=True)
+    ctx.set_algo("auto")
+    pen = np.array([sum(abs(float(c[256 + i]) - float(rmax[i])) for i in range(128)) for c in C])
+    wobj = -r["scan"] + pen * 1e5
+    assert np.array_equal(objs, wobj) and bi == int(np.argmin(wobj))
+
+
+def test_config4_full_poll(ctx, pkg, orc):
+    """512 UAVs x 16.8M cells, K=3073 (the bench workload): every candidate's area equals the
+    exact integer lattice count; the scan kernel agrees on a sample."""
+    x, y, w, C, rmax = pkg.workloads.make_config(4)
+    ctx.set_points(x, y, w)
+    ctx.set_algo("tiled")
+    got = ctx.area_batch(C)
+    ctx.set_algo("scan")
+    sample = C[::256]
+    got_scan = ctx.area_batch(sample)
+    ctx.set_algo("auto")
+    assert np.array_equal(got[::256], got_scan)
+    want = np.array([25.0 * orc.lattice_count_fast(c.astype(np.int64), 4096) for c in C])
+    assert np.array_equal(got, want)

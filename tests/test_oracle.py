@@ -1,0 +1,109 @@
+"""CPU: the oracle itself, pinned against the reference's data and integer known answers."""
+import math
+
+import numpy as np
+import pytest
+
+
+def test_c_and_numpy_restatements_agree(orc, pkg):
+    wl = pkg.workloads
+    rng = wl.SplitMix64(11)
+    for _ in range(20):
+        M = int(rng.integers(0, 3000, 1)[0])
+        x = rng.uniform(M) * 200 - 20
+        y = rng.uniform(M) * 200 - 20
+        w = rng.uniform(M) * 3
+        N = int(rng.integers(1, 12, 1)[0])
+        c = np.concatenate([rng.uniform(N) * 200, rng.uniform(N) * 200, rng.uniform(N) * 40])
+        rec = np.stack([x, y, w, w, np.zeros(M)], axis=1) if M else np.zeros((0, 5))
+        assert orc.ref_area(c, rec) == orc.np_area(c, x, y, w)
+
+
+def test_lattice_kat_matches_oracle(orc, pkg):
+    wl = pkg.workloads
+    rng = wl.SplitMix64(12)
+    x, y, w = wl.grid_points(50)
+    rec = np.stack([x, y, w, w, np.zeros_like(x)], axis=1)
+    for N in (1, 2, 7, 25):
+        c = wl.uniform_disks(N, 50, rng)
+        c[2 * N:] = rng.integers(1, 60, N)
+        assert orc.ref_area(c, rec) == 25.0 * orc.lattice_count_np(c.astype(np.int64), 50)
+    c = np.array([10.0, 20.0, 7.0])
+    assert orc.lattice_count(c, 12) == orc.lattice_count_np(c, 12)
+
+
+def test_golden_vectors_reproduce(orc, pkg, golden, firepoints):
+    """The committed vectors are what the C oracle computes now (guards oracle drift)."""
+    ACC = pkg.AreaCoverageCalculation
+    poi = ACC.createPOI(5.0, 5.0, 100.0, 100.0)
+    for c, a, o in zip(golden["A_cands"], golden["A_area"], golden["A_obj"]):
+        assert orc.ref_area(c, poi) == a
+        assert orc.ref_objective(c, poi, golden["A_rmax"]) == o
+    fp10 = np.concatenate(firepoints[:10])
+    for c, a in zip(golden["B_cands"], golden["B_area10"]):
+        assert orc.ref_area(c, fp10) == a
+    for k, c in enumerate(golden["D_cands"]):
+        N = int(golden["D_N"][k])
+        cc = c[: 3 * N]
+        x, y, w = pkg.workloads.grid_points(64)
+        rec = np.stack([x, y, w, w, np.zeros_like(x)], axis=1)
+        assert orc.ref_area(cc, rec) == 25.0 * golden["D_count"][k]
+
+
+def test_firepoints_fixture_shape(firepoints):
+    """Pins the converted reference data to SURVEY.md's measurements (68 rows, 6,276 entries,
+    3,061 unique (x,y), all weights 25, rows 1-10 = 455 entries)."""
+    assert len(firepoints) == 68
+    allp = np.concatenate(firepoints)
+    assert allp.shape == (6276, 5)
+    assert len({(a, b) for a, b in allp[:, :2]}) == 3061
+    assert np.all(allp[:, 3] == 25.0) and np.all(allp[:, 2] == 25.0)
+    assert sum(len(r) for r in firepoints[:10]) == 455
+    # half-integer offsets: multiples of 5 minus 2.5
+    assert np.all(np.mod(allp[:, :2] + 2.5, 5.0) == 0)
+
+
+def test_reference_start_covers_nothing_of_rows_1_10(orc, pkg, firepoints):
+    """the reference start point covers none of FirePoints rows 1..10."""
+    BF = pkg.Base_Functions
+    x0 = BF.allocate_even_circles(15.0, 5, 10 * math.tan(100 / 180 * math.pi / 2), 250.0, 250.0)
+    assert orc.ref_area(x0, np.concatenate(firepoints[:10])) == 0.0
+
+
+def test_inexact_error(orc):
+    with pytest.raises(orc.InexactError):
+        orc.ref_area(np.zeros(4), np.zeros((3, 5)))
+
+
+def test_threshold_exact(pkg, orc):
+    """The library's exact threshold (host build) equals the rational-arithmetic one."""
+    rs = [1.0, 2.0, 36.0, 35.75261336008773, 5e-324, 1e-310, 2.0 ** -1022, 1e308,
+          1.7976931348623157e308, math.inf, 0.0, -1.0, math.nan]
+    rng = np.random.default_rng(3)
+    rs += list(rng.uniform(0, 100, 500)) + list(np.exp(rng.uniform(-740, 709, 500)))
+    rs += [2.0 ** e for e in range(-1074, 1024, 7)]
+    for r in rs:
+        assert pkg.cover_threshold(r) == orc.exact_threshold(r) or (
+            math.isnan(r) and pkg.cover_threshold(r) == -1.0), r
+    for r in rs[:600]:
+        T = pkg.cover_threshold(r)
+        if not (T >= 0):
+            continue
+        for a in (T, math.nextafter(T, math.inf), math.nextafter(T, 0.0), r * r):
+            if 0 <= a < math.inf:
+                assert (math.sqrt(a) < r) == (a <= T)
+
+
+def test_remove_covered_oracle_order(orc, pkg, golden):
+    poi = pkg.AreaCoverageCalculation.createPOI(5.0, 5.0, 100.0, 100.0)
+    kept = orc.ref_remove_covered(golden["A_rmv_cand"], poi)
+    assert np.array_equal(kept, golden["A_rmv_kept"])
+    assert np.all(np.diff(kept) > 0)
+
+
+def test_cons3_oracle_matches_host_mirror(orc, pkg, golden):
+    TC = pkg.TDM_Constraints
+    prev = golden["A_prev"]
+    cons3 = TC.create_cons3(prev, 100 / 180 * math.pi, golden["A_dlim"])
+    for c, f in zip(golden["A_cands"], golden["A_cons3"]):
+        assert cons3(c) == bool(f) == orc.ref_cons3(prev, c, golden["A_dlim"], golden["A_tan"][0])
