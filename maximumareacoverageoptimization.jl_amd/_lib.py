@@ -27,6 +27,7 @@ MAC_E_NODEVICE = 7
 MAC_OPT_ALGO = 1
 MAC_OPT_STORAGE = 2
 MAC_OPT_TILE_POINTS = 3
+MAC_OPT_PROFILE = 4
 MAC_ALGO_AUTO = 0
 MAC_ALGO_SCAN = 1
 MAC_ALGO_TILED = 2
@@ -42,7 +43,7 @@ EXPORTS = (
     "mac_set_points_dev_f64", "mac_num_points", "mac_get_points_f64",
     "mac_remove_covered_f64", "mac_covered_flags_f64", "mac_area_f64", "mac_area_batch_f64",
     "mac_objective_batch_f64", "mac_poll_best_f64", "mac_area_batch_dev_f64",
-    "mac_poll_best_dev_f64", "mac_cover_threshold",
+    "mac_poll_best_dev_f64", "mac_cover_threshold", "mac_profile_read",
 )
 
 
@@ -93,6 +94,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mac_poll_best_dev_f64": ([_vp, _vp, _i64, _i64, _vp, ctypes.c_double, _vp, _vp,
                                    ctypes.c_double, _i64, _vp, _vp, _vp], _i32),
         "mac_cover_threshold": ([ctypes.c_double], ctypes.c_double),
+        "mac_profile_read": ([_vp, _dp, _i64p, _i64p, _i32], _i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -198,6 +200,18 @@ class Context:
         if algo not in ALGOS:
             raise ValueError(f"algo must be one of {sorted(ALGOS)}")
         self.set_option(MAC_OPT_ALGO, ALGOS[algo])
+
+    def profile(self, on: bool = True) -> None:
+        self.set_option(MAC_OPT_PROFILE, 1 if on else 0)
+
+    def profile_read(self, reset: bool = True):
+        """(coverage-kernel ms summed over launches, launches, candidates evaluated)."""
+        ms = ctypes.c_double()
+        n = _i64()
+        k = _i64()
+        _check(self._L.mac_profile_read(self._h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(k),
+                                        1 if reset else 0))
+        return ms.value, int(n.value), int(k.value)
 
     # -- point list
     def set_points(self, x, y, w) -> None:

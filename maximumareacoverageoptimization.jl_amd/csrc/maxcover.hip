@@ -104,6 +104,10 @@ struct mac_ctx {
     hipStream_t setup_stream = nullptr;
 
     int algo = MAC_ALGO_AUTO;
+    bool profile = false;
+    std::vector<hipEvent_t> ev_pool;                 // free timing events
+    struct Prof { hipEvent_t a, b; int64_t K; };
+    std::vector<Prof> prof;                          // recorded launches (guarded by mu)
     int storage = MAC_STORE_F64;
     int tile_ppt = 4;
 
@@ -310,6 +314,23 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_c
     HCK(hipGetLastError());
     const int64_t M = ctx->M;
     int G;
+    hipEvent_t ev_a = nullptr, ev_b = nullptr;
+    if (ctx->profile) {
+        {
+            std::lock_guard<std::mutex> lk(ctx->mu);
+            if (ctx->ev_pool.size() >= 2) {
+                ev_a = ctx->ev_pool.back();
+                ctx->ev_pool.pop_back();
+                ev_b = ctx->ev_pool.back();
+                ctx->ev_pool.pop_back();
+            }
+        }
+        if (!ev_a) {
+            HCK(hipEventCreate(&ev_a));
+            HCK(hipEventCreate(&ev_b));
+        }
+        HCK(hipEventRecord(ev_a, s));
+    }
     if (tiled) {
         // enough workgroups to fill the chip; each slice keeps >= 1 disk per wave
         const int target = 8 * ctx->cus;
@@ -339,6 +360,11 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_c
                            dim3(kBlock), 0, s, ctx->xys.as<double2>(), ctx->ws.as<double>(), M,
                            L->disks.as<DiskRec>(), N, K, chunk, (int)nblk, L->partial.as<double>());
         HCK(hipGetLastError());
+    }
+    if (ctx->profile) {
+        HCK(hipEventRecord(ev_b, s));
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        ctx->prof.push_back({ev_a, ev_b, (int64_t)K});
     }
     hipLaunchKernelGGL(finalize_kernel, dim3(grid1d(K, 256)), dim3(256), 0, s,
                        L->partial.as<double>(), G, K, d_cands, N, ldc, d_rmax, penalty, d_prev,
@@ -438,6 +464,37 @@ const char* mac_version(void) { return "maxcover 0.1.0 gfx950"; }
 
 double mac_cover_threshold(double r) { return cover_threshold(r); }
 
+int32_t mac_profile_read(mac_ctx* ctx, double* kernel_ms, int64_t* launches,
+                         int64_t* candidates, int32_t reset)
+{
+    ABI_BEGIN
+    if (!ctx) return fail(MAC_E_INVAL, "null context");
+    set_device(ctx);
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    double ms = 0.0;
+    int64_t n = 0, kc = 0;
+    for (auto& p : ctx->prof) {
+        HCK(hipEventSynchronize(p.b));
+        float t = 0.f;
+        HCK(hipEventElapsedTime(&t, p.a, p.b));
+        ms += t;
+        ++n;
+        kc += p.K;
+    }
+    if (kernel_ms) *kernel_ms = ms;
+    if (launches) *launches = n;
+    if (candidates) *candidates = kc;
+    if (reset) {
+        for (auto& p : ctx->prof) {
+            ctx->ev_pool.push_back(p.a);
+            ctx->ev_pool.push_back(p.b);
+        }
+        ctx->prof.clear();
+    }
+    return MAC_OK;
+    ABI_END
+}
+
 int32_t mac_device_count(int32_t* count_out)
 {
     ABI_BEGIN
@@ -489,6 +546,11 @@ void mac_ctx_destroy(mac_ctx* ctx)
                       &ctx->flags_s, &ctx->flags_o, &ctx->keep, &ctx->sel_count, &ctx->cx,
                       &ctx->cy, &ctx->cw, &ctx->cidx, &ctx->circ, &ctx->cdisk})
         b->release();
+    for (auto& p : ctx->prof) {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
     if (ctx->setup_stream) (void)hipStreamDestroy(ctx->setup_stream);
     delete ctx;
 }
@@ -506,6 +568,9 @@ int32_t mac_set_option(mac_ctx* ctx, int32_t option, int64_t value)
             return fail(MAC_E_INVAL, "bad storage");
         if (value == MAC_STORE_F32) return fail(MAC_E_INVAL, "f32 storage not available yet");
         ctx->storage = (int)value;
+        return MAC_OK;
+    case MAC_OPT_PROFILE:
+        ctx->profile = value != 0;
         return MAC_OK;
     case MAC_OPT_TILE_POINTS:
         if (value < 1 || value > 4096) return fail(MAC_E_INVAL, "tile points out of range");

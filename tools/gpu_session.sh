@@ -1,0 +1,60 @@
+#!/bin/bash
+# One GPU session on the MI355X box: parity tests, smoke, bench, rocprofv3 kernel stats.
+# Each GPU step has its own time limit; a fault / abort / segfault / timeout ends the session.
+# Usage: tools/gpu_session.sh [steps...]   steps: tests smoke bench prof pmc (default: all)
+set -u
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+STEPS=${*:-"tests smoke bench prof"}
+TAG=${TAG:-r01}
+
+run() {  # name seconds cmd...
+    local name=$1 t=$2
+    shift 2
+    echo "=== $name (limit ${t}s): $*"
+    local t0=$(date +%s)
+    timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "=== $name rc=$rc ($(( $(date +%s) - t0 ))s)"
+    tail -n 25 "gpurun_out/$name.log"
+    return $rc
+}
+fatal() {  # exit codes after which nothing more may touch the GPU
+    case $1 in 0|1|2|3|4|5) return 1 ;; *) return 0 ;; esac
+}
+
+[ -f maximumareacoverageoptimization.jl_amd/libmaxcover.so ] || make -s -C maximumareacoverageoptimization.jl_amd/csrc
+[ -f oracle/libref_cpu.so ] || make -s -C oracle
+
+for s in $STEPS; do
+    case $s in
+    tests)
+        run pytest_gpu 1500 python -m pytest tests -m gpu -q -rfE -p no:cacheprovider ; rc=$? ;;
+    smoke)
+        run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ; rc=$? ;;
+    bench)
+        run bench 900 python bench.py ; rc=$?
+        grep '^{' gpurun_out/bench.log > gpurun_out/bench_${TAG}.json ;;
+    bench3)
+        run bench3 600 python bench.py --config 3 --no-cpu ; rc=$? ;;
+    bench2)
+        run bench2 600 python bench.py --config 2 --no-cpu ; rc=$? ;;
+    prof)
+        rm -rf gpurun_out/prof
+        run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
+            -- python3 bench.py --steps 10 --warmup 2 --no-cpu ; rc=$?
+        find gpurun_out/prof -name '*stats*' | head ;;
+    pmc)
+        rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
+        run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run \
+            -- python3 bench.py --steps 5 --warmup 1 --no-cpu ; rc=$?
+        if ! fatal $rc; then
+            run pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run \
+                -- python3 bench.py --steps 5 --warmup 1 --no-cpu ; rc=$?
+        fi ;;
+    *) echo "unknown step $s"; rc=0 ;;
+    esac
+    if fatal $rc; then echo "=== stopping: $s exited $rc"; exit $rc; fi
+done
+echo "=== session done"
