@@ -85,7 +85,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=4, choices=(2, 3, 4))
-    ap.add_argument("--algo", default="auto", choices=("auto", "tiled", "scan"))
+    ap.add_argument("--algo", default="auto", choices=("auto", "tiled", "scan", "poll"))
     ap.add_argument("--polls", type=int, default=4, help="distinct poll sets cycled over steps")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -134,14 +134,20 @@ def main():
     d_polls = [torch.from_numpy(np.ascontiguousarray(p[lo:hi])).to(dev) for p in polls]
     d_rmax = torch.from_numpy(r_max).to(dev)
     d_best = torch.empty(2, dtype=torch.float64, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    h_best = torch.empty(2, dtype=torch.float64).pin_memory()
+    stream = torch.cuda.Stream(dev)
 
     def step(i):
+        """One MADS poll. It ends with the best (objective, index) on the host, because the
+        next poll's candidates depend on it: polls never overlap."""
         d = d_polls[i % len(d_polls)]
-        ctx.poll_best_dev(d, 3 * N, Kl, d_rmax, d_best, idx_base=lo, stream=stream.cuda_stream)
-        if distributed:
-            return pdist.gather_best(d_best)
-        return None
+        with torch.cuda.stream(stream):
+            ctx.poll_best_dev(d, 3 * N, Kl, d_rmax, d_best, idx_base=lo, stream=stream.cuda_stream)
+            if distributed:
+                return pdist.gather_best(d_best)
+            h_best.copy_(d_best, non_blocking=True)
+        stream.synchronize()
+        return float(h_best[0]), int(h_best.view(torch.int64)[1])
 
     for i in range(args.warmup):
         step(i)
@@ -172,7 +178,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    k_ms, k_launches, k_cands = ctx.profile_read(reset=True)
+    k_ms, k_launches, k_cands, k_walk = ctx.profile_read(reset=True)
     ctx.profile(False)
     if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -241,7 +247,7 @@ def main():
                 "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "traffic": traffic,
-                "kernel": "coverage_tiled_kernel" if args.algo != "scan" else "coverage_scan_kernel",
+                "kernel": f"coverage_{k_walk}_kernel",
                 "bytes_per_eval": b_eval,
                 "evals_per_launch": cands_per_launch,
                 "avg_launch_ms": avg_launch_ms,

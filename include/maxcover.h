@@ -53,14 +53,16 @@ extern "C" {
 #define MAC_E_NODEVICE    7  /* no HIP device / bad device index                             */
 
 /* ---- options (mac_set_option) --------------------------------------------------- */
-#define MAC_OPT_ALGO         1  /* MAC_ALGO_AUTO (default) | MAC_ALGO_SCAN | MAC_ALGO_TILED     */
+#define MAC_OPT_ALGO         1  /* MAC_ALGO_AUTO (default) | _SCAN | _TILED | _POLL             */
 #define MAC_OPT_STORAGE      2  /* MAC_STORE_F64 (default) | MAC_STORE_F32 (lossless coords)   */
 #define MAC_OPT_TILE_POINTS  3  /* target points per spatial tile (default 4), set before points */
 #define MAC_OPT_PROFILE      4  /* 1: bracket every coverage-kernel launch with HIP events       */
 
 #define MAC_ALGO_AUTO   0
 #define MAC_ALGO_SCAN   1  /* streaming brute-force scan: every point against every disk     */
-#define MAC_ALGO_TILED  2  /* disk-major walk over the tile-binned point list (exact culling) */
+#define MAC_ALGO_TILED  2  /* per-candidate walk over the tile-binned point list (exact culling) */
+#define MAC_ALGO_POLL   3  /* per-disk walk over the whole poll: region entries staged in LDS,
+                              one candidate per lane (AUTO picks it on the device when cheaper) */
 
 #define MAC_STORE_F64   0
 #define MAC_STORE_F32   1
@@ -137,9 +139,10 @@ int32_t mac_poll_best_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three
 /* With MAC_OPT_PROFILE = 1, every coverage-kernel launch (tiled walk or streaming scan) is
  * bracketed by HIP events recorded on the stream it runs on. Reads (waiting for the recorded
  * events) the summed kernel time in ms, the launch count and the candidates evaluated by
- * those launches; reset != 0 clears the record. */
+ * those launches, and the walk the LAST of them used (MAC_ALGO_SCAN / _TILED / _POLL, 0 =
+ * none); reset != 0 clears the record. */
 int32_t mac_profile_read(mac_ctx* ctx, double* kernel_ms, int64_t* launches,
-                         int64_t* candidates, int32_t reset);
+                         int64_t* candidates, int32_t* last_algo, int32_t reset);
 
 /* ---- exact predicate helpers (host) --------------------------------------------- */
 /* Largest double T with: for every double a >= 0, (sqrt(a) < r) <=> (a <= T), where sqrt is

@@ -31,10 +31,12 @@ MAC_OPT_PROFILE = 4
 MAC_ALGO_AUTO = 0
 MAC_ALGO_SCAN = 1
 MAC_ALGO_TILED = 2
+MAC_ALGO_POLL = 3
 MAC_STORE_F64 = 0
 MAC_STORE_F32 = 1
 
-ALGOS = {"auto": MAC_ALGO_AUTO, "scan": MAC_ALGO_SCAN, "tiled": MAC_ALGO_TILED}
+ALGOS = {"auto": MAC_ALGO_AUTO, "scan": MAC_ALGO_SCAN, "tiled": MAC_ALGO_TILED,
+         "poll": MAC_ALGO_POLL}
 
 # Every symbol include/maxcover.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -94,7 +96,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mac_poll_best_dev_f64": ([_vp, _vp, _i64, _i64, _vp, ctypes.c_double, _vp, _vp,
                                    ctypes.c_double, _i64, _vp, _vp, _vp], _i32),
         "mac_cover_threshold": ([ctypes.c_double], ctypes.c_double),
-        "mac_profile_read": ([_vp, _dp, _i64p, _i64p, _i32], _i32),
+        "mac_profile_read": ([_vp, _dp, _i64p, _i64p, ctypes.POINTER(_i32), _i32], _i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -205,13 +207,16 @@ class Context:
         self.set_option(MAC_OPT_PROFILE, 1 if on else 0)
 
     def profile_read(self, reset: bool = True):
-        """(coverage-kernel ms summed over launches, launches, candidates evaluated)."""
+        """(coverage-kernel ms summed over launches, launches, candidates evaluated, walk used
+        by the last launch: 'scan' | 'tiled' | 'poll' | None)."""
         ms = ctypes.c_double()
         n = _i64()
         k = _i64()
+        a = _i32()
         _check(self._L.mac_profile_read(self._h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(k),
-                                        1 if reset else 0))
-        return ms.value, int(n.value), int(k.value)
+                                        ctypes.byref(a), 1 if reset else 0))
+        name = {MAC_ALGO_SCAN: "scan", MAC_ALGO_TILED: "tiled", MAC_ALGO_POLL: "poll"}.get(a.value)
+        return ms.value, int(n.value), int(k.value), name
 
     # -- point list
     def set_points(self, x, y, w) -> None:

@@ -1,15 +1,19 @@
 // kernels.h — gfx950 (CDNA4, wave64) device code of libmaxcover.
 //
-// Hot path (one MADS poll = K candidates x full coverage scan, src/TDM_STATIC_opt.jl:82-100 via
-// src/AreaCoverageCalculation.jl:63-78):
-//   disk_prep_kernel     per (candidate, disk): {cx, cy, T(r), r} with T the exact threshold
-//   coverage_tiled_kernel disk-major walk over the tile-binned point list; one workgroup (or G)
-//                         per candidate; a point is counted by the lowest-index disk covering it
-//   coverage_scan_kernel  streaming brute force: every point against every disk (scalar-cache
-//                         disk operands, branch-free), KB candidates per pass
-//   finalize_kernel       fixed-order partial sum -> area; objective penalty; cons3 mask
+// Hot path: one MADS poll = K candidates x full coverage of the fire-point list
+// (src/TDM_STATIC_opt.jl:82-100 via src/AreaCoverageCalculation.jl:63-78), as a short chain:
+//   disk_prep*_kernel     per (candidate, disk): {cx, cy, T(r), r}, T the exact threshold
+//   region_kernel         per disk i: union of its tile spans over the K candidates + costs
+//   decide_kernel         picks the poll walk or the per-candidate walk on the device
+//   coverage_poll_kernel  workgroup = (disk i, 256 candidates): the entries of disk i's region
+//                         staged in LDS once, one candidate per lane, broadcast LDS reads
+//   coverage_tiled_kernel workgroup = candidate: each wave walks whole disks over the CSR rows
+//   coverage_scan_kernel  streaming brute force (every entry x every disk), the fallback
+//   finalize_kernel       fixed-order sum of per-slice partials -> area; penalty; cons3 mask
 //   argmin_kernel         lexicographic (objective, index) minimum
-// Set-up path (once per MPC step): bbox, tile keys, gather, offsets, covered flags.
+// An entry is credited to the LOWEST-index disk covering it (exactly-once union count), so the
+// area is the reference's first-hit-break sum (:67-78) over the same multiset of entries.
+// Partials are laid out [slice][candidate] and summed in slice order: bit-reproducible.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -24,7 +28,13 @@ namespace mac {
 constexpr int kWave = 64;
 constexpr int kBlock = 256;        // 4 waves
 constexpr int kWavesPerBlock = kBlock / kWave;
-constexpr int kNbrCap = 6;         // lower-index overlapping disks kept per disk in LDS
+constexpr int kNbrCap = 6;         // tiled walk: lower-index overlapping disks kept per disk
+constexpr int kPollCH = 1024;      // poll walk: entries staged in LDS per chunk
+constexpr int kPollRB = 64;        // poll walk: region rows per batch
+constexpr int kPollNbr = 64;       // poll walk: lower-index overlapping regions kept
+
+constexpr int kModePoll = 1;
+constexpr int kModeTiled = 2;
 
 struct Grid {
     double gx0, gy0;     // origin (bbox min of the finite points)
@@ -41,9 +51,8 @@ struct DiskRec {         // 32 B, one per (candidate, disk)
 
 __device__ __forceinline__ double wave_sum_f64(double v)
 {
-    // fixed butterfly: deterministic
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);  // fixed butterfly
     return v;
 }
 
@@ -73,9 +82,29 @@ __device__ __forceinline__ double block_sum_f64(double v, double* red /* kWavesP
     return s;
 }
 
+__device__ __forceinline__ DiskRec make_disk(double cx, double cy, double r)
+{
+    DiskRec d;
+    d.cx = cx;
+    d.cy = cy;
+    d.r = r;
+    d.T = cover_threshold(r);
+    return d;
+}
+
+__device__ __forceinline__ bool disk_span(const DiskRec& d, const Grid& g, int4& sp)
+{
+    int x0, x1, y0, y1;
+    if (!(d.T >= 0.0)) return false;
+    if (!tile_span(d.cx, d.r, g.gx0, g.invS, g.nTx, x0, x1)) return false;
+    if (!tile_span(d.cy, d.r, g.gy0, g.invS, g.nTy, y0, y1)) return false;
+    sp = make_int4(x0, x1, y0, y1);
+    return true;
+}
+
 // ------------------------------------------------------------------ per-batch disk prep
 
-// cands: 3N x K column-major (candidate k at cands + k*ldc). Writes disks[k*N + i].
+// cands: 3N x K column-major (candidate k at cands + k*ldc). Writes disks[k*N + i] (scan walk).
 __global__ void disk_prep_kernel(const double* __restrict__ cands, int N, int ldc, int K,
                                  DiskRec* __restrict__ disks)
 {
@@ -83,24 +112,107 @@ __global__ void disk_prep_kernel(const double* __restrict__ cands, int N, int ld
     if (t >= (int64_t)N * K) return;
     const int k = (int)(t / N), i = (int)(t % N);
     const double* c = cands + (int64_t)k * ldc;
-    DiskRec d;
-    d.cx = c[i];
-    d.cy = c[N + i];
-    d.r = c[2 * N + i];
-    d.T = cover_threshold(d.r);
-    disks[t] = d;
+    disks[t] = make_disk(c[i], c[N + i], c[2 * N + i]);
+}
+
+// Transposed prep: disksT[i*K + k] (disk-major, candidates contiguous). 32 x 32 tiles through
+// LDS so both the candidate reads and the record writes are coalesced.
+__global__ __launch_bounds__(kBlock) void disk_prep_T_kernel(const double* __restrict__ cands,
+                                                             int N, int ldc, int K,
+                                                             DiskRec* __restrict__ disksT)
+{
+    __shared__ double sx[32][33], sy[32][33], sr[32][33];
+    const int i0 = blockIdx.x * 32, k0 = blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+    for (int kk = ty; kk < 32; kk += 8) {
+        const int k = k0 + kk, i = i0 + tx;
+        if (k < K && i < N) {
+            const double* c = cands + (int64_t)k * ldc;
+            sx[kk][tx] = c[i];
+            sy[kk][tx] = c[N + i];
+            sr[kk][tx] = c[2 * N + i];
+        }
+    }
+    __syncthreads();
+    for (int ii = ty; ii < 32; ii += 8) {
+        const int i = i0 + ii, k = k0 + tx;
+        if (k < K && i < N) disksT[(int64_t)i * K + k] = make_disk(sx[tx][ii], sy[tx][ii], sr[tx][ii]);
+    }
+}
+
+// ------------------------------------------------------------------ region + decision
+
+// Block i: union over the K candidates of disk i's tile span (region[i]) and two costs in
+// point-visits / ppt: poll walk = K * |region|, per-candidate walk = sum_k |span_k|.
+__global__ __launch_bounds__(kBlock) void region_kernel(const DiskRec* __restrict__ disksT,
+                                                        int N, int K, Grid g,
+                                                        int4* __restrict__ region,
+                                                        double2* __restrict__ cost)
+{
+    const int i = blockIdx.x;
+    int x0 = 0x7fffffff, y0 = 0x7fffffff, x1 = -1, y1 = -1;
+    double cand = 0.0;
+    for (int k = threadIdx.x; k < K; k += kBlock) {
+        const DiskRec d = disksT[(int64_t)i * K + k];
+        int4 sp;
+        if (disk_span(d, g, sp)) {
+            x0 = min(x0, sp.x);
+            x1 = max(x1, sp.y);
+            y0 = min(y0, sp.z);
+            y1 = max(y1, sp.w);
+            cand += (double)(sp.y - sp.x + 1) * (double)(sp.w - sp.z + 1);
+        }
+    }
+    __shared__ int sh[4][kBlock];
+    __shared__ double red[kWavesPerBlock];
+    sh[0][threadIdx.x] = x0;
+    sh[1][threadIdx.x] = -x1;
+    sh[2][threadIdx.x] = y0;
+    sh[3][threadIdx.x] = -y1;
+    __syncthreads();
+    for (int s = kBlock / 2; s > 0; s >>= 1) {
+        if (threadIdx.x < s)
+            for (int q = 0; q < 4; ++q) sh[q][threadIdx.x] = min(sh[q][threadIdx.x], sh[q][threadIdx.x + s]);
+        __syncthreads();
+    }
+    const double candsum = block_sum_f64(cand, red);
+    if (threadIdx.x == 0) {
+        const int4 R = make_int4(sh[0][0], -sh[1][0], sh[2][0], -sh[3][0]);
+        region[i] = R;
+        const double rc = R.x <= R.y ? (double)(R.y - R.x + 1) * (double)(R.w - R.z + 1) : 0.0;
+        cost[i] = make_double2(rc * (double)K, candsum);
+    }
+}
+
+// One block: mode = poll walk when its point-visits stay within `ratio` x the per-candidate
+// walk's (its visits are broadcast LDS reads; the other's are scattered global loads).
+__global__ __launch_bounds__(kBlock) void decide_kernel(const double2* __restrict__ cost, int N,
+                                                        double ratio, int forced,
+                                                        int* __restrict__ mode)
+{
+    __shared__ double red[kWavesPerBlock];
+    double a = 0.0, b = 0.0;
+    for (int i = threadIdx.x; i < N; i += kBlock) {
+        a += cost[i].x;
+        b += cost[i].y;
+    }
+    const double A = block_sum_f64(a, red);
+    __syncthreads();
+    const double B = block_sum_f64(b, red);
+    if (threadIdx.x == 0) *mode = forced ? forced : (A <= ratio * B ? kModePoll : kModeTiled);
 }
 
 // ------------------------------------------------------------------ streaming scan
 
-// Every point against every disk of KB candidates. Disk operands are wave-uniform loads
-// (scalar cache); each lane holds PPT points in registers. Branch-free inner loop: the
-// first-hit `break` of the reference changes which disk is credited, never the sum.
+// Every entry against every disk of KB candidates (disks[k*N + c], wave-uniform loads through
+// the scalar cache); each lane holds PPT entries in registers. Branch-free inner loop: the
+// reference's first-hit `break` changes which disk is credited, never the sum.
+// partial[blk*K + k]: this block's share of candidate k.
 template <int KB, int PPT>
 __global__ __launch_bounds__(kBlock) void coverage_scan_kernel(
     const double2* __restrict__ xy, const double* __restrict__ w, int64_t M,
-    const DiskRec* __restrict__ disks, int N, int K, int64_t chunk, int nblk,
-    double* __restrict__ partial /* K x nblk */)
+    const DiskRec* __restrict__ disks, int N, int K, int64_t chunk,
+    double* __restrict__ partial)
 {
     __shared__ double red[kWavesPerBlock];
     const int blk = blockIdx.x;
@@ -150,67 +262,67 @@ __global__ __launch_bounds__(kBlock) void coverage_scan_kernel(
     for (int q = 0; q < KB; ++q) {
         const int k = k0 + q;
         const double s = block_sum_f64(acc[q], red);
-        if (threadIdx.x == 0 && k < K) partial[(int64_t)k * nblk + blk] = s;
+        if (threadIdx.x == 0 && k < K) partial[(int64_t)blk * K + k] = s;
         __syncthreads();
     }
 }
 
-// ------------------------------------------------------------------ tiled (culled) walk
+// ------------------------------------------------------------------ per-candidate tiled walk
 
-// LDS layout for the tiled kernel, N disks (dynamic shared memory, 16-B aligned carve):
-//   double cx[N], cy[N], T[N]; int4 span[N]; uint16 ncnt[N]; uint16 nbr[N][kNbrCap];
+// LDS layout, N disks (dynamic shared memory, 16-B aligned carve):
+//   double cx[N], cy[N], T[N], r[N]; int4 span[N]; uint16 ncnt[N]; uint16 nbr[N][kNbrCap];
 //   per wave: int rowStart[64], rowPre[64]
-__host__ __device__ inline size_t tiled_lds_bytes(int N)
+__host__ __device__ inline size_t tiled_lds_head(int N)
 {
-    size_t b = (size_t)N * 3 * sizeof(double);
+    size_t b = (size_t)N * 4 * sizeof(double);
     b += (size_t)N * 4 * sizeof(int);
     b += (size_t)N * sizeof(uint16_t) * (1 + kNbrCap);
-    b = (b + 15) & ~(size_t)15;
-    b += (size_t)kWavesPerBlock * 2 * kWave * sizeof(int);
-    return b;
+    return (b + 15) & ~(size_t)15;
+}
+__host__ __device__ inline size_t tiled_lds_bytes(int N)
+{
+    return tiled_lds_head(N) + (size_t)kWavesPerBlock * 2 * kWave * sizeof(int);
 }
 
-// One workgroup per (candidate k, slice gi of G). Each wave walks whole disks: for disk c it
-// reads the tile-row runs of c's bounding box from the CSR offsets (tile rows are contiguous
-// in the sorted list), tests every point in them, and credits a covered point only when no
-// lower-index disk also covers it (exactly-once union count; lower-index overlap candidates
-// come from a conservative disk-disk intersection list built in LDS).
+// Workgroup = (candidate k, slice gi of G). Each wave walks whole disks: for disk c it reads
+// the tile-row runs of c's span from the CSR offsets (a row of tiles is contiguous in the
+// sorted list), tests every entry in them, and credits a covered entry only when no lower-index
+// disk also covers it (candidates for that come from a conservative disk-disk intersection
+// list built in LDS). disksT[c*K + k]; partial[gi*K + k]. Runs only when *mode == kModeTiled
+// (or mode == null).
 __global__ __launch_bounds__(kBlock) void coverage_tiled_kernel(
     const double2* __restrict__ xy, const double* __restrict__ w,
     const int32_t* __restrict__ off, Grid g,
-    const DiskRec* __restrict__ disks, int N, int K, int G,
-    double* __restrict__ partial /* K x G */)
+    const DiskRec* __restrict__ disksT, int N, int K, int G, const int* __restrict__ mode,
+    double* __restrict__ partial)
 {
+    if (mode && *mode != kModeTiled) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     double* sx = (double*)lds;
     double* sy = sx + N;
     double* sT = sy + N;
-    int4* span = (int4*)(sT + N);
+    double* sR = sT + N;
+    int4* span = (int4*)(sR + N);
     uint16_t* ncnt = (uint16_t*)(span + N);
     uint16_t* nbr = ncnt + N;
-    size_t wofs = (size_t)N * 3 * sizeof(double) + (size_t)N * 4 * sizeof(int) +
-                  (size_t)N * sizeof(uint16_t) * (1 + kNbrCap);
-    wofs = (wofs + 15) & ~(size_t)15;
     const int lane = threadIdx.x & (kWave - 1);
     const int wid = threadIdx.x / kWave;
-    int* rowStart = (int*)(lds + wofs) + wid * 2 * kWave;
+    int* rowStart = (int*)(lds + tiled_lds_head(N)) + wid * 2 * kWave;
     int* rowPre = rowStart + kWave;
     __shared__ double red[kWavesPerBlock];
 
     const int k = blockIdx.x / G;
     const int gi = blockIdx.x % G;
-    const DiskRec* dk = disks + (int64_t)k * N;
 
     // 1. disks -> LDS, spans
     for (int c = threadIdx.x; c < N; c += kBlock) {
-        const DiskRec d = dk[c];
+        const DiskRec d = disksT[(int64_t)c * K + k];
         sx[c] = d.cx;
         sy[c] = d.cy;
         sT[c] = d.T;
-        int x0, x1, y0, y1;
-        const bool okx = d.T >= 0.0 && tile_span(d.cx, d.r, g.gx0, g.invS, g.nTx, x0, x1);
-        const bool oky = okx && tile_span(d.cy, d.r, g.gy0, g.invS, g.nTy, y0, y1);
-        span[c] = oky ? make_int4(x0, x1, y0, y1) : make_int4(1, 0, 1, 0);
+        sR[c] = d.r;
+        int4 sp;
+        span[c] = disk_span(d, g, sp) ? sp : make_int4(1, 0, 1, 0);
     }
     __syncthreads();
 
@@ -218,10 +330,10 @@ __global__ __launch_bounds__(kBlock) void coverage_tiled_kernel(
     for (int c = gi + G * threadIdx.x; c < N; c += G * kBlock) {
         int cnt = 0;
         if (span[c].x <= span[c].y) {
-            const double cx = sx[c], cy = sy[c], r = dk[c].r;
+            const double cx = sx[c], cy = sy[c], r = sR[c];
             for (int c2 = 0; c2 < c; ++c2) {
                 if (span[c2].x > span[c2].y) continue;  // covers nothing
-                if (disks_may_overlap(cx, cy, r, sx[c2], sy[c2], dk[c2].r)) {
+                if (disks_may_overlap(cx, cy, r, sx[c2], sy[c2], sR[c2])) {
                     if (cnt < kNbrCap) nbr[c * kNbrCap + cnt] = (uint16_t)c2;
                     ++cnt;
                 }
@@ -281,16 +393,124 @@ __global__ __launch_bounds__(kBlock) void coverage_tiled_kernel(
         }
     }
     const double s = block_sum_f64(acc, red);
-    if (threadIdx.x == 0) partial[(int64_t)k * G + gi] = s;
+    if (threadIdx.x == 0) partial[(int64_t)gi * K + k] = s;
+}
+
+// ------------------------------------------------------------------ poll walk
+
+// Workgroup = (disk i, candidates k = 256*blockIdx.y + lane). The entries of disk i's region
+// (union of its spans over the whole poll) are staged in LDS in chunks; every lane then tests
+// its own candidate's disk i against each staged entry (one broadcast LDS read per entry per
+// wave) and credits it when no lower-index disk j of the SAME candidate covers it (j ranges
+// over the disks whose regions overlap region i). partialT[i*K + k]. Runs when *mode == poll.
+__global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
+    const double2* __restrict__ xy, const double* __restrict__ w,
+    const int32_t* __restrict__ off, Grid g, const DiskRec* __restrict__ disksT,
+    const int4* __restrict__ region, int N, int K, const int* __restrict__ mode,
+    double* __restrict__ partialT)
+{
+    if (mode && *mode != kModePoll) return;
+    __shared__ double2 sxy[kPollCH];
+    __shared__ double sw[kPollCH];
+    __shared__ int rs[kPollRB], rpre[kPollRB + 1];
+    __shared__ uint16_t nbr[kPollNbr];
+    __shared__ int ncnt;
+
+    const int i = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int k = blockIdx.y * kBlock + tid;
+    const bool valid = k < K;
+    const int4 R = region[i];
+    if (R.x > R.y) {  // disk i covers nothing in any candidate
+        if (valid) partialT[(int64_t)i * K + k] = 0.0;
+        return;
+    }
+    DiskRec d;
+    if (valid) d = disksT[(int64_t)i * K + k];
+    else d = DiskRec{0.0, 0.0, -1.0, 0.0};
+
+    // lower-index disks whose regions overlap region i (order is irrelevant: boolean OR)
+    if (tid == 0) ncnt = 0;
+    __syncthreads();
+    for (int j = tid; j < i; j += kBlock) {
+        const int4 Q = region[j];
+        if (Q.x <= Q.y && Q.x <= R.y && R.x <= Q.y && Q.z <= R.w && R.z <= Q.w) {
+            const int p = atomicAdd(&ncnt, 1);
+            if (p < kPollNbr) nbr[p] = (uint16_t)j;
+        }
+    }
+    __syncthreads();
+    const int nc = ncnt;
+
+    double acc = 0.0;
+    for (int rb = R.z; rb <= R.w; rb += kPollRB) {
+        const int nr = min(kPollRB, R.w - rb + 1);
+        if (tid < nr) {
+            const int64_t rowbase = (int64_t)(rb + tid) * g.nTx;
+            const int s = off[rowbase + R.x];
+            rs[tid] = s;
+            rpre[tid + 1] = off[rowbase + R.y + 1] - s;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            rpre[0] = 0;
+            for (int r = 0; r < nr; ++r) rpre[r + 1] += rpre[r];
+        }
+        __syncthreads();
+        const int total = rpre[nr];
+        for (int base = 0; base < total; base += kPollCH) {
+            const int n = min(kPollCH, total - base);
+            for (int q = tid; q < n; q += kBlock) {
+                const int f = base + q;
+                int lo = 0, hi = nr - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (rpre[mid] <= f) lo = mid; else hi = mid - 1;
+                }
+                const int j = rs[lo] + (f - rpre[lo]);
+                sxy[q] = xy[j];
+                sw[q] = w[j];
+            }
+            __syncthreads();
+            if (d.T >= 0.0) {
+                for (int q = 0; q < n; ++q) {
+                    const double2 p = sxy[q];
+                    if (sqdist(p.x, p.y, d.cx, d.cy) <= d.T) {
+                        bool owned = true;
+                        if (nc <= kPollNbr) {
+                            for (int u = 0; u < nc; ++u) {
+                                const DiskRec e = disksT[(int64_t)nbr[u] * K + k];
+                                if (sqdist(p.x, p.y, e.cx, e.cy) <= e.T) { owned = false; break; }
+                            }
+                        } else {
+                            for (int j = 0; j < i; ++j) {
+                                const int4 Q = region[j];
+                                if (!(Q.x <= Q.y && Q.x <= R.y && R.x <= Q.y && Q.z <= R.w &&
+                                      R.z <= Q.w))
+                                    continue;
+                                const DiskRec e = disksT[(int64_t)j * K + k];
+                                if (sqdist(p.x, p.y, e.cx, e.cy) <= e.T) { owned = false; break; }
+                            }
+                        }
+                        if (owned) acc += sw[q];
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (valid) partialT[(int64_t)i * K + k] = acc;
 }
 
 // ------------------------------------------------------------------ finalize / argmin
 
-// area_k = sum_g partial[k][g] (fixed order). obj_k = -area_k + penalty * violation_k with
-// violation_k = sum_i |x[2N+i] - rmax[i]| sequentially (src/TDM_STATIC_opt.jl:89-97).
-// cons3 (src/TDM_Constraints.jl:54-75) when prev != null: infeasible -> obj = +inf and
-// feasible flag 0. The test sqrt(s) > d_lim is evaluated exactly as !(s <= T(nextup(d))).
-__global__ void finalize_kernel(const double* __restrict__ partial, int G, int K,
+// area_k = sum over slices g of partial[g*K + k] (fixed order); the slice count is n_poll when
+// *mode == poll, else n_other. obj_k = -area_k + penalty * violation_k with violation_k =
+// sum_i |x[2N+i] - rmax[i]| sequentially (src/TDM_STATIC_opt.jl:89-97). cons3
+// (src/TDM_Constraints.jl:54-75) when prev != null: infeasible -> obj = +inf; the test
+// sqrt(s) > d_lim is evaluated exactly as s > dlimT (predicate.h dlim_threshold).
+__global__ void finalize_kernel(const double* __restrict__ partial, const int* __restrict__ mode,
+                                int n_poll, int n_other, int K,
                                 const double* __restrict__ cands, int N, int ldc,
                                 const double* __restrict__ rmax, double penalty,
                                 const double* __restrict__ prev, const double* __restrict__ dlimT,
@@ -299,8 +519,9 @@ __global__ void finalize_kernel(const double* __restrict__ partial, int G, int K
 {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= K) return;
+    const int G = (mode && *mode == kModePoll) ? n_poll : n_other;
     double area = 0.0;
-    for (int g = 0; g < G; ++g) area += partial[(int64_t)k * G + g];
+    for (int g = 0; g < G; ++g) area += partial[(int64_t)g * K + k];
     if (area_out) area_out[k] = area;
     if (!obj_out) return;
     const double* x = cands + (int64_t)k * ldc;
@@ -311,7 +532,6 @@ __global__ void finalize_kernel(const double* __restrict__ partial, int G, int K
             const double x2 = x[i], y2 = x[N + i], z2 = x[2 * N + i] / tan_half_fov;
             const double ddx = x1 - x2, ddy = y1 - y2, ddz = z1 - z2;
             const double s = ddx * ddx + ddy * ddy + ddz * ddz;
-            // dlimT[i] = threshold for "sqrt(s) <= d": +inf sentinel means never infeasible
             if (s > dlimT[i]) { feasible = false; break; }
         }
     }

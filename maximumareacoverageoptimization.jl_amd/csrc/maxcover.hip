@@ -23,6 +23,9 @@
 
 using namespace mac;
 
+static constexpr int kPollMinK = 64;          // below this the per-candidate walk always wins
+static constexpr double kPollCostRatio = 4.0; // poll walk if its visits <= 4x the other's
+
 // ------------------------------------------------------------------ errors
 
 static thread_local std::string g_last_error;
@@ -90,8 +93,9 @@ struct DevBuf {
 // Per-call scratch + stream ("lane"); lanes are pooled so concurrent host threads each get one.
 struct Lane {
     hipStream_t stream = nullptr;
+    hipStream_t last = nullptr;   // stream of the most recent use
     hipEvent_t done = nullptr;
-    DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim;
+    DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode;
     std::vector<double> h_dlim;
 };
 
@@ -102,11 +106,12 @@ struct mac_ctx {
     std::vector<Lane*> lanes_free;
     std::vector<Lane*> lanes_all;
     hipStream_t setup_stream = nullptr;
+    hipStream_t dev_stream = nullptr;   // ordered stream for *_dev calls passed stream = NULL
 
     int algo = MAC_ALGO_AUTO;
     bool profile = false;
     std::vector<hipEvent_t> ev_pool;                 // free timing events
-    struct Prof { hipEvent_t a, b; int64_t K; };
+    struct Prof { hipEvent_t a, b; int64_t K; const int* mode; int algo; };
     std::vector<Prof> prof;                          // recorded launches (guarded by mu)
     int storage = MAC_STORE_F64;
     int tile_ppt = 4;
@@ -126,10 +131,21 @@ struct mac_ctx {
 
 static void set_device(mac_ctx* ctx) { HCK(hipSetDevice(ctx->device)); }
 
-static Lane* acquire_lane(mac_ctx* ctx)
+// A lane's scratch may be reused at once by a call on the SAME stream (stream order protects
+// it); on another stream only after the lane's last work has completed.
+static Lane* acquire_lane(mac_ctx* ctx, hipStream_t want)
 {
     {
         std::lock_guard<std::mutex> lk(ctx->mu);
+        if (want) {
+            for (size_t i = 0; i < ctx->lanes_free.size(); ++i) {
+                Lane* l = ctx->lanes_free[i];
+                if (l->last == want) {
+                    ctx->lanes_free.erase(ctx->lanes_free.begin() + (long)i);
+                    return l;
+                }
+            }
+        }
         for (size_t i = 0; i < ctx->lanes_free.size(); ++i) {
             Lane* l = ctx->lanes_free[i];
             if (hipEventQuery(l->done) == hipSuccess) {
@@ -142,6 +158,7 @@ static Lane* acquire_lane(mac_ctx* ctx)
     HCK(hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking));
     HCK(hipEventCreateWithFlags(&l->done, hipEventDisableTiming));
     HCK(hipEventRecord(l->done, l->stream));
+    l->last = l->stream;
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->lanes_all.push_back(l);
     return l;
@@ -150,15 +167,19 @@ static Lane* acquire_lane(mac_ctx* ctx)
 static void release_lane(mac_ctx* ctx, Lane* l, hipStream_t used)
 {
     (void)hipEventRecord(l->done, used);
+    l->last = used;
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->lanes_free.push_back(l);
 }
 
+// Host-pointer calls: a lane on its own stream (synchronised before return).
+// Device-pointer calls: the caller's stream, or the context's ordered dev stream for NULL.
 struct LaneGuard {
     mac_ctx* ctx;
     Lane* lane;
     hipStream_t used;
-    LaneGuard(mac_ctx* c) : ctx(c), lane(acquire_lane(c)), used(lane->stream) {}
+    explicit LaneGuard(mac_ctx* c) : ctx(c), lane(acquire_lane(c, nullptr)), used(lane->stream) {}
+    LaneGuard(mac_ctx* c, hipStream_t s) : ctx(c), lane(acquire_lane(c, s)), used(s) {}
     ~LaneGuard() { release_lane(ctx, lane, used); }
 };
 
@@ -280,8 +301,9 @@ static int32_t check_M(int64_t M)
 
 static bool use_tiled(mac_ctx* ctx, int N, const double* h_cands, int64_t three_n)
 {
-    if (N <= 0 || N > 2048) return false;
-    if (ctx->algo == MAC_ALGO_SCAN) return false;
+    if (N <= 0 || ctx->algo == MAC_ALGO_SCAN) return false;
+    if (ctx->algo == MAC_ALGO_POLL) return true;        // no N limit: fixed LDS footprint
+    if (N > 2048) return false;                          // per-candidate walk keeps N disks in LDS
     if (ctx->algo == MAC_ALGO_TILED) return true;
     if (!h_cands) return true;
     // AUTO with host candidates: compare the tiled walk's point visits for candidate 0 with
@@ -308,14 +330,12 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_c
                          double* d_area, double* d_obj, double* d_best, int64_t idx_base)
 {
     const int ldc = 3 * N;
-    L->disks.reserve(sizeof(DiskRec) * (size_t)std::max<int64_t>((int64_t)N * K, 1));
-    hipLaunchKernelGGL(disk_prep_kernel, dim3(grid1d((int64_t)N * K, 256)), dim3(256), 0, s,
-                       d_cands, N, ldc, K, L->disks.as<DiskRec>());
-    HCK(hipGetLastError());
     const int64_t M = ctx->M;
-    int G;
+    int n_poll = N, n_other = 1;
+    const int* d_mode = nullptr;
     hipEvent_t ev_a = nullptr, ev_b = nullptr;
-    if (ctx->profile) {
+    auto prof_begin = [&]() {
+        if (!ctx->profile) return;
         {
             std::lock_guard<std::mutex> lk(ctx->mu);
             if (ctx->ev_pool.size() >= 2) {
@@ -330,45 +350,86 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_c
             HCK(hipEventCreate(&ev_b));
         }
         HCK(hipEventRecord(ev_a, s));
-    }
-    if (tiled) {
-        // enough workgroups to fill the chip; each slice keeps >= 1 disk per wave
-        const int target = 8 * ctx->cus;
-        G = (int)std::max<int64_t>(1, std::min<int64_t>((target + K - 1) / K,
-                                                        std::max(1, N / kWavesPerBlock)));
-        L->partial.reserve(sizeof(double) * (size_t)K * G);
-        const size_t lds = tiled_lds_bytes(N);
-        hipLaunchKernelGGL(coverage_tiled_kernel, dim3((unsigned)((int64_t)K * G)), dim3(kBlock),
-                           lds, s, ctx->xys.as<double2>(), ctx->ws.as<double>(),
-                           ctx->off.as<int32_t>(), ctx->grid, L->disks.as<DiskRec>(), N, K, G,
-                           L->partial.as<double>());
+    };
+    auto prof_end = [&]() {
+        if (!ctx->profile) return;
+        HCK(hipEventRecord(ev_b, s));
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        ctx->prof.push_back({ev_a, ev_b, (int64_t)K, d_mode, tiled ? MAC_ALGO_TILED : MAC_ALGO_SCAN});
+    };
+
+    if (N == 0 || M == 0) {  // no UAV or no entry: every area is 0 (the loops never run)
+        L->partial.reserve(sizeof(double) * (size_t)K);
+        HCK(hipMemsetAsync(L->partial.p, 0, sizeof(double) * (size_t)K, s));
+    } else if (!tiled) {
+        L->disks.reserve(sizeof(DiskRec) * (size_t)N * K);
+        hipLaunchKernelGGL(disk_prep_kernel, dim3(grid1d((int64_t)N * K, 256)), dim3(256), 0, s,
+                           d_cands, N, ldc, K, L->disks.as<DiskRec>());
         HCK(hipGetLastError());
-    } else {
         constexpr int KB = 4, PPT = 4;
         const int64_t per_pass = (int64_t)kBlock * PPT;
         int64_t nblk = std::max<int64_t>(1, (M + per_pass - 1) / per_pass);
         const int kgroups = (K + KB - 1) / KB;
         const int64_t want = std::max<int64_t>(1, (int64_t)(8 * ctx->cus) / kgroups);
-        nblk = std::min(nblk, std::max<int64_t>(want, 1));
+        nblk = std::min(nblk, want);
         int64_t chunk = (M + nblk - 1) / nblk;
         chunk = ((chunk + per_pass - 1) / per_pass) * per_pass;
-        if (chunk == 0) chunk = per_pass;
         nblk = std::max<int64_t>(1, (M + chunk - 1) / chunk);
-        G = (int)nblk;
-        L->partial.reserve(sizeof(double) * (size_t)K * G);
+        n_other = (int)nblk;
+        L->partial.reserve(sizeof(double) * (size_t)K * nblk);
+        prof_begin();
         hipLaunchKernelGGL((coverage_scan_kernel<KB, PPT>), dim3((unsigned)nblk, (unsigned)kgroups),
                            dim3(kBlock), 0, s, ctx->xys.as<double2>(), ctx->ws.as<double>(), M,
-                           L->disks.as<DiskRec>(), N, K, chunk, (int)nblk, L->partial.as<double>());
+                           L->disks.as<DiskRec>(), N, K, chunk, L->partial.as<double>());
         HCK(hipGetLastError());
-    }
-    if (ctx->profile) {
-        HCK(hipEventRecord(ev_b, s));
-        std::lock_guard<std::mutex> lk(ctx->mu);
-        ctx->prof.push_back({ev_a, ev_b, (int64_t)K});
+        prof_end();
+    } else {
+        L->disks.reserve(sizeof(DiskRec) * (size_t)N * K);
+        hipLaunchKernelGGL(disk_prep_T_kernel, dim3((N + 31) / 32, (K + 31) / 32), dim3(kBlock), 0,
+                           s, d_cands, N, ldc, K, L->disks.as<DiskRec>());
+        HCK(hipGetLastError());
+        // per-candidate walk: enough workgroups to fill the chip, >= 1 disk per wave
+        const int target = 8 * ctx->cus;
+        const int G = (int)std::max<int64_t>(
+            1, std::min<int64_t>((target + K - 1) / K, std::max(1, N / kWavesPerBlock)));
+        n_other = G;
+        const bool poll_possible = ctx->algo == MAC_ALGO_POLL ||
+                                   (ctx->algo == MAC_ALGO_AUTO && K >= kPollMinK);
+        L->partial.reserve(sizeof(double) * (size_t)K * std::max(G, poll_possible ? N : 1));
+        if (poll_possible) {
+            L->region.reserve(sizeof(int4) * N);
+            L->cost.reserve(sizeof(double2) * N);
+            L->mode.reserve(sizeof(int));
+            hipLaunchKernelGGL(region_kernel, dim3(N), dim3(kBlock), 0, s, L->disks.as<DiskRec>(),
+                               N, K, ctx->grid, L->region.as<int4>(), L->cost.as<double2>());
+            HCK(hipGetLastError());
+            const int forced = ctx->algo == MAC_ALGO_POLL ? kModePoll : 0;
+            hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(kBlock), 0, s, L->cost.as<double2>(), N,
+                               kPollCostRatio, forced, L->mode.as<int>());
+            HCK(hipGetLastError());
+            d_mode = L->mode.as<int>();
+        }
+        prof_begin();
+        if (ctx->algo != MAC_ALGO_POLL) {
+            const size_t lds = tiled_lds_bytes(N);
+            hipLaunchKernelGGL(coverage_tiled_kernel, dim3((unsigned)((int64_t)K * G)), dim3(kBlock),
+                               lds, s, ctx->xys.as<double2>(), ctx->ws.as<double>(),
+                               ctx->off.as<int32_t>(), ctx->grid, L->disks.as<DiskRec>(), N, K, G,
+                               d_mode, L->partial.as<double>());
+            HCK(hipGetLastError());
+        }
+        if (poll_possible) {
+            hipLaunchKernelGGL(coverage_poll_kernel, dim3(N, (K + kBlock - 1) / kBlock), dim3(kBlock),
+                               0, s, ctx->xys.as<double2>(), ctx->ws.as<double>(),
+                               ctx->off.as<int32_t>(), ctx->grid, L->disks.as<DiskRec>(),
+                               L->region.as<int4>(), N, K, d_mode, L->partial.as<double>());
+            HCK(hipGetLastError());
+        }
+        prof_end();
     }
     hipLaunchKernelGGL(finalize_kernel, dim3(grid1d(K, 256)), dim3(256), 0, s,
-                       L->partial.as<double>(), G, K, d_cands, N, ldc, d_rmax, penalty, d_prev,
-                       d_dlimT, tan_half_fov, d_area, d_obj);
+                       L->partial.as<double>(), d_mode, n_poll, n_other, K, d_cands, N, ldc, d_rmax,
+                       penalty, d_prev, d_dlimT, tan_half_fov, d_area, d_obj);
     HCK(hipGetLastError());
     if (d_best) {
         hipLaunchKernelGGL(argmin_kernel, dim3(1), dim3(kBlock), 0, s, d_obj, K, idx_base, d_best);
@@ -465,7 +526,7 @@ const char* mac_version(void) { return "maxcover 0.1.0 gfx950"; }
 double mac_cover_threshold(double r) { return cover_threshold(r); }
 
 int32_t mac_profile_read(mac_ctx* ctx, double* kernel_ms, int64_t* launches,
-                         int64_t* candidates, int32_t reset)
+                         int64_t* candidates, int32_t* last_algo, int32_t reset)
 {
     ABI_BEGIN
     if (!ctx) return fail(MAC_E_INVAL, "null context");
@@ -473,6 +534,7 @@ int32_t mac_profile_read(mac_ctx* ctx, double* kernel_ms, int64_t* launches,
     std::lock_guard<std::mutex> lk(ctx->mu);
     double ms = 0.0;
     int64_t n = 0, kc = 0;
+    int algo = 0;
     for (auto& p : ctx->prof) {
         HCK(hipEventSynchronize(p.b));
         float t = 0.f;
@@ -481,9 +543,19 @@ int32_t mac_profile_read(mac_ctx* ctx, double* kernel_ms, int64_t* launches,
         ++n;
         kc += p.K;
     }
+    if (!ctx->prof.empty()) {
+        const auto& p = ctx->prof.back();
+        algo = p.algo;
+        if (p.mode) {  // the device's choice (the lane's mode word holds its latest decision)
+            int m = 0;
+            HCK(hipMemcpy(&m, p.mode, sizeof(int), hipMemcpyDeviceToHost));
+            algo = m == kModePoll ? MAC_ALGO_POLL : MAC_ALGO_TILED;
+        }
+    }
     if (kernel_ms) *kernel_ms = ms;
     if (launches) *launches = n;
     if (candidates) *candidates = kc;
+    if (last_algo) *last_algo = algo;
     if (reset) {
         for (auto& p : ctx->prof) {
             ctx->ev_pool.push_back(p.a);
@@ -523,6 +595,7 @@ int32_t mac_ctx_create(mac_ctx** out, int32_t device)
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         ctx->cus = prop.multiProcessorCount;
     HCK(hipStreamCreateWithFlags(&ctx->setup_stream, hipStreamNonBlocking));
+    HCK(hipStreamCreateWithFlags(&ctx->dev_stream, hipStreamNonBlocking));
     *out = ctx;
     return MAC_OK;
     ABI_END
@@ -535,7 +608,7 @@ void mac_ctx_destroy(mac_ctx* ctx)
     (void)hipDeviceSynchronize();
     for (Lane* l : ctx->lanes_all) {
         for (DevBuf* b : {&l->cands, &l->disks, &l->partial, &l->area, &l->obj, &l->best,
-                          &l->rmax, &l->prev, &l->dlim})
+                          &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode})
             b->release();
         if (l->done) (void)hipEventDestroy(l->done);
         if (l->stream) (void)hipStreamDestroy(l->stream);
@@ -552,6 +625,7 @@ void mac_ctx_destroy(mac_ctx* ctx)
     }
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
     if (ctx->setup_stream) (void)hipStreamDestroy(ctx->setup_stream);
+    if (ctx->dev_stream) (void)hipStreamDestroy(ctx->dev_stream);
     delete ctx;
 }
 
@@ -560,7 +634,7 @@ int32_t mac_set_option(mac_ctx* ctx, int32_t option, int64_t value)
     if (!ctx) return fail(MAC_E_INVAL, "null context");
     switch (option) {
     case MAC_OPT_ALGO:
-        if (value < MAC_ALGO_AUTO || value > MAC_ALGO_TILED) return fail(MAC_E_INVAL, "bad algo");
+        if (value < MAC_ALGO_AUTO || value > MAC_ALGO_POLL) return fail(MAC_E_INVAL, "bad algo");
         ctx->algo = (int)value;
         return MAC_OK;
     case MAC_OPT_STORAGE:
@@ -828,9 +902,8 @@ int32_t mac_area_batch_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t thre
     if (K == 0) return MAC_OK;
     if (!d_cands || !d_area) return fail(MAC_E_INVAL, "null device pointer");
     set_device(ctx);
-    LaneGuard lg(ctx);
-    hipStream_t s = stream ? (hipStream_t)stream : lg.lane->stream;
-    lg.used = s;
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->dev_stream;
+    LaneGuard lg(ctx, s);
     const int N = (int)(three_n / 3);
     enqueue_eval(ctx, lg.lane, s, d_cands, N, (int)K, use_tiled(ctx, N, nullptr, three_n), nullptr,
                  0.0, nullptr, nullptr, 1.0, d_area, nullptr, nullptr, 0);
@@ -849,10 +922,9 @@ int32_t mac_poll_best_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three
     if (!d_best) return fail(MAC_E_INVAL, "null d_best");
     if (K > 0 && !d_cands) return fail(MAC_E_INVAL, "null d_cands");
     set_device(ctx);
-    LaneGuard lg(ctx);
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->dev_stream;
+    LaneGuard lg(ctx, s);
     Lane* L = lg.lane;
-    hipStream_t s = stream ? (hipStream_t)stream : L->stream;
-    lg.used = s;
     const int N = (int)(three_n / 3);
     if (K == 0) {
         double hb[2] = {INFINITY, __builtin_bit_cast(double, (int64_t)-1)};

@@ -14,7 +14,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-ALGOS = ("tiled", "scan")
+ALGOS = ("tiled", "scan", "poll")
 TAN50 = math.tan(100 / 180 * math.pi / 2)
 
 
