@@ -1,0 +1,90 @@
+// k_common.h — constants, records and wave/block helpers shared by libmaxcover's kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "predicate.h"
+
+#pragma clang fp contract(off)
+
+namespace mac {
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;        // 4 waves
+constexpr int kWavesPerBlock = kBlock / kWave;
+constexpr int kNbrCap = 6;         // tiled walk: lower-index overlapping disks kept per disk
+constexpr int kPollCH = 512;       // poll walk: entries staged in LDS per chunk
+constexpr int kPollRB = 64;        // poll walk: region rows per batch
+constexpr int kPollNbr = 64;       // poll walk: lower-index overlapping regions kept
+
+constexpr int kModePoll = 1;
+constexpr int kModeTiled = 2;
+
+struct Grid {
+    double gx0, gy0;     // origin (bbox min of the finite points)
+    double invS;         // 1 / tile pitch (same pitch on both axes)
+    double S;
+    int nTx, nTy;
+};
+
+struct DiskRec {         // 32 B, one per (candidate, disk)
+    double cx, cy, T, r;
+};
+
+// ------------------------------------------------------------------ wave / block helpers
+
+__device__ __forceinline__ double wave_sum_f64(double v)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);  // fixed butterfly
+    return v;
+}
+
+__device__ __forceinline__ int wave_incl_scan_i32(int v, int lane)
+{
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const int t = __shfl_up(v, off, kWave);
+        if (lane >= off) v += t;
+    }
+    return v;
+}
+
+// Block sum in fixed order (wave butterfly, then waves 0..3 in order). Result valid in thread 0.
+__device__ __forceinline__ double block_sum_f64(double v, double* red /* kWavesPerBlock */)
+{
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    v = wave_sum_f64(v);
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    double s = 0.0;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < kWavesPerBlock; ++i) s += red[i];
+    }
+    return s;
+}
+
+__device__ __forceinline__ DiskRec make_disk(double cx, double cy, double r)
+{
+    DiskRec d;
+    d.cx = cx;
+    d.cy = cy;
+    d.r = r;
+    d.T = cover_threshold(r);
+    return d;
+}
+
+__device__ __forceinline__ bool disk_span(const DiskRec& d, const Grid& g, int4& sp)
+{
+    int x0, x1, y0, y1;
+    if (!(d.T >= 0.0)) return false;
+    if (!tile_span(d.cx, d.r, g.gx0, g.invS, g.nTx, x0, x1)) return false;
+    if (!tile_span(d.cy, d.r, g.gy0, g.invS, g.nTy, y0, y1)) return false;
+    sp = make_int4(x0, x1, y0, y1);
+    return true;
+}
+
+}  // namespace mac

@@ -1,0 +1,208 @@
+// k_walk.h — the three coverage walks (streaming scan, per-candidate tiled walk, poll walk).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "predicate.h"
+#include "k_common.h"
+
+#pragma clang fp contract(off)
+
+namespace mac {
+
+// ------------------------------------------------------------------ streaming scan
+
+// Every entry against every disk of KB candidates (disks[k*N + c], wave-uniform loads through
+// the scalar cache); each lane holds PPT entries in registers. Branch-free inner loop: the
+// reference's first-hit `break` changes which disk is credited, never the sum.
+// partial[blk*K + k]: this block's share of candidate k.
+template <int KB, int PPT>
+__global__ __launch_bounds__(kBlock) void coverage_scan_kernel(
+    const double2* __restrict__ xy, const double* __restrict__ w, int64_t M,
+    const DiskRec* __restrict__ disks, int N, int K, int64_t chunk,
+    double* __restrict__ partial)
+{
+    __shared__ double red[kWavesPerBlock];
+    const int blk = blockIdx.x;
+    const int k0 = blockIdx.y * KB;
+    const int64_t begin = (int64_t)blk * chunk;
+    const int64_t end = begin + chunk < M ? begin + chunk : M;
+
+    double acc[KB];
+#pragma unroll
+    for (int q = 0; q < KB; ++q) acc[q] = 0.0;
+
+    for (int64_t base = begin; base < end; base += (int64_t)kBlock * PPT) {
+        double px[PPT], py[PPT], pw[PPT];
+#pragma unroll
+        for (int u = 0; u < PPT; ++u) {
+            const int64_t p = base + (int64_t)u * kBlock + threadIdx.x;
+            if (p < end) {
+                const double2 v = xy[p];
+                px[u] = v.x;
+                py[u] = v.y;
+                pw[u] = w[p];
+            } else {
+                px[u] = __builtin_nan("");  // NaN: never covered
+                py[u] = 0.0;
+                pw[u] = 0.0;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < KB; ++q) {
+            const int k = k0 + q;
+            if (k >= K) break;
+            const DiskRec* dk = disks + (int64_t)k * N;
+            bool cov[PPT];
+#pragma unroll
+            for (int u = 0; u < PPT; ++u) cov[u] = false;
+            for (int c = 0; c < N; ++c) {
+                const double cx = dk[c].cx, cy = dk[c].cy, T = dk[c].T;
+#pragma unroll
+                for (int u = 0; u < PPT; ++u) cov[u] |= sqdist(px[u], py[u], cx, cy) <= T;
+            }
+#pragma unroll
+            for (int u = 0; u < PPT; ++u)
+                if (cov[u]) acc[q] += pw[u];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < KB; ++q) {
+        const int k = k0 + q;
+        const double s = block_sum_f64(acc[q], red);
+        if (threadIdx.x == 0 && k < K) partial[(int64_t)blk * K + k] = s;
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ per-candidate tiled walk
+
+// LDS layout, N disks (dynamic shared memory, 16-B aligned carve):
+//   double cx[N], cy[N], T[N], r[N]; int4 span[N]; uint16 ncnt[N]; uint16 nbr[N][kNbrCap];
+//   per wave: int rowStart[64], rowPre[64]
+__host__ __device__ inline size_t tiled_lds_head(int N)
+{
+    size_t b = (size_t)N * 4 * sizeof(double);
+    b += (size_t)N * 4 * sizeof(int);
+    b += (size_t)N * sizeof(uint16_t) * (1 + kNbrCap);
+    return (b + 15) & ~(size_t)15;
+}
+__host__ __device__ inline size_t tiled_lds_bytes(int N)
+{
+    return tiled_lds_head(N) + (size_t)kWavesPerBlock * 2 * kWave * sizeof(int);
+}
+
+// Workgroup = (candidate k, slice gi of G). Each wave walks whole disks: for disk c it reads
+// the tile-row runs of c's span from the CSR offsets (a row of tiles is contiguous in the
+// sorted list), tests every entry in them, and credits a covered entry only when no lower-index
+// disk also covers it (candidates for that come from a conservative disk-disk intersection
+// list built in LDS). disksT[c*K + k]; partial[gi*K + k]. Runs only when *mode == kModeTiled
+// (or mode == null).
+__global__ __launch_bounds__(kBlock) void coverage_tiled_kernel(
+    const double2* __restrict__ xy, const double* __restrict__ w,
+    const int32_t* __restrict__ off, Grid g,
+    const DiskRec* __restrict__ disksT, int N, int K, int G, const int* __restrict__ mode,
+    double* __restrict__ partial)
+{
+    if (mode && *mode != kModeTiled) return;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    double* sx = (double*)lds;
+    double* sy = sx + N;
+    double* sT = sy + N;
+    double* sR = sT + N;
+    int4* span = (int4*)(sR + N);
+    uint16_t* ncnt = (uint16_t*)(span + N);
+    uint16_t* nbr = ncnt + N;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    int* rowStart = (int*)(lds + tiled_lds_head(N)) + wid * 2 * kWave;
+    int* rowPre = rowStart + kWave;
+    __shared__ double red[kWavesPerBlock];
+
+    const int k = blockIdx.x / G;
+    const int gi = blockIdx.x % G;
+
+    // 1. disks -> LDS, spans
+    for (int c = threadIdx.x; c < N; c += kBlock) {
+        const DiskRec d = disksT[(int64_t)c * K + k];
+        sx[c] = d.cx;
+        sy[c] = d.cy;
+        sT[c] = d.T;
+        sR[c] = d.r;
+        int4 sp;
+        span[c] = disk_span(d, g, sp) ? sp : make_int4(1, 0, 1, 0);
+    }
+    __syncthreads();
+
+    // 2. lower-index overlap lists for this slice's disks (disk c belongs to slice c % G)
+    for (int c = gi + G * threadIdx.x; c < N; c += G * kBlock) {
+        int cnt = 0;
+        if (span[c].x <= span[c].y) {
+            const double cx = sx[c], cy = sy[c], r = sR[c];
+            for (int c2 = 0; c2 < c; ++c2) {
+                if (span[c2].x > span[c2].y) continue;  // covers nothing
+                if (disks_may_overlap(cx, cy, r, sx[c2], sy[c2], sR[c2])) {
+                    if (cnt < kNbrCap) nbr[c * kNbrCap + cnt] = (uint16_t)c2;
+                    ++cnt;
+                }
+            }
+        }
+        ncnt[c] = (uint16_t)(cnt > kNbrCap ? 0xffff : cnt);
+    }
+    __syncthreads();
+
+    // 3. walk: wave `wid` of slice gi takes disks c = gi + G*(wid + kWavesPerBlock*j)
+    double acc = 0.0;
+    const int stride = G * kWavesPerBlock;
+    for (int c = gi + G * wid; c < N; c += stride) {
+        const int4 sp = span[c];
+        if (sp.x > sp.y) continue;
+        const double cx = sx[c], cy = sy[c], T = sT[c];
+        const int nc = ncnt[c];
+        for (int rb = sp.z; rb <= sp.w; rb += kWave) {
+            const int nr = (sp.w - rb + 1) < kWave ? (sp.w - rb + 1) : kWave;
+            int s = 0, len = 0;
+            if (lane < nr) {
+                const int64_t rowbase = (int64_t)(rb + lane) * g.nTx;
+                s = off[rowbase + sp.x];
+                len = off[rowbase + sp.y + 1] - s;
+            }
+            const int incl = wave_incl_scan_i32(len, lane);
+            const int total = __shfl(incl, kWave - 1, kWave);
+            rowStart[lane] = s;
+            rowPre[lane] = incl - len;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int i = lane; i < total; i += kWave) {
+                int lo = 0, hi = nr - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (rowPre[mid] <= i) lo = mid; else hi = mid - 1;
+                }
+                const int j = rowStart[lo] + (i - rowPre[lo]);
+                const double2 p = xy[j];
+                if (sqdist(p.x, p.y, cx, cy) <= T) {
+                    bool owned = true;
+                    if (nc != 0xffff) {
+                        for (int q = 0; q < nc; ++q) {
+                            const int c2 = nbr[c * kNbrCap + q];
+                            if (sqdist(p.x, p.y, sx[c2], sy[c2]) <= sT[c2]) { owned = false; break; }
+                        }
+                    } else {
+                        for (int c2 = 0; c2 < c; ++c2) {
+                            if (sqdist(p.x, p.y, sx[c2], sy[c2]) <= sT[c2]) { owned = false; break; }
+                        }
+                    }
+                    if (owned) acc += w[j];
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    const double s = block_sum_f64(acc, red);
+    if (threadIdx.x == 0) partial[(int64_t)gi * K + k] = s;
+}
+
+}  // namespace mac

@@ -427,7 +427,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_c
         }
         prof_end();
     }
-    hipLaunchKernelGGL(finalize_kernel, dim3(grid1d(K, 256)), dim3(256), 0, s,
+    hipLaunchKernelGGL(finalize_kernel, dim3((K + kFinC - 1) / kFinC), dim3(kBlock), 0, s,
                        L->partial.as<double>(), d_mode, n_poll, n_other, K, d_cands, N, ldc, d_rmax,
                        penalty, d_prev, d_dlimT, tan_half_fov, d_area, d_obj);
     HCK(hipGetLastError());

@@ -324,3 +324,35 @@ def test_config4_full_poll(ctx, pkg, orc):
     assert np.array_equal(got[::256], got_scan)
     want = np.array([25.0 * orc.lattice_count_fast(c.astype(np.int64), 4096) for c in C])
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("case", ["real_clustered", "big_radius", "mixed_weights"])
+def test_poll_walk_stress(ctx, pkg, orc, case):
+    """The poll walk's rare paths: fp64 band decisions on real-valued coordinates, ownership
+    between overlapping disks, regions larger than one LDS chunk and more than 64 tile rows."""
+    wl = pkg.workloads
+    rng = wl.SplitMix64(4242 + len(case))
+    if case == "big_radius":
+        x, y, w = wl.grid_points(240)
+        N = 6
+        x0 = np.concatenate([rng.uniform(N) * 1200, rng.uniform(N) * 1200,
+                             rng.uniform(N) * 300 + 350])
+    else:
+        M = 60000
+        x = rng.uniform(M) * 800.0
+        y = rng.uniform(M) * 800.0
+        w = np.full(M, 25.0) if case == "real_clustered" else rng.uniform(M) * 3 + 1
+        N = 40
+        x0 = np.concatenate([400 + rng.uniform(N) * 120 - 60, 400 + rng.uniform(N) * 120 - 60,
+                             rng.uniform(N) * 30 + 10])
+    ctx.set_points(x, y, w)
+    C = np.concatenate([x0[None, :], wl.poll_candidates(x0, rng, ell=1)], axis=0)
+    C[1:, :] += (rng.uniform(C[1:].size) * 0.02 - 0.01).reshape(C[1:].shape)  # non-lattice
+    want = orc.PointerList(recs(x, y, w)).area_batch(C)
+    r = both(ctx, lambda: ctx.area_batch(C))
+    for a, got in r.items():
+        if case == "mixed_weights":
+            np.testing.assert_allclose(got, want, rtol=1e-12, atol=0, err_msg=a)
+        else:
+            assert np.array_equal(got, want), (a, np.flatnonzero(got != want)[:5])
+    assert np.array_equal(r["poll"], r["tiled"]) or case == "mixed_weights"

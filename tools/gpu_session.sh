@@ -36,6 +36,11 @@ for s in $STEPS; do
     bench)
         run bench 900 python bench.py ; rc=$?
         grep '^{' gpurun_out/bench.log > gpurun_out/bench_${TAG}.json ;;
+    algos)
+        for a in tiled poll auto; do
+            run bench_$a 600 python bench.py --no-cpu --algo $a --steps 30 ; rc=$?
+            fatal $rc && break
+        done ;;
     bench3)
         run bench3 600 python bench.py --config 3 --no-cpu ; rc=$? ;;
     bench2)
