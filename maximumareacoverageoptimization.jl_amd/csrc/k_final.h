@@ -1,4 +1,4 @@
-// k_final.h — partial-sum reduction, objective penalty, cons3 mask and the poll argmin.
+// k_final.h — objective penalty + cons3 mask, partial-sum reduction and the poll argmin.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -11,57 +11,36 @@
 
 namespace mac {
 
-constexpr int kFinC = 64;  // candidates per finalize block
-constexpr int kFinT = 64;  // UAV indices per LDS tile
+constexpr int kPenC = 64;   // candidates per penalty block
+constexpr int kPenT = 64;   // UAV indices per LDS tile
+constexpr int kFinC = 16;   // candidates per finalize block (x 16 slice groups)
 
-// Block = 64 candidates x 4 waves.
-//  area_k  = sum over slices g of partial[g*K + k]: wave w sums slices g = w (mod 4) in order,
-//            then the 4 wave sums are added in wave order (fixed => bit-reproducible). The slice
-//            count is n_poll when *mode == poll, else n_other.
-//  obj_k   = -area_k + penalty * violation_k, violation_k = sum_{i=0..N-1} |x[2N+i] - rmax[i]|
-//            accumulated SEQUENTIALLY in i from 0.0 (src/TDM_STATIC_opt.jl:89-97, bit-exact).
-//            The candidate columns are staged through LDS in 64 x 64 tiles (coalesced reads);
-//            lane k of wave 0 then runs the sequential chain over its tile row.
-//  cons3   (src/TDM_Constraints.jl:54-75) when prev != null: candidate k is infeasible when
-//            any UAV has s > dlimT[i] (exact form of sqrt(s) > d_lim[i], predicate.h); its
-//            objective becomes +inf (the extreme barrier never evaluates it).
-__global__ __launch_bounds__(kBlock) void finalize_kernel(
-    const double* __restrict__ partial, const int* __restrict__ mode, int n_poll, int n_other,
+// vp_k = violation_k * penalty with violation_k = sum_{i=0..N-1} |x[2N+i] - rmax[i]| accumulated
+// SEQUENTIALLY in i from 0.0 (src/TDM_STATIC_opt.jl:89-97, bit-exact), or +inf when candidate k
+// fails cons3 (src/TDM_Constraints.jl:54-75; prev != null; sqrt(s) > d_lim[i] evaluated exactly
+// as s > dlimT[i], predicate.h), so -area + vp is the reference objective or +inf (the extreme
+// barrier never evaluates it). Block = 64 candidates: their columns are staged through LDS in
+// 64 x 64 tiles (coalesced reads); lane k of wave 0 runs the sequential chain over its tile row.
+// Independent of the coverage walk: runs on a forked stream beside it.
+__global__ __launch_bounds__(kBlock) void penalty_kernel(
     int K, const double* __restrict__ cands, int N, int ldc, const double* __restrict__ rmax,
     double penalty, const double* __restrict__ prev, const double* __restrict__ dlimT,
-    double tan_half_fov, double* __restrict__ area_out, double* __restrict__ obj_out)
+    double tan_half_fov, double* __restrict__ vp)
 {
-    __shared__ double tile[kFinC][kFinT + 1];
-    __shared__ double red[kWavesPerBlock][kFinC];
-    __shared__ int infeas[kFinC];
+    __shared__ double tile[kPenC][kPenT + 1];
+    __shared__ int infeas[kPenC];
     const int t = threadIdx.x, lane = t & (kWave - 1), grp = t / kWave;
-    const int k0 = blockIdx.x * kFinC;
+    const int k0 = blockIdx.x * kPenC;
     const int k = k0 + lane;
-    const bool valid = k < K;
-    const int G = (mode && *mode == kModePoll) ? n_poll : n_other;
-
-    double a = 0.0;
-    if (valid)
-        for (int g = grp; g < G; g += kWavesPerBlock) a += partial[(int64_t)g * K + k];
-    red[grp][lane] = a;
-    if (t < kFinC) infeas[t] = 0;
-    __syncthreads();
-    double area = 0.0;
-    if (grp == 0) {
-#pragma unroll
-        for (int q = 0; q < kWavesPerBlock; ++q) area += red[q][lane];
-        if (valid && area_out) area_out[k] = area;
-    }
-    if (!obj_out) return;  // uniform
-
+    if (t < kPenC) infeas[t] = 0;
     double violation = 0.0;
-    for (int i0 = 0; i0 < N; i0 += kFinT) {
-        const int ni = min(kFinT, N - i0);
+    for (int i0 = 0; i0 < N; i0 += kPenT) {
+        const int ni = min(kPenT, N - i0);
         __syncthreads();
-        for (int e = t; e < kFinC * kFinT; e += kBlock) {
-            const int c = e / kFinT, ii = e % kFinT, kk = k0 + c;
-            if (kk >= K || ii >= ni) continue;
-            const double* x = cands + (int64_t)kk * ldc;
+        for (int e = t; e < kPenC * kPenT; e += kBlock) {
+            const int c = e / kPenT, ii = e % kPenT, kc = k0 + c;
+            if (kc >= K || ii >= ni) continue;
+            const double* x = cands + (int64_t)kc * ldc;
             const int i = i0 + ii;
             tile[c][ii] = rmax ? __builtin_fabs(x[2 * N + i] - rmax[i]) : 0.0;
             if (prev) {
@@ -73,13 +52,46 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(
             }
         }
         __syncthreads();
-        if (grp == 0 && valid)
+        if (grp == 0 && k < K)
             for (int ii = 0; ii < ni; ++ii) violation += tile[lane][ii];
     }
     __syncthreads();
-    if (grp == 0 && valid) {
-        const double obj = -area + violation * penalty;
-        obj_out[k] = infeas[lane] ? __builtin_inf() : obj;
+    if (grp == 0 && k < K) vp[k] = infeas[lane] ? __builtin_inf() : violation * penalty;
+}
+
+// Block = 16 candidates x 16 slice groups. area_k = sum over slices g of partial[g*K + k] in a
+// fixed order (thread (c, sg) sums g = sg, sg+16, ... into 4 interleaved accumulators combined
+// in order, then the 16 groups in order): bit-reproducible, loads kept in flight. The slice
+// count is n_poll when *mode == poll, else n_other. obj_k = -area_k + vp_k when vp != null.
+__global__ __launch_bounds__(kBlock) void finalize_kernel(
+    const double* __restrict__ partial, const int* __restrict__ mode, int n_poll, int n_other,
+    int K, const double* __restrict__ vp, double* __restrict__ area_out,
+    double* __restrict__ obj_out)
+{
+    __shared__ double red[kBlock / kFinC][kFinC];
+    const int t = threadIdx.x, c = t % kFinC, sg = t / kFinC;
+    constexpr int SG = kBlock / kFinC;
+    const int k = blockIdx.x * kFinC + c;
+    const int G = (mode && *mode == kModePoll) ? n_poll : n_other;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    if (k < K) {
+        int g = sg;
+        for (; g + 3 * SG < G; g += 4 * SG) {
+            a0 += partial[(int64_t)g * K + k];
+            a1 += partial[(int64_t)(g + SG) * K + k];
+            a2 += partial[(int64_t)(g + 2 * SG) * K + k];
+            a3 += partial[(int64_t)(g + 3 * SG) * K + k];
+        }
+        for (; g < G; g += SG) a0 += partial[(int64_t)g * K + k];
+    }
+    red[sg][c] = ((a0 + a1) + a2) + a3;
+    __syncthreads();
+    if (sg == 0 && k < K) {
+        double area = 0.0;
+#pragma unroll
+        for (int q = 0; q < SG; ++q) area += red[q][c];
+        if (area_out) area_out[k] = area;
+        if (obj_out) obj_out[k] = -area + vp[k];
     }
 }
 

@@ -1,24 +1,28 @@
-// k_poll.h — the poll walk: one workgroup per (disk i, 256 candidates) over a whole MADS poll.
+// k_poll.h — the poll walk: one workgroup per (disk i, slice of the poll's candidates).
 //
 // Across one poll, disk i of candidate k sits at x_inc + delta*d_k: a few metres around the
 // incumbent. region[i] (k_prep.h) is the union of disk i's tile spans over all K candidates.
-// The workgroup stages the entries of region[i] in LDS once (chunks of kPollCH) and every lane
-// tests ITS candidate's disk i against every staged entry: one broadcast LDS read per entry per
-// wave, no cross-lane reduction, entries read from HBM once per disk instead of once per
-// (candidate, disk). An entry is credited to disk i of candidate k only when no lower-index disk
-// j of candidate k covers it (j over the disks whose regions overlap region i): exactly-once
-// union counting, so the area is the reference's first-hit sum (src/AreaCoverageCalculation.jl:
-// 67-78) over the same multiset of entries.
+// The workgroup stages the entries of region[i] in LDS once (chunks of kPollCH) and each lane
+// tests kPollKPL of its candidates' disk i against every staged entry: one broadcast LDS read
+// per entry per wave feeds kPollKPL tests, there is no cross-lane reduction, and entries come
+// from HBM once per (disk, slice) instead of once per (candidate, disk). An entry is credited to
+// disk i of candidate k only when no lower-index disk j of candidate k covers it (j over the
+// disks whose regions overlap region i): exactly-once union counting, so the area is the
+// reference's first-hit sum (src/AreaCoverageCalculation.jl:67-78) over the same entries.
 //
-// Exact fp32 filter. Entries are staged as fp32 offsets from the region origin o, the lane's
-// centre likewise. With eps = 2^-24, |u| <= U for every staged offset and D = U + |c - o| >= |dx|,
-// |dy|: |dx32 - dx| <= 2.01 eps D, |a32 - a| <= 12.2 eps D^2 and |a64 - a| <= 6.1 * 2^-53 D^2,
-// so with delta = 2^-20 D^2 (> 12.3 eps D^2):
-//     a32 <= RD32(T - delta)          =>  a64 <= T   (covered, the reference decision)
-//     a32 >  RU32(T + delta)          =>  a64 >  T   (not covered)
-//     otherwise (the band)            =>  decided in fp64 from the staged exact coordinates.
-// On the reference lattices the band is empty: a = n + 1/2 never lies within delta of T.
-// NaN/inf coordinates fail both fp32 tests and every fp64 test, like the reference.
+// Exact fp32 filter. With o the region origin, u = px - ox, v = py - oy, cu = cx - ox,
+// cv = cy - oy: a = (u-cu)^2 + (v-cv)^2 = q - 2u*cu - 2v*cv + C, q = u^2 + v^2, C = cu^2 + cv^2.
+// Entries are staged as fp32 (u~, v~, q~); each test is t = fma(v~, -2cv~, fma(u~, -2cu~, q~))
+// compared with fp32 thresholds around T - C. With eps = 2^-24, |u|,|v| <= U (every staged
+// entry) and D = U + max(|cu|, |cv|): |t - (a - C)| <= 28.2 eps D^2 (q: 10 eps D^2, the two
+// products 8.04 eps D^2, the three roundings 10 eps D^2), while the fp64 reference value a64 and
+// the fp64 C differ from the real ones by < 2^-50 D^2. So with delta = 2^-18 D^2 (= 64 eps D^2):
+//     t <= RD32(T - C - delta)   =>  a64 <= T    covered, the reference decision
+//     t >  RU32(T - C + delta)   =>  a64 >  T    not covered
+//     otherwise (the band)       =>  decided in fp64 from the staged exact coordinates.
+// On the reference lattices the band is empty (a = n + 1/2 never lies within delta of T).
+// NaN / inf coordinates fail both fp32 tests and every fp64 test, like the reference; a lane
+// with D > 2^60 (fp32 range at risk) sends every entry to the exact pass.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -31,7 +35,8 @@
 
 namespace mac {
 
-constexpr int kPollCH2 = kPollCH / 2;  // staged fp32 pairs
+constexpr int kPollKPL = 4;                      // candidates per lane
+constexpr int kPollKPB = kBlock * kPollKPL;      // candidates per workgroup (at most)
 
 __device__ __forceinline__ float next_down_f32(float f)
 {
@@ -74,16 +79,17 @@ __device__ __forceinline__ bool box_overlap(const int4& a, const int4& b)
     return a.x <= a.y && a.x <= b.y && b.x <= a.y && a.z <= b.w && b.z <= a.w;
 }
 
-// partialT[i*K + k] = weight of the entries credited to disk i of candidate k.
+// Slice g of Gy: candidates [g*K/Gy, (g+1)*K/Gy); lane t, pass u -> k = kb + u*kBlock + t.
+// partial[i*K + k] = weight of the entries credited to disk i of candidate k.
 // Runs when mode == null or *mode == kModePoll.
 __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
     const double2* __restrict__ xy, const double* __restrict__ w,
     const int32_t* __restrict__ off, Grid g, const DiskRec* __restrict__ disksT,
     const int4* __restrict__ region, int N, int K, const int* __restrict__ mode,
-    double* __restrict__ partialT)
+    double* __restrict__ partial)
 {
     if (mode && *mode != kModePoll) return;
-    __shared__ float4 s32[kPollCH2];   // (rx, ry) of entries 2q, 2q+1
+    __shared__ float4 s32[kPollCH];    // (u~, v~, q~, 0)
     __shared__ double2 s64[kPollCH];   // exact coordinates (band + ownership tests)
     __shared__ double sw[kPollCH];
     __shared__ int rs[kPollRB], rpre[kPollRB + 1];
@@ -92,33 +98,62 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
 
     const int i = blockIdx.x;
     const int tid = threadIdx.x;
-    const int k = blockIdx.y * kBlock + tid;
-    const bool valid = k < K;
+    const int kb = blockIdx.y * kPollKPB;
+    const int ke = min(K, kb + kPollKPB);
     const int4 R = region[i];
+
+    int kk[kPollKPL];
+#pragma unroll
+    for (int u = 0; u < kPollKPL; ++u) {
+        const int k = kb + u * kBlock + tid;
+        kk[u] = k < ke ? k : -1;
+    }
     if (R.x > R.y) {  // disk i covers nothing in any candidate (uniform across the block)
-        if (valid) partialT[(int64_t)i * K + k] = 0.0;
+#pragma unroll
+        for (int u = 0; u < kPollKPL; ++u)
+            if (kk[u] >= 0) partial[(int64_t)i * K + kk[u]] = 0.0;
         return;
     }
-    DiskRec d = DiskRec{0.0, 0.0, -1.0, 0.0};
-    if (valid) d = disksT[(int64_t)i * K + k];
-    int4 sp;
-    const bool live = valid && disk_span(d, g, sp);
 
-    // region origin and the bound U on every staged offset |p - o| (entries of tile t satisfy
+    // region origin and the bound U on every staged offset (entries of tile t satisfy
     // t <= (p - g0)/S < t + 1 up to rounding; two tiles of slack absorb it)
     const double ox = g.gx0 + (double)R.x * g.S;
     const double oy = g.gy0 + (double)R.z * g.S;
     const double U = (double)max(R.y - R.x, R.w - R.z) * g.S + 2.0 * g.S;
-    float rcx = 0.0f, rcy = 0.0f, Tlo = -__builtin_inff(), Thi = -__builtin_inff();
-    if (live) {
-        const double ccx = d.cx - ox, ccy = d.cy - oy;
-        const double D = U + __builtin_fmax(__builtin_fabs(ccx), __builtin_fabs(ccy));
-        const double delta = D * D * 0x1p-20 + 0x1p-100;
-        rcx = (float)ccx;
-        rcy = (float)ccy;
-        Tlo = f32_down(d.T - delta);
-        Thi = f32_up(d.T + delta);
+
+    float m2cx[kPollKPL], m2cy[kPollKPL], Tlo[kPollKPL], Thi[kPollKPL];
+    bool live[kPollKPL];
+    double acc[kPollKPL];
+#pragma unroll
+    for (int u = 0; u < kPollKPL; ++u) {
+        acc[u] = 0.0;
+        live[u] = false;
+        m2cx[u] = m2cy[u] = 0.0f;
+        Tlo[u] = Thi[u] = -__builtin_inff();
+        if (kk[u] < 0) continue;
+        const DiskRec d = disksT[(int64_t)i * K + kk[u]];
+        int4 sp;
+        if (!disk_span(d, g, sp)) continue;
+        live[u] = true;
+        const double cu = d.cx - ox, cv = d.cy - oy;
+        const double D = U + __builtin_fmax(__builtin_fabs(cu), __builtin_fabs(cv));
+        if (!(D <= 0x1p60)) {  // keep fp32 far from overflow: exact pass for everything
+            Tlo[u] = -__builtin_inff();
+            Thi[u] = __builtin_inff();
+            continue;
+        }
+        const double C = cu * cu + cv * cv;
+        const double delta = D * D * 0x1p-18 + 0x1p-120;
+        m2cx[u] = (float)(-2.0 * cu);
+        m2cy[u] = (float)(-2.0 * cv);
+        Tlo[u] = f32_down(d.T - C - delta);
+        Thi[u] = f32_up(d.T - C + delta);
     }
+
+    bool any_live = false;
+#pragma unroll
+    for (int u = 0; u < kPollKPL; ++u) any_live |= live[u];
+    const bool wave_live = __any(any_live);
 
     // lower-index disks whose regions overlap region i (order irrelevant: a boolean OR)
     if (tid == 0) ncnt = 0;
@@ -134,10 +169,10 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
     const int nc = ncnt;
 
     // is the entry at exact coordinates p covered by a lower-index disk of candidate k?
-    auto stolen = [&](const double2 p) -> bool {
+    auto stolen = [&](const double2 p, const int k) -> bool {
         if (nc <= kPollNbr) {
-            for (int u = 0; u < nc; ++u) {
-                const DiskRec e = disksT[(int64_t)nbr[u] * K + k];
+            for (int q = 0; q < nc; ++q) {
+                const DiskRec e = disksT[(int64_t)nbr[q] * K + k];
                 if (sqdist(p.x, p.y, e.cx, e.cy) <= e.T) return true;
             }
         } else {
@@ -150,7 +185,6 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
         return false;
     };
 
-    double acc = 0.0;
     for (int rb = R.z; rb <= R.w; rb += kPollRB) {
         const int nr = min(kPollRB, R.w - rb + 1);
         if (tid < nr) {
@@ -168,7 +202,6 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
         const int total = rpre[nr];
         for (int base = 0; base < total; base += kPollCH) {
             const int n = min(kPollCH, total - base);
-            float* s32f = (float*)s32;
             for (int q = tid; q < n; q += kBlock) {
                 const int f = base + q;
                 int lo = 0, hi = nr - 1;
@@ -180,12 +213,8 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
                 const double2 p = xy[j];
                 s64[q] = p;
                 sw[q] = w[j];
-                s32f[2 * q] = (float)(p.x - ox);
-                s32f[2 * q + 1] = (float)(p.y - oy);
-            }
-            if (tid == 0 && (n & 1)) {  // pad the last pair: NaN is never covered, never in band
-                s32f[2 * n] = __builtin_nanf("");
-                s32f[2 * n + 1] = __builtin_nanf("");
+                const float fu = (float)(p.x - ox), fv = (float)(p.y - oy);
+                s32[q] = make_float4(fu, fv, __builtin_fmaf(fu, fu, fv * fv), 0.0f);
             }
             __syncthreads();
             const uint64_t w0 = __builtin_bit_cast(uint64_t, sw[0]);
@@ -193,53 +222,65 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
             for (int q = tid; q < n; q += kBlock) mixed |= __builtin_bit_cast(uint64_t, sw[q]) != w0;
             const bool uniform = !__syncthreads_or(mixed);
 
-            if (live) {
-                bool band = false;
-                if (nc == 0 && uniform) {
-                    // hot loop: two entries per iteration, count the surely covered ones
-                    int cnt = 0;
-                    const int n2 = (n + 1) >> 1;
-                    for (int q2 = 0; q2 < n2; ++q2) {
-                        const float4 v = s32[q2];
-                        const float dx0 = v.x - rcx, dy0 = v.y - rcy;
-                        const float dx1 = v.z - rcx, dy1 = v.w - rcy;
-                        const float a0 = __builtin_fmaf(dx0, dx0, dy0 * dy0);
-                        const float a1 = __builtin_fmaf(dx1, dx1, dy1 * dy1);
-                        cnt += (a0 <= Tlo) + (a1 <= Tlo);
-                        band |= (a0 > Tlo) & (a0 <= Thi);
-                        band |= (a1 > Tlo) & (a1 <= Thi);
+            bool band[kPollKPL];
+#pragma unroll
+            for (int u = 0; u < kPollKPL; ++u) band[u] = false;
+            if (!wave_live) {
+                // no candidate of this wave is live (the poll's last slice): nothing to test
+            } else if (nc == 0 && uniform) {
+                // hot loop: per staged entry, kPollKPL tests of 2 FMAs + 2 counted compares
+                int clo[kPollKPL], chi[kPollKPL];
+#pragma unroll
+                for (int u = 0; u < kPollKPL; ++u) clo[u] = chi[u] = 0;
+                for (int q = 0; q < n; ++q) {
+                    const float4 e = s32[q];
+#pragma unroll
+                    for (int u = 0; u < kPollKPL; ++u) {
+                        const float t = __builtin_fmaf(e.y, m2cy[u], __builtin_fmaf(e.x, m2cx[u], e.z));
+                        clo[u] += t <= Tlo[u];
+                        chi[u] += t <= Thi[u];
                     }
-                    if (cnt) acc += (double)cnt * sw[0];
-                } else {
-                    const float2* s2 = (const float2*)s32;
+                }
+#pragma unroll
+                for (int u = 0; u < kPollKPL; ++u) {
+                    if (clo[u]) acc[u] += (double)clo[u] * sw[0];
+                    band[u] = chi[u] != clo[u];
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < kPollKPL; ++u) {
+                    if (!live[u]) continue;
                     for (int q = 0; q < n; ++q) {
-                        const float2 v = s2[q];
-                        const float dx = v.x - rcx, dy = v.y - rcy;
-                        const float a = __builtin_fmaf(dx, dx, dy * dy);
-                        if (a <= Tlo) {
-                            if (nc == 0 || !stolen(s64[q])) acc += sw[q];
-                        } else if (a <= Thi) {
-                            band = true;
+                        const float4 e = s32[q];
+                        const float t = __builtin_fmaf(e.y, m2cy[u], __builtin_fmaf(e.x, m2cx[u], e.z));
+                        if (t <= Tlo[u]) {
+                            if (nc == 0 || !stolen(s64[q], kk[u])) acc[u] += sw[q];
+                        } else if (t <= Thi[u]) {
+                            band[u] = true;
                         }
                     }
                 }
-                if (band) {  // exact fp64 decision for the band entries (rare)
-                    const float2* s2 = (const float2*)s32;
-                    for (int q = 0; q < n; ++q) {
-                        const float2 v = s2[q];
-                        const float dx = v.x - rcx, dy = v.y - rcy;
-                        const float a = __builtin_fmaf(dx, dx, dy * dy);
-                        if (!(a > Tlo && a <= Thi)) continue;
-                        const double2 p = s64[q];
-                        if (sqdist(p.x, p.y, d.cx, d.cy) <= d.T && (nc == 0 || !stolen(p)))
-                            acc += sw[q];
-                    }
+            }
+            // exact fp64 decisions for the band entries (rare; never on reference lattices)
+#pragma unroll
+            for (int u = 0; u < kPollKPL; ++u) {
+                if (!band[u]) continue;
+                const DiskRec d = disksT[(int64_t)i * K + kk[u]];
+                for (int q = 0; q < n; ++q) {
+                    const float4 e = s32[q];
+                    const float t = __builtin_fmaf(e.y, m2cy[u], __builtin_fmaf(e.x, m2cx[u], e.z));
+                    if (!(t > Tlo[u] && t <= Thi[u])) continue;
+                    const double2 p = s64[q];
+                    if (sqdist(p.x, p.y, d.cx, d.cy) <= d.T && (nc == 0 || !stolen(p, kk[u])))
+                        acc[u] += sw[q];
                 }
             }
             __syncthreads();
         }
     }
-    if (valid) partialT[(int64_t)i * K + k] = acc;
+#pragma unroll
+    for (int u = 0; u < kPollKPL; ++u)
+        if (kk[u] >= 0) partial[(int64_t)i * K + kk[u]] = acc[u];
 }
 
 }  // namespace mac

@@ -95,7 +95,9 @@ struct Lane {
     hipStream_t stream = nullptr;
     hipStream_t last = nullptr;   // stream of the most recent use
     hipEvent_t done = nullptr;
-    DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode;
+    DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode, vp;
+    hipStream_t aux = nullptr;                 // forked stream for the penalty kernel
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::vector<double> h_dlim;
 };
 
@@ -333,6 +335,22 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_c
     const int64_t M = ctx->M;
     int n_poll = N, n_other = 1;
     const int* d_mode = nullptr;
+    if (d_obj) {
+        // objective penalty + cons3 mask do not depend on coverage: fork them onto the lane's
+        // aux stream so they run beside the walk (joined before finalize)
+        if (!L->aux) {
+            HCK(hipStreamCreateWithFlags(&L->aux, hipStreamNonBlocking));
+            HCK(hipEventCreateWithFlags(&L->ev_fork, hipEventDisableTiming));
+            HCK(hipEventCreateWithFlags(&L->ev_join, hipEventDisableTiming));
+        }
+        L->vp.reserve(sizeof(double) * (size_t)std::max(K, 1));
+        HCK(hipEventRecord(L->ev_fork, s));
+        HCK(hipStreamWaitEvent(L->aux, L->ev_fork, 0));
+        hipLaunchKernelGGL(penalty_kernel, dim3((K + kPenC - 1) / kPenC), dim3(kBlock), 0, L->aux, K,
+                           d_cands, N, ldc, d_rmax, penalty, d_prev, d_dlimT, tan_half_fov,
+                           L->vp.as<double>());
+        HCK(hipGetLastError());
+    }
     hipEvent_t ev_a = nullptr, ev_b = nullptr;
     auto prof_begin = [&]() {
         if (!ctx->profile) return;
@@ -419,7 +437,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_c
             HCK(hipGetLastError());
         }
         if (poll_possible) {
-            hipLaunchKernelGGL(coverage_poll_kernel, dim3(N, (K + kBlock - 1) / kBlock), dim3(kBlock),
+            hipLaunchKernelGGL(coverage_poll_kernel, dim3(N, (K + kPollKPB - 1) / kPollKPB), dim3(kBlock),
                                0, s, ctx->xys.as<double2>(), ctx->ws.as<double>(),
                                ctx->off.as<int32_t>(), ctx->grid, L->disks.as<DiskRec>(),
                                L->region.as<int4>(), N, K, d_mode, L->partial.as<double>());
@@ -427,9 +445,13 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_c
         }
         prof_end();
     }
+    if (d_obj) {  // join the penalty stream
+        HCK(hipEventRecord(L->ev_join, L->aux));
+        HCK(hipStreamWaitEvent(s, L->ev_join, 0));
+    }
     hipLaunchKernelGGL(finalize_kernel, dim3((K + kFinC - 1) / kFinC), dim3(kBlock), 0, s,
-                       L->partial.as<double>(), d_mode, n_poll, n_other, K, d_cands, N, ldc, d_rmax,
-                       penalty, d_prev, d_dlimT, tan_half_fov, d_area, d_obj);
+                       L->partial.as<double>(), d_mode, n_poll, n_other, K,
+                       d_obj ? L->vp.as<double>() : nullptr, d_area, d_obj);
     HCK(hipGetLastError());
     if (d_best) {
         hipLaunchKernelGGL(argmin_kernel, dim3(1), dim3(kBlock), 0, s, d_obj, K, idx_base, d_best);
@@ -608,8 +630,11 @@ void mac_ctx_destroy(mac_ctx* ctx)
     (void)hipDeviceSynchronize();
     for (Lane* l : ctx->lanes_all) {
         for (DevBuf* b : {&l->cands, &l->disks, &l->partial, &l->area, &l->obj, &l->best,
-                          &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode})
+                          &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->vp})
             b->release();
+        if (l->ev_fork) (void)hipEventDestroy(l->ev_fork);
+        if (l->ev_join) (void)hipEventDestroy(l->ev_join);
+        if (l->aux) (void)hipStreamDestroy(l->aux);
         if (l->done) (void)hipEventDestroy(l->done);
         if (l->stream) (void)hipStreamDestroy(l->stream);
         delete l;
