@@ -214,7 +214,10 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
                 s64[q] = p;
                 sw[q] = w[j];
                 const float fu = (float)(p.x - ox), fv = (float)(p.y - oy);
-                s32[q] = make_float4(fu, fv, __builtin_fmaf(fu, fu, fv * fv), 0.0f);
+                // non-finite entries (never covered) -> (0, 0, +inf): t = +inf, never NaN
+                s32[q] = __builtin_isfinite(fu) && __builtin_isfinite(fv)
+                             ? make_float4(fu, fv, __builtin_fmaf(fu, fu, fv * fv), 0.0f)
+                             : make_float4(0.0f, 0.0f, __builtin_inff(), 0.0f);
             }
             __syncthreads();
             const uint64_t w0 = __builtin_bit_cast(uint64_t, sw[0]);
@@ -228,23 +231,28 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
             if (!wave_live) {
                 // no candidate of this wave is live (the poll's last slice): nothing to test
             } else if (nc == 0 && uniform) {
-                // hot loop: per staged entry, kPollKPL tests of 2 FMAs + 2 counted compares
-                int clo[kPollKPL], chi[kPollKPL];
+                // hot loop: per staged entry, kPollKPL tests of 2 FMAs + 2 sign-bit counts.
+                // t is never NaN (non-finite entries are staged as q = +inf), and a float
+                // difference of distinct values is never zero, so sign(T - t) = [t > T]: the
+                // counts are of the entries NOT under each threshold.
+                uint32_t nlo[kPollKPL], nhi[kPollKPL];
 #pragma unroll
-                for (int u = 0; u < kPollKPL; ++u) clo[u] = chi[u] = 0;
+                for (int u = 0; u < kPollKPL; ++u) nlo[u] = nhi[u] = 0;
+#pragma unroll 4
                 for (int q = 0; q < n; ++q) {
                     const float4 e = s32[q];
 #pragma unroll
                     for (int u = 0; u < kPollKPL; ++u) {
                         const float t = __builtin_fmaf(e.y, m2cy[u], __builtin_fmaf(e.x, m2cx[u], e.z));
-                        clo[u] += t <= Tlo[u];
-                        chi[u] += t <= Thi[u];
+                        nlo[u] += __builtin_bit_cast(uint32_t, Tlo[u] - t) >> 31;
+                        nhi[u] += __builtin_bit_cast(uint32_t, Thi[u] - t) >> 31;
                     }
                 }
 #pragma unroll
                 for (int u = 0; u < kPollKPL; ++u) {
-                    if (clo[u]) acc[u] += (double)clo[u] * sw[0];
-                    band[u] = chi[u] != clo[u];
+                    const int clo = n - (int)nlo[u];
+                    if (clo) acc[u] += (double)clo * sw[0];
+                    band[u] = nhi[u] != nlo[u];
                 }
             } else {
 #pragma unroll
