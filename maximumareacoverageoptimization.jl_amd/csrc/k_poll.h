@@ -6,9 +6,14 @@
 // tests kPollKPL of its candidates' disk i against every staged entry: one broadcast LDS read
 // per entry per wave feeds kPollKPL tests, there is no cross-lane reduction, and entries come
 // from HBM once per (disk, slice) instead of once per (candidate, disk). An entry is credited to
-// disk i of candidate k only when no lower-index disk j of candidate k covers it (j over the
-// disks whose regions overlap region i): exactly-once union counting, so the area is the
-// reference's first-hit sum (src/AreaCoverageCalculation.jl:67-78) over the same entries.
+// disk i of candidate k only when no lower-index disk j of candidate k covers it (exactly-once
+// union counting), so the area is the reference's first-hit sum
+// (src/AreaCoverageCalculation.jl:67-78) over the same multiset of entries.
+//
+// Ownership. Only disks j < i whose regions overlap region i can also cover an entry of region
+// i, and only inside their region box. Entries whose tile lies in such a box ("shared") are
+// kept out of the branch-free loops and decided one by one in fp64 against those disks; all
+// other entries can only be credited to disk i.
 //
 // Exact fp32 filter. With o the region origin, u = px - ox, v = py - oy, cu = cx - ox,
 // cv = cy - oy: a = (u-cu)^2 + (v-cv)^2 = q - 2u*cu - 2v*cv + C, q = u^2 + v^2, C = cu^2 + cv^2.
@@ -21,8 +26,9 @@
 //     t >  RU32(T - C + delta)   =>  a64 >  T    not covered
 //     otherwise (the band)       =>  decided in fp64 from the staged exact coordinates.
 // On the reference lattices the band is empty (a = n + 1/2 never lies within delta of T).
-// NaN / inf coordinates fail both fp32 tests and every fp64 test, like the reference; a lane
-// with D > 2^60 (fp32 range at risk) sends every entry to the exact pass.
+// Non-finite entries (never covered) and shared entries are staged with q = +inf, so t = +inf
+// is never NaN and never under a threshold; a lane with D > 2^60 sends every entry to the exact
+// pass.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -79,7 +85,18 @@ __device__ __forceinline__ bool box_overlap(const int4& a, const int4& b)
     return a.x <= a.y && a.x <= b.y && b.x <= a.y && a.z <= b.w && b.z <= a.w;
 }
 
-// Slice g of Gy: candidates [g*K/Gy, (g+1)*K/Gy); lane t, pass u -> k = kb + u*kBlock + t.
+__device__ __forceinline__ bool box_has(const int4& b, int tx, int ty)
+{
+    return b.x <= tx && tx <= b.y && b.z <= ty && ty <= b.w;
+}
+
+// sign(T - t) as 0/1: 1 iff t > T (t never NaN, T never -0, distinct floats never subtract to 0)
+__device__ __forceinline__ uint32_t above(float T, float t)
+{
+    return __builtin_bit_cast(uint32_t, T - t) >> 31;
+}
+
+// Slice g: candidates [g*kPollKPB, min(K, (g+1)*kPollKPB)); lane t, pass u -> k = kb + u*256 + t.
 // partial[i*K + k] = weight of the entries credited to disk i of candidate k.
 // Runs when mode == null or *mode == kModePoll.
 __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
@@ -89,11 +106,13 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
     double* __restrict__ partial)
 {
     if (mode && *mode != kModePoll) return;
-    __shared__ float4 s32[kPollCH];    // (u~, v~, q~, 0)
-    __shared__ double2 s64[kPollCH];   // exact coordinates (band + ownership tests)
+    __shared__ float4 s32[kPollCH];    // (u~, v~, q~, 0); q~ = +inf for shared / non-finite
+    __shared__ double2 s64[kPollCH];   // exact coordinates
     __shared__ double sw[kPollCH];
+    __shared__ uint8_t sshared[kPollCH];
     __shared__ int rs[kPollRB], rpre[kPollRB + 1];
     __shared__ uint16_t nbr[kPollNbr];
+    __shared__ int4 nbox[kPollNbr];
     __shared__ int ncnt;
 
     const int i = blockIdx.x;
@@ -149,7 +168,6 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
         Tlo[u] = f32_down(d.T - C - delta);
         Thi[u] = f32_up(d.T - C + delta);
     }
-
     bool any_live = false;
 #pragma unroll
     for (int u = 0; u < kPollKPL; ++u) any_live |= live[u];
@@ -162,7 +180,10 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
         const int4 Q = region[j];
         if (box_overlap(Q, R)) {
             const int p = atomicAdd(&ncnt, 1);
-            if (p < kPollNbr) nbr[p] = (uint16_t)j;
+            if (p < kPollNbr) {
+                nbr[p] = (uint16_t)j;
+                nbox[p] = Q;
+            }
         }
     }
     __syncthreads();
@@ -202,6 +223,7 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
         const int total = rpre[nr];
         for (int base = 0; base < total; base += kPollCH) {
             const int n = min(kPollCH, total - base);
+            bool any_shared = false;
             for (int q = tid; q < n; q += kBlock) {
                 const int f = base + q;
                 int lo = 0, hi = nr - 1;
@@ -213,74 +235,95 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
                 const double2 p = xy[j];
                 s64[q] = p;
                 sw[q] = w[j];
+                bool shared = nc > kPollNbr;
+                if (nc > 0 && !shared) {
+                    const int ty = rb + lo, tx = tile_of(p.x, g.gx0, g.invS, g.nTx);
+                    for (int m = 0; m < nc; ++m) shared |= box_has(nbox[m], tx, ty);
+                }
+                sshared[q] = shared;
+                any_shared |= shared;
                 const float fu = (float)(p.x - ox), fv = (float)(p.y - oy);
-                // non-finite entries (never covered) -> (0, 0, +inf): t = +inf, never NaN
-                s32[q] = __builtin_isfinite(fu) && __builtin_isfinite(fv)
+                s32[q] = !shared && __builtin_isfinite(fu) && __builtin_isfinite(fv)
                              ? make_float4(fu, fv, __builtin_fmaf(fu, fu, fv * fv), 0.0f)
                              : make_float4(0.0f, 0.0f, __builtin_inff(), 0.0f);
             }
-            __syncthreads();
+            any_shared = __syncthreads_or(any_shared);
             const uint64_t w0 = __builtin_bit_cast(uint64_t, sw[0]);
             bool mixed = false;
             for (int q = tid; q < n; q += kBlock) mixed |= __builtin_bit_cast(uint64_t, sw[q]) != w0;
             const bool uniform = !__syncthreads_or(mixed);
 
-            bool band[kPollKPL];
+            if (wave_live) {
+                bool band[kPollKPL];
+                if (uniform) {
+                    // hot loop: per staged entry, kPollKPL tests of 2 FMAs + 2 sign-bit counts
+                    uint32_t nlo[kPollKPL], nhi[kPollKPL];
 #pragma unroll
-            for (int u = 0; u < kPollKPL; ++u) band[u] = false;
-            if (!wave_live) {
-                // no candidate of this wave is live (the poll's last slice): nothing to test
-            } else if (nc == 0 && uniform) {
-                // hot loop: per staged entry, kPollKPL tests of 2 FMAs + 2 sign-bit counts.
-                // t is never NaN (non-finite entries are staged as q = +inf), and a float
-                // difference of distinct values is never zero, so sign(T - t) = [t > T]: the
-                // counts are of the entries NOT under each threshold.
-                uint32_t nlo[kPollKPL], nhi[kPollKPL];
-#pragma unroll
-                for (int u = 0; u < kPollKPL; ++u) nlo[u] = nhi[u] = 0;
+                    for (int u = 0; u < kPollKPL; ++u) nlo[u] = nhi[u] = 0;
 #pragma unroll 4
-                for (int q = 0; q < n; ++q) {
-                    const float4 e = s32[q];
-#pragma unroll
-                    for (int u = 0; u < kPollKPL; ++u) {
-                        const float t = __builtin_fmaf(e.y, m2cy[u], __builtin_fmaf(e.x, m2cx[u], e.z));
-                        nlo[u] += __builtin_bit_cast(uint32_t, Tlo[u] - t) >> 31;
-                        nhi[u] += __builtin_bit_cast(uint32_t, Thi[u] - t) >> 31;
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < kPollKPL; ++u) {
-                    const int clo = n - (int)nlo[u];
-                    if (clo) acc[u] += (double)clo * sw[0];
-                    band[u] = nhi[u] != nlo[u];
-                }
-            } else {
-#pragma unroll
-                for (int u = 0; u < kPollKPL; ++u) {
-                    if (!live[u]) continue;
                     for (int q = 0; q < n; ++q) {
                         const float4 e = s32[q];
-                        const float t = __builtin_fmaf(e.y, m2cy[u], __builtin_fmaf(e.x, m2cx[u], e.z));
-                        if (t <= Tlo[u]) {
-                            if (nc == 0 || !stolen(s64[q], kk[u])) acc[u] += sw[q];
-                        } else if (t <= Thi[u]) {
-                            band[u] = true;
+#pragma unroll
+                        for (int u = 0; u < kPollKPL; ++u) {
+                            const float t = __builtin_fmaf(e.y, m2cy[u], __builtin_fmaf(e.x, m2cx[u], e.z));
+                            nlo[u] += above(Tlo[u], t);
+                            nhi[u] += above(Thi[u], t);
                         }
                     }
-                }
-            }
-            // exact fp64 decisions for the band entries (rare; never on reference lattices)
 #pragma unroll
-            for (int u = 0; u < kPollKPL; ++u) {
-                if (!band[u]) continue;
-                const DiskRec d = disksT[(int64_t)i * K + kk[u]];
-                for (int q = 0; q < n; ++q) {
-                    const float4 e = s32[q];
-                    const float t = __builtin_fmaf(e.y, m2cy[u], __builtin_fmaf(e.x, m2cx[u], e.z));
-                    if (!(t > Tlo[u] && t <= Thi[u])) continue;
-                    const double2 p = s64[q];
-                    if (sqdist(p.x, p.y, d.cx, d.cy) <= d.T && (nc == 0 || !stolen(p, kk[u])))
-                        acc[u] += sw[q];
+                    for (int u = 0; u < kPollKPL; ++u) {
+                        const int clo = n - (int)nlo[u];
+                        if (clo) acc[u] += (double)clo * sw[0];
+                        band[u] = nhi[u] != nlo[u];
+                    }
+                } else {
+                    // weighted loop: the surely covered entries add their own weight
+                    uint32_t nlo[kPollKPL], nhi[kPollKPL];
+#pragma unroll
+                    for (int u = 0; u < kPollKPL; ++u) nlo[u] = nhi[u] = 0;
+#pragma unroll 2
+                    for (int q = 0; q < n; ++q) {
+                        const float4 e = s32[q];
+                        const double wq = sw[q];
+#pragma unroll
+                        for (int u = 0; u < kPollKPL; ++u) {
+                            const float t = __builtin_fmaf(e.y, m2cy[u], __builtin_fmaf(e.x, m2cx[u], e.z));
+                            const uint32_t a = above(Tlo[u], t);
+                            acc[u] += a ? 0.0 : wq;
+                            nlo[u] += a;
+                            nhi[u] += above(Thi[u], t);
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < kPollKPL; ++u) band[u] = nhi[u] != nlo[u];
+                }
+                // exact fp64 decisions for the band entries (rare; never on reference lattices)
+#pragma unroll
+                for (int u = 0; u < kPollKPL; ++u) {
+                    if (!band[u]) continue;
+                    const DiskRec d = disksT[(int64_t)i * K + kk[u]];
+                    for (int q = 0; q < n; ++q) {
+                        if (sshared[q]) continue;  // decided (with ownership) below
+                        const float4 e = s32[q];
+                        const float t = __builtin_fmaf(e.y, m2cy[u], __builtin_fmaf(e.x, m2cx[u], e.z));
+                        if (!(t > Tlo[u] && t <= Thi[u])) continue;
+                        const double2 p = s64[q];
+                        if (sqdist(p.x, p.y, d.cx, d.cy) <= d.T) acc[u] += sw[q];
+                    }
+                }
+                // shared entries: exact fp64 decision, then ownership against disks j < i
+                if (any_shared) {
+#pragma unroll
+                    for (int u = 0; u < kPollKPL; ++u) {
+                        if (!live[u]) continue;
+                        const DiskRec d = disksT[(int64_t)i * K + kk[u]];
+                        for (int q = 0; q < n; ++q) {
+                            if (!sshared[q]) continue;
+                            const double2 p = s64[q];
+                            if (sqdist(p.x, p.y, d.cx, d.cy) <= d.T && !stolen(p, kk[u]))
+                                acc[u] += sw[q];
+                        }
+                    }
                 }
             }
             __syncthreads();
