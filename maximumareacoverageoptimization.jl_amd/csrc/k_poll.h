@@ -110,6 +110,8 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
     __shared__ double2 s64[kPollCH];   // exact coordinates
     __shared__ double sw[kPollCH];
     __shared__ uint8_t sshared[kPollCH];
+    __shared__ uint16_t slist[kPollCH];
+    __shared__ int snshared;
     __shared__ int rs[kPollRB], rpre[kPollRB + 1];
     __shared__ uint16_t nbr[kPollNbr];
     __shared__ int4 nbox[kPollNbr];
@@ -248,6 +250,16 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
                              : make_float4(0.0f, 0.0f, __builtin_inff(), 0.0f);
             }
             any_shared = __syncthreads_or(any_shared);
+            if (any_shared) {  // the shared entries in staging order (same list for every lane)
+                if (tid == 0) {
+                    int c = 0;
+                    for (int q = 0; q < n; ++q)
+                        if (sshared[q]) slist[c++] = (uint16_t)q;
+                    snshared = c;
+                }
+                __syncthreads();
+            }
+            const int nshared = any_shared ? snshared : 0;
             const uint64_t w0 = __builtin_bit_cast(uint64_t, sw[0]);
             bool mixed = false;
             for (int q = tid; q < n; q += kBlock) mixed |= __builtin_bit_cast(uint64_t, sw[q]) != w0;
@@ -311,17 +323,44 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
                         if (sqdist(p.x, p.y, d.cx, d.cy) <= d.T) acc[u] += sw[q];
                     }
                 }
-                // shared entries: exact fp64 decision, then ownership against disks j < i
+                // shared entries: exact fp64 decision, then ownership against disks j < i,
+                // 64 shared entries at a time as a per-lane bit mask, each neighbour disk loaded
+                // once per group (4 at a time) instead of once per covered entry
                 if (any_shared) {
-#pragma unroll
                     for (int u = 0; u < kPollKPL; ++u) {
                         if (!live[u]) continue;
-                        const DiskRec d = disksT[(int64_t)i * K + kk[u]];
-                        for (int q = 0; q < n; ++q) {
-                            if (!sshared[q]) continue;
-                            const double2 p = s64[q];
-                            if (sqdist(p.x, p.y, d.cx, d.cy) <= d.T && !stolen(p, kk[u]))
-                                acc[u] += sw[q];
+                        const int k = kk[u];
+                        const DiskRec d = disksT[(int64_t)i * K + k];
+                        for (int g0 = 0; g0 < nshared; g0 += 64) {
+                            const int ng = min(64, nshared - g0);
+                            const uint16_t* idx = slist + g0;
+                            uint64_t cov = 0;
+                            for (int b = 0; b < ng; ++b) {
+                                const double2 p = s64[idx[b]];
+                                if (sqdist(p.x, p.y, d.cx, d.cy) <= d.T) cov |= 1ull << b;
+                            }
+                            if (nc <= kPollNbr) {
+                                for (int m0 = 0; m0 < nc && cov; m0 += 4) {
+                                    DiskRec e[4];
+#pragma unroll
+                                    for (int m = 0; m < 4; ++m)
+                                        e[m] = m0 + m < nc ? disksT[(int64_t)nbr[m0 + m] * K + k]
+                                                           : DiskRec{0.0, 0.0, -1.0, 0.0};
+                                    for (int b = 0; b < ng; ++b) {
+                                        if (!((cov >> b) & 1)) continue;
+                                        const double2 p = s64[idx[b]];
+#pragma unroll
+                                        for (int m = 0; m < 4; ++m)
+                                            if (sqdist(p.x, p.y, e[m].cx, e[m].cy) <= e[m].T)
+                                                cov &= ~(1ull << b);
+                                    }
+                                }
+                            } else {
+                                for (int b = 0; b < ng; ++b)
+                                    if (((cov >> b) & 1) && stolen(s64[idx[b]], k)) cov &= ~(1ull << b);
+                            }
+                            for (int b = 0; b < ng; ++b)
+                                if ((cov >> b) & 1) acc[u] += sw[idx[b]];
                         }
                     }
                 }
