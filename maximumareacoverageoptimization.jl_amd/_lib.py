@@ -13,7 +13,7 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmaxcover.so")
+LIB_PATH = os.environ.get("MAXCOVER_LIB") or os.path.join(_HERE, "libmaxcover.so")
 
 MAC_OK = 0
 MAC_E_INVAL = 1

@@ -41,6 +41,11 @@
 
 namespace mac {
 
+#ifdef MAC_DIAG
+constexpr uint64_t kDiagMax = 1 << 16;
+__device__ uint64_t g_diag[4 * kDiagMax];
+#endif
+
 constexpr int kPollKPL = 4;                      // candidates per lane
 constexpr int kPollKPB = kBlock * kPollKPL;      // candidates per workgroup (at most)
 
@@ -106,6 +111,10 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
     double* __restrict__ partial)
 {
     if (mode && *mode != kModePoll) return;
+#ifdef MAC_DIAG
+    const uint64_t diag_t0 = __builtin_amdgcn_s_memrealtime();
+    int diag_entries = 0;
+#endif
     __shared__ float4 s32[kPollCH];    // (u~, v~, q~, 0); q~ = +inf for shared / non-finite
     __shared__ double2 s64[kPollCH];   // exact coordinates
     __shared__ double sw[kPollCH];
@@ -223,6 +232,9 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
         }
         __syncthreads();
         const int total = rpre[nr];
+#ifdef MAC_DIAG
+        diag_entries += total;
+#endif
         for (int base = 0; base < total; base += kPollCH) {
             const int n = min(kPollCH, total - base);
             bool any_shared = false;
@@ -371,6 +383,19 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
 #pragma unroll
     for (int u = 0; u < kPollKPL; ++u)
         if (kk[u] >= 0) partial[(int64_t)i * K + kk[u]] = acc[u];
+#ifdef MAC_DIAG
+    if (tid == 0) {
+        // diagnostic build only: per-workgroup stamps into a buffer nothing else reads
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        const uint64_t b = (uint64_t)blockIdx.y * gridDim.x + blockIdx.x;
+        if (b < kDiagMax) {
+            g_diag[4 * b + 0] = diag_t0;
+            g_diag[4 * b + 1] = t1;
+            g_diag[4 * b + 2] = ((uint64_t)nc << 32) | (uint32_t)diag_entries;
+            g_diag[4 * b + 3] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
+        }
+    }
+#endif
 }
 
 }  // namespace mac

@@ -541,6 +541,17 @@ static int32_t host_eval(mac_ctx* ctx, const double* cands, int64_t three_n, int
 
 extern "C" {
 
+#ifdef MAC_DIAG
+// diagnostic build only (not declared in maxcover.h): per-workgroup poll-walk stamps
+int32_t mac_diag_read(uint64_t* out, int64_t n)
+{
+    if (n > (int64_t)(4 * kDiagMax)) n = 4 * kDiagMax;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), sizeof(uint64_t) * n, 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return MAC_E_HIP;
+    return MAC_OK;
+}
+#endif
+
 const char* mac_last_error(void) { return g_last_error.c_str(); }
 
 const char* mac_version(void) { return "maxcover 0.1.0 gfx950"; }

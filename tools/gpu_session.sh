@@ -41,6 +41,10 @@ for s in $STEPS; do
             run bench_$a 600 python bench.py --no-cpu --algo $a --steps 30 ; rc=$?
             fatal $rc && break
         done ;;
+    diag)
+        make -s -C maximumareacoverageoptimization.jl_amd/csrc diag
+        MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
+            run diag 600 python tools/diag_poll.py ; rc=$? ;;
     bench3)
         run bench3 600 python bench.py --config 3 --no-cpu ; rc=$? ;;
     bench2)
