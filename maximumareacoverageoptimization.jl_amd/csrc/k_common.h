@@ -17,6 +17,8 @@ constexpr int kNbrCap = 6;         // tiled walk: lower-index overlapping disks 
 constexpr int kPollCH = 512;       // poll walk: entries staged in LDS per chunk
 constexpr int kPollRB = 64;        // poll walk: region rows per batch
 constexpr int kPollNbr = 64;       // poll walk: lower-index overlapping regions kept
+constexpr int kPollKPL = 4;        // poll walk: candidates per lane
+constexpr int kPollKPB = kBlock * kPollKPL;  // poll walk: candidates per workgroup (at most)
 
 constexpr int kModePoll = 1;
 constexpr int kModeTiled = 2;

@@ -12,8 +12,8 @@
 //
 // Ownership. Only disks j < i whose regions overlap region i can also cover an entry of region
 // i, and only inside their region box. Entries whose tile lies in such a box ("shared") are
-// kept out of the branch-free loops and decided one by one in fp64 against those disks; all
-// other entries can only be credited to disk i.
+// left out here and decided exactly by coverage_poll_shared_kernel (k_poll_shared.h); every
+// other entry of region i can only be credited to disk i.
 //
 // Exact fp32 filter. With o the region origin, u = px - ox, v = py - oy, cu = cx - ox,
 // cv = cy - oy: a = (u-cu)^2 + (v-cv)^2 = q - 2u*cu - 2v*cv + C, q = u^2 + v^2, C = cu^2 + cv^2.
@@ -36,6 +36,7 @@
 
 #include "predicate.h"
 #include "k_common.h"
+#include "k_poll_shared.h"
 
 #pragma clang fp contract(off)
 
@@ -45,9 +46,6 @@ namespace mac {
 constexpr uint64_t kDiagMax = 1 << 16;
 __device__ uint64_t g_diag[4 * kDiagMax];
 #endif
-
-constexpr int kPollKPL = 4;                      // candidates per lane
-constexpr int kPollKPB = kBlock * kPollKPL;      // candidates per workgroup (at most)
 
 __device__ __forceinline__ float next_down_f32(float f)
 {
@@ -85,29 +83,21 @@ __device__ __forceinline__ float f32_up(double v)
     return f;
 }
 
-__device__ __forceinline__ bool box_overlap(const int4& a, const int4& b)
+// c + [t > T] computed as c + sign(T - t): t is never NaN, T never -0, and distinct floats never
+// subtract to zero, so the sign bit of T - t is exactly [t > T] (no compare, no VCC hazard).
+__device__ __forceinline__ uint32_t count_above(uint32_t c, float T, float t)
 {
-    return a.x <= a.y && a.x <= b.y && b.x <= a.y && a.z <= b.w && b.z <= a.w;
-}
-
-__device__ __forceinline__ bool box_has(const int4& b, int tx, int ty)
-{
-    return b.x <= tx && tx <= b.y && b.z <= ty && ty <= b.w;
-}
-
-// sign(T - t) as 0/1: 1 iff t > T (t never NaN, T never -0, distinct floats never subtract to 0)
-__device__ __forceinline__ uint32_t above(float T, float t)
-{
-    return __builtin_bit_cast(uint32_t, T - t) >> 31;
+    return c + (__builtin_bit_cast(uint32_t, T - t) >> 31);
 }
 
 // Slice g: candidates [g*kPollKPB, min(K, (g+1)*kPollKPB)); lane t, pass u -> k = kb + u*256 + t.
-// partial[i*K + k] = weight of the entries credited to disk i of candidate k.
+// partial[i*K + k] = weight of the non-shared entries credited to disk i of candidate k.
 // Runs when mode == null or *mode == kModePoll.
 __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
     const double2* __restrict__ xy, const double* __restrict__ w,
     const int32_t* __restrict__ off, Grid g, const DiskRec* __restrict__ disksT,
-    const int4* __restrict__ region, int N, int K, const int* __restrict__ mode,
+    const int4* __restrict__ region, const uint16_t* __restrict__ nbrT,
+    const int* __restrict__ ncount, int N, int K, const int* __restrict__ mode,
     double* __restrict__ partial)
 {
     if (mode && *mode != kModePoll) return;
@@ -116,21 +106,17 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
     int diag_entries = 0;
 #endif
     __shared__ float4 s32[kPollCH];    // (u~, v~, q~, 0); q~ = +inf for shared / non-finite
-    __shared__ double2 s64[kPollCH];   // exact coordinates
+    __shared__ double2 s64[kPollCH];   // exact coordinates (band decisions)
     __shared__ double sw[kPollCH];
-    __shared__ uint8_t sshared[kPollCH];
-    __shared__ uint16_t slist[kPollCH];
-    __shared__ int snshared;
     __shared__ int rs[kPollRB], rpre[kPollRB + 1];
-    __shared__ uint16_t nbr[kPollNbr];
     __shared__ int4 nbox[kPollNbr];
-    __shared__ int ncnt;
 
     const int i = blockIdx.x;
     const int tid = threadIdx.x;
     const int kb = blockIdx.y * kPollKPB;
     const int ke = min(K, kb + kPollKPB);
     const int4 R = region[i];
+    const int nc = ncount[i];
 
     int kk[kPollKPL];
 #pragma unroll
@@ -144,6 +130,7 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
             if (kk[u] >= 0) partial[(int64_t)i * K + kk[u]] = 0.0;
         return;
     }
+    if (tid < min(nc, kPollNbr)) nbox[tid] = region[nbrT[i * kPollNbr + tid]];
 
     // region origin and the bound U on every staged offset (entries of tile t satisfy
     // t <= (p - g0)/S < t + 1 up to rounding; two tiles of slack absorb it)
@@ -184,39 +171,6 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
     for (int u = 0; u < kPollKPL; ++u) any_live |= live[u];
     const bool wave_live = __any(any_live);
 
-    // lower-index disks whose regions overlap region i (order irrelevant: a boolean OR)
-    if (tid == 0) ncnt = 0;
-    __syncthreads();
-    for (int j = tid; j < i; j += kBlock) {
-        const int4 Q = region[j];
-        if (box_overlap(Q, R)) {
-            const int p = atomicAdd(&ncnt, 1);
-            if (p < kPollNbr) {
-                nbr[p] = (uint16_t)j;
-                nbox[p] = Q;
-            }
-        }
-    }
-    __syncthreads();
-    const int nc = ncnt;
-
-    // is the entry at exact coordinates p covered by a lower-index disk of candidate k?
-    auto stolen = [&](const double2 p, const int k) -> bool {
-        if (nc <= kPollNbr) {
-            for (int q = 0; q < nc; ++q) {
-                const DiskRec e = disksT[(int64_t)nbr[q] * K + k];
-                if (sqdist(p.x, p.y, e.cx, e.cy) <= e.T) return true;
-            }
-        } else {
-            for (int j = 0; j < i; ++j) {
-                if (!box_overlap(region[j], R)) continue;
-                const DiskRec e = disksT[(int64_t)j * K + k];
-                if (sqdist(p.x, p.y, e.cx, e.cy) <= e.T) return true;
-            }
-        }
-        return false;
-    };
-
     for (int rb = R.z; rb <= R.w; rb += kPollRB) {
         const int nr = min(kPollRB, R.w - rb + 1);
         if (tid < nr) {
@@ -237,7 +191,8 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
 #endif
         for (int base = 0; base < total; base += kPollCH) {
             const int n = min(kPollCH, total - base);
-            bool any_shared = false;
+            bool mixed = false;
+            double wfirst = 0.0;
             for (int q = tid; q < n; q += kBlock) {
                 const int f = base + q;
                 int lo = 0, hi = nr - 1;
@@ -247,64 +202,48 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
                 }
                 const int j = rs[lo] + (f - rpre[lo]);
                 const double2 p = xy[j];
+                const double wj = w[j];
                 s64[q] = p;
-                sw[q] = w[j];
-                bool shared = nc > kPollNbr;
-                if (nc > 0 && !shared) {
-                    const int ty = rb + lo, tx = tile_of(p.x, g.gx0, g.invS, g.nTx);
-                    for (int m = 0; m < nc; ++m) shared |= box_has(nbox[m], tx, ty);
-                }
-                sshared[q] = shared;
-                any_shared |= shared;
+                sw[q] = wj;
+                const bool shared =
+                    nc > 0 && entry_shared(nc, nbox, tile_of(p.x, g.gx0, g.invS, g.nTx), rb + lo);
                 const float fu = (float)(p.x - ox), fv = (float)(p.y - oy);
                 s32[q] = !shared && __builtin_isfinite(fu) && __builtin_isfinite(fv)
                              ? make_float4(fu, fv, __builtin_fmaf(fu, fu, fv * fv), 0.0f)
                              : make_float4(0.0f, 0.0f, __builtin_inff(), 0.0f);
+                if (q == tid) wfirst = wj;
+                mixed |= __builtin_bit_cast(uint64_t, wj) != __builtin_bit_cast(uint64_t, wfirst);
             }
-            any_shared = __syncthreads_or(any_shared);
-            if (any_shared) {  // the shared entries in staging order (same list for every lane)
-                if (tid == 0) {
-                    int c = 0;
-                    for (int q = 0; q < n; ++q)
-                        if (sshared[q]) slist[c++] = (uint16_t)q;
-                    snshared = c;
-                }
-                __syncthreads();
-            }
-            const int nshared = any_shared ? snshared : 0;
+            __syncthreads();
+            // weights identical across the chunk? (compare with entry 0 after staging)
             const uint64_t w0 = __builtin_bit_cast(uint64_t, sw[0]);
-            bool mixed = false;
-            for (int q = tid; q < n; q += kBlock) mixed |= __builtin_bit_cast(uint64_t, sw[q]) != w0;
+            mixed |= (tid < n) && __builtin_bit_cast(uint64_t, sw[tid]) != w0;
             const bool uniform = !__syncthreads_or(mixed);
 
             if (wave_live) {
                 bool band[kPollKPL];
+                uint32_t nlo[kPollKPL], nhi[kPollKPL];
+#pragma unroll
+                for (int u = 0; u < kPollKPL; ++u) nlo[u] = nhi[u] = 0;
                 if (uniform) {
                     // hot loop: per staged entry, kPollKPL tests of 2 FMAs + 2 sign-bit counts
-                    uint32_t nlo[kPollKPL], nhi[kPollKPL];
-#pragma unroll
-                    for (int u = 0; u < kPollKPL; ++u) nlo[u] = nhi[u] = 0;
 #pragma unroll 4
                     for (int q = 0; q < n; ++q) {
                         const float4 e = s32[q];
 #pragma unroll
                         for (int u = 0; u < kPollKPL; ++u) {
                             const float t = __builtin_fmaf(e.y, m2cy[u], __builtin_fmaf(e.x, m2cx[u], e.z));
-                            nlo[u] += above(Tlo[u], t);
-                            nhi[u] += above(Thi[u], t);
+                            nlo[u] = count_above(nlo[u], Tlo[u], t);
+                            nhi[u] = count_above(nhi[u], Thi[u], t);
                         }
                     }
 #pragma unroll
                     for (int u = 0; u < kPollKPL; ++u) {
                         const int clo = n - (int)nlo[u];
                         if (clo) acc[u] += (double)clo * sw[0];
-                        band[u] = nhi[u] != nlo[u];
                     }
                 } else {
                     // weighted loop: the surely covered entries add their own weight
-                    uint32_t nlo[kPollKPL], nhi[kPollKPL];
-#pragma unroll
-                    for (int u = 0; u < kPollKPL; ++u) nlo[u] = nhi[u] = 0;
 #pragma unroll 2
                     for (int q = 0; q < n; ++q) {
                         const float4 e = s32[q];
@@ -312,68 +251,33 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
 #pragma unroll
                         for (int u = 0; u < kPollKPL; ++u) {
                             const float t = __builtin_fmaf(e.y, m2cy[u], __builtin_fmaf(e.x, m2cx[u], e.z));
-                            const uint32_t a = above(Tlo[u], t);
+                            const uint32_t a = count_above(0u, Tlo[u], t);
                             acc[u] += a ? 0.0 : wq;
                             nlo[u] += a;
-                            nhi[u] += above(Thi[u], t);
+                            nhi[u] = count_above(nhi[u], Thi[u], t);
                         }
                     }
-#pragma unroll
-                    for (int u = 0; u < kPollKPL; ++u) band[u] = nhi[u] != nlo[u];
                 }
-                // exact fp64 decisions for the band entries (rare; never on reference lattices)
+#pragma unroll
+                for (int u = 0; u < kPollKPL; ++u) band[u] = nhi[u] != nlo[u];
+                // exact fp64 decisions for the band entries (rare; never on reference lattices).
+                // Shared and non-finite entries have t = +inf: never in the band unless the lane
+                // is fp32-disabled (Thi = +inf), and then the exact test rejects non-finite ones
+                // while shared ones are skipped here (decided by the shared kernel).
 #pragma unroll
                 for (int u = 0; u < kPollKPL; ++u) {
                     if (!band[u]) continue;
                     const DiskRec d = disksT[(int64_t)i * K + kk[u]];
                     for (int q = 0; q < n; ++q) {
-                        if (sshared[q]) continue;  // decided (with ownership) below
                         const float4 e = s32[q];
                         const float t = __builtin_fmaf(e.y, m2cy[u], __builtin_fmaf(e.x, m2cx[u], e.z));
                         if (!(t > Tlo[u] && t <= Thi[u])) continue;
                         const double2 p = s64[q];
+                        if (e.z == __builtin_inff() && nc > 0 &&
+                            entry_shared(nc, nbox, tile_of(p.x, g.gx0, g.invS, g.nTx),
+                                         tile_of(p.y, g.gy0, g.invS, g.nTy)))
+                            continue;
                         if (sqdist(p.x, p.y, d.cx, d.cy) <= d.T) acc[u] += sw[q];
-                    }
-                }
-                // shared entries: exact fp64 decision, then ownership against disks j < i,
-                // 64 shared entries at a time as a per-lane bit mask, each neighbour disk loaded
-                // once per group (4 at a time) instead of once per covered entry
-                if (any_shared) {
-                    for (int u = 0; u < kPollKPL; ++u) {
-                        if (!live[u]) continue;
-                        const int k = kk[u];
-                        const DiskRec d = disksT[(int64_t)i * K + k];
-                        for (int g0 = 0; g0 < nshared; g0 += 64) {
-                            const int ng = min(64, nshared - g0);
-                            const uint16_t* idx = slist + g0;
-                            uint64_t cov = 0;
-                            for (int b = 0; b < ng; ++b) {
-                                const double2 p = s64[idx[b]];
-                                if (sqdist(p.x, p.y, d.cx, d.cy) <= d.T) cov |= 1ull << b;
-                            }
-                            if (nc <= kPollNbr) {
-                                for (int m0 = 0; m0 < nc && cov; m0 += 4) {
-                                    DiskRec e[4];
-#pragma unroll
-                                    for (int m = 0; m < 4; ++m)
-                                        e[m] = m0 + m < nc ? disksT[(int64_t)nbr[m0 + m] * K + k]
-                                                           : DiskRec{0.0, 0.0, -1.0, 0.0};
-                                    for (int b = 0; b < ng; ++b) {
-                                        if (!((cov >> b) & 1)) continue;
-                                        const double2 p = s64[idx[b]];
-#pragma unroll
-                                        for (int m = 0; m < 4; ++m)
-                                            if (sqdist(p.x, p.y, e[m].cx, e[m].cy) <= e[m].T)
-                                                cov &= ~(1ull << b);
-                                    }
-                                }
-                            } else {
-                                for (int b = 0; b < ng; ++b)
-                                    if (((cov >> b) & 1) && stolen(s64[idx[b]], k)) cov &= ~(1ull << b);
-                            }
-                            for (int b = 0; b < ng; ++b)
-                                if ((cov >> b) & 1) acc[u] += sw[idx[b]];
-                        }
                     }
                 }
             }

@@ -1,0 +1,191 @@
+// k_poll_shared.h — ownership for the poll walk: per-disk neighbour lists (once per poll) and
+// the exact pass over "shared" entries, the entries of region i that a lower-index disk j can
+// also cover (their tile lies in region j's box, and boxes i, j overlap).
+//
+// The main poll kernel (k_poll.h) never credits a shared entry; this kernel adds, for every
+// (disk i, candidate k), the weight of the shared entries that disk i of candidate k covers and
+// no disk j < i of candidate k covers — in fp64, exactly the reference predicate — to
+// partial[i*K + k]. Together: every entry is credited to the lowest-index disk covering it.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "predicate.h"
+#include "k_common.h"
+
+#pragma clang fp contract(off)
+
+namespace mac {
+
+__device__ __forceinline__ bool box_overlap(const int4& a, const int4& b)
+{
+    return a.x <= a.y && a.x <= b.y && b.x <= a.y && a.z <= b.w && b.z <= a.w;
+}
+
+__device__ __forceinline__ bool box_has(const int4& b, int tx, int ty)
+{
+    return b.x <= tx && tx <= b.y && b.z <= ty && ty <= b.w;
+}
+
+// Block i: the disks j < i whose region boxes overlap region i's (at most kPollNbr kept in
+// nbr[i*kPollNbr ...]; ncount[i] is the true count, > kPollNbr meaning "overflowed").
+__global__ __launch_bounds__(kBlock) void neighbors_kernel(const int4* __restrict__ region, int N,
+                                                           uint16_t* __restrict__ nbr,
+                                                           int* __restrict__ ncount)
+{
+    __shared__ int cnt;
+    const int i = blockIdx.x;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    const int4 R = region[i];
+    if (R.x <= R.y) {
+        for (int j = threadIdx.x; j < i; j += kBlock) {
+            const int4 Q = region[j];
+            if (box_overlap(Q, R)) {
+                const int p = atomicAdd(&cnt, 1);  // list order is irrelevant (a boolean OR)
+                if (p < kPollNbr) nbr[i * kPollNbr + p] = (uint16_t)j;
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) ncount[i] = cnt;
+}
+
+// Entry (tile tx, ty) of region i is shared when it lies in a neighbour's box.
+__device__ __forceinline__ bool entry_shared(int nc, const int4* nbox, int tx, int ty)
+{
+    if (nc > kPollNbr) return true;
+    bool s = false;
+    for (int m = 0; m < nc; ++m) s |= box_has(nbox[m], tx, ty);
+    return s;
+}
+
+// Same grid as coverage_poll_kernel (disk i, slice of kPollKPB candidates); returns at once for
+// disks without neighbours. Shared entries are compacted (in list order) into LDS round by
+// round; each lane then decides them for its candidates with the neighbour disks preloaded.
+__global__ __launch_bounds__(kBlock) void coverage_poll_shared_kernel(
+    const double2* __restrict__ xy, const double* __restrict__ w,
+    const int32_t* __restrict__ off, Grid g, const DiskRec* __restrict__ disksT,
+    const int4* __restrict__ region, const uint16_t* __restrict__ nbrT,
+    const int* __restrict__ ncount, int N, int K, const int* __restrict__ mode,
+    double* __restrict__ partial)
+{
+    if (mode && *mode != kModePoll) return;
+    const int i = blockIdx.x;
+    const int nc = ncount[i];
+    const int4 R = region[i];
+    if (nc == 0 || R.x > R.y) return;  // uniform across the block
+
+    __shared__ double2 sp[kBlock];
+    __shared__ double sw[kBlock];
+    __shared__ int rs[kPollRB], rpre[kPollRB + 1];
+    __shared__ int4 nbox[kPollNbr];
+    __shared__ uint16_t nbr[kPollNbr];
+    __shared__ int wcount[kWavesPerBlock];
+
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+    const int ncl = min(nc, kPollNbr);
+    if (tid < ncl) {
+        nbr[tid] = nbrT[i * kPollNbr + tid];
+        nbox[tid] = region[nbr[tid]];
+    }
+    const int kb = blockIdx.y * kPollKPB;
+    const int ke = min(K, kb + kPollKPB);
+    constexpr int KPL = kPollKPB / kBlock;
+    double acc[KPL];
+#pragma unroll
+    for (int u = 0; u < KPL; ++u) acc[u] = 0.0;
+    __syncthreads();
+
+    for (int rb = R.z; rb <= R.w; rb += kPollRB) {
+        const int nr = min(kPollRB, R.w - rb + 1);
+        if (tid < nr) {
+            const int64_t rowbase = (int64_t)(rb + tid) * g.nTx;
+            const int s = off[rowbase + R.x];
+            rs[tid] = s;
+            rpre[tid + 1] = off[rowbase + R.y + 1] - s;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            rpre[0] = 0;
+            for (int r = 0; r < nr; ++r) rpre[r + 1] += rpre[r];
+        }
+        __syncthreads();
+        const int total = rpre[nr];
+        for (int base = 0; base < total; base += kBlock) {
+            // this round's entries (one per thread), shared ones compacted in list order
+            const int f = base + tid;
+            bool shared = false;
+            double2 p = make_double2(0.0, 0.0);
+            double ww = 0.0;
+            if (f < total) {
+                int lo = 0, hi = nr - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (rpre[mid] <= f) lo = mid; else hi = mid - 1;
+                }
+                const int j = rs[lo] + (f - rpre[lo]);
+                p = xy[j];
+                ww = w[j];
+                shared = entry_shared(nc, nbox, tile_of(p.x, g.gx0, g.invS, g.nTx), rb + lo);
+            }
+            const uint64_t bal = __ballot(shared);
+            if (lane == 0) wcount[wid] = __popcll(bal);
+            __syncthreads();
+            int pos = __popcll(bal & ((1ull << lane) - 1)), ns = 0;
+            for (int q = 0; q < kWavesPerBlock; ++q) {
+                if (q < wid) pos += wcount[q];
+                ns += wcount[q];
+            }
+            if (shared) {
+                sp[pos] = p;
+                sw[pos] = ww;
+            }
+            __syncthreads();
+            if (ns) {
+                for (int u = 0; u < KPL; ++u) {
+                    const int k = kb + u * kBlock + tid;
+                    if (k >= ke) continue;
+                    const DiskRec d = disksT[(int64_t)i * K + k];
+                    if (!(d.T >= 0.0)) continue;
+                    DiskRec e[4];
+#pragma unroll
+                    for (int m = 0; m < 4; ++m)
+                        e[m] = m < ncl ? disksT[(int64_t)nbr[m] * K + k] : DiskRec{0.0, 0.0, -1.0, 0.0};
+                    for (int s = 0; s < ns; ++s) {
+                        const double2 q = sp[s];
+                        if (!(sqdist(q.x, q.y, d.cx, d.cy) <= d.T)) continue;
+                        bool stolen = false;
+#pragma unroll
+                        for (int m = 0; m < 4; ++m)
+                            stolen |= sqdist(q.x, q.y, e[m].cx, e[m].cy) <= e[m].T;
+                        if (!stolen && nc > 4) {
+                            if (nc <= kPollNbr) {
+                                for (int m = 4; m < nc && !stolen; ++m) {
+                                    const DiskRec x = disksT[(int64_t)nbr[m] * K + k];
+                                    stolen = sqdist(q.x, q.y, x.cx, x.cy) <= x.T;
+                                }
+                            } else {  // overflowed list: every lower-index overlapping region
+                                for (int j = 0; j < i && !stolen; ++j) {
+                                    if (!box_overlap(region[j], R)) continue;
+                                    const DiskRec x = disksT[(int64_t)j * K + k];
+                                    stolen = sqdist(q.x, q.y, x.cx, x.cy) <= x.T;
+                                }
+                            }
+                        }
+                        if (!stolen) acc[u] += sw[s];
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < KPL; ++u) {
+        const int k = kb + u * kBlock + tid;
+        if (k < ke) partial[(int64_t)i * K + k] += acc[u];
+    }
+}
+
+}  // namespace mac

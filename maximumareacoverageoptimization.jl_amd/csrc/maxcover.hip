@@ -95,7 +95,8 @@ struct Lane {
     hipStream_t stream = nullptr;
     hipStream_t last = nullptr;   // stream of the most recent use
     hipEvent_t done = nullptr;
-    DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode, vp;
+    DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode, vp, nbr,
+        ncount;
     hipStream_t aux = nullptr;                 // forked stream for the penalty kernel
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::vector<double> h_dlim;
@@ -421,6 +422,11 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_c
             hipLaunchKernelGGL(region_kernel, dim3(N), dim3(kBlock), 0, s, L->disks.as<DiskRec>(),
                                N, K, ctx->grid, L->region.as<int4>(), L->cost.as<double2>());
             HCK(hipGetLastError());
+            L->nbr.reserve(sizeof(uint16_t) * (size_t)N * kPollNbr);
+            L->ncount.reserve(sizeof(int) * (size_t)N);
+            hipLaunchKernelGGL(neighbors_kernel, dim3(N), dim3(kBlock), 0, s, L->region.as<int4>(),
+                               N, L->nbr.as<uint16_t>(), L->ncount.as<int>());
+            HCK(hipGetLastError());
             const int forced = ctx->algo == MAC_ALGO_POLL ? kModePoll : 0;
             hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(kBlock), 0, s, L->cost.as<double2>(), N,
                                kPollCostRatio, forced, L->mode.as<int>());
@@ -437,10 +443,18 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_c
             HCK(hipGetLastError());
         }
         if (poll_possible) {
-            hipLaunchKernelGGL(coverage_poll_kernel, dim3(N, (K + kPollKPB - 1) / kPollKPB), dim3(kBlock),
-                               0, s, ctx->xys.as<double2>(), ctx->ws.as<double>(),
+            const dim3 pgrid(N, (K + kPollKPB - 1) / kPollKPB);
+            hipLaunchKernelGGL(coverage_poll_kernel, pgrid, dim3(kBlock), 0, s,
+                               ctx->xys.as<double2>(), ctx->ws.as<double>(),
                                ctx->off.as<int32_t>(), ctx->grid, L->disks.as<DiskRec>(),
-                               L->region.as<int4>(), N, K, d_mode, L->partial.as<double>());
+                               L->region.as<int4>(), L->nbr.as<uint16_t>(), L->ncount.as<int>(), N,
+                               K, d_mode, L->partial.as<double>());
+            HCK(hipGetLastError());
+            hipLaunchKernelGGL(coverage_poll_shared_kernel, pgrid, dim3(kBlock), 0, s,
+                               ctx->xys.as<double2>(), ctx->ws.as<double>(),
+                               ctx->off.as<int32_t>(), ctx->grid, L->disks.as<DiskRec>(),
+                               L->region.as<int4>(), L->nbr.as<uint16_t>(), L->ncount.as<int>(), N,
+                               K, d_mode, L->partial.as<double>());
             HCK(hipGetLastError());
         }
         prof_end();
@@ -641,7 +655,8 @@ void mac_ctx_destroy(mac_ctx* ctx)
     (void)hipDeviceSynchronize();
     for (Lane* l : ctx->lanes_all) {
         for (DevBuf* b : {&l->cands, &l->disks, &l->partial, &l->area, &l->obj, &l->best,
-                          &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->vp})
+                          &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->vp, &l->nbr,
+                          &l->ncount})
             b->release();
         if (l->ev_fork) (void)hipEventDestroy(l->ev_fork);
         if (l->ev_join) (void)hipEventDestroy(l->ev_join);
