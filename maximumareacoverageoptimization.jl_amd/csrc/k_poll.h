@@ -15,20 +15,25 @@
 // left out here and decided exactly by coverage_poll_shared_kernel (k_poll_shared.h); every
 // other entry of region i can only be credited to disk i.
 //
-// Exact fp32 filter. With o the region origin, u = px - ox, v = py - oy, cu = cx - ox,
-// cv = cy - oy: a = (u-cu)^2 + (v-cv)^2 = q - 2u*cu - 2v*cv + C, q = u^2 + v^2, C = cu^2 + cv^2.
-// Entries are staged as fp32 (u~, v~, q~); each test is t = fma(v~, -2cv~, fma(u~, -2cu~, q~))
-// compared with fp32 thresholds around T - C. With eps = 2^-24, |u|,|v| <= U (every staged
-// entry) and D = U + max(|cu|, |cv|): |t - (a - C)| <= 28.2 eps D^2 (q: 10 eps D^2, the two
-// products 8.04 eps D^2, the three roundings 10 eps D^2), while the fp64 reference value a64 and
-// the fp64 C differ from the real ones by < 2^-50 D^2. So with delta = 2^-18 D^2 (= 64 eps D^2):
-//     t <= RD32(T - C - delta)   =>  a64 <= T    covered, the reference decision
-//     t >  RU32(T - C + delta)   =>  a64 >  T    not covered
-//     otherwise (the band)       =>  decided in fp64 from the staged exact coordinates.
-// On the reference lattices the band is empty (a = n + 1/2 never lies within delta of T).
-// Non-finite entries (never covered) and shared entries are staged with q = +inf, so t = +inf
-// is never NaN and never under a threshold; a lane with D > 2^60 sends every entry to the exact
-// pass.
+// Exact fp32 filter. With o the region centre, x = px - ox, y = py - oy, cu = cx - ox,
+// cv = cy - oy (fp64; errors relative to these small offsets): the reference decision
+// a64 <= T (sqrt(a64) < r, predicate.h) is, up to fp64 noise, sign(T - A) with
+// T - A = (T - C) - (x^2 + y^2) + 2x*cu + 2y*cv, C = cu^2 + cv^2.
+// Entries are staged once as fp32 (U, V, Q = U^2 + V^2); each lane keeps, per candidate, a
+// power of two S and fp32 Sa = S*2cu, Sb = S*2cv, STm = S*fl32(T - C), and computes
+//     d' = fma(Q, -S, fma(V, Sb, fma(U, Sa, STm)))      ( = S*(T - A) + error )
+// With M = max(Umax, |cu|, |cv|, r) and eps = 2^-24 the error is below 38.1 eps M^2 * S
+// (staging of U, V, Q: 14.1, the fp32 constants: 6, the three fmas: 18), so with
+// X = RU32(2^-18 M^2) (= 64 eps M^2) and S = 2^k such that X' = S*X is in [1, 2):
+//     d' >  X'   =>  a64 <  T   covered         (then clamp(d') = 1 exactly)
+//     d' < -X'   =>  a64 >  T   not covered     (clamp(d') = 0)
+//     |d'| <= X' (the band)     => the lane re-decides the whole chunk, band entries in fp64.
+// The hot loop is therefore, per 2 entries x 2 candidates, six packed fmas, two packed clamps
+// (v_pk_add_f32 ... clamp), two packed adds and two v_min3 (the band detector): three VALU ops
+// per test. On the reference lattices the band is empty (|a - T| >= 1/2 >> X).
+// Non-finite and shared entries are staged with (0, 0, +inf): d' = -inf, never counted, never
+// in the band. A lane whose M is outside [2^-60, 2^60] is "forced": S = 1, X' = +inf, every
+// entry goes to the exact pass.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -83,11 +88,53 @@ __device__ __forceinline__ float f32_up(double v)
     return f;
 }
 
-// c + [t > T] computed as c + sign(T - t): t is never NaN, T never -0, and distinct floats never
-// subtract to zero, so the sign bit of T - t is exactly [t > T] (no compare, no VCC hazard).
-__device__ __forceinline__ uint32_t count_above(uint32_t c, float T, float t)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// clamp to [0, 1] of both halves in one packed op (d' > X' >= 1 -> 1, d' < 0 -> 0)
+__device__ __forceinline__ f32x2 clamp01x2(f32x2 x, f32x2 zero)
 {
-    return c + (__builtin_bit_cast(uint32_t, T - t) >> 31);
+    f32x2 r;
+    asm("v_pk_add_f32 %0, %1, %2 clamp" : "=v"(r) : "v"(x), "v"(zero));
+    return r;
+}
+
+__device__ __forceinline__ f32x2 fma2(float a, f32x2 b, f32x2 c)
+{
+    return __builtin_elementwise_fma((f32x2)a, b, c);
+}
+
+// Per-candidate constants of the scaled fp32 filter (see the header comment).
+struct PollLane {
+    float sa, sb, stm, ns, xp;   // S*2cu, S*2cv, S*fl32(T - C), -S, X'
+};
+
+__device__ __forceinline__ PollLane poll_lane(const DiskRec& d, double ox, double oy, double U)
+{
+    PollLane L;
+    const double cu = d.cx - ox, cv = d.cy - oy;
+    const double M = __builtin_fmax(__builtin_fmax(U, d.r),
+                                    __builtin_fmax(__builtin_fabs(cu), __builtin_fabs(cv)));
+    if (!(M <= 0x1p60 && M >= 0x1p-60)) {  // forced: everything to the exact pass
+        L.sa = L.sb = L.stm = 0.0f;
+        L.ns = -1.0f;
+        L.xp = __builtin_inff();
+        return L;
+    }
+    const float X = f32_up(M * M * 0x1p-18 + 0x1p-120);
+    const int ex = (int)((__builtin_bit_cast(uint32_t, X) >> 23) & 0xff) - 127;  // X normal
+    const double S = __builtin_ldexp(1.0, -ex);   // S*X in [1, 2)
+    const double C = cu * cu + cv * cv;
+    L.sa = (float)(2.0 * cu * S);
+    L.sb = (float)(2.0 * cv * S);
+    L.stm = (float)((d.T - C) * S);
+    L.ns = (float)(-S);
+    L.xp = (float)((double)X * S);
+    return L;
+}
+
+__device__ __forceinline__ float poll_dprime(const float4& e, const PollLane& L)
+{
+    return __builtin_fmaf(e.z, L.ns, __builtin_fmaf(e.y, L.sb, __builtin_fmaf(e.x, L.sa, L.stm)));
 }
 
 // Slice g: candidates [g*kPollKPB, min(K, (g+1)*kPollKPB)); lane t, pass u -> k = kb + u*256 + t.
@@ -100,12 +147,13 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
     const int* __restrict__ ncount, int N, int K, const int* __restrict__ mode,
     double* __restrict__ partial)
 {
+    static_assert(kPollKPL == 4, "the hot loop pairs candidates (0,1) and (2,3)");
     if (mode && *mode != kModePoll) return;
 #ifdef MAC_DIAG
     const uint64_t diag_t0 = __builtin_amdgcn_s_memrealtime();
     int diag_entries = 0;
 #endif
-    __shared__ float4 s32[kPollCH];    // (u~, v~, q~, 0); q~ = +inf for shared / non-finite
+    __shared__ float4 s32[kPollCH];    // (U, V, Q, 0); (0, 0, +inf) for shared / non-finite
     __shared__ double2 s64[kPollCH];   // exact coordinates (band decisions)
     __shared__ double sw[kPollCH];
     __shared__ int rs[kPollRB], rpre[kPollRB + 1];
@@ -132,44 +180,35 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
     }
     if (tid < min(nc, kPollNbr)) nbox[tid] = region[nbrT[i * kPollNbr + tid]];
 
-    // region origin and the bound U on every staged offset (entries of tile t satisfy
+    // region centre and the bound Umax on every staged offset (entries of tile t satisfy
     // t <= (p - g0)/S < t + 1 up to rounding; two tiles of slack absorb it)
-    const double ox = g.gx0 + (double)R.x * g.S;
-    const double oy = g.gy0 + (double)R.z * g.S;
-    const double U = (double)max(R.y - R.x, R.w - R.z) * g.S + 2.0 * g.S;
+    const double ox = g.gx0 + 0.5 * (double)(R.x + R.y + 1) * g.S;
+    const double oy = g.gy0 + 0.5 * (double)(R.z + R.w + 1) * g.S;
+    const double Umax = 0.5 * (double)max(R.y - R.x + 1, R.w - R.z + 1) * g.S + 2.0 * g.S;
 
-    float m2cx[kPollKPL], m2cy[kPollKPL], Tlo[kPollKPL], Thi[kPollKPL];
+    PollLane pl[kPollKPL];
     bool live[kPollKPL];
     double acc[kPollKPL];
 #pragma unroll
     for (int u = 0; u < kPollKPL; ++u) {
         acc[u] = 0.0;
         live[u] = false;
-        m2cx[u] = m2cy[u] = 0.0f;
-        Tlo[u] = Thi[u] = -__builtin_inff();
+        pl[u] = PollLane{0.0f, 0.0f, -1.0f, -1.0f, 0.5f};  // d' < -X' for every entry: inert
         if (kk[u] < 0) continue;
         const DiskRec d = disksT[(int64_t)i * K + kk[u]];
         int4 sp;
         if (!disk_span(d, g, sp)) continue;
         live[u] = true;
-        const double cu = d.cx - ox, cv = d.cy - oy;
-        const double D = U + __builtin_fmax(__builtin_fabs(cu), __builtin_fabs(cv));
-        if (!(D <= 0x1p60)) {  // keep fp32 far from overflow: exact pass for everything
-            Tlo[u] = -__builtin_inff();
-            Thi[u] = __builtin_inff();
-            continue;
-        }
-        const double C = cu * cu + cv * cv;
-        const double delta = D * D * 0x1p-18 + 0x1p-120;
-        m2cx[u] = (float)(-2.0 * cu);
-        m2cy[u] = (float)(-2.0 * cv);
-        Tlo[u] = f32_down(d.T - C - delta);
-        Thi[u] = f32_up(d.T - C + delta);
+        pl[u] = poll_lane(d, ox, oy, Umax);
     }
-    bool any_live = false;
-#pragma unroll
-    for (int u = 0; u < kPollKPL; ++u) any_live |= live[u];
-    const bool wave_live = __any(any_live);
+    // wave-uniform: which candidate pairs have any live lane in this wave
+    const bool pair0 = __any(live[0] || live[1]);
+    const bool pair1 = __any(live[2] || live[3]);
+    const f32x2 zero2 = {0.0f, 0.0f};
+    const f32x2 sa01 = {pl[0].sa, pl[1].sa}, sb01 = {pl[0].sb, pl[1].sb};
+    const f32x2 st01 = {pl[0].stm, pl[1].stm}, ns01 = {pl[0].ns, pl[1].ns};
+    const f32x2 sa23 = {pl[2].sa, pl[3].sa}, sb23 = {pl[2].sb, pl[3].sb};
+    const f32x2 st23 = {pl[2].stm, pl[3].stm}, ns23 = {pl[2].ns, pl[3].ns};
 
     for (int rb = R.z; rb <= R.w; rb += kPollRB) {
         const int nr = min(kPollRB, R.w - rb + 1);
@@ -214,71 +253,96 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
                 if (q == tid) wfirst = wj;
                 mixed |= __builtin_bit_cast(uint64_t, wj) != __builtin_bit_cast(uint64_t, wfirst);
             }
+            if (tid == 0 && (n & 1)) s32[n] = make_float4(0.0f, 0.0f, __builtin_inff(), 0.0f);
             __syncthreads();
             // weights identical across the chunk? (compare with entry 0 after staging)
             const uint64_t w0 = __builtin_bit_cast(uint64_t, sw[0]);
             mixed |= (tid < n) && __builtin_bit_cast(uint64_t, sw[tid]) != w0;
             const bool uniform = !__syncthreads_or(mixed);
 
-            if (wave_live) {
-                bool band[kPollKPL];
-                uint32_t nlo[kPollKPL], nhi[kPollKPL];
+            if (pair0 || pair1) {
+                float bmin[kPollKPL];
 #pragma unroll
-                for (int u = 0; u < kPollKPL; ++u) nlo[u] = nhi[u] = 0;
+                for (int u = 0; u < kPollKPL; ++u) bmin[u] = __builtin_inff();
+                double cw[kPollKPL];   // this chunk's credited weight per candidate
                 if (uniform) {
-                    // hot loop: per staged entry, kPollKPL tests of 2 FMAs + 2 sign-bit counts
+                    // hot loop: 2 entries x 2 candidates per step, 3 VALU ops per test
+                    f32x2 h01 = zero2, h23 = zero2;
+                    if (pair1) {
+#pragma unroll 2
+                        for (int q = 0; q < n; q += 2) {
+                            const float4 e0 = s32[q], e1 = s32[q + 1];
+                            const f32x2 a0 = fma2(e0.z, ns01, fma2(e0.y, sb01, fma2(e0.x, sa01, st01)));
+                            const f32x2 a1 = fma2(e1.z, ns01, fma2(e1.y, sb01, fma2(e1.x, sa01, st01)));
+                            const f32x2 b0 = fma2(e0.z, ns23, fma2(e0.y, sb23, fma2(e0.x, sa23, st23)));
+                            const f32x2 b1 = fma2(e1.z, ns23, fma2(e1.y, sb23, fma2(e1.x, sa23, st23)));
+                            h01 += clamp01x2(a0, zero2) + clamp01x2(a1, zero2);
+                            h23 += clamp01x2(b0, zero2) + clamp01x2(b1, zero2);
+                            bmin[0] = __builtin_fminf(bmin[0], __builtin_fminf(__builtin_fabsf(a0.x), __builtin_fabsf(a1.x)));
+                            bmin[1] = __builtin_fminf(bmin[1], __builtin_fminf(__builtin_fabsf(a0.y), __builtin_fabsf(a1.y)));
+                            bmin[2] = __builtin_fminf(bmin[2], __builtin_fminf(__builtin_fabsf(b0.x), __builtin_fabsf(b1.x)));
+                            bmin[3] = __builtin_fminf(bmin[3], __builtin_fminf(__builtin_fabsf(b0.y), __builtin_fabsf(b1.y)));
+                        }
+                    } else {
 #pragma unroll 4
-                    for (int q = 0; q < n; ++q) {
-                        const float4 e = s32[q];
-#pragma unroll
-                        for (int u = 0; u < kPollKPL; ++u) {
-                            const float t = __builtin_fmaf(e.y, m2cy[u], __builtin_fmaf(e.x, m2cx[u], e.z));
-                            nlo[u] = count_above(nlo[u], Tlo[u], t);
-                            nhi[u] = count_above(nhi[u], Thi[u], t);
+                        for (int q = 0; q < n; q += 2) {
+                            const float4 e0 = s32[q], e1 = s32[q + 1];
+                            const f32x2 a0 = fma2(e0.z, ns01, fma2(e0.y, sb01, fma2(e0.x, sa01, st01)));
+                            const f32x2 a1 = fma2(e1.z, ns01, fma2(e1.y, sb01, fma2(e1.x, sa01, st01)));
+                            h01 += clamp01x2(a0, zero2) + clamp01x2(a1, zero2);
+                            bmin[0] = __builtin_fminf(bmin[0], __builtin_fminf(__builtin_fabsf(a0.x), __builtin_fabsf(a1.x)));
+                            bmin[1] = __builtin_fminf(bmin[1], __builtin_fminf(__builtin_fabsf(a0.y), __builtin_fabsf(a1.y)));
                         }
                     }
-#pragma unroll
-                    for (int u = 0; u < kPollKPL; ++u) {
-                        const int clo = n - (int)nlo[u];
-                        if (clo) acc[u] += (double)clo * sw[0];
-                    }
+                    // counts < 2^24: exact in fp32 when no entry is in the band
+                    const double wu = sw[0];
+                    cw[0] = (double)h01.x * wu;
+                    cw[1] = (double)h01.y * wu;
+                    cw[2] = (double)h23.x * wu;
+                    cw[3] = (double)h23.y * wu;
                 } else {
-                    // weighted loop: the surely covered entries add their own weight
-#pragma unroll 2
+                    // weighted loop: covered entries add their own weight (clamp(d') is 0 or 1
+                    // off the band; a band chunk is recomputed below)
+#pragma unroll
+                    for (int u = 0; u < kPollKPL; ++u) cw[u] = 0.0;
                     for (int q = 0; q < n; ++q) {
                         const float4 e = s32[q];
                         const double wq = sw[q];
 #pragma unroll
                         for (int u = 0; u < kPollKPL; ++u) {
-                            const float t = __builtin_fmaf(e.y, m2cy[u], __builtin_fmaf(e.x, m2cx[u], e.z));
-                            const uint32_t a = count_above(0u, Tlo[u], t);
-                            acc[u] += a ? 0.0 : wq;
-                            nlo[u] += a;
-                            nhi[u] = count_above(nhi[u], Thi[u], t);
+                            const float d = poll_dprime(e, pl[u]);
+                            cw[u] += d > 0.0f ? wq : 0.0;
+                            bmin[u] = __builtin_fminf(bmin[u], __builtin_fabsf(d));
                         }
                     }
                 }
-#pragma unroll
-                for (int u = 0; u < kPollKPL; ++u) band[u] = nhi[u] != nlo[u];
-                // exact fp64 decisions for the band entries (rare; never on reference lattices).
-                // Shared and non-finite entries have t = +inf: never in the band unless the lane
-                // is fp32-disabled (Thi = +inf), and then the exact test rejects non-finite ones
-                // while shared ones are skipped here (decided by the shared kernel).
+                // band: the lane re-decides this chunk; entries with |d'| <= X' in fp64.
+                // Shared entries (q = +inf, d' = -inf) are skipped: the shared kernel owns them;
+                // for a forced lane (X' = +inf) they are told apart from non-finite ones here.
 #pragma unroll
                 for (int u = 0; u < kPollKPL; ++u) {
-                    if (!band[u]) continue;
-                    const DiskRec d = disksT[(int64_t)i * K + kk[u]];
-                    for (int q = 0; q < n; ++q) {
-                        const float4 e = s32[q];
-                        const float t = __builtin_fmaf(e.y, m2cy[u], __builtin_fmaf(e.x, m2cx[u], e.z));
-                        if (!(t > Tlo[u] && t <= Thi[u])) continue;
-                        const double2 p = s64[q];
-                        if (e.z == __builtin_inff() && nc > 0 &&
-                            entry_shared(nc, nbox, tile_of(p.x, g.gx0, g.invS, g.nTx),
-                                         tile_of(p.y, g.gy0, g.invS, g.nTy)))
-                            continue;
-                        if (sqdist(p.x, p.y, d.cx, d.cy) <= d.T) acc[u] += sw[q];
+                    if (live[u] && bmin[u] <= pl[u].xp) {
+                        const DiskRec d = disksT[(int64_t)i * K + kk[u]];
+                        double c = 0.0;
+                        for (int q = 0; q < n; ++q) {
+                            const float4 e = s32[q];
+                            const float dp = poll_dprime(e, pl[u]);
+                            bool cov;
+                            if (__builtin_fabsf(dp) <= pl[u].xp) {
+                                const double2 p = s64[q];
+                                if (e.z == __builtin_inff() && nc > 0 &&
+                                    entry_shared(nc, nbox, tile_of(p.x, g.gx0, g.invS, g.nTx),
+                                                 tile_of(p.y, g.gy0, g.invS, g.nTy)))
+                                    continue;
+                                cov = sqdist(p.x, p.y, d.cx, d.cy) <= d.T;
+                            } else {
+                                cov = dp > 0.0f;
+                            }
+                            if (cov) c += sw[q];
+                        }
+                        cw[u] = c;
                     }
+                    if (live[u]) acc[u] += cw[u];
                 }
             }
             __syncthreads();

@@ -18,6 +18,8 @@
 
 namespace mac {
 
+constexpr int kSharedWG = 64;  // workgroups per candidate slice walking the disks-with-neighbours list
+
 __device__ __forceinline__ bool box_overlap(const int4& a, const int4& b)
 {
     return a.x <= a.y && a.x <= b.y && b.x <= a.y && a.z <= b.w && b.z <= a.w;
@@ -29,10 +31,14 @@ __device__ __forceinline__ bool box_has(const int4& b, int tx, int ty)
 }
 
 // Block i: the disks j < i whose region boxes overlap region i's (at most kPollNbr kept in
-// nbr[i*kPollNbr ...]; ncount[i] is the true count, > kPollNbr meaning "overflowed").
+// nbr[i*kPollNbr ...]; ncount[i] is the true count, > kPollNbr meaning "overflowed"). Disks
+// with neighbours are appended to dlist (order irrelevant: each is processed independently);
+// *dcount must be zero on entry (decide_kernel clears it).
 __global__ __launch_bounds__(kBlock) void neighbors_kernel(const int4* __restrict__ region, int N,
                                                            uint16_t* __restrict__ nbr,
-                                                           int* __restrict__ ncount)
+                                                           int* __restrict__ ncount,
+                                                           int* __restrict__ dlist,
+                                                           int* __restrict__ dcount)
 {
     __shared__ int cnt;
     const int i = blockIdx.x;
@@ -49,7 +55,10 @@ __global__ __launch_bounds__(kBlock) void neighbors_kernel(const int4* __restric
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) ncount[i] = cnt;
+    if (threadIdx.x == 0) {
+        ncount[i] = cnt;
+        if (cnt > 0) dlist[atomicAdd(dcount, 1)] = i;
+    }
 }
 
 // Entry (tile tx, ty) of region i is shared when it lies in a neighbour's box.
@@ -61,21 +70,20 @@ __device__ __forceinline__ bool entry_shared(int nc, const int4* nbox, int tx, i
     return s;
 }
 
-// Same grid as coverage_poll_kernel (disk i, slice of kPollKPB candidates); returns at once for
-// disks without neighbours. Shared entries are compacted (in list order) into LDS round by
-// round; each lane then decides them for its candidates with the neighbour disks preloaded.
+// Grid (kSharedWG, ceil(K/256)): workgroup (b, y) handles candidates [256y, 256y + 256) of the
+// disks dlist[b], dlist[b + kSharedWG], ...; one candidate per lane. Shared entries are
+// compacted (in list order) into LDS round by round and decided in fp64; the neighbour disks
+// of the lane's candidate are preloaded (first four) or read once per round (the rest).
 __global__ __launch_bounds__(kBlock) void coverage_poll_shared_kernel(
     const double2* __restrict__ xy, const double* __restrict__ w,
     const int32_t* __restrict__ off, Grid g, const DiskRec* __restrict__ disksT,
     const int4* __restrict__ region, const uint16_t* __restrict__ nbrT,
-    const int* __restrict__ ncount, int N, int K, const int* __restrict__ mode,
-    double* __restrict__ partial)
+    const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
+    int N, int K, const int* __restrict__ mode, double* __restrict__ partial)
 {
     if (mode && *mode != kModePoll) return;
-    const int i = blockIdx.x;
-    const int nc = ncount[i];
-    const int4 R = region[i];
-    if (nc == 0 || R.x > R.y) return;  // uniform across the block
+    const int nd = *dcount;
+    if ((int)blockIdx.x >= nd) return;  // uniform
 
     __shared__ double2 sp[kBlock];
     __shared__ double sw[kBlock];
@@ -85,81 +93,85 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_shared_kernel(
     __shared__ int wcount[kWavesPerBlock];
 
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
-    const int ncl = min(nc, kPollNbr);
-    if (tid < ncl) {
-        nbr[tid] = nbrT[i * kPollNbr + tid];
-        nbox[tid] = region[nbr[tid]];
-    }
-    const int kb = blockIdx.y * kPollKPB;
-    const int ke = min(K, kb + kPollKPB);
-    constexpr int KPL = kPollKPB / kBlock;
-    double acc[KPL];
-#pragma unroll
-    for (int u = 0; u < KPL; ++u) acc[u] = 0.0;
-    __syncthreads();
+    const int k = blockIdx.y * kBlock + tid;
+    const bool valid = k < K;
 
-    for (int rb = R.z; rb <= R.w; rb += kPollRB) {
-        const int nr = min(kPollRB, R.w - rb + 1);
-        if (tid < nr) {
-            const int64_t rowbase = (int64_t)(rb + tid) * g.nTx;
-            const int s = off[rowbase + R.x];
-            rs[tid] = s;
-            rpre[tid + 1] = off[rowbase + R.y + 1] - s;
+    for (int di = blockIdx.x; di < nd; di += gridDim.x) {
+        const int i = dlist[di];
+        const int nc = ncount[i];
+        const int ncl = min(nc, kPollNbr);
+        const int4 R = region[i];
+        __syncthreads();  // LDS reuse across disks
+        if (tid < ncl) {
+            nbr[tid] = nbrT[i * kPollNbr + tid];
+            nbox[tid] = region[nbr[tid]];
         }
-        __syncthreads();
-        if (tid == 0) {
-            rpre[0] = 0;
-            for (int r = 0; r < nr; ++r) rpre[r + 1] += rpre[r];
-        }
-        __syncthreads();
-        const int total = rpre[nr];
-        for (int base = 0; base < total; base += kBlock) {
-            // this round's entries (one per thread), shared ones compacted in list order
-            const int f = base + tid;
-            bool shared = false;
-            double2 p = make_double2(0.0, 0.0);
-            double ww = 0.0;
-            if (f < total) {
-                int lo = 0, hi = nr - 1;
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (rpre[mid] <= f) lo = mid; else hi = mid - 1;
-                }
-                const int j = rs[lo] + (f - rpre[lo]);
-                p = xy[j];
-                ww = w[j];
-                shared = entry_shared(nc, nbox, tile_of(p.x, g.gx0, g.invS, g.nTx), rb + lo);
-            }
-            const uint64_t bal = __ballot(shared);
-            if (lane == 0) wcount[wid] = __popcll(bal);
-            __syncthreads();
-            int pos = __popcll(bal & ((1ull << lane) - 1)), ns = 0;
-            for (int q = 0; q < kWavesPerBlock; ++q) {
-                if (q < wid) pos += wcount[q];
-                ns += wcount[q];
-            }
-            if (shared) {
-                sp[pos] = p;
-                sw[pos] = ww;
-            }
-            __syncthreads();
-            if (ns) {
-                for (int u = 0; u < KPL; ++u) {
-                    const int k = kb + u * kBlock + tid;
-                    if (k >= ke) continue;
-                    const DiskRec d = disksT[(int64_t)i * K + k];
-                    if (!(d.T >= 0.0)) continue;
-                    DiskRec e[4];
+        DiskRec d = DiskRec{0.0, 0.0, -1.0, 0.0};
+        DiskRec e[4];
 #pragma unroll
-                    for (int m = 0; m < 4; ++m)
-                        e[m] = m < ncl ? disksT[(int64_t)nbr[m] * K + k] : DiskRec{0.0, 0.0, -1.0, 0.0};
+        for (int m = 0; m < 4; ++m) e[m] = DiskRec{0.0, 0.0, -1.0, 0.0};
+        if (valid) {
+            d = disksT[(int64_t)i * K + k];
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                if (m < ncl) e[m] = disksT[(int64_t)nbrT[i * kPollNbr + m] * K + k];
+        }
+        double acc = 0.0;
+        __syncthreads();
+
+        for (int rb = R.z; rb <= R.w; rb += kPollRB) {
+            const int nr = min(kPollRB, R.w - rb + 1);
+            if (tid < nr) {
+                const int64_t rowbase = (int64_t)(rb + tid) * g.nTx;
+                const int s = off[rowbase + R.x];
+                rs[tid] = s;
+                rpre[tid + 1] = off[rowbase + R.y + 1] - s;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                rpre[0] = 0;
+                for (int r = 0; r < nr; ++r) rpre[r + 1] += rpre[r];
+            }
+            __syncthreads();
+            const int total = rpre[nr];
+            for (int base = 0; base < total; base += kBlock) {
+                // this round's entries (one per thread), shared ones compacted in list order
+                const int f = base + tid;
+                bool shared = false;
+                double2 p = make_double2(0.0, 0.0);
+                double ww = 0.0;
+                if (f < total) {
+                    int lo = 0, hi = nr - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (rpre[mid] <= f) lo = mid; else hi = mid - 1;
+                    }
+                    const int j = rs[lo] + (f - rpre[lo]);
+                    p = xy[j];
+                    ww = w[j];
+                    shared = entry_shared(nc, nbox, tile_of(p.x, g.gx0, g.invS, g.nTx), rb + lo);
+                }
+                const uint64_t bal = __ballot(shared);
+                if (lane == 0) wcount[wid] = __popcll(bal);
+                __syncthreads();
+                int pos = __popcll(bal & ((1ull << lane) - 1)), ns = 0;
+                for (int q = 0; q < kWavesPerBlock; ++q) {
+                    if (q < wid) pos += wcount[q];
+                    ns += wcount[q];
+                }
+                if (shared) {
+                    sp[pos] = p;
+                    sw[pos] = ww;
+                }
+                __syncthreads();
+                if (valid && d.T >= 0.0) {
                     for (int s = 0; s < ns; ++s) {
                         const double2 q = sp[s];
                         if (!(sqdist(q.x, q.y, d.cx, d.cy) <= d.T)) continue;
                         bool stolen = false;
 #pragma unroll
                         for (int m = 0; m < 4; ++m)
-                            stolen |= sqdist(q.x, q.y, e[m].cx, e[m].cy) <= e[m].T;
+                            if (m < ncl) stolen |= sqdist(q.x, q.y, e[m].cx, e[m].cy) <= e[m].T;
                         if (!stolen && nc > 4) {
                             if (nc <= kPollNbr) {
                                 for (int m = 4; m < nc && !stolen; ++m) {
@@ -174,17 +186,13 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_shared_kernel(
                                 }
                             }
                         }
-                        if (!stolen) acc[u] += sw[s];
+                        if (!stolen) acc += sw[s];
                     }
                 }
+                __syncthreads();
             }
-            __syncthreads();
         }
-    }
-#pragma unroll
-    for (int u = 0; u < KPL; ++u) {
-        const int k = kb + u * kBlock + tid;
-        if (k < ke) partial[(int64_t)i * K + k] += acc[u];
+        if (valid) partial[(int64_t)i * K + k] += acc;
     }
 }
 

@@ -95,6 +95,7 @@ __global__ __launch_bounds__(kBlock) void region_kernel(const DiskRec* __restric
 
 // One block: mode = poll walk when its point-visits stay within `ratio` x the per-candidate
 // walk's (its visits are broadcast LDS reads; the other's are scattered global loads).
+// mode[1] (the poll walk's disks-with-neighbours counter) is cleared here.
 __global__ __launch_bounds__(kBlock) void decide_kernel(const double2* __restrict__ cost, int N,
                                                         double ratio, int forced,
                                                         int* __restrict__ mode)
@@ -108,7 +109,10 @@ __global__ __launch_bounds__(kBlock) void decide_kernel(const double2* __restric
     const double A = block_sum_f64(a, red);
     __syncthreads();
     const double B = block_sum_f64(b, red);
-    if (threadIdx.x == 0) *mode = forced ? forced : (A <= ratio * B ? kModePoll : kModeTiled);
+    if (threadIdx.x == 0) {
+        mode[0] = forced ? forced : (A <= ratio * B ? kModePoll : kModeTiled);
+        mode[1] = 0;
+    }
 }
 
 }  // namespace mac

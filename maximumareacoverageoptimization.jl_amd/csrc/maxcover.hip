@@ -96,7 +96,7 @@ struct Lane {
     hipStream_t last = nullptr;   // stream of the most recent use
     hipEvent_t done = nullptr;
     DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode, vp, nbr,
-        ncount;
+        ncount, dlist;
     hipStream_t aux = nullptr;                 // forked stream for the penalty kernel
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::vector<double> h_dlim;
@@ -418,18 +418,20 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_c
         if (poll_possible) {
             L->region.reserve(sizeof(int4) * N);
             L->cost.reserve(sizeof(double2) * N);
-            L->mode.reserve(sizeof(int));
+            L->mode.reserve(2 * sizeof(int));  // [0] walk, [1] disks-with-neighbours count
             hipLaunchKernelGGL(region_kernel, dim3(N), dim3(kBlock), 0, s, L->disks.as<DiskRec>(),
                                N, K, ctx->grid, L->region.as<int4>(), L->cost.as<double2>());
-            HCK(hipGetLastError());
-            L->nbr.reserve(sizeof(uint16_t) * (size_t)N * kPollNbr);
-            L->ncount.reserve(sizeof(int) * (size_t)N);
-            hipLaunchKernelGGL(neighbors_kernel, dim3(N), dim3(kBlock), 0, s, L->region.as<int4>(),
-                               N, L->nbr.as<uint16_t>(), L->ncount.as<int>());
             HCK(hipGetLastError());
             const int forced = ctx->algo == MAC_ALGO_POLL ? kModePoll : 0;
             hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(kBlock), 0, s, L->cost.as<double2>(), N,
                                kPollCostRatio, forced, L->mode.as<int>());
+            HCK(hipGetLastError());
+            L->nbr.reserve(sizeof(uint16_t) * (size_t)N * kPollNbr);
+            L->ncount.reserve(sizeof(int) * (size_t)N);
+            L->dlist.reserve(sizeof(int) * (size_t)N);
+            hipLaunchKernelGGL(neighbors_kernel, dim3(N), dim3(kBlock), 0, s, L->region.as<int4>(),
+                               N, L->nbr.as<uint16_t>(), L->ncount.as<int>(), L->dlist.as<int>(),
+                               L->mode.as<int>() + 1);
             HCK(hipGetLastError());
             d_mode = L->mode.as<int>();
         }
@@ -450,11 +452,13 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_c
                                L->region.as<int4>(), L->nbr.as<uint16_t>(), L->ncount.as<int>(), N,
                                K, d_mode, L->partial.as<double>());
             HCK(hipGetLastError());
-            hipLaunchKernelGGL(coverage_poll_shared_kernel, pgrid, dim3(kBlock), 0, s,
+            const dim3 sgrid(std::min(N, kSharedWG), (K + kBlock - 1) / kBlock);
+            hipLaunchKernelGGL(coverage_poll_shared_kernel, sgrid, dim3(kBlock), 0, s,
                                ctx->xys.as<double2>(), ctx->ws.as<double>(),
                                ctx->off.as<int32_t>(), ctx->grid, L->disks.as<DiskRec>(),
-                               L->region.as<int4>(), L->nbr.as<uint16_t>(), L->ncount.as<int>(), N,
-                               K, d_mode, L->partial.as<double>());
+                               L->region.as<int4>(), L->nbr.as<uint16_t>(), L->ncount.as<int>(),
+                               L->dlist.as<int>(), L->mode.as<int>() + 1, N, K, d_mode,
+                               L->partial.as<double>());
             HCK(hipGetLastError());
         }
         prof_end();
@@ -656,7 +660,7 @@ void mac_ctx_destroy(mac_ctx* ctx)
     for (Lane* l : ctx->lanes_all) {
         for (DevBuf* b : {&l->cands, &l->disks, &l->partial, &l->area, &l->obj, &l->best,
                           &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->vp, &l->nbr,
-                          &l->ncount})
+                          &l->ncount, &l->dlist})
             b->release();
         if (l->ev_fork) (void)hipEventDestroy(l->ev_fork);
         if (l->ev_join) (void)hipEventDestroy(l->ev_join);

@@ -326,12 +326,32 @@ def test_config4_full_poll(ctx, pkg, orc):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("case", ["real_clustered", "big_radius", "mixed_weights"])
+@pytest.mark.parametrize("case", ["real_clustered", "big_radius", "mixed_weights", "pythagorean"])
 def test_poll_walk_stress(ctx, pkg, orc, case):
     """The poll walk's rare paths: fp64 band decisions on real-valued coordinates, ownership
-    between overlapping disks, regions larger than one LDS chunk and more than 64 tile rows."""
+    between overlapping disks, regions larger than one LDS chunk and more than 64 tile rows.
+    "pythagorean": integer points at distance exactly r from integer centres (3-4-5, 5-12-13,
+    7-24-25 ...), where a = r^2 sits next to the threshold T(r) < r^2: every such entry is in
+    the fp32 filter's band and must be decided in fp64 (not covered: sqrt(r^2) < r is false)."""
     wl = pkg.workloads
     rng = wl.SplitMix64(4242 + len(case))
+    if case == "pythagorean":
+        g = np.arange(200, dtype=np.float64)
+        x = np.repeat(g, 200)
+        y = np.tile(g, 200)
+        w = np.full(x.size, 25.0)
+        N = 20
+        radii = np.array([5.0, 10.0, 13.0, 25.0, 15.0, 17.0])
+        x0 = np.concatenate([np.floor(rng.uniform(N) * 120) + 40, np.floor(rng.uniform(N) * 120) + 40,
+                             radii[np.floor(rng.uniform(N) * radii.size).astype(int)]])
+        ctx.set_points(x, y, w)
+        C = np.concatenate([x0[None, :], wl.poll_candidates(x0, rng, ell=1)], axis=0)
+        C[:, 2 * N:] = np.maximum(C[:, 2 * N:], 1.0)
+        want = orc.PointerList(recs(x, y, w)).area_batch(C)
+        r = both(ctx, lambda: ctx.area_batch(C))
+        for a, got in r.items():
+            assert np.array_equal(got, want), (a, np.flatnonzero(got != want)[:5])
+        return
     if case == "big_radius":
         x, y, w = wl.grid_points(240)
         N = 6
