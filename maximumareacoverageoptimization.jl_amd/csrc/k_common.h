@@ -19,6 +19,8 @@ constexpr int kPollRB = 64;        // poll walk: region rows per batch
 constexpr int kPollNbr = 64;       // poll walk: lower-index overlapping regions kept
 constexpr int kPollKPL = 4;        // poll walk: candidates per lane
 constexpr int kPollKPB = kBlock * kPollKPL;  // poll walk: candidates per workgroup (at most)
+constexpr int kSharedWG = 32;      // poll walk: disk strides of the shared-entry workgroups
+constexpr int kPollShB = kSharedWG * kPollKPL;  // poll walk: shared-entry workgroups per slice
 
 constexpr int kModePoll = 1;
 constexpr int kModeTiled = 2;

@@ -11,68 +11,76 @@
 
 namespace mac {
 
-constexpr int kPenC = 64;   // candidates per penalty block
-constexpr int kPenT = 64;   // UAV indices per LDS tile
 constexpr int kFinC = 16;   // candidates per finalize block (x 16 slice groups)
+constexpr int kMaxMaskWords = (65535 + 31) / 32;   // N <= 65535 (mac_* argument check)
 
-// vp_k = violation_k * penalty with violation_k = sum_{i=0..N-1} |x[2N+i] - rmax[i]| accumulated
-// SEQUENTIALLY in i from 0.0 (src/TDM_STATIC_opt.jl:89-97, bit-exact), or +inf when candidate k
-// fails cons3 (src/TDM_Constraints.jl:54-75; prev != null; sqrt(s) > d_lim[i] evaluated exactly
-// as s > dlimT[i], predicate.h), so -area + vp is the reference objective or +inf (the extreme
-// barrier never evaluates it). Block = 64 candidates: their columns are staged through LDS in
-// 64 x 64 tiles (coalesced reads); lane k of wave 0 runs the sequential chain over its tile row.
-// Independent of the coverage walk: runs on a forked stream beside it.
-__global__ __launch_bounds__(kBlock) void penalty_kernel(
-    int K, const double* __restrict__ cands, int N, int ldc, const double* __restrict__ rmax,
-    double penalty, const double* __restrict__ prev, const double* __restrict__ dlimT,
-    double tan_half_fov, double* __restrict__ vp)
+// Sequential objective penalty of candidate k (src/TDM_STATIC_opt.jl:89-97): violation =
+// sum_{i=0..N-1} pen[i*K + k] accumulated IN ORDER from 0.0 (bit-exact with the reference's
+// loop); vp = violation * penalty, or +inf when a term is negative (cons3 fails,
+// src/TDM_Constraints.jl:54-75: the extreme barrier never evaluates the objective). The chain is
+// latency-bound (N dependent adds), so loads run kChainB ahead; lanes are consecutive
+// candidates (coalesced). Used by the poll kernel's leading workgroups (overlapping the walk)
+// and by penalty_chain_kernel on the other paths.
+constexpr int kChainB = 32;
+__device__ __forceinline__ void penalty_chain(const double* __restrict__ pen, int K, int N, int k,
+                                              double penalty, double* __restrict__ vp)
 {
-    __shared__ double tile[kPenC][kPenT + 1];
-    __shared__ int infeas[kPenC];
-    const int t = threadIdx.x, lane = t & (kWave - 1), grp = t / kWave;
-    const int k0 = blockIdx.x * kPenC;
-    const int k = k0 + lane;
-    if (t < kPenC) infeas[t] = 0;
     double violation = 0.0;
-    for (int i0 = 0; i0 < N; i0 += kPenT) {
-        const int ni = min(kPenT, N - i0);
-        __syncthreads();
-        for (int e = t; e < kPenC * kPenT; e += kBlock) {
-            const int c = e / kPenT, ii = e % kPenT, kc = k0 + c;
-            if (kc >= K || ii >= ni) continue;
-            const double* x = cands + (int64_t)kc * ldc;
-            const int i = i0 + ii;
-            tile[c][ii] = rmax ? __builtin_fabs(x[2 * N + i] - rmax[i]) : 0.0;
-            if (prev) {
-                const double x1 = prev[i], y1 = prev[N + i], z1 = prev[2 * N + i] / tan_half_fov;
-                const double x2 = x[i], y2 = x[N + i], z2 = x[2 * N + i] / tan_half_fov;
-                const double ddx = x1 - x2, ddy = y1 - y2, ddz = z1 - z2;
-                const double s = ddx * ddx + ddy * ddy + ddz * ddz;
-                if (s > dlimT[i]) infeas[c] = 1;  // benign race: every writer stores 1
-            }
+    bool infeasible = false;
+    int i = 0;
+    for (; i + kChainB <= N; i += kChainB) {
+        double v[kChainB];
+#pragma unroll
+        for (int j = 0; j < kChainB; ++j) v[j] = pen[(int64_t)(i + j) * K + k];
+#pragma unroll
+        for (int j = 0; j < kChainB; ++j) {
+            infeasible |= v[j] < 0.0;
+            violation += v[j];
         }
-        __syncthreads();
-        if (grp == 0 && k < K)
-            for (int ii = 0; ii < ni; ++ii) violation += tile[lane][ii];
     }
-    __syncthreads();
-    if (grp == 0 && k < K) vp[k] = infeas[lane] ? __builtin_inf() : violation * penalty;
+    for (; i < N; ++i) {
+        const double v = pen[(int64_t)i * K + k];
+        infeasible |= v < 0.0;
+        violation += v;
+    }
+    vp[k] = infeasible ? __builtin_inf() : violation * penalty;
+}
+
+__global__ __launch_bounds__(kBlock) void penalty_chain_kernel(const double* __restrict__ pen, int K,
+                                                               int N, double penalty,
+                                                               double* __restrict__ vp)
+{
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k < K) penalty_chain(pen, K, N, k, penalty, vp);
 }
 
 // Block = 16 candidates x 16 slice groups. area_k = sum over slices g of partial[g*K + k] in a
 // fixed order (thread (c, sg) sums g = sg, sg+16, ... into 4 interleaved accumulators combined
 // in order, then the 16 groups in order): bit-reproducible, loads kept in flight. The slice
-// count is n_poll when *mode == poll, else n_other. obj_k = -area_k + vp_k when vp != null.
+// count is n_poll when *mode == poll, else n_other. With spart != null and the poll walk chosen,
+// the shared-entry rows spart[i*K + k] of the disks with ncount[i] > 0 are added too (ascending
+// i within each slice group: fixed order). obj_k = -area_k + vp_k when obj_out != null.
 __global__ __launch_bounds__(kBlock) void finalize_kernel(
     const double* __restrict__ partial, const int* __restrict__ mode, int n_poll, int n_other,
-    int K, const double* __restrict__ vp, double* __restrict__ area_out,
-    double* __restrict__ obj_out)
+    int K, int N, const double* __restrict__ spart, const int* __restrict__ ncount,
+    const double* __restrict__ vp, double* __restrict__ area_out, double* __restrict__ obj_out)
 {
     __shared__ double red[kBlock / kFinC][kFinC];
+    __shared__ uint32_t smask[kMaxMaskWords];   // disks whose shared-entry row exists
     const int t = threadIdx.x, c = t % kFinC, sg = t / kFinC;
     constexpr int SG = kBlock / kFinC;
-    const int k = blockIdx.x * kFinC + c;
+    const int k0 = blockIdx.x * kFinC;
+    const int k = k0 + c;
     const int G = (mode && *mode == kModePoll) ? n_poll : n_other;
+    const bool rows = spart && mode && *mode == kModePoll;
+    if (rows) {
+        const int nw = (N + 31) / 32;
+        for (int q = t; q < nw; q += kBlock) smask[q] = 0u;
+        __syncthreads();
+        for (int i = t; i < N; i += kBlock)
+            if (ncount[i] > 0) atomicOr(&smask[i >> 5], 1u << (i & 31));
+        __syncthreads();
+    }
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
     if (k < K) {
         int g = sg;
@@ -83,8 +91,13 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(
             a3 += partial[(int64_t)(g + 3 * SG) * K + k];
         }
         for (; g < G; g += SG) a0 += partial[(int64_t)g * K + k];
+        // poll walk: the shared-entry rows of the disks that have lower-index neighbours
+        if (rows)
+            for (int i = sg; i < N; i += SG)
+                if (smask[i >> 5] & (1u << (i & 31))) a3 += spart[(int64_t)i * K + k];
     }
     red[sg][c] = ((a0 + a1) + a2) + a3;
+
     __syncthreads();
     if (sg == 0 && k < K) {
         double area = 0.0;

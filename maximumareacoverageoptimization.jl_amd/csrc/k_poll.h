@@ -42,6 +42,7 @@
 #include "predicate.h"
 #include "k_common.h"
 #include "k_poll_shared.h"
+#include "k_final.h"
 
 #pragma clang fp contract(off)
 
@@ -137,18 +138,39 @@ __device__ __forceinline__ float poll_dprime(const float4& e, const PollLane& L)
     return __builtin_fmaf(e.z, L.ns, __builtin_fmaf(e.y, L.sb, __builtin_fmaf(e.x, L.sa, L.stm)));
 }
 
-// Slice g: candidates [g*kPollKPB, min(K, (g+1)*kPollKPB)); lane t, pass u -> k = kb + u*256 + t.
-// partial[i*K + k] = weight of the non-shared entries credited to disk i of candidate k.
-// Runs when mode == null or *mode == kModePoll.
+// Grid (n_chain + kPollShB + N, slices); roles by x, in dispatch order (the first ones overlap
+// the walk): x < n_chain (row 0): objective-penalty chains of candidates [256x, 256x + 256)
+// into vp (k_final.h), whatever the walk; then, when *mode == kModePoll (or mode == null),
+// kPollShB workgroups deciding the shared entries into spart, and one workgroup per (disk i,
+// slice g): candidates [g*kPollKPB, min(K, (g+1)*kPollKPB)), lane t, pass u -> k = kb + u*256 +
+// t, partial[i*K + k] = weight of the non-shared entries credited to disk i of candidate k.
 __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
     const double2* __restrict__ xy, const double* __restrict__ w,
     const int32_t* __restrict__ off, Grid g, const DiskRec* __restrict__ disksT,
     const int4* __restrict__ region, const uint16_t* __restrict__ nbrT,
-    const int* __restrict__ ncount, int N, int K, const int* __restrict__ mode,
-    double* __restrict__ partial)
+    const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
+    int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
+    double* __restrict__ spart, int n_chain, const double* __restrict__ pen, double penalty,
+    double* __restrict__ vp)
 {
     static_assert(kPollKPL == 4, "the hot loop pairs candidates (0,1) and (2,3)");
+    if ((int)blockIdx.x < n_chain) {  // first: the objective-penalty chains (any walk)
+        const int k = blockIdx.x * kBlock + threadIdx.x;
+        if (blockIdx.y == 0 && k < K) penalty_chain(pen, K, N, k, penalty, vp);
+        return;
+    }
+    const int bx = blockIdx.x - n_chain;
     if (mode && *mode != kModePoll) return;
+    if (bx < kPollShB) {  // then: the shared entries (k_poll_shared.h)
+        const int kb0 = blockIdx.y * kPollKPB;
+        const int kbs = kb0 + (bx % kPollKPL) * kBlock;
+        const int ke0 = min(K, kb0 + kPollKPB);
+        const int nd = *dcount;
+        if (kbs < ke0 && bx / kPollKPL < nd)
+            poll_shared_block(xy, w, off, g, disksT, region, nbrT, ncount, dlist, nd,
+                              bx / kPollKPL, K, kbs, ke0, spart);
+        return;
+    }
 #ifdef MAC_DIAG
     const uint64_t diag_t0 = __builtin_amdgcn_s_memrealtime();
     int diag_entries = 0;
@@ -159,7 +181,7 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
     __shared__ int rs[kPollRB], rpre[kPollRB + 1];
     __shared__ int4 nbox[kPollNbr];
 
-    const int i = blockIdx.x;
+    const int i = bx - kPollShB;
     const int tid = threadIdx.x;
     const int kb = blockIdx.y * kPollKPB;
     const int ke = min(K, kb + kPollKPB);

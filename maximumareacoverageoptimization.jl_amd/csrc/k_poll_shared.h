@@ -18,8 +18,6 @@
 
 namespace mac {
 
-constexpr int kSharedWG = 64;  // workgroups per candidate slice walking the disks-with-neighbours list
-
 __device__ __forceinline__ bool box_overlap(const int4& a, const int4& b)
 {
     return a.x <= a.y && a.x <= b.y && b.x <= a.y && a.z <= b.w && b.z <= a.w;
@@ -70,21 +68,18 @@ __device__ __forceinline__ bool entry_shared(int nc, const int4* nbox, int tx, i
     return s;
 }
 
-// Grid (kSharedWG, ceil(K/256)): workgroup (b, y) handles candidates [256y, 256y + 256) of the
-// disks dlist[b], dlist[b + kSharedWG], ...; one candidate per lane. Shared entries are
-// compacted (in list order) into LDS round by round and decided in fp64; the neighbour disks
-// of the lane's candidate are preloaded (first four) or read once per round (the rest).
-__global__ __launch_bounds__(kBlock) void coverage_poll_shared_kernel(
+// Shared-entry pass of one workgroup of the poll kernel (k_poll.h): candidates
+// [kb, kb + 256) one per lane (k < ke), disks dlist[b], dlist[b + kSharedWG], ... Shared entries
+// are compacted (in list order) into LDS round by round and decided in fp64; the neighbour
+// disks of the lane's candidate are preloaded (first four) or read once per entry (the rest).
+// Writes spart[i*K + k] (the finalize kernel adds the rows of disks with ncount[i] > 0).
+__device__ __forceinline__ void poll_shared_block(
     const double2* __restrict__ xy, const double* __restrict__ w,
-    const int32_t* __restrict__ off, Grid g, const DiskRec* __restrict__ disksT,
+    const int32_t* __restrict__ off, const Grid& g, const DiskRec* __restrict__ disksT,
     const int4* __restrict__ region, const uint16_t* __restrict__ nbrT,
-    const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
-    int N, int K, const int* __restrict__ mode, double* __restrict__ partial)
+    const int* __restrict__ ncount, const int* __restrict__ dlist, int nd, int b, int K,
+    int kb, int ke, double* __restrict__ spart)
 {
-    if (mode && *mode != kModePoll) return;
-    const int nd = *dcount;
-    if ((int)blockIdx.x >= nd) return;  // uniform
-
     __shared__ double2 sp[kBlock];
     __shared__ double sw[kBlock];
     __shared__ int rs[kPollRB], rpre[kPollRB + 1];
@@ -93,10 +88,10 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_shared_kernel(
     __shared__ int wcount[kWavesPerBlock];
 
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
-    const int k = blockIdx.y * kBlock + tid;
-    const bool valid = k < K;
+    const int k = kb + tid;
+    const bool valid = k < ke;
 
-    for (int di = blockIdx.x; di < nd; di += gridDim.x) {
+    for (int di = b; di < nd; di += kSharedWG) {
         const int i = dlist[di];
         const int nc = ncount[i];
         const int ncl = min(nc, kPollNbr);
@@ -192,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_shared_kernel(
                 __syncthreads();
             }
         }
-        if (valid) partial[(int64_t)i * K + k] += acc;
+        if (valid) spart[(int64_t)i * K + k] = acc;
     }
 }
 

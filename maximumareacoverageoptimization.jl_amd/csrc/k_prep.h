@@ -13,22 +13,56 @@ namespace mac {
 
 // ------------------------------------------------------------------ per-batch disk prep
 
-// cands: 3N x K column-major (candidate k at cands + k*ldc). Writes disks[k*N + i] (scan walk).
+// Objective-penalty inputs (src/TDM_STATIC_opt.jl:89-97) and the cons3 constraint
+// (src/TDM_Constraints.jl:54-75). rmax == null: no penalty term; prev == null: no cons3.
+struct PenArgs {
+    const double* rmax;
+    const double* prev;
+    const double* dlimT;   // per UAV: cons3 holds iff s <= dlimT[i] (predicate.h dlim_threshold)
+    double tan_half_fov;
+};
+
+// Term i of candidate (x_i, y_i, R_i): |R_i - rmax_i| (0 without rmax), or -1 when UAV i's move
+// violates cons3 (sqrt(dx^2 + dy^2 + dz^2) > d_lim[i], z = R / tan(FOV/2), evaluated exactly as
+// s > dlimT[i]). A negative term marks the candidate infeasible; the finalize chain sums the
+// others sequentially in i (bit-exact with the reference's loop).
+__device__ __forceinline__ double pen_term(double x2, double y2, double R2, int i, int N,
+                                           const PenArgs& pa)
+{
+    if (pa.prev) {
+        const double x1 = pa.prev[i], y1 = pa.prev[N + i], z1 = pa.prev[2 * N + i] / pa.tan_half_fov;
+        const double z2 = R2 / pa.tan_half_fov;
+        const double ddx = x1 - x2, ddy = y1 - y2, ddz = z1 - z2;
+        const double s = ddx * ddx + ddy * ddy + ddz * ddz;
+        if (s > pa.dlimT[i]) return -1.0;
+    }
+    return pa.rmax ? __builtin_fabs(R2 - pa.rmax[i]) : 0.0;
+}
+
+// cands: 3N x K column-major (candidate k at cands + k*ldc). Writes disks[k*N + i] (scan walk)
+// and, when pen != null, pen[i*K + k] = pen_term (disk-major, as penalty_chain reads it).
 __global__ void disk_prep_kernel(const double* __restrict__ cands, int N, int ldc, int K,
-                                 DiskRec* __restrict__ disks)
+                                 DiskRec* __restrict__ disks, PenArgs pa, double* __restrict__ pen)
 {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (int64_t)N * K) return;
     const int k = (int)(t / N), i = (int)(t % N);
     const double* c = cands + (int64_t)k * ldc;
-    disks[t] = make_disk(c[i], c[N + i], c[2 * N + i]);
+    const double x = c[i], y = c[N + i], r = c[2 * N + i];
+    disks[t] = make_disk(x, y, r);
+    if (pen) pen[(int64_t)i * K + k] = pen_term(x, y, r, i, N, pa);
 }
 
 // Transposed prep: disksT[i*K + k] (disk-major, candidates contiguous). 32 x 32 tiles through
-// LDS so both the candidate reads and the record writes are coalesced.
-__global__ __launch_bounds__(kBlock) void disk_prep_T_kernel(const double* __restrict__ cands,
-                                                             int N, int ldc, int K,
-                                                             DiskRec* __restrict__ disksT)
+// LDS so both the candidate reads and the record writes are coalesced. Also, per tile:
+//   penT[i*K + k] = pen_term (when penT != null), and
+//   regP[kt*N + i], costP[kt*N + i] (kt = blockIdx.y): the union of disk i's tile spans over the
+//   tile's 32 candidates and the sum of their span areas (when regP != null; region_kernel
+//   finishes the reduction over kt).
+__global__ __launch_bounds__(kBlock) void disk_prep_T_kernel(
+    const double* __restrict__ cands, int N, int ldc, int K, DiskRec* __restrict__ disksT,
+    PenArgs pa, double* __restrict__ penT, Grid g, int4* __restrict__ regP,
+    double* __restrict__ costP)
 {
     __shared__ double sx[32][33], sy[32][33], sr[32][33];
     const int i0 = blockIdx.x * 32, k0 = blockIdx.y * 32;
@@ -45,51 +79,71 @@ __global__ __launch_bounds__(kBlock) void disk_prep_T_kernel(const double* __res
     __syncthreads();
     for (int ii = ty; ii < 32; ii += 8) {
         const int i = i0 + ii, k = k0 + tx;
-        if (k < K && i < N) disksT[(int64_t)i * K + k] = make_disk(sx[tx][ii], sy[tx][ii], sr[tx][ii]);
+        int4 sp = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
+        double area = 0.0;
+        if (k < K && i < N) {
+            const double x = sx[tx][ii], y = sy[tx][ii], r = sr[tx][ii];
+            const DiskRec d = make_disk(x, y, r);
+            disksT[(int64_t)i * K + k] = d;
+            if (penT) penT[(int64_t)i * K + k] = pen_term(x, y, r, i, N, pa);
+            int4 s;
+            if (regP && disk_span(d, g, s)) {
+                sp = s;
+                area = (double)(s.y - s.x + 1) * (double)(s.w - s.z + 1);
+            }
+        }
+        if (regP) {
+            // the 32 candidates of disk i sit in 32 consecutive lanes: butterfly over them
+#pragma unroll
+            for (int o = 16; o >= 1; o >>= 1) {
+                sp.x = min(sp.x, __shfl_xor(sp.x, o, 32));
+                sp.y = max(sp.y, __shfl_xor(sp.y, o, 32));
+                sp.z = min(sp.z, __shfl_xor(sp.z, o, 32));
+                sp.w = max(sp.w, __shfl_xor(sp.w, o, 32));
+                area += __shfl_xor(area, o, 32);
+            }
+            if (tx == 0 && i < N) {
+                regP[(int64_t)blockIdx.y * N + i] = sp;
+                costP[(int64_t)blockIdx.y * N + i] = area;
+            }
+        }
     }
 }
 
 // ------------------------------------------------------------------ region + decision
 
-// Block i: union over the K candidates of disk i's tile span (region[i]) and two costs in
-// point-visits / ppt: poll walk = K * |region|, per-candidate walk = sum_k |span_k|.
-__global__ __launch_bounds__(kBlock) void region_kernel(const DiskRec* __restrict__ disksT,
-                                                        int N, int K, Grid g,
-                                                        int4* __restrict__ region,
-                                                        double2* __restrict__ cost)
+// One wave per disk i: region[i] = union over the KT candidate tiles of regP (the union of
+// disk i's tile spans over all K candidates) and cost[i] = (K * |region|, sum of span areas):
+// the point visits of the poll walk and of the per-candidate walk, in units of ppt.
+__global__ __launch_bounds__(kWave) void region_kernel(const int4* __restrict__ regP,
+                                                       const double* __restrict__ costP, int N,
+                                                       int KT, int K, int4* __restrict__ region,
+                                                       double2* __restrict__ cost)
 {
-    const int i = blockIdx.x;
-    int x0 = 0x7fffffff, y0 = 0x7fffffff, x1 = -1, y1 = -1;
-    double cand = 0.0;
-    for (int k = threadIdx.x; k < K; k += kBlock) {
-        const DiskRec d = disksT[(int64_t)i * K + k];
-        int4 sp;
-        if (disk_span(d, g, sp)) {
-            x0 = min(x0, sp.x);
-            x1 = max(x1, sp.y);
-            y0 = min(y0, sp.z);
-            y1 = max(y1, sp.w);
-            cand += (double)(sp.y - sp.x + 1) * (double)(sp.w - sp.z + 1);
-        }
+    const int i = blockIdx.x, lane = threadIdx.x;
+    int4 R = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
+    double c = 0.0;
+    for (int kt = lane; kt < KT; kt += kWave) {
+        const int4 p = regP[(int64_t)kt * N + i];
+        R.x = min(R.x, p.x);
+        R.y = max(R.y, p.y);
+        R.z = min(R.z, p.z);
+        R.w = max(R.w, p.w);
+        c += costP[(int64_t)kt * N + i];
     }
-    __shared__ int sh[4][kBlock];
-    __shared__ double red[kWavesPerBlock];
-    sh[0][threadIdx.x] = x0;
-    sh[1][threadIdx.x] = -x1;
-    sh[2][threadIdx.x] = y0;
-    sh[3][threadIdx.x] = -y1;
-    __syncthreads();
-    for (int s = kBlock / 2; s > 0; s >>= 1) {
-        if (threadIdx.x < s)
-            for (int q = 0; q < 4; ++q) sh[q][threadIdx.x] = min(sh[q][threadIdx.x], sh[q][threadIdx.x + s]);
-        __syncthreads();
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        R.x = min(R.x, __shfl_xor(R.x, o, kWave));
+        R.y = max(R.y, __shfl_xor(R.y, o, kWave));
+        R.z = min(R.z, __shfl_xor(R.z, o, kWave));
+        R.w = max(R.w, __shfl_xor(R.w, o, kWave));
+        c += __shfl_xor(c, o, kWave);
     }
-    const double candsum = block_sum_f64(cand, red);
-    if (threadIdx.x == 0) {
-        const int4 R = make_int4(sh[0][0], -sh[1][0], sh[2][0], -sh[3][0]);
+    if (lane == 0) {
+        if (R.x > R.y || R.z > R.w) R = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
         region[i] = R;
         const double rc = R.x <= R.y ? (double)(R.y - R.x + 1) * (double)(R.w - R.z + 1) : 0.0;
-        cost[i] = make_double2(rc * (double)K, candsum);
+        cost[i] = make_double2(rc * (double)K, c);
     }
 }
 

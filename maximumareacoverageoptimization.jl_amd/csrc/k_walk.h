@@ -98,7 +98,7 @@ __host__ __device__ inline size_t tiled_lds_bytes(int N)
 // sorted list), tests every entry in them, and credits a covered entry only when no lower-index
 // disk also covers it (candidates for that come from a conservative disk-disk intersection
 // list built in LDS). disksT[c*K + k]; partial[gi*K + k]. Runs only when *mode == kModeTiled
-// (or mode == null).
+// (or mode == null). Workgroups loop over units (grid-stride).
 __global__ __launch_bounds__(kBlock) void coverage_tiled_kernel(
     const double2* __restrict__ xy, const double* __restrict__ w,
     const int32_t* __restrict__ off, Grid g,
@@ -120,8 +120,12 @@ __global__ __launch_bounds__(kBlock) void coverage_tiled_kernel(
     int* rowPre = rowStart + kWave;
     __shared__ double red[kWavesPerBlock];
 
-    const int k = blockIdx.x / G;
-    const int gi = blockIdx.x % G;
+    // grid-stride over the K*G (candidate, slice) units: the grid is capped so that the
+    // launch stays cheap when the device-side choice is the poll walk
+    for (int64_t unit = blockIdx.x; unit < (int64_t)K * G; unit += gridDim.x) {
+    const int k = (int)(unit / G);
+    const int gi = (int)(unit % G);
+    __syncthreads();  // LDS reuse across units
 
     // 1. disks -> LDS, spans
     for (int c = threadIdx.x; c < N; c += kBlock) {
@@ -203,6 +207,7 @@ __global__ __launch_bounds__(kBlock) void coverage_tiled_kernel(
     }
     const double s = block_sum_f64(acc, red);
     if (threadIdx.x == 0) partial[(int64_t)gi * K + k] = s;
+    }
 }
 
 }  // namespace mac

@@ -95,10 +95,8 @@ struct Lane {
     hipStream_t stream = nullptr;
     hipStream_t last = nullptr;   // stream of the most recent use
     hipEvent_t done = nullptr;
-    DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode, vp, nbr,
-        ncount, dlist;
-    hipStream_t aux = nullptr;                 // forked stream for the penalty kernel
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode, pen, nbr,
+        ncount, dlist, regP, costP, spart, vp;
     std::vector<double> h_dlim;
 };
 
@@ -336,21 +334,21 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_c
     const int64_t M = ctx->M;
     int n_poll = N, n_other = 1;
     const int* d_mode = nullptr;
+    // objective penalty terms + cons3 marks are written by the prep kernels (one term per disk
+    // and candidate); the finalize kernel runs the sequential violation chain
+    const PenArgs pa{d_rmax, d_prev, d_dlimT, tan_half_fov};
+    double* d_pen = nullptr;           // penalty terms, pen[i*K + k]
+    double* d_vp = nullptr;            // per-candidate penalty (or +inf: cons3)
+    bool chain_done = false;           // the poll kernel ran the chains
+    const double* d_spart = nullptr;   // poll walk: shared-entry rows
+    const int* d_ncount = nullptr;
     if (d_obj) {
-        // objective penalty + cons3 mask do not depend on coverage: fork them onto the lane's
-        // aux stream so they run beside the walk (joined before finalize)
-        if (!L->aux) {
-            HCK(hipStreamCreateWithFlags(&L->aux, hipStreamNonBlocking));
-            HCK(hipEventCreateWithFlags(&L->ev_fork, hipEventDisableTiming));
-            HCK(hipEventCreateWithFlags(&L->ev_join, hipEventDisableTiming));
-        }
         L->vp.reserve(sizeof(double) * (size_t)std::max(K, 1));
-        HCK(hipEventRecord(L->ev_fork, s));
-        HCK(hipStreamWaitEvent(L->aux, L->ev_fork, 0));
-        hipLaunchKernelGGL(penalty_kernel, dim3((K + kPenC - 1) / kPenC), dim3(kBlock), 0, L->aux, K,
-                           d_cands, N, ldc, d_rmax, penalty, d_prev, d_dlimT, tan_half_fov,
-                           L->vp.as<double>());
-        HCK(hipGetLastError());
+        d_vp = L->vp.as<double>();
+        if (N > 0) {
+            L->pen.reserve(sizeof(double) * (size_t)N * K);
+            d_pen = L->pen.as<double>();
+        }
     }
     hipEvent_t ev_a = nullptr, ev_b = nullptr;
     auto prof_begin = [&]() {
@@ -380,10 +378,16 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_c
     if (N == 0 || M == 0) {  // no UAV or no entry: every area is 0 (the loops never run)
         L->partial.reserve(sizeof(double) * (size_t)K);
         HCK(hipMemsetAsync(L->partial.p, 0, sizeof(double) * (size_t)K, s));
+        if (d_pen) {
+            L->disks.reserve(sizeof(DiskRec) * (size_t)N * K);
+            hipLaunchKernelGGL(disk_prep_kernel, dim3(grid1d((int64_t)N * K, 256)), dim3(256), 0, s,
+                               d_cands, N, ldc, K, L->disks.as<DiskRec>(), pa, d_pen);
+            HCK(hipGetLastError());
+        }
     } else if (!tiled) {
         L->disks.reserve(sizeof(DiskRec) * (size_t)N * K);
         hipLaunchKernelGGL(disk_prep_kernel, dim3(grid1d((int64_t)N * K, 256)), dim3(256), 0, s,
-                           d_cands, N, ldc, K, L->disks.as<DiskRec>());
+                           d_cands, N, ldc, K, L->disks.as<DiskRec>(), pa, d_pen);
         HCK(hipGetLastError());
         constexpr int KB = 4, PPT = 4;
         const int64_t per_pass = (int64_t)kBlock * PPT;
@@ -403,24 +407,32 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_c
         HCK(hipGetLastError());
         prof_end();
     } else {
+        const bool poll_possible = ctx->algo == MAC_ALGO_POLL ||
+                                   (ctx->algo == MAC_ALGO_AUTO && K >= kPollMinK);
+        const int KT = (K + 31) / 32;
         L->disks.reserve(sizeof(DiskRec) * (size_t)N * K);
-        hipLaunchKernelGGL(disk_prep_T_kernel, dim3((N + 31) / 32, (K + 31) / 32), dim3(kBlock), 0,
-                           s, d_cands, N, ldc, K, L->disks.as<DiskRec>());
+        if (poll_possible) {
+            L->regP.reserve(sizeof(int4) * (size_t)N * KT);
+            L->costP.reserve(sizeof(double) * (size_t)N * KT);
+        }
+        hipLaunchKernelGGL(disk_prep_T_kernel, dim3((N + 31) / 32, KT), dim3(kBlock), 0, s, d_cands,
+                           N, ldc, K, L->disks.as<DiskRec>(), pa, d_pen, ctx->grid,
+                           poll_possible ? L->regP.as<int4>() : nullptr,
+                           poll_possible ? L->costP.as<double>() : nullptr);
         HCK(hipGetLastError());
         // per-candidate walk: enough workgroups to fill the chip, >= 1 disk per wave
         const int target = 8 * ctx->cus;
         const int G = (int)std::max<int64_t>(
             1, std::min<int64_t>((target + K - 1) / K, std::max(1, N / kWavesPerBlock)));
         n_other = G;
-        const bool poll_possible = ctx->algo == MAC_ALGO_POLL ||
-                                   (ctx->algo == MAC_ALGO_AUTO && K >= kPollMinK);
         L->partial.reserve(sizeof(double) * (size_t)K * std::max(G, poll_possible ? N : 1));
         if (poll_possible) {
             L->region.reserve(sizeof(int4) * N);
             L->cost.reserve(sizeof(double2) * N);
             L->mode.reserve(2 * sizeof(int));  // [0] walk, [1] disks-with-neighbours count
-            hipLaunchKernelGGL(region_kernel, dim3(N), dim3(kBlock), 0, s, L->disks.as<DiskRec>(),
-                               N, K, ctx->grid, L->region.as<int4>(), L->cost.as<double2>());
+            hipLaunchKernelGGL(region_kernel, dim3(N), dim3(kWave), 0, s, L->regP.as<int4>(),
+                               L->costP.as<double>(), N, KT, K, L->region.as<int4>(),
+                               L->cost.as<double2>());
             HCK(hipGetLastError());
             const int forced = ctx->algo == MAC_ALGO_POLL ? kModePoll : 0;
             hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(kBlock), 0, s, L->cost.as<double2>(), N,
@@ -438,38 +450,40 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_c
         prof_begin();
         if (ctx->algo != MAC_ALGO_POLL) {
             const size_t lds = tiled_lds_bytes(N);
-            hipLaunchKernelGGL(coverage_tiled_kernel, dim3((unsigned)((int64_t)K * G)), dim3(kBlock),
+            const int64_t units = (int64_t)K * G;
+            const int64_t cap = poll_possible ? 4 * (int64_t)ctx->cus : units;
+            hipLaunchKernelGGL(coverage_tiled_kernel, dim3((unsigned)std::min(units, cap)), dim3(kBlock),
                                lds, s, ctx->xys.as<double2>(), ctx->ws.as<double>(),
                                ctx->off.as<int32_t>(), ctx->grid, L->disks.as<DiskRec>(), N, K, G,
                                d_mode, L->partial.as<double>());
             HCK(hipGetLastError());
         }
         if (poll_possible) {
-            const dim3 pgrid(N, (K + kPollKPB - 1) / kPollKPB);
+            L->spart.reserve(sizeof(double) * (size_t)N * K);
+            const int n_chain = d_obj ? (K + kBlock - 1) / kBlock : 0;
+            const dim3 pgrid(n_chain + kPollShB + N, (K + kPollKPB - 1) / kPollKPB);
             hipLaunchKernelGGL(coverage_poll_kernel, pgrid, dim3(kBlock), 0, s,
-                               ctx->xys.as<double2>(), ctx->ws.as<double>(),
-                               ctx->off.as<int32_t>(), ctx->grid, L->disks.as<DiskRec>(),
-                               L->region.as<int4>(), L->nbr.as<uint16_t>(), L->ncount.as<int>(), N,
-                               K, d_mode, L->partial.as<double>());
-            HCK(hipGetLastError());
-            const dim3 sgrid(std::min(N, kSharedWG), (K + kBlock - 1) / kBlock);
-            hipLaunchKernelGGL(coverage_poll_shared_kernel, sgrid, dim3(kBlock), 0, s,
                                ctx->xys.as<double2>(), ctx->ws.as<double>(),
                                ctx->off.as<int32_t>(), ctx->grid, L->disks.as<DiskRec>(),
                                L->region.as<int4>(), L->nbr.as<uint16_t>(), L->ncount.as<int>(),
                                L->dlist.as<int>(), L->mode.as<int>() + 1, N, K, d_mode,
-                               L->partial.as<double>());
+                               L->partial.as<double>(), L->spart.as<double>(), n_chain, d_pen,
+                               penalty, d_vp);
             HCK(hipGetLastError());
+            chain_done = true;
+            d_spart = L->spart.as<double>();
+            d_ncount = L->ncount.as<int>();
         }
         prof_end();
     }
-    if (d_obj) {  // join the penalty stream
-        HCK(hipEventRecord(L->ev_join, L->aux));
-        HCK(hipStreamWaitEvent(s, L->ev_join, 0));
+    if (d_obj && !chain_done) {
+        hipLaunchKernelGGL(penalty_chain_kernel, dim3((K + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+                           d_pen, K, N, penalty, d_vp);
+        HCK(hipGetLastError());
     }
     hipLaunchKernelGGL(finalize_kernel, dim3((K + kFinC - 1) / kFinC), dim3(kBlock), 0, s,
-                       L->partial.as<double>(), d_mode, n_poll, n_other, K,
-                       d_obj ? L->vp.as<double>() : nullptr, d_area, d_obj);
+                       L->partial.as<double>(), d_mode, n_poll, n_other, K, N, d_spart, d_ncount,
+                       d_vp, d_area, d_obj);
     HCK(hipGetLastError());
     if (d_best) {
         hipLaunchKernelGGL(argmin_kernel, dim3(1), dim3(kBlock), 0, s, d_obj, K, idx_base, d_best);
@@ -659,12 +673,9 @@ void mac_ctx_destroy(mac_ctx* ctx)
     (void)hipDeviceSynchronize();
     for (Lane* l : ctx->lanes_all) {
         for (DevBuf* b : {&l->cands, &l->disks, &l->partial, &l->area, &l->obj, &l->best,
-                          &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->vp, &l->nbr,
-                          &l->ncount, &l->dlist})
+                          &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->pen, &l->nbr,
+                          &l->ncount, &l->dlist, &l->regP, &l->costP, &l->spart, &l->vp})
             b->release();
-        if (l->ev_fork) (void)hipEventDestroy(l->ev_fork);
-        if (l->ev_join) (void)hipEventDestroy(l->ev_join);
-        if (l->aux) (void)hipStreamDestroy(l->aux);
         if (l->done) (void)hipEventDestroy(l->done);
         if (l->stream) (void)hipStreamDestroy(l->stream);
         delete l;
@@ -815,7 +826,8 @@ static void compute_flags(mac_ctx* ctx, hipStream_t s, const double* circles, in
     if (N > 0) {
         HCK(hipMemcpyAsync(ctx->circ.p, circles, sizeof(double) * 3 * N, hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(disk_prep_kernel, dim3(grid1d(N, 256)), dim3(256), 0, s,
-                           ctx->circ.as<double>(), N, 3 * N, 1, ctx->cdisk.as<DiskRec>());
+                           ctx->circ.as<double>(), N, 3 * N, 1, ctx->cdisk.as<DiskRec>(),
+                           PenArgs{nullptr, nullptr, nullptr, 1.0}, nullptr);
         HCK(hipGetLastError());
         const unsigned nb = (unsigned)std::max(1, std::min((N + kWavesPerBlock - 1) / kWavesPerBlock,
                                                            8 * ctx->cus));

@@ -41,14 +41,14 @@ def test_golden_static_grid(ctx, pkg, golden, orc):
     for a, got in both(ctx, lambda: ctx.objective_batch(golden["A_cands"], golden["A_rmax"])).items():
         assert np.array_equal(got, golden["A_obj"]), a
     # poll with cons3 on the device == oracle's extreme barrier + argmin
-    bo, bi, objs = ctx.poll_best(golden["A_cands"], golden["A_rmax"], 1e5, prev=golden["A_prev"],
-                                 d_lim=golden["A_dlim"], tan_half_fov=float(golden["A_tan"][0]),
-                                 want_all=True)
     feas = golden["A_cons3"].astype(bool)
     want = np.where(feas, golden["A_obj"], np.inf)
-    assert np.array_equal(objs, want)
     k = int(np.argmin(want))
-    assert bi == k and bo == want[k]
+    for a, (bo, bi, objs) in both(ctx, lambda: ctx.poll_best(
+            golden["A_cands"], golden["A_rmax"], 1e5, prev=golden["A_prev"],
+            d_lim=golden["A_dlim"], tan_half_fov=float(golden["A_tan"][0]), want_all=True)).items():
+        assert np.array_equal(objs, want), a
+        assert bi == k and bo == want[k], a
 
 
 def test_golden_firepoints(ctx, golden, firepoints):
@@ -302,12 +302,19 @@ def test_config3_full_poll(ctx, pkg, orc):
     assert np.array_equal(r["tiled"], r["scan"])
     for k in range(0, C.shape[0], 97):
         assert r["tiled"][k] == 25.0 * orc.lattice_count_fast(C[k].astype(np.int64), 2048), k
-    ctx.set_algo("tiled")
-    bo, bi, objs = ctx.poll_best(C, rmax, want_all=True)
-    ctx.set_algo("auto")
     pen = np.array([sum(abs(float(c[256 + i]) - float(rmax[i])) for i in range(128)) for c in C])
     wobj = -r["scan"] + pen * 1e5
-    assert np.array_equal(objs, wobj) and bi == int(np.argmin(wobj))
+    # cons3 around the incumbent with d_lim = 5 m: a mix of feasible and infeasible moves
+    tan = float(np.tan(100 / 180 * np.pi / 2))
+    dlim = np.full(128, 5.0)
+    feas = np.array([orc.ref_cons3(C[0], c, dlim, tan) for c in C])
+    assert 0 < feas.sum() < C.shape[0]
+    wbar = np.where(feas, wobj, np.inf)
+    for a, (bo, bi, objs) in both(ctx, lambda: ctx.poll_best(C, rmax, want_all=True)).items():
+        assert np.array_equal(objs, wobj) and bi == int(np.argmin(wobj)), a
+    for a, (bo, bi, objs) in both(ctx, lambda: ctx.poll_best(
+            C, rmax, 1e5, prev=C[0], d_lim=dlim, tan_half_fov=tan, want_all=True)).items():
+        assert np.array_equal(objs, wbar) and bi == int(np.argmin(wbar)) and bo == wbar[bi], a
 
 
 def test_config4_full_poll(ctx, pkg, orc):
