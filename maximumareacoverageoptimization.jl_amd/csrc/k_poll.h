@@ -31,8 +31,8 @@
 // The hot loop is therefore, per 2 entries x 2 candidates, six packed fmas, two packed clamps
 // (v_pk_add_f32 ... clamp), two packed adds and two v_min3 (the band detector): three VALU ops
 // per test. On the reference lattices the band is empty (|a - T| >= 1/2 >> X).
-// Non-finite and shared entries are staged with (0, 0, +inf): d' = -inf, never counted, never
-// in the band. A lane whose M is outside [2^-60, 2^60] is "forced": S = 1, X' = +inf, every
+// Non-finite and shared entries are staged with Q = +inf, U = V = 0: d' = -inf, never counted,
+// never in the band. A lane whose M is outside [2^-60, 2^60] is "forced": S = 1, X' = +inf, every
 // entry goes to the exact pass.
 #pragma once
 
@@ -135,7 +135,7 @@ __device__ __forceinline__ PollLane poll_lane(const DiskRec& d, double ox, doubl
 
 __device__ __forceinline__ float poll_dprime(const float4& e, const PollLane& L)
 {
-    return __builtin_fmaf(e.z, L.ns, __builtin_fmaf(e.y, L.sb, __builtin_fmaf(e.x, L.sa, L.stm)));
+    return __builtin_fmaf(e.x, L.ns, __builtin_fmaf(e.z, L.sb, __builtin_fmaf(e.y, L.sa, L.stm)));
 }
 
 // Grid (n_chain + kPollShB + N, slices); roles by x, in dispatch order (the first ones overlap
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
     const uint64_t diag_t0 = __builtin_amdgcn_s_memrealtime();
     int diag_entries = 0;
 #endif
-    __shared__ float4 s32[kPollCH];    // (U, V, Q, 0); (0, 0, +inf) for shared / non-finite
+    __shared__ float4 s32[kPollCH + 4];  // (Q, U, V, 0); (+inf, 0, 0) for shared / non-finite / pad
     __shared__ double2 s64[kPollCH];   // exact coordinates (band decisions)
     __shared__ double sw[kPollCH];
     __shared__ int rs[kPollRB], rpre[kPollRB + 1];
@@ -270,12 +270,13 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
                     nc > 0 && entry_shared(nc, nbox, tile_of(p.x, g.gx0, g.invS, g.nTx), rb + lo);
                 const float fu = (float)(p.x - ox), fv = (float)(p.y - oy);
                 s32[q] = !shared && __builtin_isfinite(fu) && __builtin_isfinite(fv)
-                             ? make_float4(fu, fv, __builtin_fmaf(fu, fu, fv * fv), 0.0f)
-                             : make_float4(0.0f, 0.0f, __builtin_inff(), 0.0f);
+                             ? make_float4(__builtin_fmaf(fu, fu, fv * fv), fu, fv, 0.0f)
+                             : make_float4(__builtin_inff(), 0.0f, 0.0f, 0.0f);
                 if (q == tid) wfirst = wj;
                 mixed |= __builtin_bit_cast(uint64_t, wj) != __builtin_bit_cast(uint64_t, wfirst);
             }
-            if (tid == 0 && (n & 1)) s32[n] = make_float4(0.0f, 0.0f, __builtin_inff(), 0.0f);
+            // pad to a multiple of 4 entries with inert ones (d' = -inf: never counted, never band)
+            if (tid < ((4 - (n & 3)) & 3)) s32[n + tid] = make_float4(__builtin_inff(), 0.0f, 0.0f, 0.0f);
             __syncthreads();
             // weights identical across the chunk? (compare with entry 0 after staging)
             const uint64_t w0 = __builtin_bit_cast(uint64_t, sw[0]);
@@ -290,32 +291,32 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
                 if (uniform) {
                     // hot loop: 2 entries x 2 candidates per step, 3 VALU ops per test
                     f32x2 h01 = zero2, h23 = zero2;
+                    // entries staged as (Q, U, V, 0); bmin updates chained so they form v_min3
+#define MAC_POLL_PAIR(E0, E1, SA, SB, ST, NS, H, B0, B1)                                       \
+    {                                                                                         \
+        const f32x2 d0 = fma2(E0.x, NS, fma2(E0.z, SB, fma2(E0.y, SA, ST)));                   \
+        const f32x2 d1 = fma2(E1.x, NS, fma2(E1.z, SB, fma2(E1.y, SA, ST)));                   \
+        H += clamp01x2(d0, zero2);                                                            \
+        H += clamp01x2(d1, zero2);                                                            \
+        B0 = __builtin_fminf(__builtin_fminf(B0, __builtin_fabsf(d0.x)), __builtin_fabsf(d1.x)); \
+        B1 = __builtin_fminf(__builtin_fminf(B1, __builtin_fabsf(d0.y)), __builtin_fabsf(d1.y)); \
+    }
                     if (pair1) {
-#pragma unroll 2
-                        for (int q = 0; q < n; q += 2) {
-                            const float4 e0 = s32[q], e1 = s32[q + 1];
-                            const f32x2 a0 = fma2(e0.z, ns01, fma2(e0.y, sb01, fma2(e0.x, sa01, st01)));
-                            const f32x2 a1 = fma2(e1.z, ns01, fma2(e1.y, sb01, fma2(e1.x, sa01, st01)));
-                            const f32x2 b0 = fma2(e0.z, ns23, fma2(e0.y, sb23, fma2(e0.x, sa23, st23)));
-                            const f32x2 b1 = fma2(e1.z, ns23, fma2(e1.y, sb23, fma2(e1.x, sa23, st23)));
-                            h01 += clamp01x2(a0, zero2) + clamp01x2(a1, zero2);
-                            h23 += clamp01x2(b0, zero2) + clamp01x2(b1, zero2);
-                            bmin[0] = __builtin_fminf(bmin[0], __builtin_fminf(__builtin_fabsf(a0.x), __builtin_fabsf(a1.x)));
-                            bmin[1] = __builtin_fminf(bmin[1], __builtin_fminf(__builtin_fabsf(a0.y), __builtin_fabsf(a1.y)));
-                            bmin[2] = __builtin_fminf(bmin[2], __builtin_fminf(__builtin_fabsf(b0.x), __builtin_fabsf(b1.x)));
-                            bmin[3] = __builtin_fminf(bmin[3], __builtin_fminf(__builtin_fabsf(b0.y), __builtin_fabsf(b1.y)));
+                        for (int q = 0; q < n; q += 4) {
+                            const float4 e0 = s32[q], e1 = s32[q + 1], e2 = s32[q + 2], e3 = s32[q + 3];
+                            MAC_POLL_PAIR(e0, e1, sa01, sb01, st01, ns01, h01, bmin[0], bmin[1])
+                            MAC_POLL_PAIR(e0, e1, sa23, sb23, st23, ns23, h23, bmin[2], bmin[3])
+                            MAC_POLL_PAIR(e2, e3, sa01, sb01, st01, ns01, h01, bmin[0], bmin[1])
+                            MAC_POLL_PAIR(e2, e3, sa23, sb23, st23, ns23, h23, bmin[2], bmin[3])
                         }
                     } else {
-#pragma unroll 4
-                        for (int q = 0; q < n; q += 2) {
-                            const float4 e0 = s32[q], e1 = s32[q + 1];
-                            const f32x2 a0 = fma2(e0.z, ns01, fma2(e0.y, sb01, fma2(e0.x, sa01, st01)));
-                            const f32x2 a1 = fma2(e1.z, ns01, fma2(e1.y, sb01, fma2(e1.x, sa01, st01)));
-                            h01 += clamp01x2(a0, zero2) + clamp01x2(a1, zero2);
-                            bmin[0] = __builtin_fminf(bmin[0], __builtin_fminf(__builtin_fabsf(a0.x), __builtin_fabsf(a1.x)));
-                            bmin[1] = __builtin_fminf(bmin[1], __builtin_fminf(__builtin_fabsf(a0.y), __builtin_fabsf(a1.y)));
+                        for (int q = 0; q < n; q += 4) {
+                            const float4 e0 = s32[q], e1 = s32[q + 1], e2 = s32[q + 2], e3 = s32[q + 3];
+                            MAC_POLL_PAIR(e0, e1, sa01, sb01, st01, ns01, h01, bmin[0], bmin[1])
+                            MAC_POLL_PAIR(e2, e3, sa01, sb01, st01, ns01, h01, bmin[0], bmin[1])
                         }
                     }
+#undef MAC_POLL_PAIR
                     // counts < 2^24: exact in fp32 when no entry is in the band
                     const double wu = sw[0];
                     cw[0] = (double)h01.x * wu;
@@ -352,7 +353,7 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
                             bool cov;
                             if (__builtin_fabsf(dp) <= pl[u].xp) {
                                 const double2 p = s64[q];
-                                if (e.z == __builtin_inff() && nc > 0 &&
+                                if (e.x == __builtin_inff() && nc > 0 &&
                                     entry_shared(nc, nbox, tile_of(p.x, g.gx0, g.invS, g.nTx),
                                                  tile_of(p.y, g.gy0, g.invS, g.nTy)))
                                     continue;
@@ -377,7 +378,7 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
     if (tid == 0) {
         // diagnostic build only: per-workgroup stamps into a buffer nothing else reads
         const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-        const uint64_t b = (uint64_t)blockIdx.y * gridDim.x + blockIdx.x;
+        const uint64_t b = (uint64_t)blockIdx.y * N + i;
         if (b < kDiagMax) {
             g_diag[4 * b + 0] = diag_t0;
             g_diag[4 * b + 1] = t1;
