@@ -1,0 +1,84 @@
+"""Per-launch HBM traffic of the coverage kernels from two rocprofv3 --pmc passes.
+
+    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write --config 4 \
+        --out profiles/pmc_traffic_config4.json
+
+FETCH_SIZE and WRITE_SIZE are collected in separate passes (gfx950 cannot fit both in one
+pass) with --kernel-trace-free counter collection only. Corrections, per
+/opt/skills/guides/MI355X_MICROARCH.md "HBM [CDNA4]":
+  * the counters are in KiB (rocprofv3 derived metrics: TCC_EA0_*REQ x 64 B / 1024);
+  * on gfx950 FETCH_SIZE reports 1/2 of the bytes of wide coalesced reads, so it is doubled;
+  * Infinity-Cache hits are counted by the memory-side counters, not excluded.
+The dominant kernel is coverage_poll_kernel (the bench's walk); the value stored as
+"hbm_bytes_per_launch" is 2 * FETCH + WRITE averaged over its launches, which bench.py reports
+as roofline.traffic.
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+
+
+def load(d: str, counter: str):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    per = collections.defaultdict(list)
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row["Counter_Name"] != counter:
+                    continue
+                name = row["Kernel_Name"].split("(")[0].replace("void ", "")
+                per[name].append(float(row["Counter_Value"]))
+    return per
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("--config", type=int, default=4)
+    ap.add_argument("--kernel", default="mac::coverage_poll_kernel")
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    fetch = load(a.fetch_dir, "FETCH_SIZE")
+    write = load(a.write_dir, "WRITE_SIZE")
+    kernels = {}
+    for name in sorted(set(fetch) | set(write)):
+        f = fetch.get(name, [])
+        w = write.get(name, [])
+        if not f or not w:
+            continue
+        fk = sum(f) / len(f)
+        wk = sum(w) / len(w)
+        kernels[name] = {
+            "launches": len(f),
+            "fetch_kib_raw": fk,
+            "write_kib_raw": wk,
+            "hbm_bytes_per_launch": 2.0 * fk * 1024.0 + wk * 1024.0,
+        }
+    if a.kernel not in kernels:
+        raise SystemExit(f"{a.kernel} not found; have {list(kernels)}")
+    out = {
+        "config": a.config,
+        "kernel": a.kernel,
+        "hbm_bytes_per_launch": kernels[a.kernel]["hbm_bytes_per_launch"],
+        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
+                  "`python3 bench.py --steps 5 --warmup 1 --no-cpu`; bytes = 2*FETCH_SIZE*1024 "
+                  "+ WRITE_SIZE*1024 (gfx950 FETCH correction, MI355X_MICROARCH.md)",
+        "kernels": kernels,
+    }
+    os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+    with open(a.out, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps({k: round(v["hbm_bytes_per_launch"] / 1e6, 3) for k, v in kernels.items()},
+                     indent=1))
+
+
+if __name__ == "__main__":
+    main()
