@@ -2,15 +2,20 @@
 //
 // Hot path: one MADS poll = K candidates x full coverage of the fire-point list
 // (src/TDM_STATIC_opt.jl:82-100 via src/AreaCoverageCalculation.jl:63-78), as a short chain:
-//   disk_prep*_kernel     per (candidate, disk): {cx, cy, T(r), r}, T the exact threshold
+//   disk_prep*_kernel     per (candidate, disk): {cx, cy, T(r), r}, T the exact threshold; the
+//                         objective-penalty term and cons3 mark; per-tile span unions
 //   region_kernel         per disk i: union of its tile spans over the K candidates + costs
 //   decide_kernel         picks the poll walk or the per-candidate walk on the device
-//   coverage_poll_kernel  workgroup = (disk i, 256 candidates): the entries of disk i's region
-//                         staged in LDS once, one candidate per lane, broadcast LDS reads
+//   neighbors_kernel      per disk i: lower-index disks whose regions overlap region i
+//   coverage_poll_kernel  workgroup = (disk i, 1024 candidates): the entries of disk i's region
+//                         staged in LDS once, 4 candidates per lane, exact fp32 filter; leading
+//                         workgroups run the penalty chains and the shared-entry pass
 //   coverage_tiled_kernel workgroup = candidate: each wave walks whole disks over the CSR rows
 //   coverage_scan_kernel  streaming brute force (every entry x every disk), the fallback
-//   finalize_kernel       fixed-order sum of per-slice partials -> area; penalty; cons3 mask
+//   finalize_kernel       fixed-order sum of per-slice partials -> area, objective
 //   argmin_kernel         lexicographic (objective, index) minimum
+// (Completion-counter "last block" fusions of decide/argmin were measured slower: the
+// device-scope fence each block needs writes back its XCD's L2 on gfx950.)
 // An entry is credited to the LOWEST-index disk covering it (exactly-once union count), so the
 // area is the reference's first-hit-break sum (:67-78) over the same multiset of entries.
 // Partials are laid out [slice][candidate] and summed in slice order: bit-reproducible.
