@@ -101,6 +101,12 @@ int32_t mac_remove_covered_f64(mac_ctx* ctx, const double* circles, int64_t thre
 /* Covered flags for the current list (original order), one byte per entry. */
 int32_t mac_covered_flags_f64(mac_ctx* ctx, const double* circles, int64_t three_n,
                               uint8_t* flags_out);
+/* update_POI (src/CellFunctions.jl:59-79): append m entries at the END of the list (list order
+ * = summation order), then re-index. Host SoA arrays / device-resident SoA arrays. */
+int32_t mac_append_points_f64(mac_ctx* ctx, const double* x, const double* y, const double* w,
+                              int64_t m);
+int32_t mac_append_points_dev_f64(mac_ctx* ctx, const double* d_x, const double* d_y,
+                                  const double* d_w, int64_t m);
 
 /* ---- objective ------------------------------------------------------------------ */
 /* calculateArea(circles, points): one candidate. */
@@ -143,6 +149,46 @@ int32_t mac_poll_best_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three
  * none); reset != 0 clears the record. */
 int32_t mac_profile_read(mac_ctx* ctx, double* kernel_ms, int64_t* launches,
                          int64_t* candidates, int32_t* last_algo, int32_t reset);
+
+/* ---- fire generator (src/DynamicArea.jl, config 5) ------------------------------ */
+/* Cellular-automaton forest fire on an nx x ny grid of dx x dy cells, cell (i, j) 1-based with
+ * i the row (x index) and j the column (y index), as the reference indexes grid[i, j].
+ *   init (:26-35): TREE with probability forest_density else EMPTY; the block
+ *                  [ix0, ix1] x [iy0, iy1] (inclusive, 1-based) set to FIRE.
+ *   step (:52-72): every interior TREE cell tests each FIRE cell of its 3x3 block, in column-major
+ *                  block order, with wind_speed*cos(wind_direction - atan(2-c, 2-r))*prob_spread
+ *                  > u; each success makes it FIRE in the new grid and emits one point
+ *                  (i*dx - dx/2, j*dy - dy/2, dx*dy, dx*dy, 0) — duplicates per igniting
+ *                  neighbour, cells in i-outer/j-inner order (the reference's push order).
+ * u is a counter-based hash of (seed, step, cell, neighbour) instead of the reference's unseeded
+ * rand(), so runs are reproducible and identical to the CPU restatement. */
+typedef struct mac_fire mac_fire;
+typedef struct mac_fire_params {
+    int64_t nx, ny;                 /* grid size in cells (>= 3 each)                          */
+    double dx, dy;                  /* cell pitch (m): 5, 5 in the reference (:6-7)            */
+    double forest_density;          /* 0.7 (:20)                                               */
+    double prob_spread;             /* 0.5 (:21)                                               */
+    double wind_speed;              /* 4 (:47)                                                 */
+    double wind_direction;          /* radians; deg2rad(270) (:48)                             */
+    int64_t ix0, ix1, iy0, iy1;     /* ignition block, 1-based inclusive (:35)                 */
+    uint64_t seed;
+} mac_fire_params;
+const char* mac_fire_last_error(void);
+/* the nine spread thresholds, slot q = (c-1)*3 + (r-1) (column-major block position) */
+void    mac_fire_thresholds(const mac_fire_params* p, double* out9);
+int32_t mac_fire_create(mac_fire** out, int32_t device, const mac_fire_params* p);
+void    mac_fire_destroy(mac_fire* f);
+/* :37-42: the initial points (y outer, x inner) as records of 5 doubles; *n_out = count
+ * (records written up to cap; rec nullable to query the count). */
+int32_t mac_fire_initial_points(mac_fire* f, double* rec, int64_t cap, int64_t* n_out);
+/* One update_grid step; *n_new = number of points pushed. They are appended to `append_to`'s
+ * list (device to device, update_POI) when non-null. */
+int32_t mac_fire_step(mac_fire* f, mac_ctx* append_to, int64_t* n_new);
+/* The last step's points as records of 5 doubles (up to cap); *n_out = their count. */
+int32_t mac_fire_last_points(mac_fire* f, double* rec, int64_t cap, int64_t* n_out);
+/* The current grid, nx*ny bytes, row-major in (i, j): 0 EMPTY, 1 TREE, 2 FIRE. */
+int32_t mac_fire_get_grid(mac_fire* f, uint8_t* out);
+int32_t mac_fire_set_grid(mac_fire* f, const uint8_t* in);
 
 /* ---- exact predicate helpers (host) --------------------------------------------- */
 /* Largest double T with: for every double a >= 0, (sqrt(a) < r) <=> (a <= T), where sqrt is

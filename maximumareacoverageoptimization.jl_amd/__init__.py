@@ -5,12 +5,13 @@ package is the host-side mirror of the reference's Julia modules on the hot path
 library through ctypes. Loading the package does not touch the GPU; the first evaluation
 creates a context (and fails loudly if the library or a GPU is missing).
 """
-from ._lib import (ALGOS, Context, InexactError, MaxCoverError, cover_threshold, default_context,
-                   device_count, load_library, version)
-from . import Base_Functions, workloads  # noqa: F401  (pure host modules)
-from . import AreaCoverageCalculation, CellFunctions, TDM_Constraints, TDM_STATIC_opt  # noqa: F401
+from ._lib import (ALGOS, Context, Fire, InexactError, MaxCoverError, cover_threshold,
+                   default_context, device_count, load_library, version)
+from . import Base_Functions, firepoints, workloads  # noqa: F401  (pure host modules)
+from . import AreaCoverageCalculation, CellFunctions, DynamicArea, TDM_Constraints  # noqa: F401
+from . import TDM_STATIC_opt  # noqa: F401
 
-__all__ = ["ALGOS", "Context", "InexactError", "MaxCoverError", "cover_threshold",
+__all__ = ["ALGOS", "Context", "Fire", "InexactError", "MaxCoverError", "cover_threshold",
            "default_context", "device_count", "load_library", "version",
-           "AreaCoverageCalculation", "CellFunctions", "TDM_Constraints", "TDM_STATIC_opt",
-           "Base_Functions", "workloads"]
+           "AreaCoverageCalculation", "CellFunctions", "DynamicArea", "TDM_Constraints",
+           "TDM_STATIC_opt", "Base_Functions", "firepoints", "workloads"]

@@ -46,7 +46,21 @@ EXPORTS = (
     "mac_remove_covered_f64", "mac_covered_flags_f64", "mac_area_f64", "mac_area_batch_f64",
     "mac_objective_batch_f64", "mac_poll_best_f64", "mac_area_batch_dev_f64",
     "mac_poll_best_dev_f64", "mac_cover_threshold", "mac_profile_read",
+    "mac_append_points_f64", "mac_append_points_dev_f64",
+    "mac_fire_last_error", "mac_fire_thresholds", "mac_fire_create", "mac_fire_destroy",
+    "mac_fire_initial_points", "mac_fire_step", "mac_fire_last_points", "mac_fire_get_grid",
+    "mac_fire_set_grid",
 )
+
+
+class FireParams(ctypes.Structure):
+    """mac_fire_params (include/maxcover.h)."""
+    _fields_ = [("nx", ctypes.c_int64), ("ny", ctypes.c_int64), ("dx", ctypes.c_double),
+                ("dy", ctypes.c_double), ("forest_density", ctypes.c_double),
+                ("prob_spread", ctypes.c_double), ("wind_speed", ctypes.c_double),
+                ("wind_direction", ctypes.c_double), ("ix0", ctypes.c_int64),
+                ("ix1", ctypes.c_int64), ("iy0", ctypes.c_int64), ("iy1", ctypes.c_int64),
+                ("seed", ctypes.c_uint64)]
 
 
 class MaxCoverError(RuntimeError):
@@ -97,6 +111,17 @@ def _declare(L: ctypes.CDLL) -> None:
                                    ctypes.c_double, _i64, _vp, _vp, _vp], _i32),
         "mac_cover_threshold": ([ctypes.c_double], ctypes.c_double),
         "mac_profile_read": ([_vp, _dp, _i64p, _i64p, ctypes.POINTER(_i32), _i32], _i32),
+        "mac_append_points_f64": ([_vp, _dp, _dp, _dp, _i64], _i32),
+        "mac_append_points_dev_f64": ([_vp, _vp, _vp, _vp, _i64], _i32),
+        "mac_fire_last_error": ([], ctypes.c_char_p),
+        "mac_fire_thresholds": ([ctypes.POINTER(FireParams), _dp], None),
+        "mac_fire_create": ([ctypes.POINTER(_vp), _i32, ctypes.POINTER(FireParams)], _i32),
+        "mac_fire_destroy": ([_vp], None),
+        "mac_fire_initial_points": ([_vp, _dp, _i64, _i64p], _i32),
+        "mac_fire_step": ([_vp, _vp, _i64p], _i32),
+        "mac_fire_last_points": ([_vp, _dp, _i64, _i64p], _i32),
+        "mac_fire_get_grid": ([_vp, _u8p], _i32),
+        "mac_fire_set_grid": ([_vp, _u8p], _i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -239,6 +264,17 @@ class Context:
         n = int(M if M is not None else x.numel())
         _check(self._L.mac_set_points_dev_f64(self._h, _devptr(x), _devptr(y), _devptr(w), n))
 
+    def append_points(self, x, y, w) -> None:
+        """update_POI (src/CellFunctions.jl:59-79): entries appended at the end of the list."""
+        x, y, w = _f64(x), _f64(y), _f64(w)
+        if not (x.size == y.size == w.size):
+            raise ValueError("x, y, w lengths differ")
+        _check(self._L.mac_append_points_f64(self._h, _ptr(x), _ptr(y), _ptr(w), x.size))
+
+    def append_points_device(self, x, y, w, m: int | None = None) -> None:
+        m = int(x.numel() if m is None else m)
+        _check(self._L.mac_append_points_dev_f64(self._h, _devptr(x), _devptr(y), _devptr(w), m))
+
     @property
     def num_points(self) -> int:
         m = _i64()
@@ -328,6 +364,81 @@ class Context:
             self._h, _devptr(d_cands), int(three_n), int(K), _devptr(d_rmax), float(penalty),
             _devptr(d_prev), _devptr(d_dlim), float(tan_half_fov), int(idx_base),
             _devptr(d_obj), _devptr(d_best), _devptr(stream)))
+
+
+def _fcheck(rc: int) -> None:
+    if rc != MAC_OK:
+        raise MaxCoverError(rc, load_library().mac_fire_last_error().decode(errors="replace"))
+
+
+class Fire:
+    """The GPU cellular-automaton fire of src/DynamicArea.jl (mac_fire_*, include/maxcover.h).
+
+    ``ignition`` = (ix0, ix1, iy0, iy1): 1-based inclusive cell block set on fire (:35)."""
+
+    def __init__(self, nx: int, ny: int, dx: float, dy: float, forest_density: float,
+                 prob_spread: float, wind_speed: float, wind_direction: float, ignition,
+                 seed: int, device: int = 0):
+        L = load_library()
+        self._L = L
+        ix0, ix1, iy0, iy1 = (int(v) for v in ignition)
+        self.params = FireParams(int(nx), int(ny), float(dx), float(dy), float(forest_density),
+                                 float(prob_spread), float(wind_speed), float(wind_direction),
+                                 ix0, ix1, iy0, iy1, int(seed) & (2**64 - 1))
+        h = _vp()
+        _fcheck(L.mac_fire_create(ctypes.byref(h), int(device), ctypes.byref(self.params)))
+        self._h = h
+        self.nx, self.ny = int(nx), int(ny)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.mac_fire_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def thresholds(self) -> np.ndarray:
+        out = np.zeros(9)
+        self._L.mac_fire_thresholds(ctypes.byref(self.params), _ptr(out))
+        return out
+
+    def initial_points(self) -> np.ndarray:
+        n = _i64()
+        _fcheck(self._L.mac_fire_initial_points(self._h, None, 0, ctypes.byref(n)))
+        rec = np.zeros((max(n.value, 1), 5))
+        _fcheck(self._L.mac_fire_initial_points(self._h, _ptr(rec), n.value, ctypes.byref(n)))
+        return rec[: n.value]
+
+    def step(self, append_to: Context | None = None) -> int:
+        """One update_grid step (:52-72); the new points are appended to ``append_to``'s list
+        (update_POI) when given. Returns how many points were pushed."""
+        n = _i64()
+        ctx = append_to._h if append_to is not None else None
+        _fcheck(self._L.mac_fire_step(self._h, ctx, ctypes.byref(n)))
+        return int(n.value)
+
+    def last_points(self) -> np.ndarray:
+        """The last step's points as (n, 5) records, in the reference's push order."""
+        n = _i64()
+        _fcheck(self._L.mac_fire_last_points(self._h, None, 0, ctypes.byref(n)))
+        rec = np.zeros((max(n.value, 1), 5))
+        _fcheck(self._L.mac_fire_last_points(self._h, _ptr(rec), n.value, ctypes.byref(n)))
+        return rec[: n.value]
+
+    def grid(self) -> np.ndarray:
+        g = np.empty(self.nx * self.ny, dtype=np.uint8)
+        _fcheck(self._L.mac_fire_get_grid(self._h, g.ctypes.data_as(_u8p)))
+        return g.reshape(self.nx, self.ny)
+
+    def set_grid(self, g) -> None:
+        g = np.ascontiguousarray(np.asarray(g, dtype=np.uint8).reshape(-1))
+        if g.size != self.nx * self.ny:
+            raise ValueError("grid size mismatch")
+        _fcheck(self._L.mac_fire_set_grid(self._h, g.ctypes.data_as(_u8p)))
 
 
 _default_ctx = None

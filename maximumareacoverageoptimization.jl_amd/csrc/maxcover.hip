@@ -788,6 +788,60 @@ int32_t mac_set_points_dev_f64(mac_ctx* ctx, const double* d_x, const double* d_
     ABI_END
 }
 
+// update_POI (src/CellFunctions.jl:59-79): the list grows at its end; the existing entries keep
+// their positions (list order = summation order), then the tile index is rebuilt.
+static int32_t append_common(mac_ctx* ctx, const void* x, const void* y, const void* w, int64_t m,
+                             hipMemcpyKind kind)
+{
+    if (!ctx) return fail(MAC_E_INVAL, "null context");
+    if (m < 0) return fail(MAC_E_INVAL, "m < 0");
+    if (m > 0 && (!x || !y || !w)) return fail(MAC_E_INVAL, "null point array");
+    const int64_t M0 = ctx->has_points ? ctx->M : 0;
+    int32_t rc = check_M(M0 + m);
+    if (rc) return rc;
+    set_device(ctx);
+    HCK(hipDeviceSynchronize());  // no evaluation may overlap a point-list change
+    hipStream_t s = ctx->setup_stream;
+    const size_t need = sizeof(double) * (size_t)std::max<int64_t>(M0 + m, 1);
+    if (need > ctx->x.cap) {      // grow by 1.5x, keeping the existing entries
+        const size_t b = std::max(need, ctx->x.cap + ctx->x.cap / 2);
+        for (DevBuf* d : {&ctx->x, &ctx->y, &ctx->w}) {
+            DevBuf nb;
+            nb.reserve(b);
+            if (M0 > 0) HCK(hipMemcpyAsync(nb.p, d->p, sizeof(double) * M0, hipMemcpyDeviceToDevice, s));
+            HCK(hipStreamSynchronize(s));
+            d->release();
+            *d = nb;
+            nb.p = nullptr;
+            nb.cap = 0;
+        }
+    }
+    if (m > 0) {
+        HCK(hipMemcpyAsync(ctx->x.as<double>() + M0, x, sizeof(double) * m, kind, s));
+        HCK(hipMemcpyAsync(ctx->y.as<double>() + M0, y, sizeof(double) * m, kind, s));
+        HCK(hipMemcpyAsync(ctx->w.as<double>() + M0, w, sizeof(double) * m, kind, s));
+    }
+    ctx->M = M0 + m;
+    build_index(ctx, s);
+    return MAC_OK;
+}
+
+int32_t mac_append_points_f64(mac_ctx* ctx, const double* x, const double* y, const double* w,
+                              int64_t m)
+{
+    ABI_BEGIN
+    return append_common(ctx, x, y, w, m, hipMemcpyHostToDevice);
+    ABI_END
+}
+
+int32_t mac_append_points_dev_f64(mac_ctx* ctx, const double* d_x, const double* d_y,
+                                  const double* d_w, int64_t m)
+{
+    ABI_BEGIN
+    return append_common(ctx, d_x, d_y, d_w, m, hipMemcpyDeviceToDevice);
+    ABI_END
+}
+
 int32_t mac_num_points(mac_ctx* ctx, int64_t* M_out)
 {
     if (!ctx || !M_out) return fail(MAC_E_INVAL, "null argument");

@@ -143,15 +143,6 @@ def load_firepoints(path: str):
     """FirePoints table (tests/golden/firepoints.csv, converted from src/FirePoints.xlsx):
     one line per xlsx row = timestep, flat groups of 5 [x, y, area, importance, covered]
     (src/DynamicArea.jl:100-108, read as in src/CellFunctions.jl:36-41). Returns a list of
-    (n_i x 5) arrays."""
-    rows = []
-    with open(path) as f:
-        for line in f:
-            line = line.strip()
-            if not line or line.startswith("#"):
-                continue
-            vals = np.array([float(v) for v in line.split(",")], dtype=np.float64)
-            if vals.size % 5:
-                raise ValueError("FirePoints row length is not a multiple of 5")
-            rows.append(vals.reshape(-1, 5))
-    return rows
+    (n_i x 5) arrays (firepoints.read_csv)."""
+    from .firepoints import read_csv
+    return read_csv(path)

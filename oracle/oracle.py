@@ -80,6 +80,16 @@ def lib() -> ctypes.CDLL:
         L.ref_allocate_even_circles.argtypes = [ctypes.c_double, ctypes.c_int64, ctypes.c_double,
                                                 ctypes.c_double, ctypes.c_double, _dp]
         L.ref_allocate_even_circles.restype = None
+        _u8 = ctypes.POINTER(ctypes.c_uint8)
+        L.ref_fire_thresholds.argtypes = [ctypes.c_double] * 3 + [_dp]
+        L.ref_fire_thresholds.restype = None
+        L.ref_fire_init.argtypes = [_u8, ctypes.c_int64, ctypes.c_int64, ctypes.c_double,
+                                    ctypes.c_uint64] + [ctypes.c_int64] * 4
+        L.ref_fire_init.restype = None
+        L.ref_fire_step.argtypes = [_u8, _u8, ctypes.c_int64, ctypes.c_int64, _dp, ctypes.c_double,
+                                    ctypes.c_double, ctypes.c_uint64, ctypes.c_uint64, _dp,
+                                    ctypes.c_int64]
+        L.ref_fire_step.restype = ctypes.c_int64
         _LIB = L
     return _LIB
 
@@ -307,3 +317,31 @@ def lattice_count_fast(circles_int, G: int, pitch: int = 5) -> int:
         dy = ((2 * jj - 1) * pitch - 2 * cy)[None, :]
         cov[i0 - 1:i1, j0 - 1:j1] |= (dx * dx + dy * dy) < 4 * R * R
     return int(cov.sum())
+
+
+class RefFire:
+    """src/DynamicArea.jl restated in C (ref_fire_*): the CPU checker of the GPU fire generator."""
+
+    def __init__(self, nx, ny, dx=5.0, dy=5.0, forest_density=0.7, prob_spread=0.5, wind_speed=4.0,
+                 wind_direction=math.radians(270), ignition=(40, 60, 69, 71), seed=20250216):
+        self.nx, self.ny, self.dx, self.dy, self.seed = int(nx), int(ny), float(dx), float(dy), seed
+        self.p9 = np.zeros(9)
+        lib().ref_fire_thresholds(wind_speed, wind_direction, prob_spread, _p(self.p9))
+        self.grid = np.zeros(self.nx * self.ny, dtype=np.uint8)
+        ix0, ix1, iy0, iy1 = ignition
+        lib().ref_fire_init(self.grid.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), self.nx,
+                            self.ny, forest_density, seed, ix0, ix1, iy0, iy1)
+        self.t = 0
+
+    def step(self) -> np.ndarray:
+        """One update_grid (:52-72); returns the pushed points as (n, 5) records."""
+        self.t += 1
+        gn = np.empty_like(self.grid)
+        u8 = ctypes.POINTER(ctypes.c_uint8)
+        n = lib().ref_fire_step(self.grid.ctypes.data_as(u8), gn.ctypes.data_as(u8), self.nx,
+                                self.ny, _p(self.p9), self.dx, self.dy, self.seed, self.t, None, 0)
+        rec = np.zeros((max(n, 1), 5))
+        lib().ref_fire_step(self.grid.ctypes.data_as(u8), gn.ctypes.data_as(u8), self.nx, self.ny,
+                            _p(self.p9), self.dx, self.dy, self.seed, self.t, _p(rec), n)
+        self.grid = gn
+        return rec[:n]

@@ -207,3 +207,82 @@ void ref_allocate_even_circles(double r_centering, int64_t N, double r_uav, doub
         out[2 * N + i] = r_uav;
     }
 }
+
+/* ---- src/DynamicArea.jl: cellular-automaton fire (config 5 point stream) ----------------
+ * The reference draws with an unseeded rand(); the restatement (and the GPU generator) draw
+ * u = hash(seed, step t, cell, neighbour slot q) so that runs are reproducible. The hash is
+ * part of this build's specification (splitmix64 finaliser over a keyed counter). */
+static uint64_t ref_mix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+double ref_fire_uniform(uint64_t seed, uint64_t t, uint64_t cell, uint64_t q)
+{
+    uint64_t z = seed ^ (t * 0xD1B54A32D192ED03ull);
+    z ^= (cell * 9ull + q) * 0x9E3779B97F4A7C15ull;
+    return (double)(ref_mix64(z) >> 11) * 0x1p-53;
+}
+
+/* :63 — the spread threshold of block position (r, c), 1-based: slot q = (c-1)*3 + (r-1)
+ * (findall's column-major order over grid[i-1:i+1, j-1:j+1]). */
+void ref_fire_thresholds(double wind_speed, double wind_direction, double prob_spread, double* p9)
+{
+    for (int c = 1; c <= 3; ++c)
+        for (int r = 1; r <= 3; ++r)
+            p9[(c - 1) * 3 + (r - 1)] =
+                wind_speed * cos(wind_direction - atan2((double)(2 - c), (double)(2 - r))) * prob_spread;
+}
+
+/* :26-35 — grid[i,j] (1-based, row-major storage (i-1)*ny + (j-1)): TREE (1) when
+ * u(seed, 0, cell, 0) < density else EMPTY (0); the ignition block set to FIRE (2). */
+void ref_fire_init(uint8_t* g, int64_t nx, int64_t ny, double density, uint64_t seed, int64_t ix0,
+                   int64_t ix1, int64_t iy0, int64_t iy1)
+{
+    for (int64_t i = 1; i <= nx; ++i)
+        for (int64_t j = 1; j <= ny; ++j) {
+            const int64_t cell = (i - 1) * ny + (j - 1);
+            g[cell] = ref_fire_uniform(seed, 0, (uint64_t)cell, 0) < density ? 1 : 0;
+        }
+    for (int64_t i = ix0; i <= ix1; ++i)
+        for (int64_t j = iy0; j <= iy1; ++j) g[(i - 1) * ny + (j - 1)] = 2;
+}
+
+/* :52-72 — update_grid: new_grid = copy(grid); for i in 2:nx-1, j in 2:ny-1 (i outer): a TREE
+ * cell with FIRE in its 3x3 block tests each FIRE position in column-major order; success ->
+ * new_grid[i,j] = FIRE and push!(points, i*dx - dx/2, j*dy - dy/2, dx*dy, dx*dy, false).
+ * `gn` receives the new grid; rec (nullable) up to cap records of 5 doubles. Returns the number
+ * of points pushed. */
+int64_t ref_fire_step(const uint8_t* g, uint8_t* gn, int64_t nx, int64_t ny, const double* p9,
+                      double dx, double dy, uint64_t seed, uint64_t t, double* rec, int64_t cap)
+{
+    int64_t n = 0;
+    memcpy(gn, g, (size_t)(nx * ny));
+    for (int64_t i = 2; i <= nx - 1; ++i) {
+        for (int64_t j = 2; j <= ny - 1; ++j) {
+            const int64_t cell = (i - 1) * ny + (j - 1);
+            if (g[cell] != 1) continue;
+            for (int c = 1; c <= 3; ++c) {           /* findall: column-major over the block */
+                for (int r = 1; r <= 3; ++r) {
+                    if (g[(i - 3 + r) * ny + (j - 3 + c)] != 2) continue;  /* grid[i-2+r, j-2+c], 1-based */
+                    const int q = (c - 1) * 3 + (r - 1);
+                    if (p9[q] > ref_fire_uniform(seed, t, (uint64_t)cell, (uint64_t)q)) {
+                        gn[cell] = 2;
+                        if (rec && n < cap) {
+                            double* o = rec + 5 * n;
+                            o[0] = (double)i * dx - dx / 2;
+                            o[1] = (double)j * dy - dy / 2;
+                            o[2] = dx * dy;
+                            o[3] = dx * dy;
+                            o[4] = 0.0;
+                        }
+                        ++n;
+                    }
+                }
+            }
+        }
+    }
+    return n;
+}

@@ -1,0 +1,151 @@
+"""Fire stream (config 5): the CA fire generator of src/DynamicArea.jl
+on the GPU vs its C restatement, appending points to a context (update_POI), and the
+FirePoints table converter."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+
+
+def _refire(orc, nx, ny, ign, seed, **kw):
+    return orc.RefFire(nx, ny, ignition=ign, seed=seed, **kw)
+
+
+# ---------------------------------------------------------------------------- CPU: the oracle
+
+def test_ref_fire_semantics(orc):
+    """Properties of the restated rules (:52-72): border cells never change; FIRE persists;
+    every pushed point sits on a cell that turned TREE -> FIRE this step, once per igniting
+    neighbour; points come in i-outer / j-inner cell order."""
+    nx, ny = 40, 30
+    f = _refire(orc, nx, ny, (18, 22, 14, 16), 7)
+    g0 = f.grid.reshape(nx, ny).copy()
+    total = 0
+    for _ in range(12):
+        before = f.grid.reshape(nx, ny).copy()
+        pts = f.step()
+        after = f.grid.reshape(nx, ny)
+        assert np.array_equal(after[0], before[0]) and np.array_equal(after[-1], before[-1])
+        assert np.array_equal(after[:, 0], before[:, 0]) and np.array_equal(after[:, -1], before[:, -1])
+        assert np.all(after[before == 2] == 2)
+        newly = (before == 1) & (after == 2)
+        i = np.rint((pts[:, 0] + 2.5) / 5).astype(int)
+        j = np.rint((pts[:, 1] + 2.5) / 5).astype(int)
+        assert np.all(newly[i - 1, j - 1])
+        cells = sorted(set(zip(i.tolist(), j.tolist())))
+        assert len(cells) == int(newly.sum())
+        order = (i - 1) * ny + (j - 1)
+        assert np.all(np.diff(order) >= 0)
+        for (ci, cj) in cells:                       # at most one point per FIRE neighbour
+            k = int(np.sum((i == ci) & (j == cj)))
+            block = before[ci - 2:ci + 1, cj - 2:cj + 1]
+            assert 1 <= k <= int(np.sum(block == 2))
+        assert np.all(pts[:, 2] == 25.0) and np.all(pts[:, 3] == 25.0) and np.all(pts[:, 4] == 0)
+        total += pts.shape[0]
+    assert total > 0 and not np.array_equal(g0, f.grid.reshape(nx, ny))
+
+
+def test_ref_fire_wind_thresholds(orc):
+    """:63 with the reference's wind (4, 270 deg) and prob_spread 0.5: the nine thresholds
+    2*cos(3pi/2 - atan(2-c, 2-r)) — up-wind slots always ignite (> 1), cross-wind ones at 0."""
+    f = _refire(orc, 10, 10, (4, 5, 4, 5), 1)
+    want = np.array([4 * math.cos(math.radians(270) - math.atan2(2 - c, 2 - r)) * 0.5
+                     for c in (1, 2, 3) for r in (1, 2, 3)])
+    assert np.array_equal(f.p9, want)
+
+
+def test_firepoints_converter_roundtrip(pkg, firepoints, tmp_path):
+    fp = pkg.firepoints
+    rows = firepoints + [np.zeros((0, 5))] + firepoints[:2]     # an empty timestep in the middle
+    p = fp.write_csv(rows, str(tmp_path / "fp.csv"), source="test")
+    back = fp.read_csv(p)
+    assert len(back) == len(rows)
+    assert all(np.array_equal(a, b) for a, b in zip(rows, back))
+    assert back[len(firepoints)].shape == (0, 5)
+
+
+@pytest.mark.skipif(not os.path.exists("/root/reference/src/FirePoints.xlsx"),
+                    reason="reference data not present (build container only)")
+def test_firepoints_xlsx_reader_matches_fixture(pkg, firepoints):
+    rows = pkg.firepoints.read_xlsx("/root/reference/src/FirePoints.xlsx")
+    assert len(rows) == len(firepoints) == 68
+    assert all(np.array_equal(a, b) for a, b in zip(rows, firepoints))
+
+
+# ---------------------------------------------------------------------------- GPU
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,ign,seed", [((80, 60), (30, 40, 25, 28), 11),
+                                            ((100, 100), (40, 60, 69, 71), 20250216),
+                                            ((257, 131), (100, 140, 60, 70), 3)])
+def test_fire_gpu_matches_oracle(pkg, orc, shape, ign, seed):
+    nx, ny = shape
+    kw = dict(forest_density=0.7, prob_spread=0.5, wind_speed=4.0, wind_direction=math.radians(270))
+    ref = _refire(orc, nx, ny, ign, seed, **kw)
+    gpu = pkg.Fire(nx, ny, 5.0, 5.0, kw["forest_density"], kw["prob_spread"], kw["wind_speed"],
+                   kw["wind_direction"], ign, seed)
+    assert np.array_equal(gpu.thresholds(), ref.p9)
+    assert np.array_equal(gpu.grid().reshape(-1), ref.grid)
+    for t in range(25):
+        want = ref.step()
+        n = gpu.step()
+        assert n == want.shape[0], t
+        assert np.array_equal(gpu.last_points(), want), t
+        assert np.array_equal(gpu.grid().reshape(-1), ref.grid), t
+    gpu.close()
+
+
+@pytest.mark.gpu
+def test_dynamic_area_defaults(pkg, orc):
+    """The reference's parameters (100 x 100 cells, ignition [40,60] x [69,71], wind 270 deg):
+    initial points (:37-42) and 20 steps, exported like export_data."""
+    D = pkg.DynamicArea.DynamicArea()
+    assert D.grid_size == (100, 100) and D.ignition == (40, 60, 69, 71)
+    init = D.export_data[0]
+    assert init.shape == (21 * 3, 5)
+    assert np.array_equal(init[:3, :2], [[197.5, 342.5], [202.5, 342.5], [207.5, 342.5]])
+    ref = _refire(orc, 100, 100, (40, 60, 69, 71), pkg.DynamicArea.SEED)
+    rows = D.run(20)
+    for t in range(1, 21):
+        assert np.array_equal(rows[t], ref.step()), t
+    D.close()
+
+
+@pytest.mark.gpu
+def test_append_points_and_stream(ctx, pkg, orc):
+    """update_POI appends at the end of the list (list order = summation order); a fire
+    streaming into the context gives the same list, areas and removal as the oracle."""
+    rng = pkg.workloads.SplitMix64(55)
+    a = np.stack([rng.uniform(3000) * 400, rng.uniform(3000) * 400], axis=1)
+    b = np.stack([rng.uniform(1500) * 400, rng.uniform(1500) * 400], axis=1)
+    wa = rng.uniform(3000) + 1.0
+    wb = rng.uniform(1500) + 1.0
+    ctx.set_points(a[:, 0], a[:, 1], wa)
+    ctx.append_points(b[:, 0], b[:, 1], wb)
+    x, y, w = ctx.get_points()
+    assert np.array_equal(x, np.concatenate([a[:, 0], b[:, 0]]))
+    assert np.array_equal(w, np.concatenate([wa, wb]))
+    rec = np.stack([x, y, w, w, np.zeros_like(x)], axis=1)
+    C = np.concatenate([np.concatenate([rng.uniform(6) * 400, rng.uniform(6) * 400,
+                                        rng.uniform(6) * 40 + 10])[None, :] for _ in range(5)])
+    want = orc.PointerList(rec).area_batch(C)
+    np.testing.assert_allclose(ctx.area_batch(C), want, rtol=1e-12, atol=0)
+
+    # a fire streaming into a context: initial points, then each step appended on the device
+    fire = pkg.Fire(90, 90, 5.0, 5.0, 0.7, 0.5, 4.0, math.radians(270), (35, 50, 40, 45), 99)
+    init = fire.initial_points()
+    ctx.set_points_records(init)
+    lst = [init]
+    for _ in range(15):
+        fire.step(append_to=ctx)
+        lst.append(fire.last_points())
+    full = np.concatenate(lst)
+    x, y, w = ctx.get_points()
+    assert np.array_equal(np.stack([x, y], axis=1), full[:, :2])
+    circles = np.array([200.0, 240.0, 180.0, 210.0, 230.0, 260.0, 36.0, 36.0, 30.0])
+    assert ctx.area(circles) == orc.ref_area(circles, full)
+    kept = ctx.remove_covered(circles)
+    assert np.array_equal(kept, orc.ref_remove_covered(circles, full))
+    fire.close()
