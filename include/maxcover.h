@@ -129,6 +129,34 @@ int32_t mac_poll_best_f64(mac_ctx* ctx, const double* cands, int64_t three_n, in
                           const double* prev, const double* d_lim, double tan_half_fov,
                           double* obj_out, double* best_obj, int64_t* best_idx);
 
+/* ---- native MADS driver ------------------------------------------ */
+/* A granular MADS with a complete LTMADS poll, the restatement of DirectSearch's Optimize!
+ * (src/TDM_STATIC_opt.jl:118-169; the third-party algorithm is not vendored, so this is the
+ * build's own, parity-tested against maximumareacoverageoptimization.jl_amd/TDM_STATIC_opt.mads):
+ *   f = objective(x0) (+inf if x0 fails cons3); ell = ell0; per iteration (at most n_iter,
+ *   while ell >= 0): B = L[rp][:, cp] with L lower triangular (diagonal +-2^ell, strictly lower
+ *   uniform integers in [-(2^ell-1), 2^ell-1]) and random row / column permutations, all drawn
+ *   from a splitmix64 stream seeded with `seed`; the 2n candidates x + B[:,k], x - B[:,k] are
+ *   generated ON THE DEVICE (no candidate matrix), evaluated with the objective and cons3 as an
+ *   extreme barrier; success (best < f): x, f <- best, ell <- min(ell + 1, ell_max); else
+ *   ell <- ell - 1. One 16-byte read-back per iteration. */
+typedef struct mac_mads_params {
+    int64_t n_iter;        /* iteration limit (SetIterationLimit, 100 in the reference)      */
+    int32_t ell0, ell_max; /* initial / largest mesh exponent (0 <= ell0 <= ell_max <= 52)    */
+    uint64_t seed;
+} mac_mads_params;
+typedef struct mac_mads_stats {
+    double f;              /* objective at x_out (+inf: no feasible point found)              */
+    int64_t iterations;
+    int64_t evaluations;   /* 1 + 2n per iteration                                            */
+    int32_t status;        /* 0: mesh precision limit (ell < 0); 1: iteration limit           */
+    int32_t feasible;
+    double seconds;        /* wall time inside the call                                       */
+} mac_mads_stats;
+int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const double* r_max,
+                     double penalty, const double* prev, const double* d_lim, double tan_half_fov,
+                     const mac_mads_params* params, double* x_out, mac_mads_stats* stats);
+
 /* ---- device-pointer, stream-ordered variants (inputs already resident in HBM) ----- */
 /* d_cands: 3N x K column-major on the context's device; d_area: K doubles. `stream` is a
  * hipStream_t (NULL = the context's own stream). Returns after enqueueing. */

@@ -16,7 +16,7 @@ is what the parity tests exercise. See INTEGRATION.md.
 module MaxCoverAMD
 
 export MacContext, set_points!, calculateArea, createObjective, objective_batch, poll_best,
-       rmvCoveredPOI!, area_batch
+       rmvCoveredPOI!, area_batch, mads_run
 
 const libmaxcover = get(ENV, "MAXCOVER_LIB",
     joinpath(@__DIR__, "..", "maximumareacoverageoptimization.jl_amd", "libmaxcover.so"))
@@ -153,6 +153,46 @@ function poll_best(cands::Matrix{Float64}, r_max::Vector{Float64}, ctx::MacConte
                     objs, bo, bi))
     end
     return bo[], bi[] + 1, objs
+end
+
+struct MadsParams
+    n_iter::Int64
+    ell0::Int32
+    ell_max::Int32
+    seed::UInt64
+end
+struct MadsStats
+    f::Float64
+    iterations::Int64
+    evaluations::Int64
+    status::Int32
+    feasible::Int32
+    seconds::Float64
+end
+
+"""
+mads_run(x0, r_max, ctx; prev, d_lim, tan_half_fov, n_iter, ell0, ell_max, seed) — the whole
+granular-MADS loop inside libmaxcover (complete LTMADS poll generated on the device, cons3 as
+extreme barrier): the batched stand-in for TDM_STATIC_opt.optimize (src/TDM_STATIC_opt.jl:118-169).
+Returns (x, stats::MadsStats).
+"""
+function mads_run(x0::Vector{Float64}, r_max::Vector{Float64}, ctx::MacContext;
+                  penalty::Float64 = 1e5, prev::Union{Nothing,Vector{Float64}} = nothing,
+                  d_lim::Union{Nothing,Vector{Float64}} = nothing, tan_half_fov::Float64 = 1.0,
+                  n_iter::Integer = 100, ell0::Integer = 2, ell_max::Integer = 6,
+                  seed::Integer = 20250216)
+    x = similar(x0)
+    prm = Ref(MadsParams(n_iter, ell0, ell_max, UInt64(seed)))
+    st = Ref{MadsStats}()
+    pprev = prev === nothing ? Ptr{Float64}(C_NULL) : pointer(prev)
+    pdlim = d_lim === nothing ? Ptr{Float64}(C_NULL) : pointer(d_lim)
+    GC.@preserve prev d_lim begin
+        check(ccall((:mac_mads_run, libmaxcover), Int32,
+                    (Ptr{Cvoid}, Ptr{Float64}, Int64, Ptr{Float64}, Float64, Ptr{Float64},
+                     Ptr{Float64}, Float64, Ref{MadsParams}, Ptr{Float64}, Ref{MadsStats}),
+                    ctx, x0, length(x0), r_max, penalty, pprev, pdlim, tan_half_fov, prm, x, st))
+    end
+    return x, st[]
 end
 
 """

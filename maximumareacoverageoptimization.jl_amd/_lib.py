@@ -46,11 +46,24 @@ EXPORTS = (
     "mac_remove_covered_f64", "mac_covered_flags_f64", "mac_area_f64", "mac_area_batch_f64",
     "mac_objective_batch_f64", "mac_poll_best_f64", "mac_area_batch_dev_f64",
     "mac_poll_best_dev_f64", "mac_cover_threshold", "mac_profile_read",
-    "mac_append_points_f64", "mac_append_points_dev_f64",
+    "mac_append_points_f64", "mac_append_points_dev_f64", "mac_mads_run",
     "mac_fire_last_error", "mac_fire_thresholds", "mac_fire_create", "mac_fire_destroy",
     "mac_fire_initial_points", "mac_fire_step", "mac_fire_last_points", "mac_fire_get_grid",
     "mac_fire_set_grid",
 )
+
+
+class MadsParams(ctypes.Structure):
+    """mac_mads_params (include/maxcover.h)."""
+    _fields_ = [("n_iter", ctypes.c_int64), ("ell0", ctypes.c_int32), ("ell_max", ctypes.c_int32),
+                ("seed", ctypes.c_uint64)]
+
+
+class MadsStats(ctypes.Structure):
+    """mac_mads_stats (include/maxcover.h)."""
+    _fields_ = [("f", ctypes.c_double), ("iterations", ctypes.c_int64),
+                ("evaluations", ctypes.c_int64), ("status", ctypes.c_int32),
+                ("feasible", ctypes.c_int32), ("seconds", ctypes.c_double)]
 
 
 class FireParams(ctypes.Structure):
@@ -112,6 +125,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "mac_cover_threshold": ([ctypes.c_double], ctypes.c_double),
         "mac_profile_read": ([_vp, _dp, _i64p, _i64p, ctypes.POINTER(_i32), _i32], _i32),
         "mac_append_points_f64": ([_vp, _dp, _dp, _dp, _i64], _i32),
+        "mac_mads_run": ([_vp, _dp, _i64, _dp, ctypes.c_double, _dp, _dp, ctypes.c_double,
+                          ctypes.POINTER(MadsParams), _dp, ctypes.POINTER(MadsStats)], _i32),
         "mac_append_points_dev_f64": ([_vp, _vp, _vp, _vp, _i64], _i32),
         "mac_fire_last_error": ([], ctypes.c_char_p),
         "mac_fire_thresholds": ([ctypes.POINTER(FireParams), _dp], None),
@@ -351,6 +366,25 @@ class Context:
         if want_all:
             return bo.value, int(bi.value), objs
         return bo.value, int(bi.value)
+
+    # -- native MADS driver
+    def mads_run(self, x0, r_max, penalty: float = 1e5, prev=None, d_lim=None,
+                 tan_half_fov: float = 1.0, n_iter: int = 100, ell0: int = 2, ell_max: int = 6,
+                 seed: int = 20250216):
+        """mac_mads_run: the whole MADS loop in libmaxcover (candidates generated on the device).
+        Returns (x, stats dict)."""
+        x = _f64(x0)
+        rm = _f64(r_max)
+        pv = _f64(prev) if prev is not None else None
+        dl = _f64(d_lim) if d_lim is not None else None
+        out = np.empty_like(x)
+        prm = MadsParams(int(n_iter), int(ell0), int(ell_max), int(seed) & (2**64 - 1))
+        st = MadsStats()
+        _check(self._L.mac_mads_run(self._h, _ptr(x), x.size, _ptr(rm), float(penalty),
+                                    _ptr(pv) if pv is not None else None,
+                                    _ptr(dl) if dl is not None else None, float(tan_half_fov),
+                                    ctypes.byref(prm), _ptr(out), ctypes.byref(st)))
+        return out, {k: getattr(st, k) for k, _ in MadsStats._fields_}
 
     # -- device-resident, stream-ordered
     def area_batch_dev(self, d_cands, three_n: int, K: int, d_area, stream=None) -> None:

@@ -39,28 +39,79 @@ __device__ __forceinline__ double pen_term(double x2, double y2, double R2, int 
     return pa.rmax ? __builtin_fabs(R2 - pa.rmax[i]) : 0.0;
 }
 
-// cands: 3N x K column-major (candidate k at cands + k*ldc). Writes disks[k*N + i] (scan walk)
-// and, when pen != null, pen[i*K + k] = pen_term (disk-major, as penalty_chain reads it).
-__global__ void disk_prep_kernel(const double* __restrict__ cands, int N, int ldc, int K,
-                                 DiskRec* __restrict__ disks, PenArgs pa, double* __restrict__ pen)
+// ------------------------------------------------------------------ candidate sources
+
+// splitmix64 stream value number `idx` (1-based) after `state` (workloads.SplitMix64).
+__host__ __device__ __forceinline__ uint64_t splitmix_at(uint64_t state, uint64_t idx)
+{
+    uint64_t z = state + idx * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__host__ __device__ __forceinline__ double splitmix_uniform_at(uint64_t state, uint64_t idx)
+{
+    return (double)(splitmix_at(state, idx) >> 11) * (1.0 / 9007199254740992.0);
+}
+
+// Entry (r, c) of the lower-triangular LTMADS matrix L drawn from the stream at `state`
+// (workloads.ltmads_basis): diagonal sign(u_{r+1} < 0.5 ? -1 : 1) * 2^ell; strictly lower
+// entries uniform integers in [-(2^ell - 1), 2^ell - 1] from stream values n + 1 + r(r-1)/2 + c
+// (numpy's tril_indices order); zero above the diagonal.
+__host__ __device__ __forceinline__ double ltmads_entry(uint64_t state, int64_t n, int64_t b,
+                                                        int64_t r, int64_t c)
+{
+    if (r < c) return 0.0;
+    if (r == c) return (splitmix_uniform_at(state, (uint64_t)r + 1) < 0.5 ? -1.0 : 1.0) * (double)b;
+    const int64_t lo = -b + 1, span = 2 * b - 1;
+    const double u = splitmix_uniform_at(state, (uint64_t)(n + 1 + r * (r - 1) / 2 + c));
+    return (double)(lo + (int64_t)__builtin_floor(u * (double)span));
+}
+
+// Where candidate coordinates come from: a 3N x K column-major matrix (the batch APIs), or a
+// complete LTMADS poll around an incumbent generated on the fly (the native MADS driver):
+// candidate k < n is x + B[:, k], k >= n is x - B[:, k - n], B = L[rp][:, cp] (variable v of a
+// candidate = x_i for v = i, y_i for v = N + i, r_i for v = 2N + i).
+struct CandSrc {
+    const double* cands;   // matrix source when non-null
+    int ldc;
+    const double* xinc;    // generator: incumbent (3N), row / column permutations (n each)
+    const int* rp;
+    const int* cp;
+    uint64_t state;
+    int64_t b;             // 2^ell
+    __device__ __forceinline__ double get(int k, int v, int N) const
+    {
+        if (cands) return cands[(int64_t)k * ldc + v];
+        const int n = 3 * N;
+        const int kk = k < n ? k : k - n;
+        const double d = ltmads_entry(state, n, b, rp[v], cp[kk]);
+        return k < n ? xinc[v] + d : xinc[v] - d;
+    }
+};
+
+// cands: see CandSrc. Writes disks[k*N + i] (scan walk) and, when pen != null,
+// pen[i*K + k] = pen_term (disk-major, as penalty_chain reads it).
+__global__ void disk_prep_kernel(CandSrc src, int N, int K, DiskRec* __restrict__ disks,
+                                 PenArgs pa, double* __restrict__ pen)
 {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (int64_t)N * K) return;
     const int k = (int)(t / N), i = (int)(t % N);
-    const double* c = cands + (int64_t)k * ldc;
-    const double x = c[i], y = c[N + i], r = c[2 * N + i];
+    const double x = src.get(k, i, N), y = src.get(k, N + i, N), r = src.get(k, 2 * N + i, N);
     disks[t] = make_disk(x, y, r);
     if (pen) pen[(int64_t)i * K + k] = pen_term(x, y, r, i, N, pa);
 }
 
 // Transposed prep: disksT[i*K + k] (disk-major, candidates contiguous). 32 x 32 tiles through
-// LDS so both the candidate reads and the record writes are coalesced. Also, per tile:
+// LDS so both the candidate reads (matrix source) and the record writes are coalesced. Also, per tile:
 //   penT[i*K + k] = pen_term (when penT != null), and
 //   regP[kt*N + i], costP[kt*N + i] (kt = blockIdx.y): the union of disk i's tile spans over the
 //   tile's 32 candidates and the sum of their span areas (when regP != null; region_kernel
 //   finishes the reduction over kt).
 __global__ __launch_bounds__(kBlock) void disk_prep_T_kernel(
-    const double* __restrict__ cands, int N, int ldc, int K, DiskRec* __restrict__ disksT,
+    CandSrc src, int N, int K, DiskRec* __restrict__ disksT,
     PenArgs pa, double* __restrict__ penT, Grid g, int4* __restrict__ regP,
     double* __restrict__ costP)
 {
@@ -70,10 +121,9 @@ __global__ __launch_bounds__(kBlock) void disk_prep_T_kernel(
     for (int kk = ty; kk < 32; kk += 8) {
         const int k = k0 + kk, i = i0 + tx;
         if (k < K && i < N) {
-            const double* c = cands + (int64_t)k * ldc;
-            sx[kk][tx] = c[i];
-            sy[kk][tx] = c[N + i];
-            sr[kk][tx] = c[2 * N + i];
+            sx[kk][tx] = src.get(k, i, N);
+            sy[kk][tx] = src.get(k, N + i, N);
+            sr[kk][tx] = src.get(k, 2 * N + i, N);
         }
     }
     __syncthreads();

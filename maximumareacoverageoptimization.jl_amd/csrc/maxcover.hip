@@ -7,6 +7,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -96,7 +97,7 @@ struct Lane {
     hipStream_t last = nullptr;   // stream of the most recent use
     hipEvent_t done = nullptr;
     DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode, pen, nbr,
-        ncount, dlist, regP, costP, spart, vp;
+        ncount, dlist, regP, costP, spart, vp, xinc, perm;
     std::vector<double> h_dlim;
 };
 
@@ -185,6 +186,14 @@ struct LaneGuard {
 };
 
 static inline unsigned grid1d(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
+
+static inline CandSrc matrix_src(const double* d_cands, int N)
+{
+    CandSrc c{};
+    c.cands = d_cands;
+    c.ldc = 3 * N;
+    return c;
+}
 
 // ------------------------------------------------------------------ point list set-up
 
@@ -325,12 +334,11 @@ static bool use_tiled(mac_ctx* ctx, int N, const double* h_cands, int64_t three_
 
 // Enqueue disk prep + coverage + finalize (+ argmin) on stream s. All pointers device.
 // area_out/obj_out may be null; best may be null.
-static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_cands, int N,
+static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& src, int N,
                          int K, bool tiled, const double* d_rmax, double penalty,
                          const double* d_prev, const double* d_dlimT, double tan_half_fov,
                          double* d_area, double* d_obj, double* d_best, int64_t idx_base)
 {
-    const int ldc = 3 * N;
     const int64_t M = ctx->M;
     int n_poll = N, n_other = 1;
     const int* d_mode = nullptr;
@@ -381,13 +389,13 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_c
         if (d_pen) {
             L->disks.reserve(sizeof(DiskRec) * (size_t)N * K);
             hipLaunchKernelGGL(disk_prep_kernel, dim3(grid1d((int64_t)N * K, 256)), dim3(256), 0, s,
-                               d_cands, N, ldc, K, L->disks.as<DiskRec>(), pa, d_pen);
+                               src, N, K, L->disks.as<DiskRec>(), pa, d_pen);
             HCK(hipGetLastError());
         }
     } else if (!tiled) {
         L->disks.reserve(sizeof(DiskRec) * (size_t)N * K);
         hipLaunchKernelGGL(disk_prep_kernel, dim3(grid1d((int64_t)N * K, 256)), dim3(256), 0, s,
-                           d_cands, N, ldc, K, L->disks.as<DiskRec>(), pa, d_pen);
+                           src, N, K, L->disks.as<DiskRec>(), pa, d_pen);
         HCK(hipGetLastError());
         constexpr int KB = 4, PPT = 4;
         const int64_t per_pass = (int64_t)kBlock * PPT;
@@ -415,8 +423,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const double* d_c
             L->regP.reserve(sizeof(int4) * (size_t)N * KT);
             L->costP.reserve(sizeof(double) * (size_t)N * KT);
         }
-        hipLaunchKernelGGL(disk_prep_T_kernel, dim3((N + 31) / 32, KT), dim3(kBlock), 0, s, d_cands,
-                           N, ldc, K, L->disks.as<DiskRec>(), pa, d_pen, ctx->grid,
+        hipLaunchKernelGGL(disk_prep_T_kernel, dim3((N + 31) / 32, KT), dim3(kBlock), 0, s, src,
+                           N, K, L->disks.as<DiskRec>(), pa, d_pen, ctx->grid,
                            poll_possible ? L->regP.as<int4>() : nullptr,
                            poll_possible ? L->costP.as<double>() : nullptr);
         HCK(hipGetLastError());
@@ -553,7 +561,7 @@ static int32_t host_eval(mac_ctx* ctx, const double* cands, int64_t three_n, int
         d_dlimT = L->dlim.as<double>();
     }
     const bool tiled = use_tiled(ctx, N, cands, three_n);
-    enqueue_eval(ctx, L, s, L->cands.as<double>(), N, (int)K, tiled, d_rmax, penalty, d_prev,
+    enqueue_eval(ctx, L, s, matrix_src(L->cands.as<double>(), N), N, (int)K, tiled, d_rmax, penalty, d_prev,
                  d_dlimT, tan_half_fov, L->area.as<double>(), want_obj ? L->obj.as<double>() : nullptr,
                  (best_obj || best_idx) ? L->best.as<double>() : nullptr, 0);
     if (area_out)
@@ -674,7 +682,8 @@ void mac_ctx_destroy(mac_ctx* ctx)
     for (Lane* l : ctx->lanes_all) {
         for (DevBuf* b : {&l->cands, &l->disks, &l->partial, &l->area, &l->obj, &l->best,
                           &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->pen, &l->nbr,
-                          &l->ncount, &l->dlist, &l->regP, &l->costP, &l->spart, &l->vp})
+                          &l->ncount, &l->dlist, &l->regP, &l->costP, &l->spart, &l->vp, &l->xinc,
+                          &l->perm})
             b->release();
         if (l->done) (void)hipEventDestroy(l->done);
         if (l->stream) (void)hipStreamDestroy(l->stream);
@@ -880,7 +889,7 @@ static void compute_flags(mac_ctx* ctx, hipStream_t s, const double* circles, in
     if (N > 0) {
         HCK(hipMemcpyAsync(ctx->circ.p, circles, sizeof(double) * 3 * N, hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(disk_prep_kernel, dim3(grid1d(N, 256)), dim3(256), 0, s,
-                           ctx->circ.as<double>(), N, 3 * N, 1, ctx->cdisk.as<DiskRec>(),
+                           matrix_src(ctx->circ.as<double>(), N), N, 1, ctx->cdisk.as<DiskRec>(),
                            PenArgs{nullptr, nullptr, nullptr, 1.0}, nullptr);
         HCK(hipGetLastError());
         const unsigned nb = (unsigned)std::max(1, std::min((N + kWavesPerBlock - 1) / kWavesPerBlock,
@@ -971,6 +980,133 @@ int32_t mac_remove_covered_f64(mac_ctx* ctx, const double* circles, int64_t thre
     ABI_END
 }
 
+// ------------------------------------------------------------------ native MADS driver
+
+// Stable argsort of the next n stream values after stream position `first` - 1 (numpy
+// argsort(kind="stable") of SplitMix64.next_u64(n)).
+static void stream_permutation(uint64_t state, uint64_t first, int n, std::vector<int>& out)
+{
+    std::vector<uint64_t> keys(n);
+    for (int q = 0; q < n; ++q) keys[q] = splitmix_at(state, first + (uint64_t)q);
+    out.resize(n);
+    for (int q = 0; q < n; ++q) out[q] = q;
+    std::stable_sort(out.begin(), out.end(), [&](int a, int b) { return keys[a] < keys[b]; });
+}
+
+int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const double* r_max,
+                     double penalty, const double* prev, const double* d_lim, double tan_half_fov,
+                     const mac_mads_params* prm, double* x_out, mac_mads_stats* st)
+{
+    ABI_BEGIN
+    int32_t rc = check_common(ctx, three_n, 1);
+    if (rc) return rc;
+    if (!x0 || !r_max || !prm || !x_out) return fail(MAC_E_INVAL, "null argument");
+    if (prev && !d_lim) return fail(MAC_E_INVAL, "prev given without d_lim");
+    if (prm->ell0 < 0 || prm->ell_max < prm->ell0 || prm->ell_max > 52)
+        return fail(MAC_E_INVAL, "need 0 <= ell0 <= ell_max <= 52");
+    const int N = (int)(three_n / 3);
+    const int n = (int)three_n;
+    if (N == 0) return fail(MAC_E_INVAL, "no UAV");
+    const auto t0 = std::chrono::steady_clock::now();
+    set_device(ctx);
+    LaneGuard lg(ctx);
+    Lane* L = lg.lane;
+    hipStream_t s = L->stream;
+    const int K = 2 * n;
+    L->cands.reserve(sizeof(double) * three_n);
+    L->xinc.reserve(sizeof(double) * three_n);
+    L->perm.reserve(sizeof(int) * 2 * n);
+    L->area.reserve(sizeof(double) * K);
+    L->obj.reserve(sizeof(double) * K);
+    L->best.reserve(16);
+    L->rmax.reserve(sizeof(double) * N);
+    HCK(hipMemcpyAsync(L->rmax.p, r_max, sizeof(double) * N, hipMemcpyHostToDevice, s));
+    double* d_prev = nullptr;
+    double* d_dlimT = nullptr;
+    if (prev) {
+        L->prev.reserve(sizeof(double) * three_n);
+        L->dlim.reserve(sizeof(double) * N);
+        L->h_dlim.resize(N);
+        for (int i = 0; i < N; ++i) L->h_dlim[i] = dlim_threshold(d_lim[i]);
+        HCK(hipMemcpyAsync(L->prev.p, prev, sizeof(double) * three_n, hipMemcpyHostToDevice, s));
+        HCK(hipMemcpyAsync(L->dlim.p, L->h_dlim.data(), sizeof(double) * N, hipMemcpyHostToDevice, s));
+        d_prev = L->prev.as<double>();
+        d_dlimT = L->dlim.as<double>();
+    }
+    std::vector<double> x(x0, x0 + three_n);
+    double hb[2];
+    auto best_of = [&](const CandSrc& src, int Kc) {
+        enqueue_eval(ctx, L, s, src, N, Kc, use_tiled(ctx, N, nullptr, three_n), L->rmax.as<double>(),
+                     penalty, d_prev, d_dlimT, tan_half_fov, L->area.as<double>(), L->obj.as<double>(),
+                     L->best.as<double>(), 0);
+        HCK(hipMemcpyAsync(hb, L->best.p, 16, hipMemcpyDeviceToHost, s));
+    };
+    // f(x0): the objective, +inf when x0 itself violates cons3 (mads: obj(x) if feasible(x))
+    HCK(hipMemcpyAsync(L->cands.p, x.data(), sizeof(double) * three_n, hipMemcpyHostToDevice, s));
+    best_of(matrix_src(L->cands.as<double>(), N), 1);
+    HCK(hipStreamSynchronize(s));
+    double f = __builtin_bit_cast(int64_t, hb[1]) >= 0 ? hb[0] : INFINITY;
+    int64_t evals = 1, it = 0;
+    int ell = prm->ell0;
+    uint64_t state = prm->seed;
+    const uint64_t T = (uint64_t)n * (uint64_t)(n - 1) / 2;
+    const uint64_t per_iter = (uint64_t)n + T + 2 * (uint64_t)n;   // ltmads_basis's draws
+    // the permutations do not depend on the poll outcomes: the next iteration's are computed
+    // on the host while the device evaluates the current poll
+    std::vector<int> perms(2 * (size_t)n), rp, cp, rp_next, cp_next;
+    stream_permutation(state, (uint64_t)n + T + 1, n, rp_next);
+    stream_permutation(state, (uint64_t)n + T + n + 1, n, cp_next);
+    while (it < prm->n_iter && ell >= 0) {
+        ++it;
+        const int64_t b = (int64_t)1 << ell;
+        rp.swap(rp_next);
+        cp.swap(cp_next);
+        std::copy(rp.begin(), rp.end(), perms.begin());
+        std::copy(cp.begin(), cp.end(), perms.begin() + n);
+        HCK(hipMemcpyAsync(L->perm.p, perms.data(), sizeof(int) * 2 * n, hipMemcpyHostToDevice, s));
+        HCK(hipMemcpyAsync(L->xinc.p, x.data(), sizeof(double) * three_n, hipMemcpyHostToDevice, s));
+        CandSrc src{};
+        src.xinc = L->xinc.as<double>();
+        src.rp = L->perm.as<int>();
+        src.cp = L->perm.as<int>() + n;
+        src.state = state;
+        src.b = b;
+        best_of(src, K);
+        if (it < prm->n_iter) {
+            const uint64_t ns = state + per_iter * 0x9E3779B97F4A7C15ull;
+            stream_permutation(ns, (uint64_t)n + T + 1, n, rp_next);
+            stream_permutation(ns, (uint64_t)n + T + n + 1, n, cp_next);
+        }
+        HCK(hipStreamSynchronize(s));
+        evals += K;
+        const double bo = hb[0];
+        const int64_t bi = __builtin_bit_cast(int64_t, hb[1]);
+        if (bi >= 0 && bo < f) {
+            const int kk = bi < n ? (int)bi : (int)bi - n;
+            for (int v = 0; v < n; ++v) {
+                const double d = ltmads_entry(state, n, b, rp[v], cp[kk]);
+                x[v] = bi < n ? x[v] + d : x[v] - d;
+            }
+            f = bo;
+            ell = std::min(ell + 1, (int)prm->ell_max);
+        } else {
+            --ell;
+        }
+        state += per_iter * 0x9E3779B97F4A7C15ull;
+    }
+    std::copy(x.begin(), x.end(), x_out);
+    if (st) {
+        st->f = f;
+        st->iterations = it;
+        st->evaluations = evals;
+        st->status = ell < 0 ? 0 : 1;
+        st->feasible = std::isfinite(f) ? 1 : 0;
+        st->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return MAC_OK;
+    ABI_END
+}
+
 int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, double* area_out)
 {
     ABI_BEGIN
@@ -1026,7 +1162,7 @@ int32_t mac_area_batch_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t thre
     hipStream_t s = stream ? (hipStream_t)stream : ctx->dev_stream;
     LaneGuard lg(ctx, s);
     const int N = (int)(three_n / 3);
-    enqueue_eval(ctx, lg.lane, s, d_cands, N, (int)K, use_tiled(ctx, N, nullptr, three_n), nullptr,
+    enqueue_eval(ctx, lg.lane, s, matrix_src(d_cands, N), N, (int)K, use_tiled(ctx, N, nullptr, three_n), nullptr,
                  0.0, nullptr, nullptr, 1.0, d_area, nullptr, nullptr, 0);
     return MAC_OK;
     ABI_END
@@ -1068,7 +1204,7 @@ int32_t mac_poll_best_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three
         L->obj.reserve(sizeof(double) * K);
         d_o = L->obj.as<double>();
     }
-    enqueue_eval(ctx, L, s, d_cands, N, (int)K, use_tiled(ctx, N, nullptr, three_n), d_rmax,
+    enqueue_eval(ctx, L, s, matrix_src(d_cands, N), N, (int)K, use_tiled(ctx, N, nullptr, three_n), d_rmax,
                  penalty, d_prev, d_dlimT, tan_half_fov, nullptr, d_o, (double*)d_best, idx_base);
     return MAC_OK;
     ABI_END

@@ -383,3 +383,37 @@ def test_poll_walk_stress(ctx, pkg, orc, case):
         else:
             assert np.array_equal(got, want), (a, np.flatnonzero(got != want)[:5])
     assert np.array_equal(r["poll"], r["tiled"]) or case == "mixed_weights"
+
+
+# ---------------------------------------------------------------------------- native MADS driver
+
+@pytest.mark.parametrize("with_cons3", [False, True])
+def test_native_mads_matches_python_driver(ctx, pkg, with_cons3):
+    """mac_mads_run (candidates generated on the device from the splitmix64 stream) == the
+    Python restatement TDM_STATIC_opt.mads evaluating explicit candidate matrices: same iterates,
+    objective, iteration and evaluation counts, step by step."""
+    wl = pkg.workloads
+    TS = pkg.TDM_STATIC_opt
+    TC = pkg.TDM_Constraints
+    x, y, w = wl.grid_points(160)
+    rng = wl.SplitMix64(77)
+    N = 6
+    x0 = np.concatenate([np.round(300 + rng.uniform(N) * 200), np.round(300 + rng.uniform(N) * 200),
+                         np.full(N, 30.0)])
+    r_max = np.full(N, 30.0 * math.tan(100 / 180 * math.pi / 2))
+    rec = np.stack([x, y, w, w, np.zeros_like(x)], axis=1)
+    obj = TS.createObjective(rec, N, r_max, ctx)
+    cons = [TC.cons1]
+    kw = {}
+    if with_cons3:
+        c3 = TC.create_cons3(x0, 100 / 180 * math.pi, np.full(N, 10.0))
+        cons.append(c3)
+        kw = dict(prev=c3.prev, d_lim=c3.d_lim, tan_half_fov=c3.tan_half_fov)
+    res = TS.mads(x0, obj, cons, N_iter=40, ell0=2, ell_max=5, seed=4321)
+    xn, st = ctx.mads_run(x0, r_max, 1e5, n_iter=40, ell0=2, ell_max=5, seed=4321, **kw)
+    want_x = res.x if res.x is not None else res.i
+    assert np.array_equal(xn, want_x)
+    assert st["f"] == res.x_cost
+    assert st["iterations"] == res.status.iteration
+    assert st["evaluations"] == res.status.function_evaluations
+    assert (st["status"] == 0) == (res.status.optimization_status == "MeshPrecisionLimit")
