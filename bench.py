@@ -90,6 +90,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=20250216)
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="nccl (= RCCL on ROCm) for the real multi-GPU run; gloo only to rehearse "
+                         "N>1 with several ranks sharing one GPU (MAXCOVER_BENCH_DEVICE)")
     args = ap.parse_args()
 
     import torch
@@ -99,11 +102,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
+    # one process per GPU; MAXCOVER_BENCH_DEVICE pins every rank to one device (rehearsal only)
+    dev_index = int(os.environ.get("MAXCOVER_BENCH_DEVICE", local))
     if distributed:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev_index)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group("gloo")
+    dev = torch.device("cuda", dev_index)
     torch.cuda.set_device(dev)
+    coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
     pkg = ge.load_package()
     from importlib import import_module
@@ -127,7 +136,7 @@ def main():
     lo, hi = pdist.shard_range(K, rank, world)
     Kl = hi - lo
 
-    ctx = pkg.Context(local, algo=args.algo)
+    ctx = pkg.Context(dev_index, algo=args.algo)
     t_set = time.perf_counter()
     ctx.set_points(x, y, w)   # once per MPC step: upload + tile index (not part of an eval)
     t_set = time.perf_counter() - t_set
@@ -144,7 +153,7 @@ def main():
         with torch.cuda.stream(stream):
             ctx.poll_best_dev(d, 3 * N, Kl, d_rmax, d_best, idx_base=lo, stream=stream.cuda_stream)
             if distributed:
-                return pdist.gather_best(d_best)
+                return pdist.gather_best(d_best if coll_dev.type == "cuda" else d_best.cpu())
             h_best.copy_(d_best, non_blocking=True)
         stream.synchronize()
         return float(h_best[0]), int(h_best.view(torch.int64)[1])
@@ -181,7 +190,7 @@ def main():
     k_ms, k_launches, k_cands, k_walk = ctx.profile_read(reset=True)
     ctx.profile(False)
     if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     if result is None:
@@ -200,7 +209,7 @@ def main():
     achieved = b_eval * cands_per_launch / (avg_launch_ms * 1e-3) / 1e9 if k_launches else None
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_config{args.config}.json")
-    if os.path.exists(pmc_path):
+    if world == 1 and args.algo == "auto" and os.path.exists(pmc_path):  # the profiled launch
         try:
             with open(pmc_path) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
