@@ -152,6 +152,10 @@ typedef struct mac_mads_stats {
     int32_t status;        /* 0: mesh precision limit (ell < 0); 1: iteration limit           */
     int32_t feasible;
     double seconds;        /* wall time inside the call                                       */
+    double host_enqueue_s; /* of which: enqueueing the polls (uploads + kernel launches)       */
+    double host_perm_s;    /*           next iteration's permutations (overlaps the device)    */
+    double wait_s;         /*           waiting for the device                                 */
+    double host_post_s;    /*           incumbent update after each poll                       */
 } mac_mads_stats;
 int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const double* r_max,
                      double penalty, const double* prev, const double* d_lim, double tan_half_fov,

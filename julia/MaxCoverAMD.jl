@@ -168,6 +168,10 @@ struct MadsStats
     status::Int32
     feasible::Int32
     seconds::Float64
+    host_enqueue_s::Float64
+    host_perm_s::Float64
+    wait_s::Float64
+    host_post_s::Float64
 end
 
 """

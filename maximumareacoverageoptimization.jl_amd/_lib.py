@@ -63,7 +63,9 @@ class MadsStats(ctypes.Structure):
     """mac_mads_stats (include/maxcover.h)."""
     _fields_ = [("f", ctypes.c_double), ("iterations", ctypes.c_int64),
                 ("evaluations", ctypes.c_int64), ("status", ctypes.c_int32),
-                ("feasible", ctypes.c_int32), ("seconds", ctypes.c_double)]
+                ("feasible", ctypes.c_int32), ("seconds", ctypes.c_double),
+                ("host_enqueue_s", ctypes.c_double), ("host_perm_s", ctypes.c_double),
+                ("wait_s", ctypes.c_double), ("host_post_s", ctypes.c_double)]
 
 
 class FireParams(ctypes.Structure):

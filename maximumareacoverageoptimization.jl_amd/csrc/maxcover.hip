@@ -91,6 +91,28 @@ struct DevBuf {
     T* as() const { return (T*)p; }
 };
 
+// Page-locked host staging owned by a lane (async copies must not target pageable memory, or
+// HIP performs them synchronously).
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    void reserve(size_t b)
+    {
+        if (b <= cap) return;
+        if (p) HCK(hipHostFree(p));
+        p = nullptr;
+        cap = 0;
+        HCK(hipHostMalloc(&p, b, hipHostMallocDefault));
+        cap = b;
+    }
+    void release()
+    {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
 // Per-call scratch + stream ("lane"); lanes are pooled so concurrent host threads each get one.
 struct Lane {
     hipStream_t stream = nullptr;
@@ -99,6 +121,7 @@ struct Lane {
     DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode, pen, nbr,
         ncount, dlist, regP, costP, spart, vp, xinc, perm;
     std::vector<double> h_dlim;
+    PinnedBuf h_stage;                         // native MADS driver: best, permutations, incumbent
 };
 
 struct mac_ctx {
@@ -680,6 +703,7 @@ void mac_ctx_destroy(mac_ctx* ctx)
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
     for (Lane* l : ctx->lanes_all) {
+        l->h_stage.release();
         for (DevBuf* b : {&l->cands, &l->disks, &l->partial, &l->area, &l->obj, &l->best,
                           &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->pen, &l->nbr,
                           &l->ncount, &l->dlist, &l->regP, &l->costP, &l->spart, &l->vp, &l->xinc,
@@ -986,12 +1010,35 @@ int32_t mac_remove_covered_f64(mac_ctx* ctx, const double* circles, int64_t thre
 // argsort(kind="stable") of SplitMix64.next_u64(n)).
 static void stream_permutation(uint64_t state, uint64_t first, int n, std::vector<int>& out)
 {
+    // A stable argsort of the keys, i.e. the order of the (key, index) pairs: bucketed by the
+    // keys' top bits (uniform keys: O(n)), then insertion-sorted inside each bucket.
+    int bits = 1;
+    while ((1 << bits) < n && bits < 20) ++bits;
+    const int nb = 1 << bits;
     std::vector<uint64_t> keys(n);
-    for (int q = 0; q < n; ++q) keys[q] = splitmix_at(state, first + (uint64_t)q);
-    out.resize(n);
-    for (int q = 0; q < n; ++q) out[q] = q;
-    std::stable_sort(out.begin(), out.end(), [&](int a, int b) { return keys[a] < keys[b]; });
+    std::vector<int> start(nb + 1, 0);
+    for (int q = 0; q < n; ++q) {
+        keys[q] = splitmix_at(state, first + (uint64_t)q);
+        ++start[(keys[q] >> (64 - bits)) + 1];
+    }
+    for (int b = 0; b < nb; ++b) start[b + 1] += start[b];
+    out.assign(n, 0);
+    std::vector<int> fill(start.begin(), start.end() - 1);
+    for (int q = 0; q < n; ++q) out[fill[keys[q] >> (64 - bits)]++] = q;  // ascending q per bucket
+    for (int b = 0; b < nb; ++b) {
+        for (int a = start[b] + 1; a < start[b + 1]; ++a) {
+            const int v = out[a];
+            int c = a - 1;
+            while (c >= start[b] && keys[out[c]] > keys[v]) {  // strict: equal keys keep q order
+                out[c + 1] = out[c];
+                --c;
+            }
+            out[c + 1] = v;
+        }
+    }
 }
+
+
 
 int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const double* r_max,
                      double penalty, const double* prev, const double* d_lim, double tan_half_fov,
@@ -1034,7 +1081,11 @@ int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const doub
         d_dlimT = L->dlim.as<double>();
     }
     std::vector<double> x(x0, x0 + three_n);
-    double hb[2];
+    // pinned staging: [best 16 B][incumbent 8*3N][permutations 4*2n]
+    L->h_stage.reserve(16 + sizeof(double) * three_n + sizeof(int) * 2 * n);
+    double* hb = (double*)L->h_stage.p;
+    double* hx = hb + 2;
+    int* hperm = (int*)(hx + three_n);
     auto best_of = [&](const CandSrc& src, int Kc) {
         enqueue_eval(ctx, L, s, src, N, Kc, use_tiled(ctx, N, nullptr, three_n), L->rmax.as<double>(),
                      penalty, d_prev, d_dlimT, tan_half_fov, L->area.as<double>(), L->obj.as<double>(),
@@ -1042,7 +1093,8 @@ int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const doub
         HCK(hipMemcpyAsync(hb, L->best.p, 16, hipMemcpyDeviceToHost, s));
     };
     // f(x0): the objective, +inf when x0 itself violates cons3 (mads: obj(x) if feasible(x))
-    HCK(hipMemcpyAsync(L->cands.p, x.data(), sizeof(double) * three_n, hipMemcpyHostToDevice, s));
+    std::copy(x.begin(), x.end(), hx);
+    HCK(hipMemcpyAsync(L->cands.p, hx, sizeof(double) * three_n, hipMemcpyHostToDevice, s));
     best_of(matrix_src(L->cands.as<double>(), N), 1);
     HCK(hipStreamSynchronize(s));
     double f = __builtin_bit_cast(int64_t, hb[1]) >= 0 ? hb[0] : INFINITY;
@@ -1053,18 +1105,23 @@ int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const doub
     const uint64_t per_iter = (uint64_t)n + T + 2 * (uint64_t)n;   // ltmads_basis's draws
     // the permutations do not depend on the poll outcomes: the next iteration's are computed
     // on the host while the device evaluates the current poll
-    std::vector<int> perms(2 * (size_t)n), rp, cp, rp_next, cp_next;
+    std::vector<int> rp, cp, rp_next, cp_next;
     stream_permutation(state, (uint64_t)n + T + 1, n, rp_next);
     stream_permutation(state, (uint64_t)n + T + n + 1, n, cp_next);
+    using clk = std::chrono::steady_clock;
+    double h_enq = 0, h_perm = 0, h_wait = 0, h_post = 0;
     while (it < prm->n_iter && ell >= 0) {
         ++it;
+        const auto ta = clk::now();
         const int64_t b = (int64_t)1 << ell;
         rp.swap(rp_next);
         cp.swap(cp_next);
-        std::copy(rp.begin(), rp.end(), perms.begin());
-        std::copy(cp.begin(), cp.end(), perms.begin() + n);
-        HCK(hipMemcpyAsync(L->perm.p, perms.data(), sizeof(int) * 2 * n, hipMemcpyHostToDevice, s));
-        HCK(hipMemcpyAsync(L->xinc.p, x.data(), sizeof(double) * three_n, hipMemcpyHostToDevice, s));
+        // (the staging is free: the previous iteration's copies completed at its sync)
+        std::copy(rp.begin(), rp.end(), hperm);
+        std::copy(cp.begin(), cp.end(), hperm + n);
+        std::copy(x.begin(), x.end(), hx);
+        HCK(hipMemcpyAsync(L->perm.p, hperm, sizeof(int) * 2 * n, hipMemcpyHostToDevice, s));
+        HCK(hipMemcpyAsync(L->xinc.p, hx, sizeof(double) * three_n, hipMemcpyHostToDevice, s));
         CandSrc src{};
         src.xinc = L->xinc.as<double>();
         src.rp = L->perm.as<int>();
@@ -1072,12 +1129,15 @@ int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const doub
         src.state = state;
         src.b = b;
         best_of(src, K);
+        const auto tb = clk::now();
         if (it < prm->n_iter) {
             const uint64_t ns = state + per_iter * 0x9E3779B97F4A7C15ull;
             stream_permutation(ns, (uint64_t)n + T + 1, n, rp_next);
             stream_permutation(ns, (uint64_t)n + T + n + 1, n, cp_next);
         }
+        const auto tc = clk::now();
         HCK(hipStreamSynchronize(s));
+        const auto td = clk::now();
         evals += K;
         const double bo = hb[0];
         const int64_t bi = __builtin_bit_cast(int64_t, hb[1]);
@@ -1093,6 +1153,11 @@ int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const doub
             --ell;
         }
         state += per_iter * 0x9E3779B97F4A7C15ull;
+        const auto te = clk::now();
+        h_enq += std::chrono::duration<double>(tb - ta).count();
+        h_perm += std::chrono::duration<double>(tc - tb).count();
+        h_wait += std::chrono::duration<double>(td - tc).count();
+        h_post += std::chrono::duration<double>(te - td).count();
     }
     std::copy(x.begin(), x.end(), x_out);
     if (st) {
@@ -1102,6 +1167,10 @@ int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const doub
         st->status = ell < 0 ? 0 : 1;
         st->feasible = std::isfinite(f) ? 1 : 0;
         st->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        st->host_enqueue_s = h_enq;
+        st->host_perm_s = h_perm;
+        st->wait_s = h_wait;
+        st->host_post_s = h_post;
     }
     return MAC_OK;
     ABI_END
