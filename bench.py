@@ -79,12 +79,94 @@ def cpu_baseline(x, y, w, cands, seconds_target: float, threads: int):
     return n / dt, desc
 
 
+def bench_config5(args, pkg, dev_index):
+    """Config 5: src/FullSimulation.jl's optimisation loop with the CA fire (src/DynamicArea.jl)
+    streamed into the device list. One step = one MPC timestep: fire step + append/re-index,
+    rmvCoveredPOI by the previous circles, and a native MADS run (mac_mads_run, N_iter
+    iterations of a complete 2n-candidate poll). value = candidates evaluated / second over the
+    timed MPC steps, everything inside the step included."""
+    import torch
+    wl = pkg.workloads
+    cfg = wl.CONFIGS[5]
+    rng = wl.SplitMix64(args.seed)
+    fire_kw, x0 = wl.config5_setup(rng, cfg["G"], cfg["N"], cfg["ignition"])
+    ctx = pkg.Context(dev_index)
+    t_set = time.perf_counter()
+    D = pkg.DynamicArea.DynamicArea(**fire_kw, seed=args.seed, device=dev_index)
+    sim = pkg.FullSimulation.Simulation(ctx, x0, fire=D, N_iter=args.mads_iters, seed=args.seed)
+    t_set = time.perf_counter() - t_set
+    for _ in range(args.warmup):
+        sim.step()
+    torch.cuda.synchronize()
+    ctx.profile(True)
+    ctx.profile_read(reset=True)
+    recs = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        recs.append(sim.step())
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    k_ms, k_launches, k_cands, k_walk = ctx.profile_read(reset=True)
+    ctx.profile(False)
+    evals = sum(r["evaluations"] for r in recs)
+    M_avg = float(np.mean([r["points"] for r in recs]))
+    b_eval = 24 * M_avg + 24 * cfg["N"] + 8
+    avg_launch_ms = k_ms / max(k_launches, 1)
+    cands_per_launch = k_cands / max(k_launches, 1)
+    achieved = b_eval * cands_per_launch / (avg_launch_ms * 1e-3) / 1e9 if k_launches else None
+    cpu = None
+    if not args.no_cpu:
+        x, y, w = ctx.get_points()
+        polls = wl.poll_candidates(sim.x_prev, wl.SplitMix64(args.seed + 1))
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
+        threads = max(1, min(threads, 16))
+        try:
+            v, desc = cpu_baseline(x, y, w, polls, args.cpu_seconds, threads)
+            cpu = {"value": v, "unit": "evals/s", "cores": threads, "kind": "port",
+                   "sample": desc + " (the final config-5 point list)"}
+        except Exception as e:  # report, never fake
+            log("cpu baseline failed:", e)
+    out = {
+        "metric": METRIC, "value": evals / elapsed, "unit": "evals/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (seeded CA fire)",
+        "config": {
+            "workload": f"config 5: {cfg['name']}", "uavs": cfg["N"],
+            "fire_grid": f"{cfg['G']}x{cfg['G']} cells @ 5 m, ignition {cfg['ignition']}^2 cells",
+            "step": "one MPC timestep: fire CA step + append + rmvCoveredPOI + native MADS run",
+            "mads_iterations_per_step": args.mads_iters,
+            "candidates_per_poll": 6 * cfg["N"],
+            "points_mean": M_avg,
+            "evaluations": evals,
+            "time_split_s": {k: float(np.sum([r[k] for r in recs]))
+                             for k in ("fire_s", "remove_s", "mads_s")},
+            "parallelism": "1 GPU",
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+            "kernel": f"coverage_{k_walk}_kernel", "bytes_per_eval": b_eval,
+            "evals_per_launch": cands_per_launch, "avg_launch_ms": avg_launch_ms,
+            "note": "SURVEY 8(d) algorithmic bytes at the mean list length; frac > 1 by design",
+        },
+        "cpu_baseline": cpu,
+        "setup_s": t_set,
+    }
+    print(json.dumps(out), flush=True)
+    D.close()
+    ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=4, choices=(2, 3, 4))
+    ap.add_argument("--config", type=int, default=4, choices=(2, 3, 4, 5),
+                    help="4 (default): one MADS poll per step; 5: one end-to-end MPC step "
+                         "(CA fire stream + rmvCoveredPOI + a MADS run) per step")
+    ap.add_argument("--mads-iters", type=int, default=100, help="config 5: N_iter per MPC step")
     ap.add_argument("--algo", default="auto", choices=("auto", "tiled", "scan", "poll"))
     ap.add_argument("--polls", type=int, default=4, help="distinct poll sets cycled over steps")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -118,6 +200,10 @@ def main():
     from importlib import import_module
     pdist = import_module(pkg.__name__ + ".dist")
     wl = pkg.workloads
+    if args.config == 5:
+        if world != 1:
+            raise SystemExit("config 5 runs on one GPU (the native MADS loop is not sharded yet)")
+        return bench_config5(args, pkg, dev_index)
 
     cfg = wl.CONFIGS[args.config]
     G, N = cfg["G"], cfg["N"]

@@ -9,9 +9,10 @@ from ._lib import (ALGOS, Context, Fire, InexactError, MaxCoverError, cover_thre
                    default_context, device_count, load_library, version)
 from . import Base_Functions, firepoints, workloads  # noqa: F401  (pure host modules)
 from . import AreaCoverageCalculation, CellFunctions, DynamicArea, TDM_Constraints  # noqa: F401
-from . import TDM_STATIC_opt  # noqa: F401
+from . import FullSimulation, TDM_STATIC_opt  # noqa: F401
 
 __all__ = ["ALGOS", "Context", "Fire", "InexactError", "MaxCoverError", "cover_threshold",
            "default_context", "device_count", "load_library", "version",
-           "AreaCoverageCalculation", "CellFunctions", "DynamicArea", "TDM_Constraints",
+           "AreaCoverageCalculation", "CellFunctions", "DynamicArea", "FullSimulation",
+           "TDM_Constraints",
            "TDM_STATIC_opt", "Base_Functions", "firepoints", "workloads"]

@@ -16,12 +16,29 @@ SEED = 20250216
 PITCH = 5.0
 RADIUS = 36.0
 
-# BASELINE.json configs 2..4 (config 1 is the FirePoints fixture, config 5 the CA fire).
+# BASELINE.json configs 2..5 (config 1 is the FirePoints fixture).
 CONFIGS = {
     2: dict(G=1024, N=32, K=1, name="32 UAVs, 1M-cell synthetic fire grid, fp64, single eval"),
     3: dict(G=2048, N=128, K=769, name="128 UAVs, 4M-cell grid, full MADS poll batch"),
     4: dict(G=4096, N=512, K=3073, name="512 UAVs, 16M-cell grid, full MADS poll batch"),
+    # config 5: src/DynamicArea.jl's automaton on a 4096 x 4096 grid of 5 m cells, a central
+    # 512 x 512-cell ignition block, 512 UAVs over the burning block, MPC steps of FullSimulation
+    5: dict(G=4096, N=512, K=3072, ignition=512,
+            name="512 UAVs, CA fire on a 4096^2 grid streamed per MPC step, end-to-end loop"),
 }
+
+
+def config5_setup(rng: "SplitMix64", G: int = 4096, N: int = 512, ignition: int = 512):
+    """(fire kwargs for DynamicArea, starting circles [x;y;R]) of config 5."""
+    c0 = G // 2 - ignition // 2 + 1
+    fire = dict(X=G * PITCH, Y=G * PITCH, dx=PITCH, dy=PITCH,
+                x_start1=c0 * PITCH, x_start2=(c0 + ignition - 1) * PITCH,
+                y_start1=c0 * PITCH, y_start2=(c0 + ignition - 1) * PITCH)
+    lo = (c0 - 1) * PITCH
+    span = ignition * PITCH
+    cx = np.round(lo + rng.uniform(N) * span)
+    cy = np.round(lo + rng.uniform(N) * span)
+    return fire, np.concatenate([cx, cy, np.full(N, RADIUS)])
 
 _M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
 

@@ -149,3 +149,43 @@ def test_append_points_and_stream(ctx, pkg, orc):
     kept = ctx.remove_covered(circles)
     assert np.array_equal(kept, orc.ref_remove_covered(circles, full))
     fire.close()
+
+
+@pytest.mark.gpu
+def test_full_simulation_dynamic_matches_replay(ctx, pkg, orc):
+    """Config 5 in miniature (src/FullSimulation.jl:42-100 with the fire stream): per MPC step
+    the device list equals the oracle's replay (fire points appended, then rmvCoveredPOI by the
+    previous circles), and the native MADS output equals the Python driver's on that list, with
+    the oracle's objective."""
+    FS = pkg.FullSimulation
+    TS = pkg.TDM_STATIC_opt
+    TC = pkg.TDM_Constraints
+    tan50 = math.tan(100 / 180 * math.pi / 2)
+    x0 = orc.ref_allocate_even_circles(15.0, 5, 10 * tan50, 250.0, 250.0)   # :803
+    x0 = np.round(x0)
+    D = pkg.DynamicArea.DynamicArea(x_start1=200, x_start2=300, y_start1=200, y_start2=260)
+    sim = FS.Simulation(ctx, x0, fire=D, N_iter=25, seed=99)
+    ref = _refire(orc, 100, 100, D.ignition, pkg.DynamicArea.SEED)
+    lst = D.initial_points()
+    ctx2 = pkg.Context(0)
+    x_prev = x0.copy()
+    for t in range(1, 5):
+        rec = sim.step()
+        lst = np.concatenate([lst, ref.step()])
+        kept = orc.ref_remove_covered(x_prev, lst)
+        lst = lst[kept]
+        x, y, w = ctx.get_points()
+        assert np.array_equal(np.stack([x, y, w], axis=1), lst[:, [0, 1, 3]]), t
+        # the Python driver on the replayed list, same input / seed / constraint
+        obj = TS.createObjective(lst, 5, sim.r_max, ctx2)
+        c3 = TC.create_cons3(x_prev, 100 / 180 * math.pi, np.full(5, 10.0))
+        res = TS.mads(rec["input"], obj, [TC.cons1, c3], N_iter=25, ell0=2, ell_max=6,
+                      seed=99 + t)
+        want = res.x if res.x is not None else res.i
+        assert np.array_equal(sim.outputs[-1], want), t
+        assert rec["f"] == res.x_cost, t
+        if np.isfinite(rec["f"]):
+            assert rec["f"] == orc.ref_objective(want, lst, sim.r_max), t
+        x_prev = sim.outputs[-1]
+    ctx2.close()
+    D.close()
