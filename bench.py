@@ -169,6 +169,8 @@ def main():
     ap.add_argument("--mads-iters", type=int, default=100, help="config 5: N_iter per MPC step")
     ap.add_argument("--algo", default="auto", choices=("auto", "tiled", "scan", "poll"))
     ap.add_argument("--polls", type=int, default=4, help="distinct poll sets cycled over steps")
+    ap.add_argument("--tile-points", type=int, default=None,
+                    help="points per spatial tile of the index (library default when omitted)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=20250216)
@@ -222,7 +224,7 @@ def main():
     lo, hi = pdist.shard_range(K, rank, world)
     Kl = hi - lo
 
-    ctx = pkg.Context(dev_index, algo=args.algo)
+    ctx = pkg.Context(dev_index, algo=args.algo, tile_points=args.tile_points)
     t_set = time.perf_counter()
     ctx.set_points(x, y, w)   # once per MPC step: upload + tile index (not part of an eval)
     t_set = time.perf_counter() - t_set

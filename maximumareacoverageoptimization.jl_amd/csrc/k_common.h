@@ -18,7 +18,9 @@ constexpr int kPollCH = 512;       // poll walk: entries staged in LDS per chunk
 constexpr int kPollRB = 64;        // poll walk: region rows per batch
 constexpr int kPollNbr = 64;       // poll walk: lower-index overlapping regions kept
 constexpr int kPollKPL = 4;        // poll walk: candidates per lane
-constexpr int kPollKPB = kBlock * kPollKPL;  // poll walk: candidates per workgroup (at most)
+constexpr int kPollThreads = 512;  // poll walk: workgroup size (8 waves share one staging)
+constexpr int kPollWaves = kPollThreads / kWave;
+constexpr int kPollKPB = kPollThreads * kPollKPL;  // poll walk: candidates per workgroup
 constexpr int kSharedWG = 32;      // poll walk: disk strides of the shared-entry workgroups
 constexpr int kPollShB = kSharedWG * kPollKPL;  // poll walk: shared-entry workgroups per slice
 

@@ -12,7 +12,7 @@
 //
 // Ownership. Only disks j < i whose regions overlap region i can also cover an entry of region
 // i, and only inside their region box. Entries whose tile lies in such a box ("shared") are
-// left out here and decided exactly by coverage_poll_shared_kernel (k_poll_shared.h); every
+// left out here and decided exactly by the shared-entry workgroups (k_poll_shared.h); every
 // other entry of region i can only be credited to disk i.
 //
 // Exact fp32 filter. With o the region centre, x = px - ox, y = py - oy, cu = cx - ox,
@@ -139,12 +139,13 @@ __device__ __forceinline__ float poll_dprime(const float4& e, const PollLane& L)
 }
 
 // Grid (n_chain + kPollShB + N, slices); roles by x, in dispatch order (the first ones overlap
-// the walk): x < n_chain (row 0): objective-penalty chains of candidates [256x, 256x + 256)
+// the walk): x < n_chain (row 0): objective-penalty chains of candidates [512x, 512x + 512)
 // into vp (k_final.h), whatever the walk; then, when *mode == kModePoll (or mode == null),
 // kPollShB workgroups deciding the shared entries into spart, and one workgroup per (disk i,
-// slice g): candidates [g*kPollKPB, min(K, (g+1)*kPollKPB)), lane t, pass u -> k = kb + u*256 +
+// slice g): candidates [g*kPollKPB, min(K, (g+1)*kPollKPB)), lane t, pass u -> k = kb + u*512 +
 // t, partial[i*K + k] = weight of the non-shared entries credited to disk i of candidate k.
-__global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
+// Workgroups are 512 threads: eight waves share one staging of the region's entries.
+__global__ __launch_bounds__(kPollThreads) void coverage_poll_kernel(
     const double2* __restrict__ xy, const double* __restrict__ w,
     const int32_t* __restrict__ off, Grid g, const DiskRec* __restrict__ disksT,
     const int4* __restrict__ region, const uint16_t* __restrict__ nbrT,
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
 {
     static_assert(kPollKPL == 4, "the hot loop pairs candidates (0,1) and (2,3)");
     if ((int)blockIdx.x < n_chain) {  // first: the objective-penalty chains (any walk)
-        const int k = blockIdx.x * kBlock + threadIdx.x;
+        const int k = blockIdx.x * kPollThreads + threadIdx.x;
         if (blockIdx.y == 0 && k < K) penalty_chain(pen, K, N, k, penalty, vp);
         return;
     }
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
     if (mode && *mode != kModePoll) return;
     if (bx < kPollShB) {  // then: the shared entries (k_poll_shared.h)
         const int kb0 = blockIdx.y * kPollKPB;
-        const int kbs = kb0 + (bx % kPollKPL) * kBlock;
+        const int kbs = kb0 + (bx % kPollKPL) * kPollThreads;
         const int ke0 = min(K, kb0 + kPollKPB);
         const int nd = *dcount;
         if (kbs < ke0 && bx / kPollKPL < nd)
@@ -191,7 +192,7 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
     int kk[kPollKPL];
 #pragma unroll
     for (int u = 0; u < kPollKPL; ++u) {
-        const int k = kb + u * kBlock + tid;
+        const int k = kb + u * kPollThreads + tid;
         kk[u] = k < ke ? k : -1;
     }
     if (R.x > R.y) {  // disk i covers nothing in any candidate (uniform across the block)
@@ -254,7 +255,7 @@ __global__ __launch_bounds__(kBlock) void coverage_poll_kernel(
             const int n = min(kPollCH, total - base);
             bool mixed = false;
             double wfirst = 0.0;
-            for (int q = tid; q < n; q += kBlock) {
+            for (int q = tid; q < n; q += kPollThreads) {
                 const int f = base + q;
                 int lo = 0, hi = nr - 1;
                 while (lo < hi) {

@@ -31,13 +31,32 @@ __device__ __forceinline__ bool box_has(const int4& b, int tx, int ty)
 // Block i: the disks j < i whose region boxes overlap region i's (at most kPollNbr kept in
 // nbr[i*kPollNbr ...]; ncount[i] is the true count, > kPollNbr meaning "overflowed"). Disks
 // with neighbours are appended to dlist (order irrelevant: each is processed independently);
-// *dcount must be zero on entry (decide_kernel clears it).
+// *dcount must be zero on entry (region_kernel clears it).
+// Block 0 also picks the walk: mode[0] = poll when its point-visits (cost[i].x summed) stay
+// within `ratio` x the per-candidate walk's (cost[i].y summed) — its visits are broadcast LDS
+// reads, the other's scattered global loads — or `forced`.
 __global__ __launch_bounds__(kBlock) void neighbors_kernel(const int4* __restrict__ region, int N,
                                                            uint16_t* __restrict__ nbr,
                                                            int* __restrict__ ncount,
                                                            int* __restrict__ dlist,
-                                                           int* __restrict__ dcount)
+                                                           int* __restrict__ dcount,
+                                                           const double2* __restrict__ cost,
+                                                           double ratio, int forced,
+                                                           int* __restrict__ mode)
 {
+    if (blockIdx.x == 0) {
+        __shared__ double red[kWavesPerBlock];
+        double a = 0.0, b = 0.0;
+        for (int j = threadIdx.x; j < N; j += kBlock) {
+            a += cost[j].x;
+            b += cost[j].y;
+        }
+        const double A = block_sum_f64(a, red);
+        __syncthreads();
+        const double B = block_sum_f64(b, red);
+        if (threadIdx.x == 0) mode[0] = forced ? forced : (A <= ratio * B ? kModePoll : kModeTiled);
+        __syncthreads();
+    }
     __shared__ int cnt;
     const int i = blockIdx.x;
     if (threadIdx.x == 0) cnt = 0;
@@ -69,7 +88,7 @@ __device__ __forceinline__ bool entry_shared(int nc, const int4* nbox, int tx, i
 }
 
 // Shared-entry pass of one workgroup of the poll kernel (k_poll.h): candidates
-// [kb, kb + 256) one per lane (k < ke), disks dlist[b], dlist[b + kSharedWG], ... Shared entries
+// [kb, kb + 512) one per lane (k < ke), disks dlist[b], dlist[b + kSharedWG], ... Shared entries
 // are compacted (in list order) into LDS round by round and decided in fp64; the neighbour
 // disks of the lane's candidate are preloaded (first four) or read once per entry (the rest).
 // Writes spart[i*K + k] (the finalize kernel adds the rows of disks with ncount[i] > 0).
@@ -80,12 +99,12 @@ __device__ __forceinline__ void poll_shared_block(
     const int* __restrict__ ncount, const int* __restrict__ dlist, int nd, int b, int K,
     int kb, int ke, double* __restrict__ spart)
 {
-    __shared__ double2 sp[kBlock];
-    __shared__ double sw[kBlock];
+    __shared__ double2 sp[kPollThreads];
+    __shared__ double sw[kPollThreads];
     __shared__ int rs[kPollRB], rpre[kPollRB + 1];
     __shared__ int4 nbox[kPollNbr];
     __shared__ uint16_t nbr[kPollNbr];
-    __shared__ int wcount[kWavesPerBlock];
+    __shared__ int wcount[kPollWaves];
 
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
     const int k = kb + tid;
@@ -129,7 +148,7 @@ __device__ __forceinline__ void poll_shared_block(
             }
             __syncthreads();
             const int total = rpre[nr];
-            for (int base = 0; base < total; base += kBlock) {
+            for (int base = 0; base < total; base += kPollThreads) {
                 // this round's entries (one per thread), shared ones compacted in list order
                 const int f = base + tid;
                 bool shared = false;
@@ -150,7 +169,7 @@ __device__ __forceinline__ void poll_shared_block(
                 if (lane == 0) wcount[wid] = __popcll(bal);
                 __syncthreads();
                 int pos = __popcll(bal & ((1ull << lane) - 1)), ns = 0;
-                for (int q = 0; q < kWavesPerBlock; ++q) {
+                for (int q = 0; q < kPollWaves; ++q) {
                     if (q < wid) pos += wcount[q];
                     ns += wcount[q];
                 }

@@ -165,11 +165,14 @@ __global__ __launch_bounds__(kBlock) void disk_prep_T_kernel(
 // One wave per disk i: region[i] = union over the KT candidate tiles of regP (the union of
 // disk i's tile spans over all K candidates) and cost[i] = (K * |region|, sum of span areas):
 // the point visits of the poll walk and of the per-candidate walk, in units of ppt.
+// Block 0 also clears the poll walk's disks-with-neighbours counter.
 __global__ __launch_bounds__(kWave) void region_kernel(const int4* __restrict__ regP,
                                                        const double* __restrict__ costP, int N,
                                                        int KT, int K, int4* __restrict__ region,
-                                                       double2* __restrict__ cost)
+                                                       double2* __restrict__ cost,
+                                                       int* __restrict__ dcount)
 {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *dcount = 0;  // neighbors_kernel appends after us
     const int i = blockIdx.x, lane = threadIdx.x;
     int4 R = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
     double c = 0.0;
@@ -194,28 +197,6 @@ __global__ __launch_bounds__(kWave) void region_kernel(const int4* __restrict__ 
         region[i] = R;
         const double rc = R.x <= R.y ? (double)(R.y - R.x + 1) * (double)(R.w - R.z + 1) : 0.0;
         cost[i] = make_double2(rc * (double)K, c);
-    }
-}
-
-// One block: mode = poll walk when its point-visits stay within `ratio` x the per-candidate
-// walk's (its visits are broadcast LDS reads; the other's are scattered global loads).
-// mode[1] (the poll walk's disks-with-neighbours counter) is cleared here.
-__global__ __launch_bounds__(kBlock) void decide_kernel(const double2* __restrict__ cost, int N,
-                                                        double ratio, int forced,
-                                                        int* __restrict__ mode)
-{
-    __shared__ double red[kWavesPerBlock];
-    double a = 0.0, b = 0.0;
-    for (int i = threadIdx.x; i < N; i += kBlock) {
-        a += cost[i].x;
-        b += cost[i].y;
-    }
-    const double A = block_sum_f64(a, red);
-    __syncthreads();
-    const double B = block_sum_f64(b, red);
-    if (threadIdx.x == 0) {
-        mode[0] = forced ? forced : (A <= ratio * B ? kModePoll : kModeTiled);
-        mode[1] = 0;
     }
 }
 

@@ -5,8 +5,8 @@
 //   disk_prep*_kernel     per (candidate, disk): {cx, cy, T(r), r}, T the exact threshold; the
 //                         objective-penalty term and cons3 mark; per-tile span unions
 //   region_kernel         per disk i: union of its tile spans over the K candidates + costs
-//   decide_kernel         picks the poll walk or the per-candidate walk on the device
-//   neighbors_kernel      per disk i: lower-index disks whose regions overlap region i
+//   neighbors_kernel      per disk i: lower-index disks whose regions overlap region i; its
+//                         block 0 picks the poll walk or the per-candidate walk on the device
 //   coverage_poll_kernel  workgroup = (disk i, 1024 candidates): the entries of disk i's region
 //                         staged in LDS once, 4 candidates per lane, exact fp32 filter; leading
 //                         workgroups run the penalty chains and the shared-entry pass

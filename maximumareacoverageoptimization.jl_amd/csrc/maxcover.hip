@@ -463,18 +463,16 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             L->mode.reserve(2 * sizeof(int));  // [0] walk, [1] disks-with-neighbours count
             hipLaunchKernelGGL(region_kernel, dim3(N), dim3(kWave), 0, s, L->regP.as<int4>(),
                                L->costP.as<double>(), N, KT, K, L->region.as<int4>(),
-                               L->cost.as<double2>());
+                               L->cost.as<double2>(), L->mode.as<int>() + 1);
             HCK(hipGetLastError());
             const int forced = ctx->algo == MAC_ALGO_POLL ? kModePoll : 0;
-            hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(kBlock), 0, s, L->cost.as<double2>(), N,
-                               kPollCostRatio, forced, L->mode.as<int>());
-            HCK(hipGetLastError());
             L->nbr.reserve(sizeof(uint16_t) * (size_t)N * kPollNbr);
             L->ncount.reserve(sizeof(int) * (size_t)N);
             L->dlist.reserve(sizeof(int) * (size_t)N);
             hipLaunchKernelGGL(neighbors_kernel, dim3(N), dim3(kBlock), 0, s, L->region.as<int4>(),
                                N, L->nbr.as<uint16_t>(), L->ncount.as<int>(), L->dlist.as<int>(),
-                               L->mode.as<int>() + 1);
+                               L->mode.as<int>() + 1, L->cost.as<double2>(), kPollCostRatio, forced,
+                               L->mode.as<int>());
             HCK(hipGetLastError());
             d_mode = L->mode.as<int>();
         }
@@ -491,9 +489,9 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         }
         if (poll_possible) {
             L->spart.reserve(sizeof(double) * (size_t)N * K);
-            const int n_chain = d_obj ? (K + kBlock - 1) / kBlock : 0;
+            const int n_chain = d_obj ? (K + kPollThreads - 1) / kPollThreads : 0;
             const dim3 pgrid(n_chain + kPollShB + N, (K + kPollKPB - 1) / kPollKPB);
-            hipLaunchKernelGGL(coverage_poll_kernel, pgrid, dim3(kBlock), 0, s,
+            hipLaunchKernelGGL(coverage_poll_kernel, pgrid, dim3(kPollThreads), 0, s,
                                ctx->xys.as<double2>(), ctx->ws.as<double>(),
                                ctx->off.as<int32_t>(), ctx->grid, L->disks.as<DiskRec>(),
                                L->region.as<int4>(), L->nbr.as<uint16_t>(), L->ncount.as<int>(),

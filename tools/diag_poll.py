@@ -32,7 +32,7 @@ def main():
         ctx.poll_best(C, rmax)
     N = C.shape[1] // 3
     K = C.shape[0]
-    nwg = N * ((K + 1023) // 1024)
+    nwg = N * ((K + 2047) // 2048)  # kPollKPB = 2048 candidates per workgroup
     buf = (ctypes.c_uint64 * (4 * nwg))()
     assert L.mac_diag_read(buf, 4 * nwg) == 0
     a = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 4).astype(np.int64)
