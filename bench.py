@@ -231,20 +231,18 @@ def main():
     d_polls = [torch.from_numpy(np.ascontiguousarray(p[lo:hi])).to(dev) for p in polls]
     d_rmax = torch.from_numpy(r_max).to(dev)
     d_best = torch.empty(2, dtype=torch.float64, device=dev)
-    h_best = torch.empty(2, dtype=torch.float64).pin_memory()
     stream = torch.cuda.Stream(dev)
+    s_handle = stream.cuda_stream
 
     def step(i):
         """One MADS poll. It ends with the best (objective, index) on the host, because the
         next poll's candidates depend on it: polls never overlap."""
         d = d_polls[i % len(d_polls)]
-        with torch.cuda.stream(stream):
-            ctx.poll_best_dev(d, 3 * N, Kl, d_rmax, d_best, idx_base=lo, stream=stream.cuda_stream)
-            if distributed:
+        ctx.poll_best_dev(d, 3 * N, Kl, d_rmax, d_best, idx_base=lo, stream=s_handle)
+        if distributed:
+            with torch.cuda.stream(stream):
                 return pdist.gather_best(d_best if coll_dev.type == "cuda" else d_best.cpu())
-            h_best.copy_(d_best, non_blocking=True)
-        stream.synchronize()
-        return float(h_best[0]), int(h_best.view(torch.int64)[1])
+        return ctx.best_fetch(d_best, stream=s_handle)   # pinned 16-B copy + stream sync
 
     for i in range(args.warmup):
         step(i)

@@ -172,6 +172,10 @@ int32_t mac_poll_best_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three
                               const double* d_rmax, double penalty,
                               const double* d_prev, const double* d_dlim, double tan_half_fov,
                               int64_t idx_base, double* d_obj, void* d_best, void* stream);
+/* Waits for `stream` (NULL = the context's own stream) and returns the 16 bytes a device poll
+ * wrote to d_best, through a pinned staging buffer: the host side of one MADS poll step. */
+int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* best_obj,
+                       int64_t* best_idx);
 
 /* ---- measurement ----------------------------------------------------------------- */
 /* With MAC_OPT_PROFILE = 1, every coverage-kernel launch (tiled walk or streaming scan) is

@@ -45,7 +45,7 @@ EXPORTS = (
     "mac_set_points_dev_f64", "mac_num_points", "mac_get_points_f64",
     "mac_remove_covered_f64", "mac_covered_flags_f64", "mac_area_f64", "mac_area_batch_f64",
     "mac_objective_batch_f64", "mac_poll_best_f64", "mac_area_batch_dev_f64",
-    "mac_poll_best_dev_f64", "mac_cover_threshold", "mac_profile_read",
+    "mac_poll_best_dev_f64", "mac_best_fetch", "mac_cover_threshold", "mac_profile_read",
     "mac_append_points_f64", "mac_append_points_dev_f64", "mac_mads_run",
     "mac_fire_last_error", "mac_fire_thresholds", "mac_fire_create", "mac_fire_destroy",
     "mac_fire_initial_points", "mac_fire_step", "mac_fire_last_points", "mac_fire_get_grid",
@@ -124,6 +124,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mac_area_batch_dev_f64": ([_vp, _vp, _i64, _i64, _vp, _vp], _i32),
         "mac_poll_best_dev_f64": ([_vp, _vp, _i64, _i64, _vp, ctypes.c_double, _vp, _vp,
                                    ctypes.c_double, _i64, _vp, _vp, _vp], _i32),
+        "mac_best_fetch": ([_vp, _vp, _vp, _dp, _i64p], _i32),
         "mac_cover_threshold": ([ctypes.c_double], ctypes.c_double),
         "mac_profile_read": ([_vp, _dp, _i64p, _i64p, ctypes.POINTER(_i32), _i32], _i32),
         "mac_append_points_f64": ([_vp, _dp, _dp, _dp, _i64], _i32),
@@ -400,6 +401,14 @@ class Context:
             self._h, _devptr(d_cands), int(three_n), int(K), _devptr(d_rmax), float(penalty),
             _devptr(d_prev), _devptr(d_dlim), float(tan_half_fov), int(idx_base),
             _devptr(d_obj), _devptr(d_best), _devptr(stream)))
+
+    def best_fetch(self, d_best, stream=None):
+        """Wait for ``stream`` and return the (objective, index) a device poll wrote to d_best."""
+        self._bo = getattr(self, "_bo", None) or (ctypes.c_double(), ctypes.c_int64())
+        bo, bi = self._bo
+        _check(self._L.mac_best_fetch(self._h, _devptr(d_best), _devptr(stream),
+                                      ctypes.byref(bo), ctypes.byref(bi)))
+        return bo.value, bi.value
 
 
 def _fcheck(rc: int) -> None:

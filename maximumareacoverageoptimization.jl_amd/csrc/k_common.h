@@ -18,11 +18,10 @@ constexpr int kPollCH = 512;       // poll walk: entries staged in LDS per chunk
 constexpr int kPollRB = 64;        // poll walk: region rows per batch
 constexpr int kPollNbr = 64;       // poll walk: lower-index overlapping regions kept
 constexpr int kPollKPL = 4;        // poll walk: candidates per lane
-constexpr int kPollThreads = 512;  // poll walk: workgroup size (8 waves share one staging)
+constexpr int kPollThreads = 256;  // poll walk: workgroup size (4 waves share one staging)
 constexpr int kPollWaves = kPollThreads / kWave;
 constexpr int kPollKPB = kPollThreads * kPollKPL;  // poll walk: candidates per workgroup
 constexpr int kSharedWG = 32;      // poll walk: disk strides of the shared-entry workgroups
-constexpr int kPollShB = kSharedWG * kPollKPL;  // poll walk: shared-entry workgroups per slice
 
 constexpr int kModePoll = 1;
 constexpr int kModeTiled = 2;
@@ -58,7 +57,8 @@ __device__ __forceinline__ int wave_incl_scan_i32(int v, int lane)
 }
 
 // Block sum in fixed order (wave butterfly, then waves 0..3 in order). Result valid in thread 0.
-__device__ __forceinline__ double block_sum_f64(double v, double* red /* kWavesPerBlock */)
+template <int W = kWavesPerBlock>
+__device__ __forceinline__ double block_sum_f64(double v, double* red /* W */)
 {
     const int lane = threadIdx.x & (kWave - 1);
     const int wid = threadIdx.x / kWave;
@@ -68,7 +68,7 @@ __device__ __forceinline__ double block_sum_f64(double v, double* red /* kWavesP
     double s = 0.0;
     if (threadIdx.x == 0) {
 #pragma unroll
-        for (int i = 0; i < kWavesPerBlock; ++i) s += red[i];
+        for (int i = 0; i < W; ++i) s += red[i];
     }
     return s;
 }

@@ -15,23 +15,29 @@ constexpr int kFinC = 16;   // candidates per finalize block (x 16 slice groups)
 constexpr int kMaxMaskWords = (65535 + 31) / 32;   // N <= 65535 (mac_* argument check)
 
 // Sequential objective penalty of candidate k (src/TDM_STATIC_opt.jl:89-97): violation =
-// sum_{i=0..N-1} pen[i*K + k] accumulated IN ORDER from 0.0 (bit-exact with the reference's
+// sum_{i=0..N-1} pen[i*K + umap[i*K + k]] (the disk index, k_index.h; pen[i*K + k] without a
+// map) accumulated IN ORDER from 0.0 (bit-exact with the reference's
 // loop); vp = violation * penalty, or +inf when a term is negative (cons3 fails,
 // src/TDM_Constraints.jl:54-75: the extreme barrier never evaluates the objective). The chain is
 // latency-bound (N dependent adds), so loads run kChainB ahead; lanes are consecutive
 // candidates (coalesced). Used by the poll kernel's leading workgroups (overlapping the walk)
 // and by penalty_chain_kernel on the other paths.
 constexpr int kChainB = 32;
-__device__ __forceinline__ void penalty_chain(const double* __restrict__ pen, int K, int N, int k,
+__device__ __forceinline__ void penalty_chain(const double* __restrict__ pen,
+                                              const int* __restrict__ umap, int K, int N, int k,
                                               double penalty, double* __restrict__ vp)
 {
     double violation = 0.0;
     bool infeasible = false;
     int i = 0;
     for (; i + kChainB <= N; i += kChainB) {
+        int pos[kChainB];
+#pragma unroll
+        for (int j = 0; j < kChainB; ++j)
+            pos[j] = umap ? umap[(int64_t)(i + j) * K + k] : k;
         double v[kChainB];
 #pragma unroll
-        for (int j = 0; j < kChainB; ++j) v[j] = pen[(int64_t)(i + j) * K + k];
+        for (int j = 0; j < kChainB; ++j) v[j] = pen[(int64_t)(i + j) * K + pos[j]];
 #pragma unroll
         for (int j = 0; j < kChainB; ++j) {
             infeasible |= v[j] < 0.0;
@@ -39,19 +45,21 @@ __device__ __forceinline__ void penalty_chain(const double* __restrict__ pen, in
         }
     }
     for (; i < N; ++i) {
-        const double v = pen[(int64_t)i * K + k];
+        const int64_t r = (int64_t)i * K;
+        const double v = pen[r + (umap ? umap[r + k] : k)];
         infeasible |= v < 0.0;
         violation += v;
     }
     vp[k] = infeasible ? __builtin_inf() : violation * penalty;
 }
 
-__global__ __launch_bounds__(kBlock) void penalty_chain_kernel(const double* __restrict__ pen, int K,
+__global__ __launch_bounds__(kBlock) void penalty_chain_kernel(const double* __restrict__ pen,
+                                                               const int* __restrict__ umap, int K,
                                                                int N, double penalty,
                                                                double* __restrict__ vp)
 {
     const int k = blockIdx.x * kBlock + threadIdx.x;
-    if (k < K) penalty_chain(pen, K, N, k, penalty, vp);
+    if (k < K) penalty_chain(pen, umap, K, N, k, penalty, vp);
 }
 
 // Block = 16 candidates x 16 slice groups. area_k = sum over slices g of partial[g*K + k] in a
@@ -62,7 +70,8 @@ __global__ __launch_bounds__(kBlock) void penalty_chain_kernel(const double* __r
 // i within each slice group: fixed order). obj_k = -area_k + vp_k when obj_out != null.
 __global__ __launch_bounds__(kBlock) void finalize_kernel(
     const double* __restrict__ partial, const int* __restrict__ mode, int n_poll, int n_other,
-    int K, int N, const double* __restrict__ spart, const int* __restrict__ ncount,
+    int K, int N, const int* __restrict__ map, const double* __restrict__ spart,
+    const int* __restrict__ ncount,
     const double* __restrict__ vp, double* __restrict__ area_out, double* __restrict__ obj_out)
 {
     __shared__ double red[kBlock / kFinC][kFinC];
@@ -82,15 +91,21 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(
         __syncthreads();
     }
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    // poll walk with distinct-disk positions: row g's credit for candidate k sits at map[g*K+k]
+    const int* mp = (map && rows) ? map : nullptr;
+    auto at = [&](int g) -> double {
+        const int64_t r = (int64_t)g * K;
+        return partial[r + (mp ? mp[r + k] : k)];
+    };
     if (k < K) {
         int g = sg;
         for (; g + 3 * SG < G; g += 4 * SG) {
-            a0 += partial[(int64_t)g * K + k];
-            a1 += partial[(int64_t)(g + SG) * K + k];
-            a2 += partial[(int64_t)(g + 2 * SG) * K + k];
-            a3 += partial[(int64_t)(g + 3 * SG) * K + k];
+            a0 += at(g);
+            a1 += at(g + SG);
+            a2 += at(g + 2 * SG);
+            a3 += at(g + 3 * SG);
         }
-        for (; g < G; g += SG) a0 += partial[(int64_t)g * K + k];
+        for (; g < G; g += SG) a0 += at(g);
         // poll walk: the shared-entry rows of the disks that have lower-index neighbours
         if (rows)
             for (int i = sg; i < N; i += SG)

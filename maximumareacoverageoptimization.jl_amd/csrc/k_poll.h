@@ -43,6 +43,7 @@
 #include "k_common.h"
 #include "k_poll_shared.h"
 #include "k_final.h"
+#include "k_index.h"
 
 #pragma clang fp contract(off)
 
@@ -51,6 +52,24 @@ namespace mac {
 #ifdef MAC_DIAG
 constexpr uint64_t kDiagMax = 1 << 16;
 __device__ uint64_t g_diag[4 * kDiagMax];
+#endif
+
+#ifdef MAC_DIAG
+// diagnostic build only: per-workgroup (start, end, role << 56 | info, XCC) stamps indexed by the
+// linear block id; nothing else reads them
+__device__ __forceinline__ void diag_stamp(uint64_t t0, uint64_t role, uint64_t info)
+{
+    if (threadIdx.x != 0) return;
+    const uint64_t b = (uint64_t)blockIdx.y * gridDim.x + blockIdx.x;
+    if (b >= kDiagMax) return;
+    g_diag[4 * b + 0] = t0;
+    g_diag[4 * b + 1] = __builtin_amdgcn_s_memrealtime();
+    g_diag[4 * b + 2] = (role << 56) | (info & 0xffffffffffffffull);
+    g_diag[4 * b + 3] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
+}
+#define MAC_DIAG_STAMP(t0, role, info) diag_stamp(t0, role, info)
+#else
+#define MAC_DIAG_STAMP(t0, role, info)
 #endif
 
 __device__ __forceinline__ float next_down_f32(float f)
@@ -138,42 +157,49 @@ __device__ __forceinline__ float poll_dprime(const float4& e, const PollLane& L)
     return __builtin_fmaf(e.x, L.ns, __builtin_fmaf(e.z, L.sb, __builtin_fmaf(e.y, L.sa, L.stm)));
 }
 
-// Grid (n_chain + kPollShB + N, slices); roles by x, in dispatch order (the first ones overlap
-// the walk): x < n_chain (row 0): objective-penalty chains of candidates [512x, 512x + 512)
+// Grid (n_chain + n_shared + N, slices); roles by x, in dispatch order (the first ones overlap
+// the walk): x < n_chain (row 0): objective-penalty chains of candidates [256x, 256x + 256)
 // into vp (k_final.h), whatever the walk; then, when *mode == kModePoll (or mode == null),
-// kPollShB workgroups deciding the shared entries into spart, and one workgroup per (disk i,
-// slice g): candidates [g*kPollKPB, min(K, (g+1)*kPollKPB)), lane t, pass u -> k = kb + u*512 +
-// t, partial[i*K + k] = weight of the non-shared entries credited to disk i of candidate k.
-// Workgroups are 512 threads: eight waves share one staging of the region's entries.
-__global__ __launch_bounds__(kPollThreads) void coverage_poll_kernel(
+// n_shared = kSharedWG x ceil(K/256) workgroups (row 0) deciding the shared entries into spart
+// (disk stride b = x % kSharedWG, candidates [256 s, 256 s + 256), s = x / kSharedWG), and one
+// workgroup per (disk i,
+// slice g): positions [g*kPollKPB, min(U_i, (g+1)*kPollKPB)) of disk i's distinct disks
+// (urec / ucount, k_index.h), thread t pass u ->
+// p = kb + 256u + t; partial[i*K + p] = weight of the non-shared entries credited to that disk
+// (finalize gathers it for every candidate through the map).
+__global__ __launch_bounds__(kPollThreads) __attribute__((amdgpu_waves_per_eu(4))) void coverage_poll_kernel(
     const double2* __restrict__ xy, const double* __restrict__ w,
-    const int32_t* __restrict__ off, Grid g, const DiskRec* __restrict__ disksT,
+    const int32_t* __restrict__ off, Grid g, const DiskRec* __restrict__ urec,
+    const int* __restrict__ umap, const int* __restrict__ ucount,
     const int4* __restrict__ region, const uint16_t* __restrict__ nbrT,
     const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
     int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
     double* __restrict__ spart, int n_chain, const double* __restrict__ pen, double penalty,
-    double* __restrict__ vp)
+    double* __restrict__ vp, int n_shared)
 {
     static_assert(kPollKPL == 4, "the hot loop pairs candidates (0,1) and (2,3)");
+#ifdef MAC_DIAG
+    const uint64_t diag_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     if ((int)blockIdx.x < n_chain) {  // first: the objective-penalty chains (any walk)
         const int k = blockIdx.x * kPollThreads + threadIdx.x;
-        if (blockIdx.y == 0 && k < K) penalty_chain(pen, K, N, k, penalty, vp);
+        if (blockIdx.y == 0 && k < K) penalty_chain(pen, umap, K, N, k, penalty, vp);
+        MAC_DIAG_STAMP(diag_t0, 1, 0);
         return;
     }
     const int bx = blockIdx.x - n_chain;
     if (mode && *mode != kModePoll) return;
-    if (bx < kPollShB) {  // then: the shared entries (k_poll_shared.h)
-        const int kb0 = blockIdx.y * kPollKPB;
-        const int kbs = kb0 + (bx % kPollKPL) * kPollThreads;
-        const int ke0 = min(K, kb0 + kPollKPB);
+    if (bx < n_shared) {  // then (row 0 only): the shared entries (k_poll_shared.h)
+        const int sub = bx / kSharedWG;                   // 256-candidate sub-slice
+        const int kbs = sub * kPollThreads;
         const int nd = *dcount;
-        if (kbs < ke0 && bx / kPollKPL < nd)
-            poll_shared_block(xy, w, off, g, disksT, region, nbrT, ncount, dlist, nd,
-                              bx / kPollKPL, K, kbs, ke0, spart);
+        if (blockIdx.y == 0 && kbs < K && bx % kSharedWG < nd)
+            poll_shared_block(xy, w, off, g, urec, umap, region, nbrT, ncount, dlist, nd,
+                              bx % kSharedWG, K, kbs, min(K, kbs + kPollThreads), spart);
+        MAC_DIAG_STAMP(diag_t0, 2, (uint64_t)nd);
         return;
     }
 #ifdef MAC_DIAG
-    const uint64_t diag_t0 = __builtin_amdgcn_s_memrealtime();
     int diag_entries = 0;
 #endif
     __shared__ float4 s32[kPollCH + 4];  // (Q, U, V, 0); (+inf, 0, 0) for shared / non-finite / pad
@@ -182,23 +208,29 @@ __global__ __launch_bounds__(kPollThreads) void coverage_poll_kernel(
     __shared__ int rs[kPollRB], rpre[kPollRB + 1];
     __shared__ int4 nbox[kPollNbr];
 
-    const int i = bx - kPollShB;
+    const int i = bx - n_shared;
     const int tid = threadIdx.x;
+    // positions p = distinct disks of disk i (k_dedup.h; all K candidates without dedup)
+    const int U = ucount[i];
     const int kb = blockIdx.y * kPollKPB;
-    const int ke = min(K, kb + kPollKPB);
+    if (kb >= U) return;  // uniform: this slice has no position
+    const int ke = min(U, kb + kPollKPB);
     const int4 R = region[i];
     const int nc = ncount[i];
+    const int64_t row = (int64_t)i * K;
 
+    // lane-major positions p = kb + 256u + t: a disk's few hundred distinct disks spread over
+    // all four waves first (latency hiding beats packing them into fewer waves)
     int kk[kPollKPL];
 #pragma unroll
     for (int u = 0; u < kPollKPL; ++u) {
-        const int k = kb + u * kPollThreads + tid;
-        kk[u] = k < ke ? k : -1;
+        const int p = kb + u * kPollThreads + tid;
+        kk[u] = p < ke ? p : -1;
     }
     if (R.x > R.y) {  // disk i covers nothing in any candidate (uniform across the block)
 #pragma unroll
         for (int u = 0; u < kPollKPL; ++u)
-            if (kk[u] >= 0) partial[(int64_t)i * K + kk[u]] = 0.0;
+            if (kk[u] >= 0) partial[row + kk[u]] = 0.0;
         return;
     }
     if (tid < min(nc, kPollNbr)) nbox[tid] = region[nbrT[i * kPollNbr + tid]];
@@ -218,7 +250,7 @@ __global__ __launch_bounds__(kPollThreads) void coverage_poll_kernel(
         live[u] = false;
         pl[u] = PollLane{0.0f, 0.0f, -1.0f, -1.0f, 0.5f};  // d' < -X' for every entry: inert
         if (kk[u] < 0) continue;
-        const DiskRec d = disksT[(int64_t)i * K + kk[u]];
+        const DiskRec d = urec[row + kk[u]];
         int4 sp;
         if (!disk_span(d, g, sp)) continue;
         live[u] = true;
@@ -346,7 +378,7 @@ __global__ __launch_bounds__(kPollThreads) void coverage_poll_kernel(
 #pragma unroll
                 for (int u = 0; u < kPollKPL; ++u) {
                     if (live[u] && bmin[u] <= pl[u].xp) {
-                        const DiskRec d = disksT[(int64_t)i * K + kk[u]];
+                        const DiskRec d = urec[row + kk[u]];
                         double c = 0.0;
                         for (int q = 0; q < n; ++q) {
                             const float4 e = s32[q];
@@ -374,20 +406,8 @@ __global__ __launch_bounds__(kPollThreads) void coverage_poll_kernel(
     }
 #pragma unroll
     for (int u = 0; u < kPollKPL; ++u)
-        if (kk[u] >= 0) partial[(int64_t)i * K + kk[u]] = acc[u];
-#ifdef MAC_DIAG
-    if (tid == 0) {
-        // diagnostic build only: per-workgroup stamps into a buffer nothing else reads
-        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-        const uint64_t b = (uint64_t)blockIdx.y * N + i;
-        if (b < kDiagMax) {
-            g_diag[4 * b + 0] = diag_t0;
-            g_diag[4 * b + 1] = t1;
-            g_diag[4 * b + 2] = ((uint64_t)nc << 32) | (uint32_t)diag_entries;
-            g_diag[4 * b + 3] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
-        }
-    }
-#endif
+        if (kk[u] >= 0) partial[row + kk[u]] = acc[u];
+    MAC_DIAG_STAMP(diag_t0, 3, ((uint64_t)nc << 40) | ((uint64_t)(ke - kb) << 20) | (uint64_t)diag_entries);
 }
 
 }  // namespace mac

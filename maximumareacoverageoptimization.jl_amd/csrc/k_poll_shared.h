@@ -13,6 +13,7 @@
 
 #include "predicate.h"
 #include "k_common.h"
+#include "k_index.h"
 
 #pragma clang fp contract(off)
 
@@ -88,14 +89,14 @@ __device__ __forceinline__ bool entry_shared(int nc, const int4* nbox, int tx, i
 }
 
 // Shared-entry pass of one workgroup of the poll kernel (k_poll.h): candidates
-// [kb, kb + 512) one per lane (k < ke), disks dlist[b], dlist[b + kSharedWG], ... Shared entries
+// [kb, kb + 256) one per lane (k < ke), disks dlist[b], dlist[b + kSharedWG], ... Shared entries
 // are compacted (in list order) into LDS round by round and decided in fp64; the neighbour
 // disks of the lane's candidate are preloaded (first four) or read once per entry (the rest).
 // Writes spart[i*K + k] (the finalize kernel adds the rows of disks with ncount[i] > 0).
 __device__ __forceinline__ void poll_shared_block(
     const double2* __restrict__ xy, const double* __restrict__ w,
-    const int32_t* __restrict__ off, const Grid& g, const DiskRec* __restrict__ disksT,
-    const int4* __restrict__ region, const uint16_t* __restrict__ nbrT,
+    const int32_t* __restrict__ off, const Grid& g, const DiskRec* __restrict__ urec,
+    const int* __restrict__ umap, const int4* __restrict__ region, const uint16_t* __restrict__ nbrT,
     const int* __restrict__ ncount, const int* __restrict__ dlist, int nd, int b, int K,
     int kb, int ke, double* __restrict__ spart)
 {
@@ -125,10 +126,10 @@ __device__ __forceinline__ void poll_shared_block(
 #pragma unroll
         for (int m = 0; m < 4; ++m) e[m] = DiskRec{0.0, 0.0, -1.0, 0.0};
         if (valid) {
-            d = disksT[(int64_t)i * K + k];
+            d = rec_of(urec, umap, i, K, k);
 #pragma unroll
             for (int m = 0; m < 4; ++m)
-                if (m < ncl) e[m] = disksT[(int64_t)nbrT[i * kPollNbr + m] * K + k];
+                if (m < ncl) e[m] = rec_of(urec, umap, nbrT[i * kPollNbr + m], K, k);
         }
         double acc = 0.0;
         __syncthreads();
@@ -189,13 +190,13 @@ __device__ __forceinline__ void poll_shared_block(
                         if (!stolen && nc > 4) {
                             if (nc <= kPollNbr) {
                                 for (int m = 4; m < nc && !stolen; ++m) {
-                                    const DiskRec x = disksT[(int64_t)nbr[m] * K + k];
+                                    const DiskRec x = rec_of(urec, umap, nbr[m], K, k);
                                     stolen = sqdist(q.x, q.y, x.cx, x.cy) <= x.T;
                                 }
                             } else {  // overflowed list: every lower-index overlapping region
                                 for (int j = 0; j < i && !stolen; ++j) {
                                     if (!box_overlap(region[j], R)) continue;
-                                    const DiskRec x = disksT[(int64_t)j * K + k];
+                                    const DiskRec x = rec_of(urec, umap, j, K, k);
                                     stolen = sqdist(q.x, q.y, x.cx, x.cy) <= x.T;
                                 }
                             }

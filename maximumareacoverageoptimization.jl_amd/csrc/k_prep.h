@@ -76,6 +76,8 @@ __host__ __device__ __forceinline__ double ltmads_entry(uint64_t state, int64_t 
 struct CandSrc {
     const double* cands;   // matrix source when non-null
     int ldc;
+    const double* candsT;  // the same matrix variable-major (candsT[v*K + k]) when non-null
+    int64_t ldt;           // K
     const double* xinc;    // generator: incumbent (3N), row / column permutations (n each)
     const int* rp;
     const int* cp;
@@ -83,6 +85,7 @@ struct CandSrc {
     int64_t b;             // 2^ell
     __device__ __forceinline__ double get(int k, int v, int N) const
     {
+        if (candsT) return candsT[(int64_t)v * ldt + k];
         if (cands) return cands[(int64_t)k * ldc + v];
         const int n = 3 * N;
         const int kk = k < n ? k : k - n;
@@ -90,6 +93,26 @@ struct CandSrc {
         return k < n ? xinc[v] + d : xinc[v] - d;
     }
 };
+
+// cands (3N x K column-major) -> candsT (3N x K row-major: variable-major, candidates
+// contiguous), through 32 x 32 LDS tiles so that both sides are coalesced.
+__global__ __launch_bounds__(kBlock) void cands_transpose_kernel(const double* __restrict__ cands,
+                                                                 int n, int K,
+                                                                 double* __restrict__ candsT)
+{
+    __shared__ double t[32][33];
+    const int v0 = blockIdx.x * 32, k0 = blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
+    for (int kk = ty; kk < 32; kk += 8) {
+        const int k = k0 + kk, v = v0 + tx;
+        if (k < K && v < n) t[kk][tx] = cands[(int64_t)k * n + v];
+    }
+    __syncthreads();
+    for (int vv = ty; vv < 32; vv += 8) {
+        const int v = v0 + vv, k = k0 + tx;
+        if (k < K && v < n) candsT[(int64_t)v * K + k] = t[tx][vv];
+    }
+}
 
 // cands: see CandSrc. Writes disks[k*N + i] (scan walk) and, when pen != null,
 // pen[i*K + k] = pen_term (disk-major, as penalty_chain reads it).
@@ -102,102 +125,6 @@ __global__ void disk_prep_kernel(CandSrc src, int N, int K, DiskRec* __restrict_
     const double x = src.get(k, i, N), y = src.get(k, N + i, N), r = src.get(k, 2 * N + i, N);
     disks[t] = make_disk(x, y, r);
     if (pen) pen[(int64_t)i * K + k] = pen_term(x, y, r, i, N, pa);
-}
-
-// Transposed prep: disksT[i*K + k] (disk-major, candidates contiguous). 32 x 32 tiles through
-// LDS so both the candidate reads (matrix source) and the record writes are coalesced. Also, per tile:
-//   penT[i*K + k] = pen_term (when penT != null), and
-//   regP[kt*N + i], costP[kt*N + i] (kt = blockIdx.y): the union of disk i's tile spans over the
-//   tile's 32 candidates and the sum of their span areas (when regP != null; region_kernel
-//   finishes the reduction over kt).
-__global__ __launch_bounds__(kBlock) void disk_prep_T_kernel(
-    CandSrc src, int N, int K, DiskRec* __restrict__ disksT,
-    PenArgs pa, double* __restrict__ penT, Grid g, int4* __restrict__ regP,
-    double* __restrict__ costP)
-{
-    __shared__ double sx[32][33], sy[32][33], sr[32][33];
-    const int i0 = blockIdx.x * 32, k0 = blockIdx.y * 32;
-    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
-    for (int kk = ty; kk < 32; kk += 8) {
-        const int k = k0 + kk, i = i0 + tx;
-        if (k < K && i < N) {
-            sx[kk][tx] = src.get(k, i, N);
-            sy[kk][tx] = src.get(k, N + i, N);
-            sr[kk][tx] = src.get(k, 2 * N + i, N);
-        }
-    }
-    __syncthreads();
-    for (int ii = ty; ii < 32; ii += 8) {
-        const int i = i0 + ii, k = k0 + tx;
-        int4 sp = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
-        double area = 0.0;
-        if (k < K && i < N) {
-            const double x = sx[tx][ii], y = sy[tx][ii], r = sr[tx][ii];
-            const DiskRec d = make_disk(x, y, r);
-            disksT[(int64_t)i * K + k] = d;
-            if (penT) penT[(int64_t)i * K + k] = pen_term(x, y, r, i, N, pa);
-            int4 s;
-            if (regP && disk_span(d, g, s)) {
-                sp = s;
-                area = (double)(s.y - s.x + 1) * (double)(s.w - s.z + 1);
-            }
-        }
-        if (regP) {
-            // the 32 candidates of disk i sit in 32 consecutive lanes: butterfly over them
-#pragma unroll
-            for (int o = 16; o >= 1; o >>= 1) {
-                sp.x = min(sp.x, __shfl_xor(sp.x, o, 32));
-                sp.y = max(sp.y, __shfl_xor(sp.y, o, 32));
-                sp.z = min(sp.z, __shfl_xor(sp.z, o, 32));
-                sp.w = max(sp.w, __shfl_xor(sp.w, o, 32));
-                area += __shfl_xor(area, o, 32);
-            }
-            if (tx == 0 && i < N) {
-                regP[(int64_t)blockIdx.y * N + i] = sp;
-                costP[(int64_t)blockIdx.y * N + i] = area;
-            }
-        }
-    }
-}
-
-// ------------------------------------------------------------------ region + decision
-
-// One wave per disk i: region[i] = union over the KT candidate tiles of regP (the union of
-// disk i's tile spans over all K candidates) and cost[i] = (K * |region|, sum of span areas):
-// the point visits of the poll walk and of the per-candidate walk, in units of ppt.
-// Block 0 also clears the poll walk's disks-with-neighbours counter.
-__global__ __launch_bounds__(kWave) void region_kernel(const int4* __restrict__ regP,
-                                                       const double* __restrict__ costP, int N,
-                                                       int KT, int K, int4* __restrict__ region,
-                                                       double2* __restrict__ cost,
-                                                       int* __restrict__ dcount)
-{
-    if (blockIdx.x == 0 && threadIdx.x == 0) *dcount = 0;  // neighbors_kernel appends after us
-    const int i = blockIdx.x, lane = threadIdx.x;
-    int4 R = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
-    double c = 0.0;
-    for (int kt = lane; kt < KT; kt += kWave) {
-        const int4 p = regP[(int64_t)kt * N + i];
-        R.x = min(R.x, p.x);
-        R.y = max(R.y, p.y);
-        R.z = min(R.z, p.z);
-        R.w = max(R.w, p.w);
-        c += costP[(int64_t)kt * N + i];
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        R.x = min(R.x, __shfl_xor(R.x, o, kWave));
-        R.y = max(R.y, __shfl_xor(R.y, o, kWave));
-        R.z = min(R.z, __shfl_xor(R.z, o, kWave));
-        R.w = max(R.w, __shfl_xor(R.w, o, kWave));
-        c += __shfl_xor(c, o, kWave);
-    }
-    if (lane == 0) {
-        if (R.x > R.y || R.z > R.w) R = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
-        region[i] = R;
-        const double rc = R.x <= R.y ? (double)(R.y - R.x + 1) * (double)(R.w - R.z + 1) : 0.0;
-        cost[i] = make_double2(rc * (double)K, c);
-    }
 }
 
 }  // namespace mac

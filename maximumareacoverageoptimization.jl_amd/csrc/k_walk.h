@@ -6,6 +6,7 @@
 
 #include "predicate.h"
 #include "k_common.h"
+#include "k_index.h"
 
 #pragma clang fp contract(off)
 
@@ -97,13 +98,14 @@ __host__ __device__ inline size_t tiled_lds_bytes(int N)
 // the tile-row runs of c's span from the CSR offsets (a row of tiles is contiguous in the
 // sorted list), tests every entry in them, and credits a covered entry only when no lower-index
 // disk also covers it (candidates for that come from a conservative disk-disk intersection
-// list built in LDS). disksT[c*K + k]; partial[gi*K + k]. Runs only when *mode == kModeTiled
+// list built in LDS). Disk c of candidate k through the disk index (k_index.h);
+// partial[gi*K + k]. Runs only when *mode == kModeTiled
 // (or mode == null). Workgroups loop over units (grid-stride).
 __global__ __launch_bounds__(kBlock) void coverage_tiled_kernel(
     const double2* __restrict__ xy, const double* __restrict__ w,
     const int32_t* __restrict__ off, Grid g,
-    const DiskRec* __restrict__ disksT, int N, int K, int G, const int* __restrict__ mode,
-    double* __restrict__ partial)
+    const DiskRec* __restrict__ urec, const int* __restrict__ umap, int N, int K, int G,
+    const int* __restrict__ mode, double* __restrict__ partial)
 {
     if (mode && *mode != kModeTiled) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -129,7 +131,7 @@ __global__ __launch_bounds__(kBlock) void coverage_tiled_kernel(
 
     // 1. disks -> LDS, spans
     for (int c = threadIdx.x; c < N; c += kBlock) {
-        const DiskRec d = disksT[(int64_t)c * K + k];
+        const DiskRec d = rec_of(urec, umap, c, K, k);
         sx[c] = d.cx;
         sy[c] = d.cy;
         sT[c] = d.T;

@@ -2,9 +2,11 @@
 //
 // Hot path: one MADS poll = K candidates x full coverage of the fire-point list
 // (src/TDM_STATIC_opt.jl:82-100 via src/AreaCoverageCalculation.jl:63-78), as a short chain:
-//   disk_prep*_kernel     per (candidate, disk): {cx, cy, T(r), r}, T the exact threshold; the
-//                         objective-penalty term and cons3 mark; per-tile span unions
-//   region_kernel         per disk i: union of its tile spans over the K candidates + costs
+//   disk_prep_kernel      (streaming scan) per (candidate, disk): {cx, cy, T(r), r}, T the exact
+//                         threshold, and the objective-penalty term / cons3 mark
+//   disk_index_kernel     (tiled / poll walks) per disk over all K candidates: the distinct disks
+//                         (records, penalty terms), the candidate -> distinct map, the region
+//                         and the two walk costs
 //   neighbors_kernel      per disk i: lower-index disks whose regions overlap region i; its
 //                         block 0 picks the poll walk or the per-candidate walk on the device
 //   coverage_poll_kernel  workgroup = (disk i, 1024 candidates): the entries of disk i's region
@@ -23,6 +25,7 @@
 
 #include "k_common.h"
 #include "k_prep.h"
+#include "k_index.h"
 #include "k_walk.h"
 #include "k_poll.h"
 #include "k_final.h"

@@ -119,7 +119,7 @@ struct Lane {
     hipStream_t last = nullptr;   // stream of the most recent use
     hipEvent_t done = nullptr;
     DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode, pen, nbr,
-        ncount, dlist, regP, costP, spart, vp, xinc, perm;
+        ncount, dlist, spart, vp, xinc, perm, ucount, umap, candsT;
     std::vector<double> h_dlim;
     PinnedBuf h_stage;                         // native MADS driver: best, permutations, incumbent
 };
@@ -131,6 +131,7 @@ struct mac_ctx {
     std::vector<Lane*> lanes_free;
     std::vector<Lane*> lanes_all;
     hipStream_t setup_stream = nullptr;
+    PinnedBuf h_best;                   // mac_best_fetch staging (guarded by mu)
     hipStream_t dev_stream = nullptr;   // ordered stream for *_dev calls passed stream = NULL
 
     int algo = MAC_ALGO_AUTO;
@@ -372,6 +373,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
     double* d_vp = nullptr;            // per-candidate penalty (or +inf: cons3)
     bool chain_done = false;           // the poll kernel ran the chains
     const double* d_spart = nullptr;   // poll walk: shared-entry rows
+    const int* d_umap = nullptr;       // poll walk: candidate -> distinct-disk position
     const int* d_ncount = nullptr;
     if (d_obj) {
         L->vp.reserve(sizeof(double) * (size_t)std::max(K, 1));
@@ -440,17 +442,30 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
     } else {
         const bool poll_possible = ctx->algo == MAC_ALGO_POLL ||
                                    (ctx->algo == MAC_ALGO_AUTO && K >= kPollMinK);
-        const int KT = (K + 31) / 32;
+        // the disk index: distinct disks per UAV, their records / penalty terms, the map, and
+        // each disk's region and walk costs (k_index.h)
         L->disks.reserve(sizeof(DiskRec) * (size_t)N * K);
-        if (poll_possible) {
-            L->regP.reserve(sizeof(int4) * (size_t)N * KT);
-            L->costP.reserve(sizeof(double) * (size_t)N * KT);
+        L->umap.reserve(sizeof(int) * (size_t)N * K);
+        L->ucount.reserve(sizeof(int) * (size_t)N);
+        L->region.reserve(sizeof(int4) * N);
+        L->cost.reserve(sizeof(double2) * N);
+        L->mode.reserve(2 * sizeof(int));  // [0] walk, [1] disks-with-neighbours count
+        const IndexOut io{L->disks.as<DiskRec>(), d_pen, L->umap.as<int>(), L->ucount.as<int>(),
+                          L->region.as<int4>(), L->cost.as<double2>(), L->mode.as<int>() + 1};
+        CandSrc isrc = src;
+        if (src.cands) {  // matrix: variable-major copy first, so each disk's K values are a row
+            L->candsT.reserve(sizeof(double) * (size_t)3 * N * K);
+            hipLaunchKernelGGL(cands_transpose_kernel, dim3((3 * N + 31) / 32, (K + 31) / 32),
+                               dim3(kBlock), 0, s, src.cands, 3 * N, K, L->candsT.as<double>());
+            HCK(hipGetLastError());
+            isrc.candsT = L->candsT.as<double>();
+            isrc.ldt = K;
         }
-        hipLaunchKernelGGL(disk_prep_T_kernel, dim3((N + 31) / 32, KT), dim3(kBlock), 0, s, src,
-                           N, K, L->disks.as<DiskRec>(), pa, d_pen, ctx->grid,
-                           poll_possible ? L->regP.as<int4>() : nullptr,
-                           poll_possible ? L->costP.as<double>() : nullptr);
+        hipLaunchKernelGGL(disk_index_kernel, dim3(8 * ((N + 7) / 8)), dim3(kIdxThreads), 0, s, isrc, N,
+                           K, ctx->grid, pa, 1, io);
         HCK(hipGetLastError());
+        const DiskRec* d_urec = L->disks.as<DiskRec>();
+        const int* d_map = L->umap.as<int>();
         // per-candidate walk: enough workgroups to fill the chip, >= 1 disk per wave
         const int target = 8 * ctx->cus;
         const int G = (int)std::max<int64_t>(
@@ -458,13 +473,6 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         n_other = G;
         L->partial.reserve(sizeof(double) * (size_t)K * std::max(G, poll_possible ? N : 1));
         if (poll_possible) {
-            L->region.reserve(sizeof(int4) * N);
-            L->cost.reserve(sizeof(double2) * N);
-            L->mode.reserve(2 * sizeof(int));  // [0] walk, [1] disks-with-neighbours count
-            hipLaunchKernelGGL(region_kernel, dim3(N), dim3(kWave), 0, s, L->regP.as<int4>(),
-                               L->costP.as<double>(), N, KT, K, L->region.as<int4>(),
-                               L->cost.as<double2>(), L->mode.as<int>() + 1);
-            HCK(hipGetLastError());
             const int forced = ctx->algo == MAC_ALGO_POLL ? kModePoll : 0;
             L->nbr.reserve(sizeof(uint16_t) * (size_t)N * kPollNbr);
             L->ncount.reserve(sizeof(int) * (size_t)N);
@@ -475,6 +483,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                                L->mode.as<int>());
             HCK(hipGetLastError());
             d_mode = L->mode.as<int>();
+            d_umap = d_map;
         }
         prof_begin();
         if (ctx->algo != MAC_ALGO_POLL) {
@@ -483,35 +492,41 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             const int64_t cap = poll_possible ? 4 * (int64_t)ctx->cus : units;
             hipLaunchKernelGGL(coverage_tiled_kernel, dim3((unsigned)std::min(units, cap)), dim3(kBlock),
                                lds, s, ctx->xys.as<double2>(), ctx->ws.as<double>(),
-                               ctx->off.as<int32_t>(), ctx->grid, L->disks.as<DiskRec>(), N, K, G,
+                               ctx->off.as<int32_t>(), ctx->grid, d_urec, d_map, N, K, G,
                                d_mode, L->partial.as<double>());
             HCK(hipGetLastError());
         }
         if (poll_possible) {
             L->spart.reserve(sizeof(double) * (size_t)N * K);
             const int n_chain = d_obj ? (K + kPollThreads - 1) / kPollThreads : 0;
-            const dim3 pgrid(n_chain + kPollShB + N, (K + kPollKPB - 1) / kPollKPB);
+            const int n_shared = kSharedWG * ((K + kPollThreads - 1) / kPollThreads);
+            const dim3 pgrid(n_chain + n_shared + N, (K + kPollKPB - 1) / kPollKPB);
             hipLaunchKernelGGL(coverage_poll_kernel, pgrid, dim3(kPollThreads), 0, s,
                                ctx->xys.as<double2>(), ctx->ws.as<double>(),
-                               ctx->off.as<int32_t>(), ctx->grid, L->disks.as<DiskRec>(),
-                               L->region.as<int4>(), L->nbr.as<uint16_t>(), L->ncount.as<int>(),
-                               L->dlist.as<int>(), L->mode.as<int>() + 1, N, K, d_mode,
-                               L->partial.as<double>(), L->spart.as<double>(), n_chain, d_pen,
-                               penalty, d_vp);
+                               ctx->off.as<int32_t>(), ctx->grid, d_urec, d_map,
+                               L->ucount.as<int>(), L->region.as<int4>(), L->nbr.as<uint16_t>(),
+                               L->ncount.as<int>(), L->dlist.as<int>(), L->mode.as<int>() + 1, N, K,
+                               d_mode, L->partial.as<double>(), L->spart.as<double>(), n_chain, d_pen,
+                               penalty, d_vp, n_shared);
             HCK(hipGetLastError());
             chain_done = true;
             d_spart = L->spart.as<double>();
             d_ncount = L->ncount.as<int>();
+        } else if (d_obj) {
+            hipLaunchKernelGGL(penalty_chain_kernel, dim3((K + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                               s, d_pen, d_map, K, N, penalty, d_vp);
+            HCK(hipGetLastError());
+            chain_done = true;
         }
         prof_end();
     }
     if (d_obj && !chain_done) {
         hipLaunchKernelGGL(penalty_chain_kernel, dim3((K + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
-                           d_pen, K, N, penalty, d_vp);
+                           d_pen, nullptr, K, N, penalty, d_vp);
         HCK(hipGetLastError());
     }
     hipLaunchKernelGGL(finalize_kernel, dim3((K + kFinC - 1) / kFinC), dim3(kBlock), 0, s,
-                       L->partial.as<double>(), d_mode, n_poll, n_other, K, N, d_spart, d_ncount,
+                       L->partial.as<double>(), d_mode, n_poll, n_other, K, N, d_umap, d_spart, d_ncount,
                        d_vp, d_area, d_obj);
     HCK(hipGetLastError());
     if (d_best) {
@@ -604,6 +619,15 @@ extern "C" {
 
 #ifdef MAC_DIAG
 // diagnostic build only (not declared in maxcover.h): per-workgroup poll-walk stamps
+int32_t mac_diag_index_read(uint64_t* out, int64_t n)
+{
+    if (n > (int64_t)(8 * 65536)) n = 8 * 65536;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_index), sizeof(uint64_t) * n, 0,
+                            hipMemcpyDeviceToHost) != hipSuccess)
+        return MAC_E_HIP;
+    return MAC_OK;
+}
+
 int32_t mac_diag_read(uint64_t* out, int64_t n)
 {
     if (n > (int64_t)(4 * kDiagMax)) n = 4 * kDiagMax;
@@ -700,12 +724,13 @@ void mac_ctx_destroy(mac_ctx* ctx)
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
+    ctx->h_best.release();
     for (Lane* l : ctx->lanes_all) {
         l->h_stage.release();
         for (DevBuf* b : {&l->cands, &l->disks, &l->partial, &l->area, &l->obj, &l->best,
                           &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->pen, &l->nbr,
-                          &l->ncount, &l->dlist, &l->regP, &l->costP, &l->spart, &l->vp, &l->xinc,
-                          &l->perm})
+                          &l->ncount, &l->dlist, &l->spart, &l->vp, &l->xinc,
+                          &l->perm, &l->ucount, &l->umap, &l->candsT})
             b->release();
         if (l->done) (void)hipEventDestroy(l->done);
         if (l->stream) (void)hipStreamDestroy(l->stream);
@@ -1273,6 +1298,25 @@ int32_t mac_poll_best_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three
     }
     enqueue_eval(ctx, L, s, matrix_src(d_cands, N), N, (int)K, use_tiled(ctx, N, nullptr, three_n), d_rmax,
                  penalty, d_prev, d_dlimT, tan_half_fov, nullptr, d_o, (double*)d_best, idx_base);
+    return MAC_OK;
+    ABI_END
+}
+
+int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* best_obj,
+                       int64_t* best_idx)
+{
+    ABI_BEGIN
+    if (!ctx) return fail(MAC_E_INVAL, "null context");
+    if (!d_best) return fail(MAC_E_INVAL, "null d_best");
+    set_device(ctx);
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->dev_stream;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->h_best.reserve(16);
+    HCK(hipMemcpyAsync(ctx->h_best.p, d_best, 16, hipMemcpyDeviceToHost, s));
+    HCK(hipStreamSynchronize(s));
+    const double* hb = (const double*)ctx->h_best.p;
+    if (best_obj) *best_obj = hb[0];
+    if (best_idx) *best_idx = __builtin_bit_cast(int64_t, hb[1]);
     return MAC_OK;
     ABI_END
 }

@@ -1,7 +1,9 @@
-"""Diagnostic: per-workgroup timing of the poll walk (diagnostic build libmaxcover_diag.so).
+"""Diagnostic: per-workgroup timing of the poll kernel's roles (diagnostic build
+libmaxcover_diag.so).
 
 MAXCOVER_LIB=.../libmaxcover_diag.so python tools/diag_poll.py [--config 4]
-Stamps are s_memrealtime (100 MHz) per workgroup: start, end, (neighbours << 32 | entries), XCC.
+Stamps are s_memrealtime (100 MHz) per workgroup, indexed by linear block id: start, end,
+(role << 56 | info), XCC. Roles: 1 = penalty chains, 2 = shared entries, 3 = disk walk.
 Only the diagnostic build executes stamps; never quote its timings as kernel performance.
 """
 import argparse
@@ -14,6 +16,10 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import __graft_entry__ as ge  # noqa: E402
+
+KPB = 1024        # kPollKPB
+THREADS = 256     # kPollThreads
+SHB = 32          # kSharedWG (x ceil(K/256) shared-entry workgroups)
 
 
 def main():
@@ -32,34 +38,39 @@ def main():
         ctx.poll_best(C, rmax)
     N = C.shape[1] // 3
     K = C.shape[0]
-    nwg = N * ((K + 2047) // 2048)  # kPollKPB = 2048 candidates per workgroup
-    buf = (ctypes.c_uint64 * (4 * nwg))()
-    assert L.mac_diag_read(buf, 4 * nwg) == 0
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 4).astype(np.int64)
+    gx = (K + THREADS - 1) // THREADS + SHB * ((K + THREADS - 1) // THREADS) + N
+    gy = (K + KPB - 1) // KPB
+    nb = gx * gy
+    buf = (ctypes.c_uint64 * (4 * nb))()
+    assert L.mac_diag_read(buf, 4 * nb) == 0
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 4)
+    ok = a[:, 0] > 0
+    a = a[ok].astype(np.int64)
     t0, t1 = a[:, 0], a[:, 1]
-    dur = (t1 - t0) / 100.0  # us
-    start = (t0 - t0.min()) / 100.0
-    end = (t1 - t0.min()) / 100.0
-    nc = a[:, 2] >> 32
-    ent = a[:, 2] & 0xFFFFFFFF
-    xcc = a[:, 3] & 0xF
-    ks = np.arange(nwg) // N  # slice
-    out = {
-        "workgroups": int(nwg),
-        "kernel_span_us": float(end.max()),
-        "dur_us": {q: float(np.percentile(dur, q)) for q in (0, 10, 50, 90, 99, 100)},
-        "start_us": {q: float(np.percentile(start, q)) for q in (0, 50, 90, 100)},
-        "end_us": {q: float(np.percentile(end, q)) for q in (0, 50, 90, 100)},
-        "entries": {q: float(np.percentile(ent, q)) for q in (0, 50, 100)},
-        "nc>0": int((nc > 0).sum()),
-        "dur_nc0_median": float(np.median(dur[nc == 0])),
-        "dur_nc_pos_median": float(np.median(dur[nc > 0])) if (nc > 0).any() else None,
-        "dur_by_slice_median": [float(np.median(dur[ks == s])) for s in range(ks.max() + 1)],
-        "concurrency_avg": float(dur.sum() / end.max()),
-        "slowest": [dict(wg=int(j), dur=float(dur[j]), nc=int(nc[j]), entries=int(ent[j]),
-                         slice=int(ks[j]), xcc=int(xcc[j]), start=float(start[j]))
-                    for j in np.argsort(-dur)[:8]],
-    }
+    role = (a[:, 2].astype(np.uint64) >> np.uint64(56)).astype(np.int64)
+    info = a[:, 2] & ((1 << 56) - 1)
+    base = t0.min()
+    dur = (t1 - t0) / 100.0
+    out = {"blocks_stamped": int(ok.sum()), "span_us": float((t1.max() - base) / 100.0)}
+    for r, name in ((1, "chains"), (2, "shared"), (3, "walk")):
+        m = role == r
+        if not m.any():
+            continue
+        d = dur[m]
+        out[name] = {
+            "blocks": int(m.sum()),
+            "dur_us": {q: float(np.percentile(d, q)) for q in (0, 50, 90, 100)},
+            "start_us": float((t0[m].min() - base) / 100.0),
+            "end_us": float((t1[m].max() - base) / 100.0),
+            "concurrency_avg": float(d.sum() / max((t1[m].max() - t0[m].min()) / 100.0, 1e-9)),
+        }
+        if r == 3:
+            ent = info[m] & 0xFFFFF
+            pos = (info[m] >> 20) & 0xFFFFF
+            out[name]["entries_median"] = float(np.median(ent))
+            out[name]["positions_median"] = float(np.median(pos))
+        if r == 2:
+            out[name]["disks_with_neighbours"] = int(info[m].max())
     print(json.dumps(out, indent=1))
 
 

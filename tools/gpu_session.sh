@@ -45,6 +45,10 @@ for s in $STEPS; do
         make -s -C maximumareacoverageoptimization.jl_amd/csrc diag
         MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
             run diag 600 python tools/diag_poll.py ; rc=$? ;;
+    diagidx)
+        make -s -C maximumareacoverageoptimization.jl_amd/csrc diag
+        MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
+            run diagidx 600 python tools/diag_index.py ; rc=$? ;;
     bench3)
         run bench3 600 python bench.py --config 3 --no-cpu ; rc=$? ;;
     bench2)
