@@ -11,107 +11,142 @@
 
 namespace mac {
 
-constexpr int kFinC = 16;   // candidates per finalize block (x 16 slice groups)
+constexpr int kFinC = 16;   // candidates per finalize block (x 64 slice groups)
+constexpr int kFinThreads = 1024;
 constexpr int kMaxMaskWords = (65535 + 31) / 32;   // N <= 65535 (mac_* argument check)
 
-// Sequential objective penalty of candidate k (src/TDM_STATIC_opt.jl:89-97): violation =
-// sum_{i=0..N-1} pen[i*K + umap[i*K + k]] (the disk index, k_index.h; pen[i*K + k] without a
-// map) accumulated IN ORDER from 0.0 (bit-exact with the reference's
-// loop); vp = violation * penalty, or +inf when a term is negative (cons3 fails,
-// src/TDM_Constraints.jl:54-75: the extreme barrier never evaluates the objective). The chain is
-// latency-bound (N dependent adds), so loads run kChainB ahead; lanes are consecutive
-// candidates (coalesced). Used by the poll kernel's leading workgroups (overlapping the walk)
-// and by penalty_chain_kernel on the other paths.
-constexpr int kChainB = 32;
-__device__ __forceinline__ void penalty_chain(const double* __restrict__ pen,
-                                              const int* __restrict__ umap, int K, int N, int k,
-                                              double penalty, double* __restrict__ vp)
+// Sequential objective penalty (src/TDM_STATIC_opt.jl:88-92): violation_k = sum over i = 0..N-1
+// of pen[i*K + k] (the index's per-candidate term, k_index.h), accumulated IN ORDER from 0.0
+// (bit-exact with the reference's loop); vp_k = violation_k * penalty, or +inf when a term is
+// negative (cons3 fails, src/TDM_Constraints.jl:54-75: the extreme barrier never evaluates the
+// objective).
+//
+// One workgroup = kChainC candidates x kChainG disk groups. Thread (c, grp) loads its group's
+// kChainSeg consecutive disks of candidate k0 + c in one go (rows of 16 consecutive candidates:
+// one cache line per row; every load in flight at once), then the running sum is relayed through
+// LDS: group 0 adds its terms, then group 1, ... (one barrier per group), so the additions stay
+// in order while the loads cost one latency per kChainG * kChainSeg disks instead of one per
+// disk. Used by the poll kernel's chain workgroups (overlapping the walk) and by
+// penalty_chain_kernel on the other paths. Needs kChainG * kChainC == kBlock threads.
+constexpr int kChainC = 16;
+constexpr int kChainG = kBlock / kChainC;
+constexpr int kChainSeg = 32;
+__device__ __forceinline__ void penalty_chain_block(const double* __restrict__ pen, int K, int N,
+                                                    int k0, double penalty,
+                                                    double* __restrict__ vp)
 {
-    double violation = 0.0;
-    bool infeasible = false;
-    int i = 0;
-    for (; i + kChainB <= N; i += kChainB) {
-        int pos[kChainB];
+    __shared__ double carry[kChainC];
+    __shared__ int bad[kChainC];
+    const int t = threadIdx.x, c = t % kChainC, grp = t / kChainC;
+    const int k = k0 + c;
+    if (t < kChainC) {
+        carry[t] = 0.0;
+        bad[t] = 0;
+    }
+    for (int base = 0; base < N; base += kChainG * kChainSeg) {
+        const int i0 = base + grp * kChainSeg;
+        double v[kChainSeg];
 #pragma unroll
-        for (int j = 0; j < kChainB; ++j)
-            pos[j] = umap ? umap[(int64_t)(i + j) * K + k] : k;
-        double v[kChainB];
+        for (int j = 0; j < kChainSeg; ++j) {
+            const int ii = i0 + j;
+            v[j] = (k < K && ii < N) ? pen[(int64_t)ii * K + k] : 0.0;   // pad: + 0.0, exact
+        }
+        __syncthreads();
+        for (int sgrp = 0; sgrp < kChainG; ++sgrp) {
+            if (grp == sgrp) {
+                double acc = carry[c];
+                bool neg = false;
 #pragma unroll
-        for (int j = 0; j < kChainB; ++j) v[j] = pen[(int64_t)(i + j) * K + pos[j]];
-#pragma unroll
-        for (int j = 0; j < kChainB; ++j) {
-            infeasible |= v[j] < 0.0;
-            violation += v[j];
+                for (int j = 0; j < kChainSeg; ++j) {
+                    neg |= v[j] < 0.0;
+                    acc += v[j];
+                }
+                carry[c] = acc;
+                if (neg) bad[c] = 1;
+            }
+            __syncthreads();
         }
     }
-    for (; i < N; ++i) {
-        const int64_t r = (int64_t)i * K;
-        const double v = pen[r + (umap ? umap[r + k] : k)];
-        infeasible |= v < 0.0;
-        violation += v;
-    }
-    vp[k] = infeasible ? __builtin_inf() : violation * penalty;
+    if (t < kChainC && k < K) vp[k] = bad[t] ? __builtin_inf() : carry[t] * penalty;
 }
 
 __global__ __launch_bounds__(kBlock) void penalty_chain_kernel(const double* __restrict__ pen,
-                                                               const int* __restrict__ umap, int K,
-                                                               int N, double penalty,
+                                                               int K, int N, double penalty,
                                                                double* __restrict__ vp)
 {
-    const int k = blockIdx.x * kBlock + threadIdx.x;
-    if (k < K) penalty_chain(pen, umap, K, N, k, penalty, vp);
+    penalty_chain_block(pen, K, N, blockIdx.x * kChainC, penalty, vp);
 }
 
-// Block = 16 candidates x 16 slice groups. area_k = sum over slices g of partial[g*K + k] in a
-// fixed order (thread (c, sg) sums g = sg, sg+16, ... into 4 interleaved accumulators combined
-// in order, then the 16 groups in order): bit-reproducible, loads kept in flight. The slice
+// Block = 16 candidates x 64 slice groups. area_k = sum over slices g of partial[g*K + k] in a
+// fixed order (thread (c, sg) sums g = sg, sg+64, ... in batches of 8, then the 64 groups in
+// order): bit-reproducible, loads kept in flight. The slice
 // count is n_poll when *mode == poll, else n_other. With spart != null and the poll walk chosen,
 // the shared-entry rows spart[i*K + k] of the disks with ncount[i] > 0 are added too (ascending
 // i within each slice group: fixed order). obj_k = -area_k + vp_k when obj_out != null.
-__global__ __launch_bounds__(kBlock) void finalize_kernel(
+__global__ __launch_bounds__(kFinThreads) void finalize_kernel(
     const double* __restrict__ partial, const int* __restrict__ mode, int n_poll, int n_other,
     int K, int N, const int* __restrict__ map, const double* __restrict__ spart,
     const int* __restrict__ ncount,
     const double* __restrict__ vp, double* __restrict__ area_out, double* __restrict__ obj_out)
 {
-    __shared__ double red[kBlock / kFinC][kFinC];
+    __shared__ double red[kFinThreads / kFinC][kFinC];
     __shared__ uint32_t smask[kMaxMaskWords];   // disks whose shared-entry row exists
     const int t = threadIdx.x, c = t % kFinC, sg = t / kFinC;
-    constexpr int SG = kBlock / kFinC;
+    constexpr int SG = kFinThreads / kFinC;
     const int k0 = blockIdx.x * kFinC;
     const int k = k0 + c;
     const int G = (mode && *mode == kModePoll) ? n_poll : n_other;
     const bool rows = spart && mode && *mode == kModePoll;
     if (rows) {
         const int nw = (N + 31) / 32;
-        for (int q = t; q < nw; q += kBlock) smask[q] = 0u;
+        for (int q = t; q < nw; q += kFinThreads) smask[q] = 0u;
         __syncthreads();
-        for (int i = t; i < N; i += kBlock)
+        for (int i = t; i < N; i += kFinThreads)
             if (ncount[i] > 0) atomicOr(&smask[i >> 5], 1u << (i & 31));
         __syncthreads();
     }
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    // Rows in batches of kFinB per thread, every load of a batch issued before any is used (the
+    // map loads, then the gathers they index): latency paid once per batch, not per row. Each
+    // batch is added in order to one accumulator: fixed order.
+    constexpr int kFinB = 8;
+    double acc = 0.0;
     // poll walk with distinct-disk positions: row g's credit for candidate k sits at map[g*K+k]
     const int* mp = (map && rows) ? map : nullptr;
-    auto at = [&](int g) -> double {
-        const int64_t r = (int64_t)g * K;
-        return partial[r + (mp ? mp[r + k] : k)];
-    };
     if (k < K) {
-        int g = sg;
-        for (; g + 3 * SG < G; g += 4 * SG) {
-            a0 += at(g);
-            a1 += at(g + SG);
-            a2 += at(g + 2 * SG);
-            a3 += at(g + 3 * SG);
+        for (int g = sg; g < G; g += kFinB * SG) {
+            int pos[kFinB];
+#pragma unroll
+            for (int b = 0; b < kFinB; ++b) {
+                const int gb = g + b * SG;
+                pos[b] = gb < G ? (mp ? mp[(int64_t)gb * K + k] : k) : -1;
+            }
+            double v[kFinB];
+#pragma unroll
+            for (int b = 0; b < kFinB; ++b)
+                v[b] = pos[b] >= 0 ? partial[(int64_t)(g + b * SG) * K + pos[b]] : 0.0;
+            double bs = 0.0;
+#pragma unroll
+            for (int b = 0; b < kFinB; ++b) bs += v[b];
+            acc += bs;
         }
-        for (; g < G; g += SG) a0 += at(g);
-        // poll walk: the shared-entry rows of the disks that have lower-index neighbours
+        // poll walk: the shared-entry rows of the disks that have lower-index neighbours (the
+        // other rows are never written; they are read as 0: areas are sums of weights >= 0)
         if (rows)
-            for (int i = sg; i < N; i += SG)
-                if (smask[i >> 5] & (1u << (i & 31))) a3 += spart[(int64_t)i * K + k];
+            for (int i = sg; i < N; i += kFinB * SG) {
+                double v[kFinB];
+#pragma unroll
+                for (int b = 0; b < kFinB; ++b) {
+                    const int ib = i + b * SG;
+                    v[b] = (ib < N && (smask[ib >> 5] & (1u << (ib & 31))))
+                               ? spart[(int64_t)ib * K + k] : 0.0;
+                }
+                double bs = 0.0;
+#pragma unroll
+                for (int b = 0; b < kFinB; ++b) bs += v[b];
+                acc += bs;
+            }
     }
-    red[sg][c] = ((a0 + a1) + a2) + a3;
+    red[sg][c] = acc;
 
     __syncthreads();
     if (sg == 0 && k < K) {

@@ -15,8 +15,8 @@
 // disk_index_kernel reads the K candidates' (x_i, y_i, r_i) once, straight from the candidate
 // source (the matrix, or the LTMADS generator). It numbers the distinct disks in an LDS hash table
 // (exact keys: the bit patterns of the three doubles) and writes per distinct disk u the record
-// urec[i*K + u] and the penalty term upen[i*K + u], plus the map umap[i*K + k] = u for every
-// candidate and the count ucount[i]. It also writes disk i's region (the union of its tile
+// urec[i*K + u], plus the map umap[i*K + k] = u and the penalty term pen[i*K + k] for every
+// candidate (computed once per distinct disk) and the count ucount[i]. It also writes disk i's region (the union of its tile
 // spans over the K candidates) and the two walk costs (K * |region|, sum of span areas).
 // Consumers read disk i of candidate k as urec[i*K + umap[i*K + k]]: the result is bit-identical
 // to per-candidate records (same inputs, same arithmetic), and every candidate is still
@@ -73,7 +73,7 @@ constexpr int kIdxWaves = kIdxThreads / kWave;
 
 struct IndexOut {
     DiskRec* urec;
-    double* upen;    // null: no objective
+    double* pen;     // per candidate: pen[i*K + k] (null: no objective)
     int* umap;
     int* ucount;
     int4* region;
@@ -89,6 +89,7 @@ __global__ __launch_bounds__(kIdxThreads) void disk_index_kernel(CandSrc src, in
     __shared__ uint16_t slot_of[kIndexMaxK];
     __shared__ uint16_t owner_of[kIndexMaxK];
     __shared__ int mult[kIndexMaxK];         // candidates per distinct disk
+    __shared__ double s_pen[kIndexMaxK];     // penalty term per distinct disk
     __shared__ int ucnt;
     __shared__ int sred[4][kIdxWaves];
     __shared__ double dred[kIdxWaves];
@@ -120,7 +121,7 @@ __global__ __launch_bounds__(kIdxThreads) void disk_index_kernel(CandSrc src, in
             const double x = src.get(k, i, N), y = src.get(k, N + i, N), r = src.get(k, 2 * N + i, N);
             add_span(x, y, r, 1.0);
             o.urec[row + k] = make_disk(x, y, r);
-            if (o.upen) o.upen[row + k] = pen_term(x, y, r, i, N, pa);
+            if (o.pen) o.pen[row + k] = pen_term(x, y, r, i, N, pa);
             o.umap[row + k] = k;
         }
         if (tid == 0) o.ucount[i] = K;
@@ -197,22 +198,28 @@ __global__ __launch_bounds__(kIdxThreads) void disk_index_kernel(CandSrc src, in
             }
         }
         __syncthreads();
-        // ---- the map and the multiplicities
-        for (int k = tid; k < K; k += kIdxThreads) {
-            const int u = table[slot_of[k]] & 0xfff;
-            o.umap[row + k] = u;
-            atomicAdd(&mult[u], 1);
-        }
-        __syncthreads();
-        MAC_IDX_STAMP(3);
-        // ---- per distinct disk: record, penalty term, span (weighted by multiplicity)
         const int U = ucnt;
+        // ---- per distinct disk: record and penalty term
         for (int u = tid; u < U; u += kIdxThreads) {
             const int k = owner_of[u];
             const double x = kx[k], y = ky[k], r = kr[k];
             o.urec[row + u] = make_disk(x, y, r);
-            if (o.upen) o.upen[row + u] = pen_term(x, y, r, i, N, pa);
-            add_span(x, y, r, (double)mult[u]);
+            if (o.pen) s_pen[u] = pen_term(x, y, r, i, N, pa);
+        }
+        __syncthreads();
+        MAC_IDX_STAMP(3);
+        // ---- per candidate: the map, the penalty term, and the multiplicities
+        for (int k = tid; k < K; k += kIdxThreads) {
+            const int u = table[slot_of[k]] & 0xfff;
+            o.umap[row + k] = u;
+            if (o.pen) o.pen[row + k] = s_pen[u];
+            atomicAdd(&mult[u], 1);
+        }
+        __syncthreads();
+        // ---- spans of the distinct disks, weighted by multiplicity (region and walk costs)
+        for (int u = tid; u < U; u += kIdxThreads) {
+            const int k = owner_of[u];
+            add_span(kx[k], ky[k], kr[k], (double)mult[u]);
         }
         if (tid == 0) o.ucount[i] = U;
     }

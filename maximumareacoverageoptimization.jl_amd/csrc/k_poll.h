@@ -158,10 +158,10 @@ __device__ __forceinline__ float poll_dprime(const float4& e, const PollLane& L)
 }
 
 // Grid (n_chain + n_shared + N, slices); roles by x, in dispatch order (the first ones overlap
-// the walk): x < n_chain (row 0): objective-penalty chains of candidates [256x, 256x + 256)
-// into vp (k_final.h), whatever the walk; then, when *mode == kModePoll (or mode == null),
-// n_shared = kSharedWG x ceil(K/256) workgroups (row 0) deciding the shared entries into spart
-// (disk stride b = x % kSharedWG, candidates [256 s, 256 s + 256), s = x / kSharedWG), and one
+// the walk): x < n_chain: objective-penalty chains of candidates [16c, 16c + 16),
+// c = y * n_chain + x, into vp (k_final.h), whatever the walk; then, when *mode == kModePoll (or mode == null),
+// n_shared workgroups (row 0) deciding the shared entries into spart, grid-striding over the
+// jobs (disk with neighbours x kShC-candidate slice, k_poll_shared.h), and one
 // workgroup per (disk i,
 // slice g): positions [g*kPollKPB, min(U_i, (g+1)*kPollKPB)) of disk i's distinct disks
 // (urec / ucount, k_index.h), thread t pass u ->
@@ -182,20 +182,21 @@ __global__ __launch_bounds__(kPollThreads) __attribute__((amdgpu_waves_per_eu(4)
     const uint64_t diag_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
     if ((int)blockIdx.x < n_chain) {  // first: the objective-penalty chains (any walk)
-        const int k = blockIdx.x * kPollThreads + threadIdx.x;
-        if (blockIdx.y == 0 && k < K) penalty_chain(pen, umap, K, N, k, penalty, vp);
+        static_assert(kPollThreads == kBlock, "penalty_chain_block needs kBlock threads");
+        const int k0 = (blockIdx.y * n_chain + blockIdx.x) * kChainC;
+        if (k0 < K) penalty_chain_block(pen, K, N, k0, penalty, vp);
         MAC_DIAG_STAMP(diag_t0, 1, 0);
         return;
     }
     const int bx = blockIdx.x - n_chain;
     if (mode && *mode != kModePoll) return;
     if (bx < n_shared) {  // then (row 0 only): the shared entries (k_poll_shared.h)
-        const int sub = bx / kSharedWG;                   // 256-candidate sub-slice
-        const int kbs = sub * kPollThreads;
         const int nd = *dcount;
-        if (blockIdx.y == 0 && kbs < K && bx % kSharedWG < nd)
-            poll_shared_block(xy, w, off, g, urec, umap, region, nbrT, ncount, dlist, nd,
-                              bx % kSharedWG, K, kbs, min(K, kbs + kPollThreads), spart);
+        const int nsub = (K + kShC - 1) / kShC;
+        if (blockIdx.y == 0)
+            for (int job = bx; job < nd * nsub; job += n_shared)
+                poll_shared_job(xy, w, off, g, urec, umap, region, nbrT, ncount,
+                                dlist[job / nsub], K, (job % nsub) * kShC, spart);
         MAC_DIAG_STAMP(diag_t0, 2, (uint64_t)nd);
         return;
     }

@@ -88,17 +88,22 @@ __device__ __forceinline__ bool entry_shared(int nc, const int4* nbox, int tx, i
     return s;
 }
 
-// Shared-entry pass of one workgroup of the poll kernel (k_poll.h): candidates
-// [kb, kb + 256) one per lane (k < ke), disks dlist[b], dlist[b + kSharedWG], ... Shared entries
-// are compacted (in list order) into LDS round by round and decided in fp64; the neighbour
-// disks of the lane's candidate are preloaded (first four) or read once per entry (the rest).
-// Writes spart[i*K + k] (the finalize kernel adds the rows of disks with ncount[i] > 0).
-__device__ __forceinline__ void poll_shared_block(
+// Shared-entry pass of the poll kernel (k_poll.h). A job is (disk dlist[job / nsub], candidates
+// [kb, kb + kShC), kb = (job % nsub) * kShC); the workgroup's threads are kShC candidates x kShG
+// entry groups. Shared entries are compacted (in list order) into LDS round by round; thread
+// (c, eg) decides entries eg, eg + kShG, ... of each round in fp64 for candidate kb + c (the
+// neighbour disks of the candidate preloaded — first four — or read once per entry — the rest),
+// and the kShG group sums are added in group order at the end: fixed order. Splitting the entries
+// over groups keeps a heavily overlapped disk from serialising one lane per candidate over all
+// of its shared entries. Writes spart[i*K + k] (the finalize kernel adds the rows of the disks
+// with ncount[i] > 0).
+constexpr int kShC = 32;
+constexpr int kShG = kPollThreads / kShC;
+__device__ __forceinline__ void poll_shared_job(
     const double2* __restrict__ xy, const double* __restrict__ w,
     const int32_t* __restrict__ off, const Grid& g, const DiskRec* __restrict__ urec,
     const int* __restrict__ umap, const int4* __restrict__ region, const uint16_t* __restrict__ nbrT,
-    const int* __restrict__ ncount, const int* __restrict__ dlist, int nd, int b, int K,
-    int kb, int ke, double* __restrict__ spart)
+    const int* __restrict__ ncount, int i, int K, int kb, double* __restrict__ spart)
 {
     __shared__ double2 sp[kPollThreads];
     __shared__ double sw[kPollThreads];
@@ -106,108 +111,114 @@ __device__ __forceinline__ void poll_shared_block(
     __shared__ int4 nbox[kPollNbr];
     __shared__ uint16_t nbr[kPollNbr];
     __shared__ int wcount[kPollWaves];
+    __shared__ double gsum[kShG][kShC];
 
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
-    const int k = kb + tid;
-    const bool valid = k < ke;
+    const int c = tid % kShC, eg = tid / kShC;
+    const int k = kb + c;
+    const bool valid = k < K;
 
-    for (int di = b; di < nd; di += kSharedWG) {
-        const int i = dlist[di];
-        const int nc = ncount[i];
-        const int ncl = min(nc, kPollNbr);
-        const int4 R = region[i];
-        __syncthreads();  // LDS reuse across disks
-        if (tid < ncl) {
-            nbr[tid] = nbrT[i * kPollNbr + tid];
-            nbox[tid] = region[nbr[tid]];
-        }
-        DiskRec d = DiskRec{0.0, 0.0, -1.0, 0.0};
-        DiskRec e[4];
+    const int nc = ncount[i];
+    const int ncl = min(nc, kPollNbr);
+    const int4 R = region[i];
+    __syncthreads();  // LDS reuse across jobs
+    if (tid < ncl) {
+        nbr[tid] = nbrT[i * kPollNbr + tid];
+        nbox[tid] = region[nbr[tid]];
+    }
+    DiskRec d = DiskRec{0.0, 0.0, -1.0, 0.0};
+    DiskRec e[4];
 #pragma unroll
-        for (int m = 0; m < 4; ++m) e[m] = DiskRec{0.0, 0.0, -1.0, 0.0};
-        if (valid) {
-            d = rec_of(urec, umap, i, K, k);
+    for (int m = 0; m < 4; ++m) e[m] = DiskRec{0.0, 0.0, -1.0, 0.0};
+    if (valid) {
+        d = rec_of(urec, umap, i, K, k);
 #pragma unroll
-            for (int m = 0; m < 4; ++m)
-                if (m < ncl) e[m] = rec_of(urec, umap, nbrT[i * kPollNbr + m], K, k);
+        for (int m = 0; m < 4; ++m)
+            if (m < ncl) e[m] = rec_of(urec, umap, nbrT[i * kPollNbr + m], K, k);
+    }
+    double acc = 0.0;
+    __syncthreads();
+
+    for (int rb = R.z; rb <= R.w; rb += kPollRB) {
+        const int nr = min(kPollRB, R.w - rb + 1);
+        if (tid < nr) {
+            const int64_t rowbase = (int64_t)(rb + tid) * g.nTx;
+            const int s0 = off[rowbase + R.x];
+            rs[tid] = s0;
+            rpre[tid + 1] = off[rowbase + R.y + 1] - s0;
         }
-        double acc = 0.0;
         __syncthreads();
-
-        for (int rb = R.z; rb <= R.w; rb += kPollRB) {
-            const int nr = min(kPollRB, R.w - rb + 1);
-            if (tid < nr) {
-                const int64_t rowbase = (int64_t)(rb + tid) * g.nTx;
-                const int s = off[rowbase + R.x];
-                rs[tid] = s;
-                rpre[tid + 1] = off[rowbase + R.y + 1] - s;
+        if (tid == 0) {
+            rpre[0] = 0;
+            for (int r = 0; r < nr; ++r) rpre[r + 1] += rpre[r];
+        }
+        __syncthreads();
+        const int total = rpre[nr];
+        for (int base = 0; base < total; base += kPollThreads) {
+            // this round's entries (one per thread), shared ones compacted in list order
+            const int f = base + tid;
+            bool shared = false;
+            double2 p = make_double2(0.0, 0.0);
+            double ww = 0.0;
+            if (f < total) {
+                int lo = 0, hi = nr - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (rpre[mid] <= f) lo = mid; else hi = mid - 1;
+                }
+                const int j = rs[lo] + (f - rpre[lo]);
+                p = xy[j];
+                ww = w[j];
+                shared = entry_shared(nc, nbox, tile_of(p.x, g.gx0, g.invS, g.nTx), rb + lo);
+            }
+            const uint64_t bal = __ballot(shared);
+            if (lane == 0) wcount[wid] = __popcll(bal);
+            __syncthreads();
+            int pos = __popcll(bal & ((1ull << lane) - 1)), ns = 0;
+            for (int q = 0; q < kPollWaves; ++q) {
+                if (q < wid) pos += wcount[q];
+                ns += wcount[q];
+            }
+            if (shared) {
+                sp[pos] = p;
+                sw[pos] = ww;
             }
             __syncthreads();
-            if (tid == 0) {
-                rpre[0] = 0;
-                for (int r = 0; r < nr; ++r) rpre[r + 1] += rpre[r];
-            }
-            __syncthreads();
-            const int total = rpre[nr];
-            for (int base = 0; base < total; base += kPollThreads) {
-                // this round's entries (one per thread), shared ones compacted in list order
-                const int f = base + tid;
-                bool shared = false;
-                double2 p = make_double2(0.0, 0.0);
-                double ww = 0.0;
-                if (f < total) {
-                    int lo = 0, hi = nr - 1;
-                    while (lo < hi) {
-                        const int mid = (lo + hi + 1) >> 1;
-                        if (rpre[mid] <= f) lo = mid; else hi = mid - 1;
-                    }
-                    const int j = rs[lo] + (f - rpre[lo]);
-                    p = xy[j];
-                    ww = w[j];
-                    shared = entry_shared(nc, nbox, tile_of(p.x, g.gx0, g.invS, g.nTx), rb + lo);
-                }
-                const uint64_t bal = __ballot(shared);
-                if (lane == 0) wcount[wid] = __popcll(bal);
-                __syncthreads();
-                int pos = __popcll(bal & ((1ull << lane) - 1)), ns = 0;
-                for (int q = 0; q < kPollWaves; ++q) {
-                    if (q < wid) pos += wcount[q];
-                    ns += wcount[q];
-                }
-                if (shared) {
-                    sp[pos] = p;
-                    sw[pos] = ww;
-                }
-                __syncthreads();
-                if (valid && d.T >= 0.0) {
-                    for (int s = 0; s < ns; ++s) {
-                        const double2 q = sp[s];
-                        if (!(sqdist(q.x, q.y, d.cx, d.cy) <= d.T)) continue;
-                        bool stolen = false;
+            if (valid && d.T >= 0.0) {
+                for (int s = eg; s < ns; s += kShG) {
+                    const double2 q = sp[s];
+                    if (!(sqdist(q.x, q.y, d.cx, d.cy) <= d.T)) continue;
+                    bool stolen = false;
 #pragma unroll
-                        for (int m = 0; m < 4; ++m)
-                            if (m < ncl) stolen |= sqdist(q.x, q.y, e[m].cx, e[m].cy) <= e[m].T;
-                        if (!stolen && nc > 4) {
-                            if (nc <= kPollNbr) {
-                                for (int m = 4; m < nc && !stolen; ++m) {
-                                    const DiskRec x = rec_of(urec, umap, nbr[m], K, k);
-                                    stolen = sqdist(q.x, q.y, x.cx, x.cy) <= x.T;
-                                }
-                            } else {  // overflowed list: every lower-index overlapping region
-                                for (int j = 0; j < i && !stolen; ++j) {
-                                    if (!box_overlap(region[j], R)) continue;
-                                    const DiskRec x = rec_of(urec, umap, j, K, k);
-                                    stolen = sqdist(q.x, q.y, x.cx, x.cy) <= x.T;
-                                }
+                    for (int m = 0; m < 4; ++m)
+                        if (m < ncl) stolen |= sqdist(q.x, q.y, e[m].cx, e[m].cy) <= e[m].T;
+                    if (!stolen && nc > 4) {
+                        if (nc <= kPollNbr) {
+                            for (int m = 4; m < nc && !stolen; ++m) {
+                                const DiskRec x = rec_of(urec, umap, nbr[m], K, k);
+                                stolen = sqdist(q.x, q.y, x.cx, x.cy) <= x.T;
+                            }
+                        } else {  // overflowed list: every lower-index overlapping region
+                            for (int j = 0; j < i && !stolen; ++j) {
+                                if (!box_overlap(region[j], R)) continue;
+                                const DiskRec x = rec_of(urec, umap, j, K, k);
+                                stolen = sqdist(q.x, q.y, x.cx, x.cy) <= x.T;
                             }
                         }
-                        if (!stolen) acc += sw[s];
                     }
+                    if (!stolen) acc += sw[s];
                 }
-                __syncthreads();
             }
+            __syncthreads();
         }
-        if (valid) spart[(int64_t)i * K + k] = acc;
+    }
+    gsum[eg][c] = acc;
+    __syncthreads();
+    if (eg == 0 && valid) {
+        double t = 0.0;
+#pragma unroll
+        for (int q = 0; q < kShG; ++q) t += gsum[q][c];
+        spart[(int64_t)i * K + k] = t;
     }
 }
 

@@ -498,9 +498,11 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         }
         if (poll_possible) {
             L->spart.reserve(sizeof(double) * (size_t)N * K);
-            const int n_chain = d_obj ? (K + kPollThreads - 1) / kPollThreads : 0;
-            const int n_shared = kSharedWG * ((K + kPollThreads - 1) / kPollThreads);
-            const dim3 pgrid(n_chain + n_shared + N, (K + kPollKPB - 1) / kPollKPB);
+            const int gy = (K + kPollKPB - 1) / kPollKPB;
+            const int chains = (K + kChainC - 1) / kChainC;          // spread over the gy rows
+            const int n_chain = d_obj ? (chains + gy - 1) / gy : 0;
+            const int n_shared = kSharedWG;
+            const dim3 pgrid(n_chain + n_shared + N, gy);
             hipLaunchKernelGGL(coverage_poll_kernel, pgrid, dim3(kPollThreads), 0, s,
                                ctx->xys.as<double2>(), ctx->ws.as<double>(),
                                ctx->off.as<int32_t>(), ctx->grid, d_urec, d_map,
@@ -513,19 +515,19 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             d_spart = L->spart.as<double>();
             d_ncount = L->ncount.as<int>();
         } else if (d_obj) {
-            hipLaunchKernelGGL(penalty_chain_kernel, dim3((K + kBlock - 1) / kBlock), dim3(kBlock), 0,
-                               s, d_pen, d_map, K, N, penalty, d_vp);
+            hipLaunchKernelGGL(penalty_chain_kernel, dim3((K + kChainC - 1) / kChainC), dim3(kBlock), 0,
+                               s, d_pen, K, N, penalty, d_vp);
             HCK(hipGetLastError());
             chain_done = true;
         }
         prof_end();
     }
     if (d_obj && !chain_done) {
-        hipLaunchKernelGGL(penalty_chain_kernel, dim3((K + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
-                           d_pen, nullptr, K, N, penalty, d_vp);
+        hipLaunchKernelGGL(penalty_chain_kernel, dim3((K + kChainC - 1) / kChainC), dim3(kBlock), 0, s,
+                           d_pen, K, N, penalty, d_vp);
         HCK(hipGetLastError());
     }
-    hipLaunchKernelGGL(finalize_kernel, dim3((K + kFinC - 1) / kFinC), dim3(kBlock), 0, s,
+    hipLaunchKernelGGL(finalize_kernel, dim3((K + kFinC - 1) / kFinC), dim3(kFinThreads), 0, s,
                        L->partial.as<double>(), d_mode, n_poll, n_other, K, N, d_umap, d_spart, d_ncount,
                        d_vp, d_area, d_obj);
     HCK(hipGetLastError());

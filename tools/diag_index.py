@@ -23,4 +23,4 @@ print(json.dumps({"span_us": float((a[:, 5].max() - base) / 100.0),
                   "phase_us_median": [float(v) for v in np.median(ph, axis=0)],
                   "phase_us_max": [float(v) for v in ph.max(axis=0)],
                   "start_us": {q: float(np.percentile((a[:, 0] - base) / 100.0, q)) for q in (0, 50, 100)},
-                  "names": ["loads", "hash insert", "number+map+mult", "records+spans", "reduce"]}))
+                  "names": ["loads", "hash insert", "number+records", "map+pen+spans", "reduce"]}))

@@ -19,7 +19,8 @@ import __graft_entry__ as ge  # noqa: E402
 
 KPB = 1024        # kPollKPB
 THREADS = 256     # kPollThreads
-SHB = 32          # kSharedWG (x ceil(K/256) shared-entry workgroups)
+SHB = 512         # kSharedWG (shared-entry workgroups)
+CHAINC = 16       # kChainC (candidates per penalty-chain workgroup)
 
 
 def main():
@@ -38,8 +39,9 @@ def main():
         ctx.poll_best(C, rmax)
     N = C.shape[1] // 3
     K = C.shape[0]
-    gx = (K + THREADS - 1) // THREADS + SHB * ((K + THREADS - 1) // THREADS) + N
     gy = (K + KPB - 1) // KPB
+    n_chain = ((K + CHAINC - 1) // CHAINC + gy - 1) // gy
+    gx = n_chain + SHB + N
     nb = gx * gy
     buf = (ctypes.c_uint64 * (4 * nb))()
     assert L.mac_diag_read(buf, 4 * nb) == 0
