@@ -129,8 +129,9 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
             for (int b = 0; b < kFinB; ++b) bs += v[b];
             acc += bs;
         }
-        // poll walk: the shared-entry rows of the disks that have lower-index neighbours (the
-        // other rows are never written; they are read as 0: areas are sums of weights >= 0)
+        // poll walk: the shared-entry rows of the disks that have lower-index neighbours (other
+        // disks' rows are never written and never read; a batch's idle slots add +0.0, which
+        // leaves every sum unchanged)
         if (rows)
             for (int i = sg; i < N; i += kFinB * SG) {
                 double v[kFinB];
@@ -159,9 +160,12 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
 }
 
 // Single block: lexicographic minimum over (obj, index); NaN / +inf never selected.
-// best[0] = objective, best[1] = index (int64 bits), index = idx_base + k, -1 if none.
+// best[0] = objective, best[1] = index (int64 bits), index = idx_base + k, -1 if none. With a
+// mirror (mapped pinned host memory), the two words are also written there followed by seq in
+// mirror[2], so the host reads the result without a copy (mac_best_fetch).
 __global__ __launch_bounds__(kBlock) void argmin_kernel(const double* __restrict__ obj, int K,
-                                                        int64_t idx_base, double* __restrict__ best)
+                                                        int64_t idx_base, double* __restrict__ best,
+                                                        double* __restrict__ mirror, uint64_t seq)
 {
     __shared__ double sv[kBlock];
     __shared__ int si[kBlock];
@@ -190,6 +194,13 @@ __global__ __launch_bounds__(kBlock) void argmin_kernel(const double* __restrict
         best[0] = i >= 0 ? sv[0] : __builtin_inf();
         const int64_t gidx = i >= 0 ? idx_base + i : (int64_t)-1;
         best[1] = __builtin_bit_cast(double, gidx);
+        if (mirror) {  // pinned coherent host words: the result, then (released) its sequence number
+            mirror[0] = best[0];
+            mirror[1] = best[1];
+            __threadfence_system();
+            __hip_atomic_store(reinterpret_cast<uint64_t*>(mirror + 2), seq, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 

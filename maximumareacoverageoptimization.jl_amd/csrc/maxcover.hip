@@ -4,6 +4,7 @@
 // Reference seam: src/TDM_STATIC_opt.jl:82-100 (AreaMaxObjective / createObjective) and
 // src/AreaCoverageCalculation.jl:63-110 (calculateArea). See DESIGN.md.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -96,13 +97,13 @@ struct DevBuf {
 struct PinnedBuf {
     void* p = nullptr;
     size_t cap = 0;
-    void reserve(size_t b)
+    void reserve(size_t b, unsigned flags = hipHostMallocDefault)
     {
         if (b <= cap) return;
         if (p) HCK(hipHostFree(p));
         p = nullptr;
         cap = 0;
-        HCK(hipHostMalloc(&p, b, hipHostMallocDefault));
+        HCK(hipHostMalloc(&p, b, flags));
         cap = b;
     }
     void release()
@@ -131,13 +132,20 @@ struct mac_ctx {
     std::vector<Lane*> lanes_free;
     std::vector<Lane*> lanes_all;
     hipStream_t setup_stream = nullptr;
-    PinnedBuf h_best;                   // mac_best_fetch staging (guarded by mu)
+    // device polls' result mirror (guarded by mu): mapped coherent host words {obj, idx, seq}
+    // written by the argmin kernel of the latest mac_poll_best_dev_f64 on mirror_for
+    PinnedBuf h_best;
+    double* d_mirror = nullptr;
+    uint64_t mirror_seq = 0;
+    const void* mirror_for = nullptr;
     hipStream_t dev_stream = nullptr;   // ordered stream for *_dev calls passed stream = NULL
 
     int algo = MAC_ALGO_AUTO;
     bool profile = false;
     std::vector<hipEvent_t> ev_pool;                 // free timing events
-    struct Prof { hipEvent_t a, b; int64_t K; const int* mode; int algo; };
+    // a / b: the walk launch's start / stop; c / d: the poll kernel's when the device picks the
+    // walk (mode != null): the pair of the walk that ran is read
+    struct Prof { hipEvent_t a, b, c, d; int64_t K; const int* mode; int algo; };
     std::vector<Prof> prof;                          // recorded launches (guarded by mu)
     int storage = MAC_STORE_F64;
     int tile_ppt = 4;
@@ -361,7 +369,8 @@ static bool use_tiled(mac_ctx* ctx, int N, const double* h_cands, int64_t three_
 static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& src, int N,
                          int K, bool tiled, const double* d_rmax, double penalty,
                          const double* d_prev, const double* d_dlimT, double tan_half_fov,
-                         double* d_area, double* d_obj, double* d_best, int64_t idx_base)
+                         double* d_area, double* d_obj, double* d_best, int64_t idx_base,
+                         double* d_mirror = nullptr, uint64_t mirror_seq = 0)
 {
     const int64_t M = ctx->M;
     int n_poll = N, n_other = 1;
@@ -383,29 +392,35 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             d_pen = L->pen.as<double>();
         }
     }
-    hipEvent_t ev_a = nullptr, ev_b = nullptr;
-    auto prof_begin = [&]() {
-        if (!ctx->profile) return;
+    // Profiling: the measured launches carry start / stop events stamped by the dispatch itself
+    // (hipExtLaunchKernelGGL), so measuring adds no marker packets (and no gaps) to the stream.
+    hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr, ev_d = nullptr;
+    auto take_ev = [&]() -> hipEvent_t {
+        hipEvent_t e = nullptr;
         {
             std::lock_guard<std::mutex> lk(ctx->mu);
-            if (ctx->ev_pool.size() >= 2) {
-                ev_a = ctx->ev_pool.back();
-                ctx->ev_pool.pop_back();
-                ev_b = ctx->ev_pool.back();
+            if (!ctx->ev_pool.empty()) {
+                e = ctx->ev_pool.back();
                 ctx->ev_pool.pop_back();
             }
         }
-        if (!ev_a) {
-            HCK(hipEventCreate(&ev_a));
-            HCK(hipEventCreate(&ev_b));
+        if (!e) HCK(hipEventCreate(&e));
+        return e;
+    };
+    auto prof_begin = [&](bool two) {
+        if (!ctx->profile) return;
+        ev_a = take_ev();
+        ev_b = take_ev();
+        if (two) {
+            ev_c = take_ev();
+            ev_d = take_ev();
         }
-        HCK(hipEventRecord(ev_a, s));
     };
     auto prof_end = [&]() {
         if (!ctx->profile) return;
-        HCK(hipEventRecord(ev_b, s));
         std::lock_guard<std::mutex> lk(ctx->mu);
-        ctx->prof.push_back({ev_a, ev_b, (int64_t)K, d_mode, tiled ? MAC_ALGO_TILED : MAC_ALGO_SCAN});
+        ctx->prof.push_back({ev_a, ev_b, ev_c, ev_d, (int64_t)K, d_mode,
+                             tiled ? MAC_ALGO_TILED : MAC_ALGO_SCAN});
     };
 
     if (N == 0 || M == 0) {  // no UAV or no entry: every area is 0 (the loops never run)
@@ -433,9 +448,9 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         nblk = std::max<int64_t>(1, (M + chunk - 1) / chunk);
         n_other = (int)nblk;
         L->partial.reserve(sizeof(double) * (size_t)K * nblk);
-        prof_begin();
-        hipLaunchKernelGGL((coverage_scan_kernel<KB, PPT>), dim3((unsigned)nblk, (unsigned)kgroups),
-                           dim3(kBlock), 0, s, ctx->xys.as<double2>(), ctx->ws.as<double>(), M,
+        prof_begin(false);
+        hipExtLaunchKernelGGL((coverage_scan_kernel<KB, PPT>), dim3((unsigned)nblk, (unsigned)kgroups),
+                           dim3(kBlock), 0, s, ev_a, ev_b, 0, ctx->xys.as<double2>(), ctx->ws.as<double>(), M,
                            L->disks.as<DiskRec>(), N, K, chunk, L->partial.as<double>());
         HCK(hipGetLastError());
         prof_end();
@@ -485,25 +500,28 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             d_mode = L->mode.as<int>();
             d_umap = d_map;
         }
-        prof_begin();
-        if (ctx->algo != MAC_ALGO_POLL) {
+        const bool run_tiled = ctx->algo != MAC_ALGO_POLL;
+        prof_begin(run_tiled && poll_possible);
+        // events: tiled -> (a, b) and poll -> (c, d) when both run, else the one that runs -> (a, b)
+        hipEvent_t pa0 = run_tiled ? ev_c : ev_a, pb0 = run_tiled ? ev_d : ev_b;
+        if (run_tiled) {
             const size_t lds = tiled_lds_bytes(N);
             const int64_t units = (int64_t)K * G;
             const int64_t cap = poll_possible ? 4 * (int64_t)ctx->cus : units;
-            hipLaunchKernelGGL(coverage_tiled_kernel, dim3((unsigned)std::min(units, cap)), dim3(kBlock),
-                               lds, s, ctx->xys.as<double2>(), ctx->ws.as<double>(),
+            hipExtLaunchKernelGGL(coverage_tiled_kernel, dim3((unsigned)std::min(units, cap)), dim3(kBlock),
+                               (uint32_t)lds, s, ev_a, ev_b, 0, ctx->xys.as<double2>(), ctx->ws.as<double>(),
                                ctx->off.as<int32_t>(), ctx->grid, d_urec, d_map, N, K, G,
                                d_mode, L->partial.as<double>());
             HCK(hipGetLastError());
         }
         if (poll_possible) {
-            L->spart.reserve(sizeof(double) * (size_t)N * K);
             const int gy = (K + kPollKPB - 1) / kPollKPB;
             const int chains = (K + kChainC - 1) / kChainC;          // spread over the gy rows
             const int n_chain = d_obj ? (chains + gy - 1) / gy : 0;
+            L->spart.reserve(sizeof(double) * (size_t)N * K);
             const int n_shared = kSharedWG;
             const dim3 pgrid(n_chain + n_shared + N, gy);
-            hipLaunchKernelGGL(coverage_poll_kernel, pgrid, dim3(kPollThreads), 0, s,
+            hipExtLaunchKernelGGL(coverage_poll_kernel, pgrid, dim3(kPollThreads), 0, s, pa0, pb0, 0,
                                ctx->xys.as<double2>(), ctx->ws.as<double>(),
                                ctx->off.as<int32_t>(), ctx->grid, d_urec, d_map,
                                L->ucount.as<int>(), L->region.as<int4>(), L->nbr.as<uint16_t>(),
@@ -532,7 +550,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                        d_vp, d_area, d_obj);
     HCK(hipGetLastError());
     if (d_best) {
-        hipLaunchKernelGGL(argmin_kernel, dim3(1), dim3(kBlock), 0, s, d_obj, K, idx_base, d_best);
+        hipLaunchKernelGGL(argmin_kernel, dim3(1), dim3(kBlock), 0, s, d_obj, K, idx_base, d_best,
+                           d_mirror, mirror_seq);
         HCK(hipGetLastError());
     }
 }
@@ -656,31 +675,33 @@ int32_t mac_profile_read(mac_ctx* ctx, double* kernel_ms, int64_t* launches,
     int64_t n = 0, kc = 0;
     int algo = 0;
     for (auto& p : ctx->prof) {
-        HCK(hipEventSynchronize(p.b));
-        float t = 0.f;
-        HCK(hipEventElapsedTime(&t, p.a, p.b));
-        ms += t;
-        ++n;
-        kc += p.K;
-    }
-    if (!ctx->prof.empty()) {
-        const auto& p = ctx->prof.back();
         algo = p.algo;
+        hipEvent_t a = p.a, b = p.b;
         if (p.mode) {  // the device's choice (the lane's mode word holds its latest decision)
+            HCK(hipEventSynchronize(p.d ? p.d : p.b));
             int m = 0;
             HCK(hipMemcpy(&m, p.mode, sizeof(int), hipMemcpyDeviceToHost));
             algo = m == kModePoll ? MAC_ALGO_POLL : MAC_ALGO_TILED;
+            if (p.c && m == kModePoll) {
+                a = p.c;
+                b = p.d;
+            }
         }
+        HCK(hipEventSynchronize(b));
+        float t = 0.f;
+        HCK(hipEventElapsedTime(&t, a, b));
+        ms += t;
+        ++n;
+        kc += p.K;
     }
     if (kernel_ms) *kernel_ms = ms;
     if (launches) *launches = n;
     if (candidates) *candidates = kc;
     if (last_algo) *last_algo = algo;
     if (reset) {
-        for (auto& p : ctx->prof) {
-            ctx->ev_pool.push_back(p.a);
-            ctx->ev_pool.push_back(p.b);
-        }
+        for (auto& p : ctx->prof)
+            for (hipEvent_t e : {p.a, p.b, p.c, p.d})
+                if (e) ctx->ev_pool.push_back(e);
         ctx->prof.clear();
     }
     return MAC_OK;
@@ -743,10 +764,9 @@ void mac_ctx_destroy(mac_ctx* ctx)
                       &ctx->flags_s, &ctx->flags_o, &ctx->keep, &ctx->sel_count, &ctx->cx,
                       &ctx->cy, &ctx->cw, &ctx->cidx, &ctx->circ, &ctx->cdisk})
         b->release();
-    for (auto& p : ctx->prof) {
-        (void)hipEventDestroy(p.a);
-        (void)hipEventDestroy(p.b);
-    }
+    for (auto& p : ctx->prof)
+        for (hipEvent_t e : {p.a, p.b, p.c, p.d})
+            if (e) (void)hipEventDestroy(e);
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
     if (ctx->setup_stream) (void)hipStreamDestroy(ctx->setup_stream);
     if (ctx->dev_stream) (void)hipStreamDestroy(ctx->dev_stream);
@@ -1278,6 +1298,10 @@ int32_t mac_poll_best_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three
     Lane* L = lg.lane;
     const int N = (int)(three_n / 3);
     if (K == 0) {
+        {
+            std::lock_guard<std::mutex> lk(ctx->mu);
+            ctx->mirror_for = nullptr;
+        }
         double hb[2] = {INFINITY, __builtin_bit_cast(double, (int64_t)-1)};
         L->best.reserve(16);
         HCK(hipMemcpyAsync(d_best, hb, 16, hipMemcpyHostToDevice, s));
@@ -1298,8 +1322,24 @@ int32_t mac_poll_best_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three
         L->obj.reserve(sizeof(double) * K);
         d_o = L->obj.as<double>();
     }
+    double* d_mirror = nullptr;
+    uint64_t seq = 0;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        if (!ctx->d_mirror) {
+            ctx->h_best.reserve(64, hipHostMallocMapped | hipHostMallocCoherent);
+            std::memset(ctx->h_best.p, 0, 64);
+            void* dp = nullptr;
+            HCK(hipHostGetDevicePointer(&dp, ctx->h_best.p, 0));
+            ctx->d_mirror = (double*)dp;
+        }
+        d_mirror = ctx->d_mirror;
+        seq = ++ctx->mirror_seq;
+        ctx->mirror_for = d_best;
+    }
     enqueue_eval(ctx, L, s, matrix_src(d_cands, N), N, (int)K, use_tiled(ctx, N, nullptr, three_n), d_rmax,
-                 penalty, d_prev, d_dlimT, tan_half_fov, nullptr, d_o, (double*)d_best, idx_base);
+                 penalty, d_prev, d_dlimT, tan_half_fov, nullptr, d_o, (double*)d_best, idx_base,
+                 d_mirror, seq);
     return MAC_OK;
     ABI_END
 }
@@ -1313,12 +1353,35 @@ int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* b
     set_device(ctx);
     hipStream_t s = stream ? (hipStream_t)stream : ctx->dev_stream;
     std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->h_best.reserve(16);
-    HCK(hipMemcpyAsync(ctx->h_best.p, d_best, 16, hipMemcpyDeviceToHost, s));
-    HCK(hipStreamSynchronize(s));
     const double* hb = (const double*)ctx->h_best.p;
-    if (best_obj) *best_obj = hb[0];
-    if (best_idx) *best_idx = __builtin_bit_cast(int64_t, hb[1]);
+    if (ctx->mirror_for == d_best && hb) {
+        // the latest device poll on d_best mirrors its result: spin on its sequence number (the
+        // poll takes ~0.1 ms), and after 2 ms wait for the stream instead (which also reports a
+        // failed launch)
+        const uint64_t want = ctx->mirror_seq;
+        const uint64_t* flag = (const uint64_t*)(hb + 2);
+        const auto t0 = std::chrono::steady_clock::now();
+        bool ready = false;
+        for (int spin = 0; !ready; ++spin) {
+            ready = __atomic_load_n(flag, __ATOMIC_ACQUIRE) == want;
+            if (!ready && (spin & 1023) == 1023 &&
+                std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+                HCK(hipStreamSynchronize(s));
+                ready = __atomic_load_n(flag, __ATOMIC_ACQUIRE) == want;
+                break;
+            }
+        }
+        if (ready) {
+            if (best_obj) *best_obj = hb[0];
+            if (best_idx) *best_idx = __builtin_bit_cast(int64_t, hb[1]);
+            return MAC_OK;
+        }
+    }
+    double tmp[2];
+    HCK(hipMemcpyAsync(tmp, d_best, 16, hipMemcpyDeviceToHost, s));
+    HCK(hipStreamSynchronize(s));
+    if (best_obj) *best_obj = tmp[0];
+    if (best_idx) *best_idx = __builtin_bit_cast(int64_t, tmp[1]);
     return MAC_OK;
     ABI_END
 }

@@ -278,6 +278,17 @@ def test_device_pointer_api(ctx, pkg, orc):
     assert np.array_equal(tO.cpu().numpy(), wobj)
     b = tB.cpu()
     assert b[0].item() == wobj.min() and b.view(torch.int64)[1].item() == 100 + int(np.argmin(wobj))
+    # the host side of a poll step: mirrored result of the latest poll, then the copy fallback
+    # (another buffer), then a new poll on other candidates through the mirror again
+    assert ctx.best_fetch(tB, stream=s.cuda_stream) == (wobj.min(), 100 + int(np.argmin(wobj)))
+    tB2 = tB.clone()
+    torch.cuda.synchronize(dev)
+    assert ctx.best_fetch(tB2, stream=s.cuda_stream) == (wobj.min(), 100 + int(np.argmin(wobj)))
+    C2 = C[::-1].copy()
+    ctx.poll_best_dev(torch.from_numpy(C2).to(dev), C.shape[1], C.shape[0], tR, tB,
+                      stream=s.cuda_stream)
+    w2 = wobj[::-1]
+    assert ctx.best_fetch(tB, stream=s.cuda_stream) == (w2.min(), int(np.argmin(w2)))
 
 
 # ---------------------------------------------------------------------------- full size
@@ -333,13 +344,18 @@ def test_config4_full_poll(ctx, pkg, orc):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("case", ["real_clustered", "big_radius", "mixed_weights", "pythagorean"])
+@pytest.mark.parametrize("case", ["real_clustered", "big_radius", "mixed_weights", "pythagorean",
+                                  "crowded", "lattice_mixed"])
 def test_poll_walk_stress(ctx, pkg, orc, case):
     """The poll walk's rare paths: fp64 band decisions on real-valued coordinates, ownership
     between overlapping disks, regions larger than one LDS chunk and more than 64 tile rows.
     "pythagorean": integer points at distance exactly r from integer centres (3-4-5, 5-12-13,
     7-24-25 ...), where a = r^2 sits next to the threshold T(r) < r^2: every such entry is in
-    the fp32 filter's band and must be decided in fp64 (not covered: sqrt(r^2) < r is false)."""
+    the fp32 filter's band and must be decided in fp64 (not covered: sqrt(r^2) < r is false).
+    "crowded": 100 disks over one small square, so disks past the 64th have more lower-index
+    neighbours than the list keeps (per-candidate shared path) and the rest take the coverage-
+    word path; "lattice_mixed": lattice polls (few distinct positions) with unequal weights
+    (the word path's bit-by-bit credit)."""
     wl = pkg.workloads
     rng = wl.SplitMix64(4242 + len(case))
     if case == "pythagorean":
@@ -354,6 +370,23 @@ def test_poll_walk_stress(ctx, pkg, orc, case):
         ctx.set_points(x, y, w)
         C = np.concatenate([x0[None, :], wl.poll_candidates(x0, rng, ell=1)], axis=0)
         C[:, 2 * N:] = np.maximum(C[:, 2 * N:], 1.0)
+        want = orc.PointerList(recs(x, y, w)).area_batch(C)
+        r = both(ctx, lambda: ctx.area_batch(C))
+        for a, got in r.items():
+            assert np.array_equal(got, want), (a, np.flatnonzero(got != want)[:5])
+        return
+    if case in ("crowded", "lattice_mixed"):
+        M = 40000
+        x = np.floor(rng.uniform(M) * 400.0)
+        y = np.floor(rng.uniform(M) * 400.0)
+        w = np.full(M, 25.0) if case == "crowded" else np.floor(rng.uniform(M) * 7) + 1
+        N = 100 if case == "crowded" else 30
+        span = 60 if case == "crowded" else 160
+        x0 = np.concatenate([np.floor(200 + rng.uniform(N) * span - span / 2),
+                             np.floor(200 + rng.uniform(N) * span - span / 2),
+                             np.floor(rng.uniform(N) * 20 + 15)])
+        ctx.set_points(x, y, w)
+        C = np.concatenate([x0[None, :], wl.poll_candidates(x0, rng, ell=2)], axis=0)
         want = orc.PointerList(recs(x, y, w)).area_batch(C)
         r = both(ctx, lambda: ctx.area_batch(C))
         for a, got in r.items():

@@ -23,22 +23,8 @@ SHB = 512         # kSharedWG (shared-entry workgroups)
 CHAINC = 16       # kChainC (candidates per penalty-chain workgroup)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--config", type=int, default=4)
-    args = ap.parse_args()
-    pkg = ge.load_package()
-    L = pkg.load_library()
-    if not hasattr(L, "mac_diag_read"):
-        raise SystemExit("not the diagnostic build (set MAXCOVER_LIB)")
-    L.mac_diag_read.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int64]
-    x, y, w, C, rmax = pkg.workloads.make_config(args.config)
-    ctx = pkg.Context(0, algo="poll")
-    ctx.set_points(x, y, w)
-    for _ in range(3):
-        ctx.poll_best(C, rmax)
-    N = C.shape[1] // 3
-    K = C.shape[0]
+def analyze(L, N, K):
+    """Role timings of the LAST poll-kernel launch (N disks, K candidates)."""
     gy = (K + KPB - 1) // KPB
     n_chain = ((K + CHAINC - 1) // CHAINC + gy - 1) // gy
     gx = n_chain + SHB + N
@@ -51,9 +37,12 @@ def main():
     t0, t1 = a[:, 0], a[:, 1]
     role = (a[:, 2].astype(np.uint64) >> np.uint64(56)).astype(np.int64)
     info = a[:, 2] & ((1 << 56) - 1)
+    # the last launch only: blocks that started within 5 ms of the latest start
+    last = t0 >= t0.max() - 500000
+    t0, t1, role, info = t0[last], t1[last], role[last], info[last]
     base = t0.min()
     dur = (t1 - t0) / 100.0
-    out = {"blocks_stamped": int(ok.sum()), "span_us": float((t1.max() - base) / 100.0)}
+    out = {"blocks_stamped": int(last.sum()), "span_us": float((t1.max() - base) / 100.0)}
     for r, name in ((1, "chains"), (2, "shared"), (3, "walk")):
         m = role == r
         if not m.any():
@@ -70,9 +59,43 @@ def main():
             ent = info[m] & 0xFFFFF
             pos = (info[m] >> 20) & 0xFFFFF
             out[name]["entries_median"] = float(np.median(ent))
+            out[name]["entries_max"] = float(np.max(ent))
             out[name]["positions_median"] = float(np.median(pos))
+            out[name]["neighbours_median"] = float(np.median(info[m] >> 40))
         if r == 2:
             out[name]["disks_with_neighbours"] = int(info[m].max())
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=4)
+    args = ap.parse_args()
+    pkg = ge.load_package()
+    L = pkg.load_library()
+    if not hasattr(L, "mac_diag_read"):
+        raise SystemExit("not the diagnostic build (set MAXCOVER_LIB)")
+    L.mac_diag_read.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int64]
+    if args.config == 5:  # the last MADS iteration's poll of the second MPC step (config 5)
+        wl = pkg.workloads
+        rng = wl.SplitMix64(wl.SEED)
+        cfg = wl.CONFIGS[5]
+        fire_kw, x0 = wl.config5_setup(rng, cfg["G"], cfg["N"], cfg["ignition"])
+        ctx = pkg.Context(0, algo="poll")
+        D = pkg.DynamicArea.DynamicArea(**fire_kw, seed=wl.SEED, device=0)
+        sim = pkg.FullSimulation.Simulation(ctx, x0, fire=D, N_iter=100, seed=wl.SEED)
+        for _ in range(2):
+            rec = sim.step()
+        N = x0.size // 3
+        out = analyze(L, N, 2 * 3 * N)
+        out["mpc_step"] = {k: rec[k] for k in ("points", "kept", "evaluations", "mads_s")}
+    else:
+        x, y, w, C, rmax = pkg.workloads.make_config(args.config)
+        ctx = pkg.Context(0, algo="poll")
+        ctx.set_points(x, y, w)
+        for _ in range(3):
+            ctx.poll_best(C, rmax)
+        out = analyze(L, C.shape[1] // 3, C.shape[0])
     print(json.dumps(out, indent=1))
 
 
