@@ -21,7 +21,7 @@ constexpr int kPollKPL = 4;        // poll walk: candidates per lane
 constexpr int kPollThreads = 256;  // poll walk: workgroup size (4 waves share one staging)
 constexpr int kPollWaves = kPollThreads / kWave;
 constexpr int kPollKPB = kPollThreads * kPollKPL;  // poll walk: candidates per workgroup
-constexpr int kSharedWG = 512;     // poll walk: shared-entry workgroups (grid-stride over jobs)
+constexpr int kSharedWG = 1024;    // poll walk: shared-entry workgroups (grid-stride over jobs)
 
 constexpr int kModePoll = 1;
 constexpr int kModeTiled = 2;

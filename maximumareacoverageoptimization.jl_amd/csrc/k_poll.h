@@ -160,7 +160,7 @@ __device__ __forceinline__ float poll_dprime(const float4& e, const PollLane& L)
 // Grid (n_chain + n_shared + N, slices); roles by x, in dispatch order (the first ones overlap
 // the walk): x < n_chain: objective-penalty chains of candidates [16c, 16c + 16),
 // c = y * n_chain + x, into vp (k_final.h), whatever the walk; then, when *mode == kModePoll (or mode == null),
-// n_shared workgroups (row 0) deciding the shared entries into spart, grid-striding over the
+// n_shared x slices workgroups deciding the shared entries into spart, grid-striding over the
 // jobs (disk with neighbours x kShC-candidate slice, k_poll_shared.h), and one
 // workgroup per (disk i,
 // slice g): positions [g*kPollKPB, min(U_i, (g+1)*kPollKPB)) of disk i's distinct disks
@@ -190,11 +190,10 @@ __global__ __launch_bounds__(kPollThreads) __attribute__((amdgpu_waves_per_eu(4)
     }
     const int bx = blockIdx.x - n_chain;
     if (mode && *mode != kModePoll) return;
-    if (bx < n_shared) {  // then (row 0 only): the shared entries (k_poll_shared.h)
+    if (bx < n_shared) {  // then: the shared entries (k_poll_shared.h), over every row
         const int nd = *dcount;
         const int nsub = (K + kShC - 1) / kShC;
-        if (blockIdx.y == 0)
-            for (int job = bx; job < nd * nsub; job += n_shared)
+        for (int job = blockIdx.y * n_shared + bx; job < nd * nsub; job += n_shared * gridDim.y)
                 poll_shared_job(xy, w, off, g, urec, umap, region, nbrT, ncount,
                                 dlist[job / nsub], K, (job % nsub) * kShC, spart);
         MAC_DIAG_STAMP(diag_t0, 2, (uint64_t)nd);

@@ -97,7 +97,7 @@ __device__ __forceinline__ bool entry_shared(int nc, const int4* nbox, int tx, i
 // over groups keeps a heavily overlapped disk from serialising one lane per candidate over all
 // of its shared entries. Writes spart[i*K + k] (the finalize kernel adds the rows of the disks
 // with ncount[i] > 0).
-constexpr int kShC = 32;
+constexpr int kShC = 128;
 constexpr int kShG = kPollThreads / kShC;
 __device__ __forceinline__ void poll_shared_job(
     const double2* __restrict__ xy, const double* __restrict__ w,

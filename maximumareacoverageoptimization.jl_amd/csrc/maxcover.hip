@@ -519,7 +519,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             const int chains = (K + kChainC - 1) / kChainC;          // spread over the gy rows
             const int n_chain = d_obj ? (chains + gy - 1) / gy : 0;
             L->spart.reserve(sizeof(double) * (size_t)N * K);
-            const int n_shared = kSharedWG;
+            const int n_shared = (kSharedWG + gy - 1) / gy;
             const dim3 pgrid(n_chain + n_shared + N, gy);
             hipExtLaunchKernelGGL(coverage_poll_kernel, pgrid, dim3(kPollThreads), 0, s, pa0, pb0, 0,
                                ctx->xys.as<double2>(), ctx->ws.as<double>(),

@@ -19,7 +19,7 @@ import __graft_entry__ as ge  # noqa: E402
 
 KPB = 1024        # kPollKPB
 THREADS = 256     # kPollThreads
-SHB = 512         # kSharedWG (shared-entry workgroups)
+SHB = 1024        # kSharedWG (shared-entry workgroups, spread over the grid rows)
 CHAINC = 16       # kChainC (candidates per penalty-chain workgroup)
 
 
@@ -27,7 +27,7 @@ def analyze(L, N, K):
     """Role timings of the LAST poll-kernel launch (N disks, K candidates)."""
     gy = (K + KPB - 1) // KPB
     n_chain = ((K + CHAINC - 1) // CHAINC + gy - 1) // gy
-    gx = n_chain + SHB + N
+    gx = n_chain + (SHB + gy - 1) // gy + N
     nb = gx * gy
     buf = (ctypes.c_uint64 * (4 * nb))()
     assert L.mac_diag_read(buf, 4 * nb) == 0
