@@ -2,9 +2,15 @@
 
 One step = one complete MADS poll over a synthetic fire grid: K = 6N+1 candidates (incumbent +
 2n LTMADS directions, n = 3N) evaluated by libmaxcover, objective + argmin on the device, and
-— for N GPUs > 1 — the 16-byte-per-rank all-gather of the local best (RCCL over xGMI). The poll
-candidates are sharded across ranks (strong scaling: the poll is fixed, ranks split it). Each
+— for N GPUs > 1 — the 16-byte-per-rank all-gather of the local best (RCCL over xGMI). Each
 rank holds a full replica of the point list in HBM; inputs are resident before timing starts.
+
+Multi-GPU (`--scaling`):
+  weak (default)  every rank evaluates a complete K-candidate poll set of its own (independent
+                  LTMADS bases around the same incumbent, rank 0's being the single-GPU poll), so
+                  one step polls P*K candidates and the all-gather picks the best of all of
+                  them: per-GPU work fixed as P grows;
+  strong          the single K-candidate poll is split into P contiguous candidate shards.
 
 Default workload: BASELINE config 4 (512 UAVs, 4096 x 4096 = 16.8M-cell grid, K = 3073, fp64),
 the configuration the north-star targets are quoted on and the one the 1/2/4/8-GPU scaling
@@ -174,6 +180,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=20250216)
+    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
+                    help="N>1: weak = one full poll set per GPU (P*K candidates per step); "
+                         "strong = the single poll split over the GPUs")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL on ROCm) for the real multi-GPU run; gloo only to rehearse "
                          "N>1 with several ranks sharing one GPU (MAXCOVER_BENCH_DEVICE)")
@@ -217,11 +226,21 @@ def main():
         for p in polls[1:]:
             p[0, : 2 * N] += rng.integers(-2, 2, 2 * N)
     else:
-        polls = [wl.poll_candidates(x0, rng) for _ in range(args.polls)]
+        # weak scaling: rank r > 0 draws its own poll sets (rank 0's are the single-GPU polls)
+        prng = rng if (rank == 0 or args.scaling == "strong") else \
+            wl.SplitMix64(args.seed ^ (0x9E3779B97F4A7C15 * rank & 0xFFFFFFFFFFFFFFFF))
+        polls = [wl.poll_candidates(x0, prng) for _ in range(args.polls)]
     K = polls[0].shape[0]
     r_max = np.full(N, 30.0 * np.tan(100 / 180 * np.pi / 2))
     M = x.size
-    lo, hi = pdist.shard_range(K, rank, world)
+    if args.scaling == "weak":
+        lo, hi = 0, K                      # a whole poll set per rank
+        idx_base = rank * K                # global candidate index = rank * K + k
+        K_step = K * world                 # candidates evaluated per step, all ranks
+    else:
+        lo, hi = pdist.shard_range(K, rank, world)
+        idx_base = lo
+        K_step = K
     Kl = hi - lo
 
     ctx = pkg.Context(dev_index, algo=args.algo, tile_points=args.tile_points)
@@ -238,7 +257,7 @@ def main():
         """One MADS poll. It ends with the best (objective, index) on the host, because the
         next poll's candidates depend on it: polls never overlap."""
         d = d_polls[i % len(d_polls)]
-        ctx.poll_best_dev(d, 3 * N, Kl, d_rmax, d_best, idx_base=lo, stream=s_handle)
+        ctx.poll_best_dev(d, 3 * N, Kl, d_rmax, d_best, idx_base=idx_base, stream=s_handle)
         if distributed:
             with torch.cuda.stream(stream):
                 return pdist.gather_best(d_best if coll_dev.type == "cuda" else d_best.cpu())
@@ -283,7 +302,7 @@ def main():
         b = d_best.cpu()
         result = (float(b[0]), int(b.view(torch.int64)[1]))
 
-    total_evals = K * args.steps
+    total_evals = K_step * args.steps
     value = total_evals / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
@@ -323,16 +342,20 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {
                 "workload": f"config {args.config}: {cfg['name']}",
                 "uavs": N, "cells": M, "grid": f"{G}x{G} @ 5 m", "candidates_per_poll": K,
+                "candidates_per_step": K_step,
                 "poll": "incumbent + 2n LTMADS directions (n=3N), l=2, delta=1",
                 "disks": "integer centres uniform over the domain, R=36",
-                "parallelism": f"candidates sharded over {world} GPU(s), 16-B argmin all-gather",
+                "parallelism": (f"{world} GPU(s), one full poll set each, 16-B argmin all-gather"
+                                if args.scaling == "weak" else
+                                f"one poll's candidates sharded over {world} GPU(s), "
+                                f"16-B argmin all-gather"),
                 "algo": args.algo,
             },
             "roofline": {
@@ -346,8 +369,9 @@ def main():
                 "bytes_per_eval": b_eval,
                 "evals_per_launch": cands_per_launch,
                 "avg_launch_ms": avg_launch_ms,
+                "timing": "in-kernel workgroup stamps (s_memrealtime) over the timed steps",
                 "note": "achieved = SURVEY 8(d) algorithmic bytes (24 B x M entries + disks) per "
-                        "eval x evals per launch / launch time; the tiled walk reads only the "
+                        "eval x evals per launch / launch time; the walks read only the "
                         "entries near the disks, so frac > 1 is by design (see DESIGN.md)",
             },
             "cpu_baseline": cpu,

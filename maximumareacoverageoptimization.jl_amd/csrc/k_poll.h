@@ -167,7 +167,7 @@ __device__ __forceinline__ float poll_dprime(const float4& e, const PollLane& L)
 // (urec / ucount, k_index.h), thread t pass u ->
 // p = kb + 256u + t; partial[i*K + p] = weight of the non-shared entries credited to that disk
 // (finalize gathers it for every candidate through the map).
-__global__ __launch_bounds__(kPollThreads) __attribute__((amdgpu_waves_per_eu(4))) void coverage_poll_kernel(
+__device__ __forceinline__ void coverage_poll_body(
     const double2* __restrict__ xy, const double* __restrict__ w,
     const int32_t* __restrict__ off, Grid g, const DiskRec* __restrict__ urec,
     const int* __restrict__ umap, const int* __restrict__ ucount,
@@ -408,6 +408,23 @@ __global__ __launch_bounds__(kPollThreads) __attribute__((amdgpu_waves_per_eu(4)
     for (int u = 0; u < kPollKPL; ++u)
         if (kk[u] >= 0) partial[row + kk[u]] = acc[u];
     MAC_DIAG_STAMP(diag_t0, 3, ((uint64_t)nc << 40) | ((uint64_t)(ke - kb) << 20) | (uint64_t)diag_entries);
+}
+
+// timed entry point (ts: in-kernel launch timing, k_common.h)
+__global__ __launch_bounds__(kPollThreads) __attribute__((amdgpu_waves_per_eu(4))) void coverage_poll_kernel(
+    uint64_t* ts, const double2* __restrict__ xy, const double* __restrict__ w,
+    const int32_t* __restrict__ off, Grid g, const DiskRec* __restrict__ urec,
+    const int* __restrict__ umap, const int* __restrict__ ucount,
+    const int4* __restrict__ region, const uint16_t* __restrict__ nbrT,
+    const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
+    int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
+    double* __restrict__ spart, int n_chain, const double* __restrict__ pen, double penalty,
+    double* __restrict__ vp, int n_shared)
+{
+    ts_begin(ts);
+    coverage_poll_body(xy, w, off, g, urec, umap, ucount, region, nbrT, ncount, dlist, dcount, N, K,
+                       mode, partial, spart, n_chain, pen, penalty, vp, n_shared);
+    ts_end(ts);
 }
 
 }  // namespace mac

@@ -19,7 +19,7 @@ namespace mac {
 // reference's first-hit `break` changes which disk is credited, never the sum.
 // partial[blk*K + k]: this block's share of candidate k.
 template <int KB, int PPT>
-__global__ __launch_bounds__(kBlock) void coverage_scan_kernel(
+__device__ __forceinline__ void coverage_scan_body(
     const double2* __restrict__ xy, const double* __restrict__ w, int64_t M,
     const DiskRec* __restrict__ disks, int N, int K, int64_t chunk,
     double* __restrict__ partial)
@@ -101,7 +101,7 @@ __host__ __device__ inline size_t tiled_lds_bytes(int N)
 // list built in LDS). Disk c of candidate k through the disk index (k_index.h);
 // partial[gi*K + k]. Runs only when *mode == kModeTiled
 // (or mode == null). Workgroups loop over units (grid-stride).
-__global__ __launch_bounds__(kBlock) void coverage_tiled_kernel(
+__device__ __forceinline__ void coverage_tiled_body(
     const double2* __restrict__ xy, const double* __restrict__ w,
     const int32_t* __restrict__ off, Grid g,
     const DiskRec* __restrict__ urec, const int* __restrict__ umap, int N, int K, int G,
@@ -210,6 +210,28 @@ __global__ __launch_bounds__(kBlock) void coverage_tiled_kernel(
     const double s = block_sum_f64(acc, red);
     if (threadIdx.x == 0) partial[(int64_t)gi * K + k] = s;
     }
+}
+
+// timed entry points (ts: in-kernel launch timing, k_common.h)
+template <int KB, int PPT>
+__global__ __launch_bounds__(kBlock) void coverage_scan_kernel(
+    uint64_t* ts, const double2* __restrict__ xy, const double* __restrict__ w, int64_t M,
+    const DiskRec* __restrict__ disks, int N, int K, int64_t chunk, double* __restrict__ partial)
+{
+    ts_begin(ts);
+    coverage_scan_body<KB, PPT>(xy, w, M, disks, N, K, chunk, partial);
+    ts_end(ts);
+}
+
+__global__ __launch_bounds__(kBlock) void coverage_tiled_kernel(
+    uint64_t* ts, const double2* __restrict__ xy, const double* __restrict__ w,
+    const int32_t* __restrict__ off, Grid g, const DiskRec* __restrict__ urec,
+    const int* __restrict__ umap, int N, int K, int G, const int* __restrict__ mode,
+    double* __restrict__ partial)
+{
+    ts_begin(ts);
+    coverage_tiled_body(xy, w, off, g, urec, umap, N, K, G, mode, partial);
+    ts_end(ts);
 }
 
 }  // namespace mac

@@ -142,11 +142,13 @@ struct mac_ctx {
 
     int algo = MAC_ALGO_AUTO;
     bool profile = false;
-    std::vector<hipEvent_t> ev_pool;                 // free timing events
-    // a / b: the walk launch's start / stop; c / d: the poll kernel's when the device picks the
-    // walk (mode != null): the pair of the walk that ran is read
-    struct Prof { hipEvent_t a, b, c, d; int64_t K; const int* mode; int algo; };
+    // In-kernel launch timing (k_common.h ts_begin / ts_end): each profiled walk launch takes
+    // nwg consecutive {start, end} slots of `stamps`. a: the scan / tiled launch, b: the poll
+    // launch when the device picks the walk (mode != null): the launch that ran is read.
+    struct Prof { int64_t a, na, b, nb; int64_t K; const int* mode; int algo; };
     std::vector<Prof> prof;                          // recorded launches (guarded by mu)
+    DevBuf stamps;
+    int64_t stamp_cap = 0, stamp_used = 0;           // in workgroup slots (guarded by mu)
     int storage = MAC_STORE_F64;
     int tile_ppt = 4;
 
@@ -392,34 +394,22 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             d_pen = L->pen.as<double>();
         }
     }
-    // Profiling: the measured launches carry start / stop events stamped by the dispatch itself
-    // (hipExtLaunchKernelGGL), so measuring adds no marker packets (and no gaps) to the stream.
-    hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_c = nullptr, ev_d = nullptr;
-    auto take_ev = [&]() -> hipEvent_t {
-        hipEvent_t e = nullptr;
-        {
-            std::lock_guard<std::mutex> lk(ctx->mu);
-            if (!ctx->ev_pool.empty()) {
-                e = ctx->ev_pool.back();
-                ctx->ev_pool.pop_back();
-            }
-        }
-        if (!e) HCK(hipEventCreate(&e));
-        return e;
-    };
-    auto prof_begin = [&](bool two) {
-        if (!ctx->profile) return;
-        ev_a = take_ev();
-        ev_b = take_ev();
-        if (two) {
-            ev_c = take_ev();
-            ev_d = take_ev();
-        }
+    // Profiling: the measured walk launches stamp their own workgroups' start / end times
+    // (k_common.h), so measuring adds no packet, event or dependency to the stream.
+    int64_t ts_a = -1, ts_na = 0, ts_b = -1, ts_nb = 0;
+    auto take_ts = [&](int64_t nwg, int64_t& base, int64_t& n) -> uint64_t* {
+        if (!ctx->profile) return nullptr;
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        if (ctx->stamp_used + nwg > ctx->stamp_cap) return nullptr;   // full: not recorded
+        base = ctx->stamp_used;
+        n = nwg;
+        ctx->stamp_used += nwg;
+        return ctx->stamps.as<uint64_t>() + 2 * base;
     };
     auto prof_end = [&]() {
-        if (!ctx->profile) return;
+        if (!ctx->profile || (ts_a < 0 && ts_b < 0)) return;
         std::lock_guard<std::mutex> lk(ctx->mu);
-        ctx->prof.push_back({ev_a, ev_b, ev_c, ev_d, (int64_t)K, d_mode,
+        ctx->prof.push_back({ts_a, ts_na, ts_b, ts_nb, (int64_t)K, d_mode,
                              tiled ? MAC_ALGO_TILED : MAC_ALGO_SCAN});
     };
 
@@ -448,9 +438,9 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         nblk = std::max<int64_t>(1, (M + chunk - 1) / chunk);
         n_other = (int)nblk;
         L->partial.reserve(sizeof(double) * (size_t)K * nblk);
-        prof_begin(false);
-        hipExtLaunchKernelGGL((coverage_scan_kernel<KB, PPT>), dim3((unsigned)nblk, (unsigned)kgroups),
-                           dim3(kBlock), 0, s, ev_a, ev_b, 0, ctx->xys.as<double2>(), ctx->ws.as<double>(), M,
+        uint64_t* ts = take_ts(nblk * kgroups, ts_a, ts_na);
+        hipLaunchKernelGGL((coverage_scan_kernel<KB, PPT>), dim3((unsigned)nblk, (unsigned)kgroups),
+                           dim3(kBlock), 0, s, ts, ctx->xys.as<double2>(), ctx->ws.as<double>(), M,
                            L->disks.as<DiskRec>(), N, K, chunk, L->partial.as<double>());
         HCK(hipGetLastError());
         prof_end();
@@ -501,15 +491,14 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             d_umap = d_map;
         }
         const bool run_tiled = ctx->algo != MAC_ALGO_POLL;
-        prof_begin(run_tiled && poll_possible);
-        // events: tiled -> (a, b) and poll -> (c, d) when both run, else the one that runs -> (a, b)
-        hipEvent_t pa0 = run_tiled ? ev_c : ev_a, pb0 = run_tiled ? ev_d : ev_b;
         if (run_tiled) {
             const size_t lds = tiled_lds_bytes(N);
             const int64_t units = (int64_t)K * G;
             const int64_t cap = poll_possible ? 4 * (int64_t)ctx->cus : units;
-            hipExtLaunchKernelGGL(coverage_tiled_kernel, dim3((unsigned)std::min(units, cap)), dim3(kBlock),
-                               (uint32_t)lds, s, ev_a, ev_b, 0, ctx->xys.as<double2>(), ctx->ws.as<double>(),
+            const unsigned nwg = (unsigned)std::min(units, cap);
+            uint64_t* ts = take_ts(nwg, ts_a, ts_na);
+            hipLaunchKernelGGL(coverage_tiled_kernel, dim3(nwg), dim3(kBlock),
+                               (uint32_t)lds, s, ts, ctx->xys.as<double2>(), ctx->ws.as<double>(),
                                ctx->off.as<int32_t>(), ctx->grid, d_urec, d_map, N, K, G,
                                d_mode, L->partial.as<double>());
             HCK(hipGetLastError());
@@ -521,7 +510,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             L->spart.reserve(sizeof(double) * (size_t)N * K);
             const int n_shared = (kSharedWG + gy - 1) / gy;
             const dim3 pgrid(n_chain + n_shared + N, gy);
-            hipExtLaunchKernelGGL(coverage_poll_kernel, pgrid, dim3(kPollThreads), 0, s, pa0, pb0, 0,
+            uint64_t* ts = take_ts((int64_t)pgrid.x * pgrid.y, ts_b, ts_nb);
+            hipLaunchKernelGGL(coverage_poll_kernel, pgrid, dim3(kPollThreads), 0, s, ts,
                                ctx->xys.as<double2>(), ctx->ws.as<double>(),
                                ctx->off.as<int32_t>(), ctx->grid, d_urec, d_map,
                                L->ucount.as<int>(), L->region.as<int4>(), L->nbr.as<uint16_t>(),
@@ -670,27 +660,37 @@ int32_t mac_profile_read(mac_ctx* ctx, double* kernel_ms, int64_t* launches,
     ABI_BEGIN
     if (!ctx) return fail(MAC_E_INVAL, "null context");
     set_device(ctx);
+    HCK(hipDeviceSynchronize());   // every recorded launch has completed
     std::lock_guard<std::mutex> lk(ctx->mu);
+    std::vector<uint64_t> st((size_t)(2 * ctx->stamp_used));
+    if (!st.empty())
+        HCK(hipMemcpy(st.data(), ctx->stamps.p, sizeof(uint64_t) * st.size(), hipMemcpyDeviceToHost));
     double ms = 0.0;
     int64_t n = 0, kc = 0;
     int algo = 0;
+    // launch time = last wave end - first workgroup start over the launch's workgroups
+    auto span_ms = [&](int64_t base, int64_t nwg) {
+        uint64_t t0 = ~(uint64_t)0, t1 = 0;
+        for (int64_t q = base; q < base + nwg; ++q) {
+            t0 = std::min(t0, st[(size_t)(2 * q)]);
+            t1 = std::max(t1, st[(size_t)(2 * q + 1)]);
+        }
+        return t1 > t0 ? (double)(t1 - t0) / kRealtimeHz * 1e3 : 0.0;
+    };
     for (auto& p : ctx->prof) {
         algo = p.algo;
-        hipEvent_t a = p.a, b = p.b;
+        int64_t a = p.a, na = p.na;
         if (p.mode) {  // the device's choice (the lane's mode word holds its latest decision)
-            HCK(hipEventSynchronize(p.d ? p.d : p.b));
             int m = 0;
             HCK(hipMemcpy(&m, p.mode, sizeof(int), hipMemcpyDeviceToHost));
             algo = m == kModePoll ? MAC_ALGO_POLL : MAC_ALGO_TILED;
-            if (p.c && m == kModePoll) {
-                a = p.c;
-                b = p.d;
+            if (m == kModePoll) {
+                a = p.b;
+                na = p.nb;
             }
         }
-        HCK(hipEventSynchronize(b));
-        float t = 0.f;
-        HCK(hipEventElapsedTime(&t, a, b));
-        ms += t;
+        if (a < 0) continue;
+        ms += span_ms(a, na);
         ++n;
         kc += p.K;
     }
@@ -699,10 +699,9 @@ int32_t mac_profile_read(mac_ctx* ctx, double* kernel_ms, int64_t* launches,
     if (candidates) *candidates = kc;
     if (last_algo) *last_algo = algo;
     if (reset) {
-        for (auto& p : ctx->prof)
-            for (hipEvent_t e : {p.a, p.b, p.c, p.d})
-                if (e) ctx->ev_pool.push_back(e);
         ctx->prof.clear();
+        if (ctx->stamp_used) HCK(hipMemset(ctx->stamps.p, 0, sizeof(uint64_t) * 2 * ctx->stamp_used));
+        ctx->stamp_used = 0;
     }
     return MAC_OK;
     ABI_END
@@ -764,10 +763,7 @@ void mac_ctx_destroy(mac_ctx* ctx)
                       &ctx->flags_s, &ctx->flags_o, &ctx->keep, &ctx->sel_count, &ctx->cx,
                       &ctx->cy, &ctx->cw, &ctx->cidx, &ctx->circ, &ctx->cdisk})
         b->release();
-    for (auto& p : ctx->prof)
-        for (hipEvent_t e : {p.a, p.b, p.c, p.d})
-            if (e) (void)hipEventDestroy(e);
-    for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
+    ctx->stamps.release();
     if (ctx->setup_stream) (void)hipStreamDestroy(ctx->setup_stream);
     if (ctx->dev_stream) (void)hipStreamDestroy(ctx->dev_stream);
     delete ctx;
@@ -787,9 +783,23 @@ int32_t mac_set_option(mac_ctx* ctx, int32_t option, int64_t value)
         if (value == MAC_STORE_F32) return fail(MAC_E_INVAL, "f32 storage not available yet");
         ctx->storage = (int)value;
         return MAC_OK;
-    case MAC_OPT_PROFILE:
+    case MAC_OPT_PROFILE: {
+        ABI_BEGIN
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        if (value && !ctx->profile) {  // fresh, zeroed stamp slots (outside any timed region)
+            set_device(ctx);
+            constexpr int64_t kSlots = (int64_t)1 << 20;   // 16 MB: ~600 config-4 poll launches
+            ctx->stamps.reserve(sizeof(uint64_t) * 2 * kSlots);
+            HCK(hipDeviceSynchronize());
+            HCK(hipMemset(ctx->stamps.p, 0, sizeof(uint64_t) * 2 * kSlots));
+            ctx->stamp_cap = kSlots;
+            ctx->stamp_used = 0;
+            ctx->prof.clear();
+        }
         ctx->profile = value != 0;
         return MAC_OK;
+        ABI_END
+    }
     case MAC_OPT_TILE_POINTS:
         if (value < 1 || value > 4096) return fail(MAC_E_INVAL, "tile points out of range");
         ctx->tile_ppt = (int)value;

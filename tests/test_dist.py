@@ -16,7 +16,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, mode="strong"):
     import sys
     import torch
     import torch.distributed as dist
@@ -38,8 +38,19 @@ def _worker(rank, world, port, q):
     # make ties: duplicate the best candidate at a later index on the other shard
     C = np.concatenate([C, C[:3]], axis=0)
     rmax = np.full(6, 36.0)
-    lo, hi = d.shard_range(C.shape[0], rank, world)
-    objs = np.array([orc.ref_objective(c, rec, rmax) for c in C[lo:hi]])
+    if mode == "weak":
+        # bench.py --scaling weak: every rank polls a whole candidate set of its own (rank r's set
+        # drawn from its own stream), global index = r * K + k; the step's poll is the union
+        sets = [C] + [wl.poll_candidates(x0, wl.SplitMix64(1000 + r)) for r in range(1, world)]
+        K = C.shape[0]
+        sets[1:] = [np.concatenate([s_, s_[:3]], axis=0) for s_ in sets[1:]]   # same K
+        mine = sets[rank]
+        lo = rank * K
+        objs = np.array([orc.ref_objective(c, rec, rmax) for c in mine])
+        C = np.concatenate(sets, axis=0)
+    else:
+        lo, hi = d.shard_range(C.shape[0], rank, world)
+        objs = np.array([orc.ref_objective(c, rec, rmax) for c in C[lo:hi]])
     k = int(np.argmin(objs)) if objs.size else -1
     best = d.pack_best(objs[k] if k >= 0 else np.inf, lo + k if k >= 0 else -1)
     got = d.gather_best(best)
@@ -49,11 +60,15 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_gloo_world2_poll_argmin():
+import pytest
+
+
+@pytest.mark.parametrize("mode", ["strong", "weak"])
+def test_gloo_world2_poll_argmin(mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, mode)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in procs]

@@ -30,11 +30,11 @@ fatal() {  # exit codes after which nothing more may touch the GPU
 for s in $STEPS; do
     case $s in
     tests)
-        run pytest_gpu 1500 python -m pytest tests -m gpu -q -rfE -p no:cacheprovider ; rc=$? ;;
+        run pytest_gpu 600 python -u -m pytest tests -m gpu -x -v -rfE -p no:cacheprovider --timeout 120 --timeout-method thread ; rc=$? ;;
     smoke)
         run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ; rc=$? ;;
     bench)
-        run bench 900 python bench.py ; rc=$?
+        run bench 400 python bench.py ; rc=$?
         grep '^{' gpurun_out/bench.log > gpurun_out/bench_${TAG}.json ;;
     algos)
         for a in tiled poll auto; do
@@ -49,13 +49,17 @@ for s in $STEPS; do
         make -s -C maximumareacoverageoptimization.jl_amd/csrc diag
         MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
             run diagidx 600 python tools/diag_index.py ; rc=$? ;;
+    weak2)   # rehearsal of the N=2 path on one GPU (gloo; both ranks on device 0)
+        MAXCOVER_BENCH_DEVICE=0 run weak2 300 python -m torch.distributed.run --nnodes=1 \
+            --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 \
+            --no-cpu --dist-backend gloo --steps 20 ; rc=$? ;;
     bench3)
         run bench3 600 python bench.py --config 3 --no-cpu ; rc=$? ;;
     bench2)
         run bench2 600 python bench.py --config 2 --no-cpu ; rc=$? ;;
     prof)
         rm -rf gpurun_out/prof
-        run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
+        run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
             -- python3 bench.py --steps 10 --warmup 2 --no-cpu ; rc=$?
         find gpurun_out/prof -name '*stats*' | head ;;
     pmc)
