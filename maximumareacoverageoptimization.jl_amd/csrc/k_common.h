@@ -95,10 +95,11 @@ __device__ __forceinline__ bool disk_span(const DiskRec& d, const Grid& g, int4&
 
 
 // ------------------------------------------------------------------ in-kernel launch timing
-// Profiling only (ts == null otherwise): workgroup b writes ts[2b] = its first wave's start and
-// raises ts[2b+1] to each wave's end, in s_memrealtime ticks (the constant 100 MHz clock, 10 ns).
-// The host takes max(end) - min(start) over the launch's workgroups. Unlike HIP events this puts
-// no extra packet or dependency into the stream, so the timed region runs as it does unprofiled.
+// Profiling only (ts == null otherwise): workgroup b writes ts[2b] = its start and ts[2b+1] = the
+// end of its last wave, in s_memrealtime ticks (the constant 100 MHz clock, 10 ns). The host takes
+// max(end) - min(start) over the launch's workgroups. Unlike HIP events this puts no extra packet
+// or dependency into the stream, so the timed region runs as it does unprofiled; per workgroup
+// it costs two plain stores, one barrier at entry and one LDS atomic per wave.
 constexpr double kRealtimeHz = 100.0e6;
 
 __device__ __forceinline__ uint64_t* ts_slot(uint64_t* ts)
@@ -106,16 +107,29 @@ __device__ __forceinline__ uint64_t* ts_slot(uint64_t* ts)
     return ts + 2 * ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x);
 }
 
+__device__ __forceinline__ int& ts_waves_done()
+{
+    __shared__ int done;
+    return done;
+}
+
 __device__ __forceinline__ void ts_begin(uint64_t* ts)
 {
-    if (ts && threadIdx.x == 0) ts_slot(ts)[0] = __builtin_amdgcn_s_memrealtime();
+    if (!ts) return;   // uniform
+    if (threadIdx.x == 0) {
+        ts_slot(ts)[0] = __builtin_amdgcn_s_memrealtime();
+        ts_waves_done() = 0;
+    }
+    __syncthreads();
 }
 
 __device__ __forceinline__ void ts_end(uint64_t* ts)
 {
-    if (ts && (threadIdx.x & (kWave - 1)) == 0)
-        atomicMax((unsigned long long*)(ts_slot(ts) + 1),
-                  (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (ts && (threadIdx.x & (kWave - 1)) == 0) {
+        const int nw = (int)((blockDim.x + kWave - 1) / kWave);
+        if (atomicAdd(&ts_waves_done(), 1) == nw - 1)   // the workgroup's last wave
+            ts_slot(ts)[1] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 }  // namespace mac

@@ -13,18 +13,16 @@
 // at ell = 2 in the config-4 polls.
 //
 // disk_index_kernel reads the K candidates' (x_i, y_i, r_i) once, straight from the candidate
-// source (the matrix, or the LTMADS generator). It numbers the distinct disks in an LDS hash table
-// (exact keys: the bit patterns of the three doubles) and writes per distinct disk u the record
-// urec[i*K + u], plus the map umap[i*K + k] = u and the penalty term pen[i*K + k] for every
-// candidate (computed once per distinct disk) and the count ucount[i]. It also writes disk i's region (the union of its tile
+// source (the matrix's fp32 keys, or the LTMADS generator). It numbers the distinct disks in an
+// LDS hash table (exact keys, see "Keys" below) and writes per distinct disk u the record
+// urec[i*K + u], plus, for every candidate, the map umap[i*K + k] = u and the penalty term
+// pen[i*K + k], and the count ucount[i]. It also writes disk i's region (the union of its tile
 // spans over the K candidates) and the two walk costs (K * |region|, sum of span areas).
 // Consumers read disk i of candidate k as urec[i*K + umap[i*K + k]]: the result is bit-identical
 // to per-candidate records (same inputs, same arithmetic), and every candidate is still
-// evaluated. Polls larger than kIndexMaxK use the identity map (one position per candidate).
+// evaluated. Polls larger than kIndexMaxK + 1 use the identity map (one position per candidate).
 //
-// Workgroup b handles disk (b % 8) * ceil(N/8) + b / 8. Workgroups go to the 8 XCDs round-robin,
-// so consecutive disks run on one XCD and share its L2 for the candidate matrix's cache lines
-// (8 consecutive doubles of a column: 8 consecutive disks).
+// Workgroup b handles disk (b % 8) * ceil(N/8) + b / 8: consecutive disks on one XCD.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -45,13 +43,17 @@ __device__ uint64_t g_diag_index[8 * 65536];  // diagnostic build only: per-disk
 #else
 #define MAC_IDX_STAMP(q)
 #endif
-constexpr int kIndexMaxK = 3584;             // larger polls: identity map (load <= 7/8)
+constexpr int kIdxThreads = 1024;            // 16 waves: the phases are latency-bound
+constexpr int kIdxWaves = kIdxThreads / kWave;
+constexpr int kIdxPer = 3;                   // candidates per thread, held in registers
+constexpr int kIndexMaxK = kIdxThreads * kIdxPer;   // 3072 + 1 (below): larger polls use the
+                                                    // identity map (table load <= 3/4)
 
-__device__ __forceinline__ uint32_t key_hash(uint64_t a, uint64_t b, uint64_t c)
+__device__ __forceinline__ uint32_t key_hash(uint32_t a, uint32_t b, uint32_t c)
 {
-    uint64_t z = a * 0x9E3779B97F4A7C15ull;
-    z ^= b + 0xBF58476D1CE4E5B9ull + (z << 6) + (z >> 2);
-    z ^= c + 0x94D049BB133111EBull + (z << 6) + (z >> 2);
+    uint64_t z = (uint64_t)a * 0x9E3779B97F4A7C15ull;
+    z ^= (uint64_t)b + 0xBF58476D1CE4E5B9ull + (z << 6) + (z >> 2);
+    z ^= (uint64_t)c + 0x94D049BB133111EBull + (z << 6) + (z >> 2);
     z = (z ^ (z >> 31)) * 0xD6E8FEB86659FD93ull;
     return (uint32_t)(z ^ (z >> 32));
 }
@@ -68,9 +70,6 @@ __device__ __forceinline__ bool span_of(double x, double y, double r, const Grid
     return true;
 }
 
-constexpr int kIdxThreads = 1024;            // 16 waves: the phases are latency-bound
-constexpr int kIdxWaves = kIdxThreads / kWave;
-
 struct IndexOut {
     DiskRec* urec;
     double* pen;     // per candidate: pen[i*K + k] (null: no objective)
@@ -81,15 +80,31 @@ struct IndexOut {
     int* dcount;     // the poll walk's disks-with-neighbours counter, cleared here
 };
 
-__global__ __launch_bounds__(kIdxThreads) void disk_index_kernel(CandSrc src, int N, int K, Grid g,
-                                                            PenArgs pa, int dedup, IndexOut o)
+// fp32 key of value v relative to the base b: exact when b + (double)key reproduces v bit for bit
+__device__ __forceinline__ float key_of(double v, double b, bool& ok)
 {
-    __shared__ double kx[kIndexMaxK], ky[kIndexMaxK], kr[kIndexMaxK];
+    const float f = (float)(v - b);
+    ok &= __builtin_bit_cast(uint64_t, b + (double)f) == __builtin_bit_cast(uint64_t, v);
+    return f;
+}
+
+// Keys. A candidate's disk (x, y, r) is keyed by three fp32 offsets from candidate 0's disk,
+// kept only when they reproduce the doubles exactly (b + (double)key == value, bit for bit): then
+// equal keys mean equal disks, so two candidates share a position only when their disks are
+// identical. A MADS poll moves a UAV by mesh multiples, which always compress; a disk whose K
+// values do not all compress gets the identity map (one position per candidate: still exact,
+// only slower walks). Each thread holds its kIdxPer candidates' doubles in registers through
+// every phase, and the LDS holds only the fp32 keys, the table and the owners (~60 KB), so two
+// workgroups fit a CU and the whole index runs in one round at N = 512.
+// kKeys: a candidate matrix, whose fp32 keys and exactness flags cands_keys_kernel wrote
+// (src.keysT, src.kbad; exact doubles from src.cands); else the generator (src.get), keyed here.
+template <bool kKeys>
+__global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(8))) void disk_index_kernel(
+    CandSrc src, int N, int K, Grid g, PenArgs pa, int dedup, IndexOut o)
+{
+    __shared__ float kx[kIndexMaxK + 1], ky[kIndexMaxK + 1], kr[kIndexMaxK + 1];
     __shared__ int table[kIndexSlots];       // owner candidate, then (owner << 12 | id)
-    __shared__ uint16_t slot_of[kIndexMaxK];
-    __shared__ uint16_t owner_of[kIndexMaxK];
-    __shared__ int mult[kIndexMaxK];         // candidates per distinct disk
-    __shared__ double s_pen[kIndexMaxK];     // penalty term per distinct disk
+    __shared__ uint16_t owner_of[kIndexMaxK + 1];
     __shared__ int ucnt;
     __shared__ int sred[4][kIdxWaves];
     __shared__ double dred[kIdxWaves];
@@ -101,76 +116,115 @@ __global__ __launch_bounds__(kIdxThreads) void disk_index_kernel(CandSrc src, in
     if (blockIdx.x == 0 && threadIdx.x == 0) *o.dcount = 0;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
     const int64_t row = (int64_t)i * K;
-    const bool hashed = dedup && K <= kIndexMaxK;
+    // candidates of this thread: k = tid + j * kIdxThreads (j < kIdxPer), and thread 0 also
+    // takes k = kIndexMaxK (a full MADS poll is 2n + 1 = kIndexMaxK + 1 candidates at most here)
+    const bool fits = dedup && K > 0 && K <= kIndexMaxK + 1;
 
     int4 R = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
     double span_area = 0.0;
-    auto add_span = [&](double x, double y, double r, double m) {
+    auto add_span = [&](double x, double y, double r) {
         int4 sp;
         if (span_of(x, y, r, g, sp)) {
             R.x = min(R.x, sp.x);
             R.y = max(R.y, sp.y);
             R.z = min(R.z, sp.z);
             R.w = max(R.w, sp.w);
-            span_area += m * ((double)(sp.y - sp.x + 1) * (double)(sp.w - sp.z + 1));
+            span_area += (double)(sp.y - sp.x + 1) * (double)(sp.w - sp.z + 1);
+        }
+    };
+    auto get3 = [&](int k, double& x, double& y, double& r) {
+        if constexpr (kKeys) {  // the column-major matrix (strided: identity path and bases only)
+            const double* c = src.cands + (int64_t)k * src.ldc;
+            x = c[i];
+            y = c[N + i];
+            r = c[2 * N + i];
+        } else {
+            x = src.get(k, i, N);
+            y = src.get(k, N + i, N);
+            r = src.get(k, 2 * N + i, N);
         }
     };
 
+    bool hashed = false;
+    constexpr int P = kIdxPer + 1;
+    int slot[P];
+    double bx = 0.0, by = 0.0, br = 0.0;   // candidate 0's disk: the key base
+    if (fits && kKeys) {
+        // ---- keys: rows of the fp32 key matrix (coalesced) and the tiles' exactness flags
+        get3(0, bx, by, br);
+        const float* fx = src.keysT + row;
+        const float* fy = fx + (int64_t)N * K;
+        const float* fr = fy + (int64_t)N * K;
+        float qx[P], qy[P], qr[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int k = min(j < kIdxPer ? tid + j * kIdxThreads : (tid == 0 ? kIndexMaxK : K), K - 1);
+            qx[j] = fx[k];
+            qy[j] = fy[k];
+            qr[j] = fr[k];
+        }
+        bool bad = false;
+        for (int q = tid; q < 3 * src.nkt; q += kIdxThreads) {
+            const int a = q / src.nkt;
+            bad |= src.kbad[(int64_t)(a * N + i) * src.nkt + (q - a * src.nkt)] != 0;
+        }
+        for (int q = tid; q < kIndexSlots; q += kIdxThreads) table[q] = -1;
+        if (tid == 0) ucnt = 0;
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int k = j < kIdxPer ? tid + j * kIdxThreads : (tid == 0 ? kIndexMaxK : K);
+            if (k < K) {
+                kx[k] = qx[j];
+                ky[k] = qy[j];
+                kr[k] = qr[j];
+            }
+        }
+        hashed = !__syncthreads_or(bad);                  // (the barrier also publishes the keys)
+    } else if (fits) {
+        double cx[P], cy[P], cr[P];
+        // ---- keys: every load in flight at once, then the fp32 offsets (exactness voted)
+        get3(0, bx, by, br);
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int k = j < kIdxPer ? tid + j * kIdxThreads : (tid == 0 ? kIndexMaxK : K);
+            get3(min(k, K - 1), cx[j], cy[j], cr[j]);
+        }
+        for (int q = tid; q < kIndexSlots; q += kIdxThreads) table[q] = -1;
+        if (tid == 0) ucnt = 0;
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int k = j < kIdxPer ? tid + j * kIdxThreads : (tid == 0 ? kIndexMaxK : K);
+            if (k < K) {
+                kx[k] = key_of(cx[j], bx, ok);
+                ky[k] = key_of(cy[j], by, ok);
+                kr[k] = key_of(cr[j], br, ok);
+            }
+        }
+        hashed = !__syncthreads_or(!ok);                  // (the barrier also publishes the keys)
+    }
+    MAC_IDX_STAMP(1);
     if (!hashed) {  // identity: one position per candidate
         for (int k = tid; k < K; k += kIdxThreads) {
-            const double x = src.get(k, i, N), y = src.get(k, N + i, N), r = src.get(k, 2 * N + i, N);
-            add_span(x, y, r, 1.0);
+            double x, y, r;
+            get3(k, x, y, r);
+            add_span(x, y, r);
             o.urec[row + k] = make_disk(x, y, r);
             if (o.pen) o.pen[row + k] = pen_term(x, y, r, i, N, pa);
             o.umap[row + k] = k;
         }
         if (tid == 0) o.ucount[i] = K;
     } else {
-        // ---- keys to LDS (batched loads), table cleared
-        constexpr int kIdxB = 4;
-        const double* tx = src.candsT ? src.candsT + (int64_t)i * src.ldt : nullptr;
-        const double* ty = tx ? tx + (int64_t)N * src.ldt : nullptr;
-        const double* tr = tx ? ty + (int64_t)N * src.ldt : nullptr;
-        for (int k0 = tid; k0 < K; k0 += kIdxThreads * kIdxB) {
-            double bx_[kIdxB], by_[kIdxB], br_[kIdxB];
-            if (tx) {  // rows of the transposed matrix: coalesced, all loads in flight
-#pragma unroll
-                for (int b = 0; b < kIdxB; ++b) {
-                    const int kc = min(k0 + b * kIdxThreads, K - 1);
-                    bx_[b] = tx[kc];
-                    by_[b] = ty[kc];
-                    br_[b] = tr[kc];
-                }
-            } else {
-#pragma unroll
-                for (int b = 0; b < kIdxB; ++b) {
-                    const int kc = min(k0 + b * kIdxThreads, K - 1);
-                    bx_[b] = src.get(kc, i, N);
-                    by_[b] = src.get(kc, N + i, N);
-                    br_[b] = src.get(kc, 2 * N + i, N);
-                }
-            }
-#pragma unroll
-            for (int b = 0; b < kIdxB; ++b) {
-                const int k = k0 + b * kIdxThreads;
-                if (k < K) {
-                    kx[k] = bx_[b];
-                    ky[k] = by_[b];
-                    kr[k] = br_[b];
-                }
-            }
-        }
-        for (int q = tid; q < kIndexSlots; q += kIdxThreads) table[q] = -1;
-        for (int q = tid; q < K; q += kIdxThreads) mult[q] = 0;
-        if (tid == 0) ucnt = 0;
-        __syncthreads();
-        MAC_IDX_STAMP(1);
-        // ---- insert (exact keys; linear probing)
+        // ---- insert (exact fp32 keys; linear probing)
         constexpr uint32_t mask = kIndexSlots - 1;
-        for (int k = tid; k < K; k += kIdxThreads) {
-            const uint64_t bx = __builtin_bit_cast(uint64_t, kx[k]);
-            const uint64_t by = __builtin_bit_cast(uint64_t, ky[k]);
-            const uint64_t br = __builtin_bit_cast(uint64_t, kr[k]);
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int k = j < kIdxPer ? tid + j * kIdxThreads : (tid == 0 ? kIndexMaxK : K);
+            slot[j] = 0;
+            if (k >= K) continue;
+            const uint32_t bx = __builtin_bit_cast(uint32_t, kx[k]);
+            const uint32_t by = __builtin_bit_cast(uint32_t, ky[k]);
+            const uint32_t br = __builtin_bit_cast(uint32_t, kr[k]);
             uint32_t s = key_hash(bx, by, br) & mask;
             for (;;) {
                 int cur = table[s];
@@ -178,13 +232,13 @@ __global__ __launch_bounds__(kIdxThreads) void disk_index_kernel(CandSrc src, in
                     cur = atomicCAS(&table[s], -1, k);
                     if (cur < 0) break;                      // claimed an empty slot
                 }
-                if (__builtin_bit_cast(uint64_t, kx[cur]) == bx &&
-                    __builtin_bit_cast(uint64_t, ky[cur]) == by &&
-                    __builtin_bit_cast(uint64_t, kr[cur]) == br)
+                if (__builtin_bit_cast(uint32_t, kx[cur]) == bx &&
+                    __builtin_bit_cast(uint32_t, ky[cur]) == by &&
+                    __builtin_bit_cast(uint32_t, kr[cur]) == br)
                     break;                                   // same disk: share the slot
                 s = (s + 1) & mask;                          // another disk: probe on
             }
-            slot_of[k] = (uint16_t)s;
+            slot[j] = (int)s;
         }
         __syncthreads();
         MAC_IDX_STAMP(2);
@@ -198,28 +252,24 @@ __global__ __launch_bounds__(kIdxThreads) void disk_index_kernel(CandSrc src, in
             }
         }
         __syncthreads();
-        const int U = ucnt;
-        // ---- per distinct disk: record and penalty term
-        for (int u = tid; u < U; u += kIdxThreads) {
-            const int k = owner_of[u];
-            const double x = kx[k], y = ky[k], r = kr[k];
-            o.urec[row + u] = make_disk(x, y, r);
-            if (o.pen) s_pen[u] = pen_term(x, y, r, i, N, pa);
-        }
-        __syncthreads();
         MAC_IDX_STAMP(3);
-        // ---- per candidate: the map, the penalty term, and the multiplicities
-        for (int k = tid; k < K; k += kIdxThreads) {
-            const int u = table[slot_of[k]] & 0xfff;
+        // ---- per candidate: the map, the penalty term and the span (exact doubles rebuilt from
+        // the keys: base + offset)
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int k = j < kIdxPer ? tid + j * kIdxThreads : (tid == 0 ? kIndexMaxK : K);
+            if (k >= K) continue;
+            const int u = table[slot[j]] & 0xfff;
+            const double x = bx + (double)kx[k], y = by + (double)ky[k], r = br + (double)kr[k];
             o.umap[row + k] = u;
-            if (o.pen) o.pen[row + k] = s_pen[u];
-            atomicAdd(&mult[u], 1);
+            if (o.pen) o.pen[row + k] = pen_term(x, y, r, i, N, pa);
+            add_span(x, y, r);
         }
-        __syncthreads();
-        // ---- spans of the distinct disks, weighted by multiplicity (region and walk costs)
+        // ---- per distinct disk: its record, from the owner's exact key (base + offset)
+        const int U = ucnt;
         for (int u = tid; u < U; u += kIdxThreads) {
             const int k = owner_of[u];
-            add_span(kx[k], ky[k], kr[k], (double)mult[u]);
+            o.urec[row + u] = make_disk(bx + (double)kx[k], by + (double)ky[k], br + (double)kr[k]);
         }
         if (tid == 0) o.ucount[i] = U;
     }

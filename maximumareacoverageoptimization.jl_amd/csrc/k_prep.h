@@ -76,8 +76,9 @@ __host__ __device__ __forceinline__ double ltmads_entry(uint64_t state, int64_t 
 struct CandSrc {
     const double* cands;   // matrix source when non-null
     int ldc;
-    const double* candsT;  // the same matrix variable-major (candsT[v*K + k]) when non-null
-    int64_t ldt;           // K
+    const float* keysT;    // matrix: fp32 keys, variable-major (cands_keys_kernel), when non-null
+    const int* kbad;       // matrix: per (variable, 32-candidate tile) "a key is inexact" flags
+    int nkt;               // tiles per variable
     const double* xinc;    // generator: incumbent (3N), row / column permutations (n each)
     const int* rp;
     const int* cp;
@@ -85,7 +86,6 @@ struct CandSrc {
     int64_t b;             // 2^ell
     __device__ __forceinline__ double get(int k, int v, int N) const
     {
-        if (candsT) return candsT[(int64_t)v * ldt + k];
         if (cands) return cands[(int64_t)k * ldc + v];
         const int n = 3 * N;
         const int kk = k < n ? k : k - n;
@@ -94,24 +94,45 @@ struct CandSrc {
     }
 };
 
-// cands (3N x K column-major) -> candsT (3N x K row-major: variable-major, candidates
-// contiguous), through 32 x 32 LDS tiles so that both sides are coalesced.
-__global__ __launch_bounds__(kBlock) void cands_transpose_kernel(const double* __restrict__ cands,
-                                                                 int n, int K,
-                                                                 double* __restrict__ candsT)
+// cands (3N x K column-major) -> keysT (3N x K variable-major: candidates contiguous) of fp32
+// keys, key = fl32(x - x0) with x0 = the variable's value in candidate 0, through 32 x 32 LDS
+// tiles so that both sides are coalesced. A key is exact when x0 + (double)key reproduces x bit
+// for bit (k_index.h "Keys"); kbad[v*nkt + tile] = 1 when some key of variable v in this tile is
+// not (every tile writes its flag, so nothing needs clearing). Half the bytes of a transposed
+// fp64 copy are written here and read by the index.
+__global__ __launch_bounds__(kBlock) void cands_keys_kernel(const double* __restrict__ cands, int n,
+                                                            int K, float* __restrict__ keysT,
+                                                            int* __restrict__ kbad, int nkt)
 {
-    __shared__ double t[32][33];
+    __shared__ float t[32][33];
+    __shared__ int sbad[32];
     const int v0 = blockIdx.x * 32, k0 = blockIdx.y * 32;
     const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
-    for (int kk = ty; kk < 32; kk += 8) {
-        const int k = k0 + kk, v = v0 + tx;
-        if (k < K && v < n) t[kk][tx] = cands[(int64_t)k * n + v];
+    if (threadIdx.x < 32) sbad[threadIdx.x] = 0;
+    const int vr = v0 + tx;
+    const double base = vr < n ? cands[vr] : 0.0;
+    bool ok = true;
+    double x[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int k = k0 + ty + 8 * j;
+        x[j] = (k < K && vr < n) ? cands[(int64_t)k * n + vr] : base;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float f = (float)(x[j] - base);
+        ok &= __builtin_bit_cast(uint64_t, base + (double)f) == __builtin_bit_cast(uint64_t, x[j]);
+        t[ty + 8 * j][tx] = f;
     }
     __syncthreads();
-    for (int vv = ty; vv < 32; vv += 8) {
-        const int v = v0 + vv, k = k0 + tx;
-        if (k < K && v < n) candsT[(int64_t)v * K + k] = t[tx][vv];
+    if (!ok) atomicOr(&sbad[tx], 1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int v = v0 + ty + 8 * j, k = k0 + tx;
+        if (k < K && v < n) keysT[(int64_t)v * K + k] = t[tx][ty + 8 * j];
     }
+    __syncthreads();
+    if (threadIdx.x < 32 && vr < n) kbad[(int64_t)vr * nkt + blockIdx.y] = sbad[threadIdx.x];
 }
 
 // cands: see CandSrc. Writes disks[k*N + i] (scan walk) and, when pen != null,

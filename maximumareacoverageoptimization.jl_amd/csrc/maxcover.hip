@@ -120,7 +120,7 @@ struct Lane {
     hipStream_t last = nullptr;   // stream of the most recent use
     hipEvent_t done = nullptr;
     DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode, pen, nbr,
-        ncount, dlist, spart, vp, xinc, perm, ucount, umap, candsT;
+        ncount, dlist, spart, vp, xinc, perm, ucount, umap, keysT, kbad;
     std::vector<double> h_dlim;
     PinnedBuf h_stage;                         // native MADS driver: best, permutations, incumbent
 };
@@ -458,16 +458,24 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         const IndexOut io{L->disks.as<DiskRec>(), d_pen, L->umap.as<int>(), L->ucount.as<int>(),
                           L->region.as<int4>(), L->cost.as<double2>(), L->mode.as<int>() + 1};
         CandSrc isrc = src;
-        if (src.cands) {  // matrix: variable-major copy first, so each disk's K values are a row
-            L->candsT.reserve(sizeof(double) * (size_t)3 * N * K);
-            hipLaunchKernelGGL(cands_transpose_kernel, dim3((3 * N + 31) / 32, (K + 31) / 32),
-                               dim3(kBlock), 0, s, src.cands, 3 * N, K, L->candsT.as<double>());
+        if (src.cands && K <= kIndexMaxK + 1) {  // matrix: fp32 keys, variable-major, so each
+                                                 // disk's K keys are a row
+            const int nkt = (K + 31) / 32;
+            L->keysT.reserve(sizeof(float) * (size_t)3 * N * K);
+            L->kbad.reserve(sizeof(int) * (size_t)3 * N * nkt);
+            hipLaunchKernelGGL(cands_keys_kernel, dim3((3 * N + 31) / 32, nkt), dim3(kBlock), 0, s,
+                               src.cands, 3 * N, K, L->keysT.as<float>(), L->kbad.as<int>(), nkt);
             HCK(hipGetLastError());
-            isrc.candsT = L->candsT.as<double>();
-            isrc.ldt = K;
+            isrc.keysT = L->keysT.as<float>();
+            isrc.kbad = L->kbad.as<int>();
+            isrc.nkt = nkt;
         }
-        hipLaunchKernelGGL(disk_index_kernel, dim3(8 * ((N + 7) / 8)), dim3(kIdxThreads), 0, s, isrc, N,
-                           K, ctx->grid, pa, 1, io);
+        if (isrc.cands)
+            hipLaunchKernelGGL(disk_index_kernel<true>, dim3(8 * ((N + 7) / 8)), dim3(kIdxThreads), 0, s,
+                               isrc, N, K, ctx->grid, pa, 1, io);
+        else
+            hipLaunchKernelGGL(disk_index_kernel<false>, dim3(8 * ((N + 7) / 8)), dim3(kIdxThreads), 0, s,
+                               isrc, N, K, ctx->grid, pa, 1, io);
         HCK(hipGetLastError());
         const DiskRec* d_urec = L->disks.as<DiskRec>();
         const int* d_map = L->umap.as<int>();
@@ -494,7 +502,9 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         if (run_tiled) {
             const size_t lds = tiled_lds_bytes(N);
             const int64_t units = (int64_t)K * G;
-            const int64_t cap = poll_possible ? 4 * (int64_t)ctx->cus : units;
+            // when the device may pick the poll walk, this launch usually just exits: one
+            // workgroup per CU keeps that cheap (a chosen tiled walk grid-strides over its units)
+            const int64_t cap = poll_possible ? (int64_t)ctx->cus : units;
             const unsigned nwg = (unsigned)std::min(units, cap);
             uint64_t* ts = take_ts(nwg, ts_a, ts_na);
             hipLaunchKernelGGL(coverage_tiled_kernel, dim3(nwg), dim3(kBlock),
@@ -752,7 +762,7 @@ void mac_ctx_destroy(mac_ctx* ctx)
         for (DevBuf* b : {&l->cands, &l->disks, &l->partial, &l->area, &l->obj, &l->best,
                           &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->pen, &l->nbr,
                           &l->ncount, &l->dlist, &l->spart, &l->vp, &l->xinc,
-                          &l->perm, &l->ucount, &l->umap, &l->candsT})
+                          &l->perm, &l->ucount, &l->umap, &l->keysT, &l->kbad})
             b->release();
         if (l->done) (void)hipEventDestroy(l->done);
         if (l->stream) (void)hipStreamDestroy(l->stream);
