@@ -13,7 +13,6 @@ namespace mac {
 
 constexpr int kFinC = 16;   // candidates per finalize block (x 64 slice groups)
 constexpr int kFinThreads = 1024;
-constexpr int kMaxMaskWords = (65535 + 31) / 32;   // N <= 65535 (mac_* argument check)
 
 // Sequential objective penalty (src/TDM_STATIC_opt.jl:88-92): violation_k = sum over i = 0..N-1
 // of pen[i*K + k] (the index's per-candidate term, k_index.h), accumulated IN ORDER from 0.0
@@ -77,12 +76,15 @@ __global__ __launch_bounds__(kBlock) void penalty_chain_kernel(const double* __r
     penalty_chain_block(pen, K, N, blockIdx.x * kChainC, penalty, vp);
 }
 
-// Block = 16 candidates x 64 slice groups. area_k = sum over slices g of partial[g*K + k] in a
+// Block = 16 candidates x 64 slice groups. area_k = sum over slices g of the slice's credit in a
 // fixed order (thread (c, sg) sums g = sg, sg+64, ... in batches of 8, then the 64 groups in
-// order): bit-reproducible, loads kept in flight. The slice
-// count is n_poll when *mode == poll, else n_other. With spart != null and the poll walk chosen,
-// the shared-entry rows spart[i*K + k] of the disks with ncount[i] > 0 are added too (ascending
-// i within each slice group: fixed order). obj_k = -area_k + vp_k when obj_out != null.
+// order): bit-reproducible. The slice count is n_poll when *mode == poll, else n_other.
+// Poll walk (mode == poll, map and spart given): slice g is disk g; its credit for candidate k is
+// partial[g*K + map[g*K + k]] (the distinct-disk position, k_index.h) plus, when disk g has
+// lower-index neighbours (ncount[g] > 0), its shared-entry row spart[g*K + k] (rows of other
+// disks are never written and never read). Per batch the map and ncount loads go first, then the
+// gathers and shared rows they select: two memory round trips per batch.
+// obj_k = -area_k + vp_k when obj_out != null.
 __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
     const double* __restrict__ partial, const int* __restrict__ mode, int n_poll, int n_other,
     int K, int N, const int* __restrict__ map, const double* __restrict__ spart,
@@ -90,62 +92,38 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
     const double* __restrict__ vp, double* __restrict__ area_out, double* __restrict__ obj_out)
 {
     __shared__ double red[kFinThreads / kFinC][kFinC];
-    __shared__ uint32_t smask[kMaxMaskWords];   // disks whose shared-entry row exists
     const int t = threadIdx.x, c = t % kFinC, sg = t / kFinC;
     constexpr int SG = kFinThreads / kFinC;
     const int k0 = blockIdx.x * kFinC;
     const int k = k0 + c;
-    const int G = (mode && *mode == kModePoll) ? n_poll : n_other;
-    const bool rows = spart && mode && *mode == kModePoll;
-    if (rows) {
-        const int nw = (N + 31) / 32;
-        for (int q = t; q < nw; q += kFinThreads) smask[q] = 0u;
-        __syncthreads();
-        for (int i = t; i < N; i += kFinThreads)
-            if (ncount[i] > 0) atomicOr(&smask[i >> 5], 1u << (i & 31));
-        __syncthreads();
-    }
-    // Rows in batches of kFinB per thread, every load of a batch issued before any is used (the
-    // map loads, then the gathers they index): latency paid once per batch, not per row. Each
-    // batch is added in order to one accumulator: fixed order.
+    const bool poll = mode && *mode == kModePoll;
+    const int G = poll ? n_poll : n_other;
+    const bool rows = spart && poll;
+    const int* mp = (map && poll) ? map : nullptr;
     constexpr int kFinB = 8;
     double acc = 0.0;
-    // poll walk with distinct-disk positions: row g's credit for candidate k sits at map[g*K+k]
-    const int* mp = (map && rows) ? map : nullptr;
     if (k < K) {
         for (int g = sg; g < G; g += kFinB * SG) {
             int pos[kFinB];
+            bool sh[kFinB];
 #pragma unroll
             for (int b = 0; b < kFinB; ++b) {
                 const int gb = g + b * SG;
                 pos[b] = gb < G ? (mp ? mp[(int64_t)gb * K + k] : k) : -1;
+                sh[b] = rows && gb < G && ncount[gb] > 0;
             }
-            double v[kFinB];
+            double v[kFinB], sv[kFinB];
 #pragma unroll
-            for (int b = 0; b < kFinB; ++b)
-                v[b] = pos[b] >= 0 ? partial[(int64_t)(g + b * SG) * K + pos[b]] : 0.0;
+            for (int b = 0; b < kFinB; ++b) {
+                const int64_t rb = (int64_t)(g + b * SG) * K;
+                v[b] = pos[b] >= 0 ? partial[rb + pos[b]] : 0.0;
+                sv[b] = sh[b] ? spart[rb + k] : 0.0;
+            }
             double bs = 0.0;
 #pragma unroll
-            for (int b = 0; b < kFinB; ++b) bs += v[b];
+            for (int b = 0; b < kFinB; ++b) bs += v[b] + sv[b];
             acc += bs;
         }
-        // poll walk: the shared-entry rows of the disks that have lower-index neighbours (other
-        // disks' rows are never written and never read; a batch's idle slots add +0.0, which
-        // leaves every sum unchanged)
-        if (rows)
-            for (int i = sg; i < N; i += kFinB * SG) {
-                double v[kFinB];
-#pragma unroll
-                for (int b = 0; b < kFinB; ++b) {
-                    const int ib = i + b * SG;
-                    v[b] = (ib < N && (smask[ib >> 5] & (1u << (ib & 31))))
-                               ? spart[(int64_t)ib * K + k] : 0.0;
-                }
-                double bs = 0.0;
-#pragma unroll
-                for (int b = 0; b < kFinB; ++b) bs += v[b];
-                acc += bs;
-            }
     }
     red[sg][c] = acc;
 
@@ -163,31 +141,52 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
 // best[0] = objective, best[1] = index (int64 bits), index = idx_base + k, -1 if none. With a
 // mirror (mapped pinned host memory), the two words are also written there followed by seq in
 // mirror[2], so the host reads the result without a copy (mac_best_fetch).
-__global__ __launch_bounds__(kBlock) void argmin_kernel(const double* __restrict__ obj, int K,
-                                                        int64_t idx_base, double* __restrict__ best,
-                                                        double* __restrict__ mirror, uint64_t seq)
+// 16 waves; each thread keeps its first minimum over k = t, t + 1024, ... (4 loads in flight),
+// then wave butterflies and one pass over the 16 wave results.
+constexpr int kArgThreads = 1024;
+
+__device__ __forceinline__ void argmin_take(double& v1, int& i1, double v2, int i2)
 {
-    __shared__ double sv[kBlock];
-    __shared__ int si[kBlock];
+    if ((i2 >= 0) && (i1 < 0 || v2 < v1 || (v2 == v1 && i2 < i1))) {
+        v1 = v2;
+        i1 = i2;
+    }
+}
+
+__global__ __launch_bounds__(kArgThreads) void argmin_kernel(const double* __restrict__ obj, int K,
+                                                             int64_t idx_base, double* __restrict__ best,
+                                                             double* __restrict__ mirror, uint64_t seq)
+{
+    __shared__ double sv[kArgThreads / kWave];
+    __shared__ int si[kArgThreads / kWave];
     double bv = __builtin_inf();
     int bi = -1;
-    for (int k = threadIdx.x; k < K; k += kBlock) {
-        const double v = obj[k];
-        if (v < bv) { bv = v; bi = k; }  // ascending k per thread: first minimum kept
-    }
-    sv[threadIdx.x] = bv;
-    si[threadIdx.x] = bi;
-    __syncthreads();
-    for (int s = kBlock / 2; s > 0; s >>= 1) {
-        if (threadIdx.x < s) {
-            const double v2 = sv[threadIdx.x + s];
-            const int i2 = si[threadIdx.x + s];
-            const double v1 = sv[threadIdx.x];
-            const int i1 = si[threadIdx.x];
-            const bool take = (i2 >= 0) && (i1 < 0 || v2 < v1 || (v2 == v1 && i2 < i1));
-            if (take) { sv[threadIdx.x] = v2; si[threadIdx.x] = i2; }
+    constexpr int B = 4;
+    for (int k0 = threadIdx.x; k0 < K; k0 += B * kArgThreads) {
+        double v[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const int k = k0 + b * kArgThreads;
+            v[b] = k < K ? obj[k] : __builtin_inf();
         }
-        __syncthreads();
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+            if (v[b] < bv) {  // ascending k per thread: first minimum kept
+                bv = v[b];
+                bi = k0 + b * kArgThreads;
+            }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+        argmin_take(bv, bi, __shfl_xor(bv, off, kWave), __shfl_xor(bi, off, kWave));
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    if (lane == 0) {
+        sv[wid] = bv;
+        si[wid] = bi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int q = 1; q < kArgThreads / kWave; ++q) argmin_take(sv[0], si[0], sv[q], si[q]);
     }
     if (threadIdx.x == 0) {
         const int i = si[0];

@@ -68,8 +68,11 @@ __device__ __forceinline__ void diag_stamp(uint64_t t0, uint64_t role, uint64_t 
     g_diag[4 * b + 3] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
 }
 #define MAC_DIAG_STAMP(t0, role, info) diag_stamp(t0, role, info)
+__device__ uint64_t g_diag_walk[8 * 65536];   // walk role, grid row 0: per-disk phase stamps
+#define MAC_WALK_STAMP(q) if (threadIdx.x == 0 && blockIdx.y == 0 && i < 65536) g_diag_walk[8 * i + (q)] = __builtin_amdgcn_s_memrealtime()
 #else
 #define MAC_DIAG_STAMP(t0, role, info)
+#define MAC_WALK_STAMP(q)
 #endif
 
 __device__ __forceinline__ float next_down_f32(float f)
@@ -214,6 +217,7 @@ __device__ __forceinline__ void coverage_poll_body(
     const int U = ucount[i];
     const int kb = blockIdx.y * kPollKPB;
     if (kb >= U) return;  // uniform: this slice has no position
+    MAC_WALK_STAMP(0);
     const int ke = min(U, kb + kPollKPB);
     const int4 R = region[i];
     const int nc = ncount[i];
@@ -265,6 +269,7 @@ __device__ __forceinline__ void coverage_poll_body(
     const f32x2 sa23 = {pl[2].sa, pl[3].sa}, sb23 = {pl[2].sb, pl[3].sb};
     const f32x2 st23 = {pl[2].stm, pl[3].stm}, ns23 = {pl[2].ns, pl[3].ns};
 
+    MAC_WALK_STAMP(1);
     for (int rb = R.z; rb <= R.w; rb += kPollRB) {
         const int nr = min(kPollRB, R.w - rb + 1);
         if (tid < nr) {
@@ -282,6 +287,7 @@ __device__ __forceinline__ void coverage_poll_body(
         const int total = rpre[nr];
 #ifdef MAC_DIAG
         diag_entries += total;
+        if (rb == R.z) MAC_WALK_STAMP(2);
 #endif
         for (int base = 0; base < total; base += kPollCH) {
             const int n = min(kPollCH, total - base);
@@ -315,6 +321,9 @@ __device__ __forceinline__ void coverage_poll_body(
             const uint64_t w0 = __builtin_bit_cast(uint64_t, sw[0]);
             mixed |= (tid < n) && __builtin_bit_cast(uint64_t, sw[tid]) != w0;
             const bool uniform = !__syncthreads_or(mixed);
+#ifdef MAC_DIAG
+            if (rb == R.z && base == 0) MAC_WALK_STAMP(3);
+#endif
 
             if (pair0 || pair1) {
                 float bmin[kPollKPL];
@@ -401,12 +410,16 @@ __device__ __forceinline__ void coverage_poll_body(
                     if (live[u]) acc[u] += cw[u];
                 }
             }
+#ifdef MAC_DIAG
+            if (rb == R.z && base == 0) MAC_WALK_STAMP(4);
+#endif
             __syncthreads();
         }
     }
 #pragma unroll
     for (int u = 0; u < kPollKPL; ++u)
         if (kk[u] >= 0) partial[row + kk[u]] = acc[u];
+    MAC_WALK_STAMP(5);
     MAC_DIAG_STAMP(diag_t0, 3, ((uint64_t)nc << 40) | ((uint64_t)(ke - kb) << 20) | (uint64_t)diag_entries);
 }
 

@@ -550,7 +550,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                        d_vp, d_area, d_obj);
     HCK(hipGetLastError());
     if (d_best) {
-        hipLaunchKernelGGL(argmin_kernel, dim3(1), dim3(kBlock), 0, s, d_obj, K, idx_base, d_best,
+        hipLaunchKernelGGL(argmin_kernel, dim3(1), dim3(kArgThreads), 0, s, d_obj, K, idx_base, d_best,
                            d_mirror, mirror_seq);
         HCK(hipGetLastError());
     }
@@ -644,6 +644,15 @@ int32_t mac_diag_index_read(uint64_t* out, int64_t n)
 {
     if (n > (int64_t)(8 * 65536)) n = 8 * 65536;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_index), sizeof(uint64_t) * n, 0,
+                            hipMemcpyDeviceToHost) != hipSuccess)
+        return MAC_E_HIP;
+    return MAC_OK;
+}
+
+int32_t mac_diag_walk_read(uint64_t* out, int64_t n)
+{
+    if (n > (int64_t)(8 * 65536)) n = 8 * 65536;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_walk), sizeof(uint64_t) * n, 0,
                             hipMemcpyDeviceToHost) != hipSuccess)
         return MAC_E_HIP;
     return MAC_OK;

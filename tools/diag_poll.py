@@ -96,6 +96,19 @@ def main():
         for _ in range(3):
             ctx.poll_best(C, rmax)
         out = analyze(L, C.shape[1] // 3, C.shape[0])
+        N = C.shape[1] // 3
+        L.mac_diag_walk_read.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int64]
+        buf = (ctypes.c_uint64 * (8 * N))()
+        assert L.mac_diag_walk_read(buf, 8 * N) == 0
+        a = np.frombuffer(buf, dtype=np.uint64).reshape(N, 8).astype(np.int64)[:, :6]
+        a = a[(a > 0).all(axis=1)]
+        ph = np.diff(a, axis=1) / 100.0
+        out["walk_phases"] = {
+            "names": ["prologue (urec, lanes)", "off + prefix", "staging", "tests", "rest + write"],
+            "median_us": [float(v) for v in np.median(ph, axis=0)],
+            "max_us": [float(v) for v in ph.max(axis=0)],
+            "start_us_pct": [float(v) for v in np.percentile((a[:, 0] - a[:, 0].min()) / 100.0,
+                                                            (0, 50, 100))]}
     print(json.dumps(out, indent=1))
 
 
