@@ -17,11 +17,12 @@ constexpr int kNbrCap = 6;         // tiled walk: lower-index overlapping disks 
 constexpr int kPollCH = 512;       // poll walk: entries staged in LDS per chunk
 constexpr int kPollRB = 64;        // poll walk: region rows per batch
 constexpr int kPollNbr = 64;       // poll walk: lower-index overlapping regions kept
-constexpr int kPollKPL = 4;        // poll walk: candidates per lane
+constexpr int kPollSlots = 8;      // poll walk: candidate positions per lane (every wave)
+constexpr int kPollPairs = kPollSlots / 2;
 constexpr int kPollThreads = 256;  // poll walk: workgroup size (4 waves share one staging)
 constexpr int kPollWaves = kPollThreads / kWave;
-constexpr int kPollKPB = kPollThreads * kPollKPL;  // poll walk: candidates per workgroup
-constexpr int kSharedWG = 1024;    // poll walk: shared-entry workgroups (grid-stride over jobs)
+constexpr int kPollKPB = kWave * kPollSlots;  // poll walk: positions per slice
+constexpr int kSharedWG = 256;     // poll walk: shared-entry workgroups (grid-stride over jobs)
 
 constexpr int kModePoll = 1;
 constexpr int kModeTiled = 2;

@@ -160,16 +160,50 @@ __device__ __forceinline__ float poll_dprime(const float4& e, const PollLane& L)
     return __builtin_fmaf(e.x, L.ns, __builtin_fmaf(e.z, L.sb, __builtin_fmaf(e.y, L.sa, L.stm)));
 }
 
-// Grid (n_chain + n_shared + N, slices); roles by x, in dispatch order (the first ones overlap
-// the walk): x < n_chain: objective-penalty chains of candidates [16c, 16c + 16),
-// c = y * n_chain + x, into vp (k_final.h), whatever the walk; then, when *mode == kModePoll (or mode == null),
-// n_shared x slices workgroups deciding the shared entries into spart, grid-striding over the
-// jobs (disk with neighbours x kShC-candidate slice, k_poll_shared.h), and one
-// workgroup per (disk i,
-// slice g): positions [g*kPollKPB, min(U_i, (g+1)*kPollKPB)) of disk i's distinct disks
-// (urec / ucount, k_index.h), thread t pass u ->
-// p = kb + 256u + t; partial[i*K + p] = weight of the non-shared entries credited to that disk
-// (finalize gathers it for every candidate through the map).
+// Hot loop of the poll walk over this wave's groups of 4 staged entries (q4 = w, w + 4, ...):
+// NP candidate pairs per entry pair, per 2 entries x 2 candidates six packed fmas, two packed
+// clamps (count), two packed adds and two v_min3 (band detector). h[j]: covered counts of pair j.
+template <int NP>
+__device__ __forceinline__ void poll_hot(const float4* __restrict__ s32, int ng, int w,
+                                         const f32x2 (&sa)[kPollPairs], const f32x2 (&sb)[kPollPairs],
+                                         const f32x2 (&st)[kPollPairs], const f32x2 (&ns)[kPollPairs],
+                                         f32x2 (&h)[kPollPairs], float (&bmin)[kPollSlots])
+{
+    const f32x2 zero2 = {0.0f, 0.0f};
+#pragma unroll
+    for (int j = 0; j < kPollPairs; ++j) h[j] = zero2;
+#define MAC_POLL_PAIR(E0, E1, J)                                                                \
+    {                                                                                         \
+        const f32x2 d0 = fma2(E0.x, ns[J], fma2(E0.z, sb[J], fma2(E0.y, sa[J], st[J])));       \
+        const f32x2 d1 = fma2(E1.x, ns[J], fma2(E1.z, sb[J], fma2(E1.y, sa[J], st[J])));       \
+        h[J] += clamp01x2(d0, zero2);                                                         \
+        h[J] += clamp01x2(d1, zero2);                                                         \
+        bmin[2 * J] = __builtin_fminf(__builtin_fminf(bmin[2 * J], __builtin_fabsf(d0.x)),     \
+                                      __builtin_fabsf(d1.x));                                  \
+        bmin[2 * J + 1] = __builtin_fminf(__builtin_fminf(bmin[2 * J + 1], __builtin_fabsf(d0.y)), \
+                                          __builtin_fabsf(d1.y));                              \
+    }
+    for (int q4 = w; q4 < ng; q4 += kPollWaves) {
+        const float4 e0 = s32[4 * q4], e1 = s32[4 * q4 + 1], e2 = s32[4 * q4 + 2], e3 = s32[4 * q4 + 3];
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            MAC_POLL_PAIR(e0, e1, j)
+            MAC_POLL_PAIR(e2, e3, j)
+        }
+    }
+#undef MAC_POLL_PAIR
+}
+
+// Grid (N + n_shared + n_chain); roles by x, in dispatch order (the longest first): x < N, when
+// *mode == kModePoll (or mode == null): one workgroup per disk i, over slices of kPollKPB
+// positions of disk i's distinct disks (urec / ucount, k_index.h): partial[i*K + p] = weight of
+// the non-shared entries credited to position p (finalize gathers it for every candidate through
+// the map). Within a slice every wave holds all positions (8 per lane) and the waves split the
+// staged entries: per entry group the LDS reads feed up to 4 candidate pairs, so the loop is
+// VALU-dense even when a disk has only a few hundred positions. Then n_shared workgroups
+// deciding the shared entries into spart, grid-striding over the jobs (disk with neighbours x
+// kShC-candidate slice, k_poll_shared.h); last, whatever the walk, the objective-penalty chains
+// of candidates [16c, 16c + 16), c = x - N - n_shared, into vp (k_final.h).
 __device__ __forceinline__ void coverage_poll_body(
     const double2* __restrict__ xy, const double* __restrict__ w,
     const int32_t* __restrict__ off, Grid g, const DiskRec* __restrict__ urec,
@@ -180,61 +214,54 @@ __device__ __forceinline__ void coverage_poll_body(
     double* __restrict__ spart, int n_chain, const double* __restrict__ pen, double penalty,
     double* __restrict__ vp, int n_shared)
 {
-    static_assert(kPollKPL == 4, "the hot loop pairs candidates (0,1) and (2,3)");
+    static_assert(kPollSlots == 2 * kPollPairs, "the hot loop pairs candidate slots");
 #ifdef MAC_DIAG
     const uint64_t diag_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    if ((int)blockIdx.x < n_chain) {  // first: the objective-penalty chains (any walk)
+    const int bx = blockIdx.x;
+    if (bx >= N + n_shared) {  // last: the objective-penalty chains (whatever the walk)
         static_assert(kPollThreads == kBlock, "penalty_chain_block needs kBlock threads");
-        const int k0 = (blockIdx.y * n_chain + blockIdx.x) * kChainC;
+        const int k0 = (bx - N - n_shared) * kChainC;
         if (k0 < K) penalty_chain_block(pen, K, N, k0, penalty, vp);
         MAC_DIAG_STAMP(diag_t0, 1, 0);
         return;
     }
-    const int bx = blockIdx.x - n_chain;
     if (mode && *mode != kModePoll) return;
-    if (bx < n_shared) {  // then: the shared entries (k_poll_shared.h), over every row
+    if (bx >= N) {  // then: the shared entries (k_poll_shared.h)
         const int nd = *dcount;
         const int nsub = (K + kShC - 1) / kShC;
-        for (int job = blockIdx.y * n_shared + bx; job < nd * nsub; job += n_shared * gridDim.y)
-                poll_shared_job(xy, w, off, g, urec, umap, region, nbrT, ncount,
-                                dlist[job / nsub], K, (job % nsub) * kShC, spart);
+        for (int job = bx - N; job < nd * nsub; job += n_shared)
+            poll_shared_job(xy, w, off, g, urec, umap, region, nbrT, ncount, dlist[job / nsub], K,
+                            (job % nsub) * kShC, spart);
         MAC_DIAG_STAMP(diag_t0, 2, (uint64_t)nd);
         return;
     }
 #ifdef MAC_DIAG
     int diag_entries = 0;
 #endif
-    __shared__ float4 s32[kPollCH + 4];  // (Q, U, V, 0); (+inf, 0, 0) for shared / non-finite / pad
-    __shared__ double2 s64[kPollCH];   // exact coordinates (band decisions)
+    // s32: (Q, U, V, 0) per staged entry, (+inf, 0, 0) for shared / non-finite / pad; s64: exact
+    // coordinates (band decisions); red: per-wave credit of each position, used only between
+    // slices, over the staging area
+    constexpr int kStageBytes = (kPollCH + 4) * (int)sizeof(float4) + kPollCH * (int)sizeof(double2);
+    constexpr int kRedBytes = kPollWaves * kPollKPB * (int)sizeof(double);
+    static_assert(kRedBytes <= kStageBytes, "red aliases the staging arrays");
+    __shared__ __attribute__((aligned(16))) unsigned char stage[kStageBytes];
+    float4* const s32 = (float4*)stage;
+    double2* const s64 = (double2*)(stage + (kPollCH + 4) * sizeof(float4));
+    double (*const red)[kPollKPB] = (double (*)[kPollKPB])stage;
     __shared__ double sw[kPollCH];
     __shared__ int rs[kPollRB], rpre[kPollRB + 1];
     __shared__ int4 nbox[kPollNbr];
 
-    const int i = bx - n_shared;
-    const int tid = threadIdx.x;
-    // positions p = distinct disks of disk i (k_dedup.h; all K candidates without dedup)
+    const int i = bx;
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+    // positions p = distinct disks of disk i (k_index.h; all K candidates without dedup)
     const int U = ucount[i];
-    const int kb = blockIdx.y * kPollKPB;
-    if (kb >= U) return;  // uniform: this slice has no position
-    MAC_WALK_STAMP(0);
-    const int ke = min(U, kb + kPollKPB);
     const int4 R = region[i];
     const int nc = ncount[i];
     const int64_t row = (int64_t)i * K;
-
-    // lane-major positions p = kb + 256u + t: a disk's few hundred distinct disks spread over
-    // all four waves first (latency hiding beats packing them into fewer waves)
-    int kk[kPollKPL];
-#pragma unroll
-    for (int u = 0; u < kPollKPL; ++u) {
-        const int p = kb + u * kPollThreads + tid;
-        kk[u] = p < ke ? p : -1;
-    }
     if (R.x > R.y) {  // disk i covers nothing in any candidate (uniform across the block)
-#pragma unroll
-        for (int u = 0; u < kPollKPL; ++u)
-            if (kk[u] >= 0) partial[row + kk[u]] = 0.0;
+        for (int p = tid; p < U; p += kPollThreads) partial[row + p] = 0.0;
         return;
     }
     if (tid < min(nc, kPollNbr)) nbox[tid] = region[nbrT[i * kPollNbr + tid]];
@@ -245,155 +272,124 @@ __device__ __forceinline__ void coverage_poll_body(
     const double oy = g.gy0 + 0.5 * (double)(R.z + R.w + 1) * g.S;
     const double Umax = 0.5 * (double)max(R.y - R.x + 1, R.w - R.z + 1) * g.S + 2.0 * g.S;
 
-    PollLane pl[kPollKPL];
-    bool live[kPollKPL];
-    double acc[kPollKPL];
+    // slices of kPollKPB positions (one for any MADS poll: a few hundred distinct disks)
+    for (int kb = 0; kb < U; kb += kPollKPB) {
+        const int ke = min(U, kb + kPollKPB);
+        MAC_WALK_STAMP(0);
+        // every wave holds every position of the slice: p = kb + 64 s + lane (slot s); the waves
+        // split the staged entries instead (groups of 4, wave w takes groups w, w + 4, ...)
+        // per slot: the lane constants as pair vectors (slots 2j, 2j+1), X', liveness bits
+        f32x2 sa[kPollPairs], sb[kPollPairs], st[kPollPairs], ns[kPollPairs];
+        float xp[kPollSlots];
+        uint32_t live = 0;
+        double acc[kPollSlots];
 #pragma unroll
-    for (int u = 0; u < kPollKPL; ++u) {
-        acc[u] = 0.0;
-        live[u] = false;
-        pl[u] = PollLane{0.0f, 0.0f, -1.0f, -1.0f, 0.5f};  // d' < -X' for every entry: inert
-        if (kk[u] < 0) continue;
-        const DiskRec d = urec[row + kk[u]];
-        int4 sp;
-        if (!disk_span(d, g, sp)) continue;
-        live[u] = true;
-        pl[u] = poll_lane(d, ox, oy, Umax);
-    }
-    // wave-uniform: which candidate pairs have any live lane in this wave
-    const bool pair0 = __any(live[0] || live[1]);
-    const bool pair1 = __any(live[2] || live[3]);
-    const f32x2 zero2 = {0.0f, 0.0f};
-    const f32x2 sa01 = {pl[0].sa, pl[1].sa}, sb01 = {pl[0].sb, pl[1].sb};
-    const f32x2 st01 = {pl[0].stm, pl[1].stm}, ns01 = {pl[0].ns, pl[1].ns};
-    const f32x2 sa23 = {pl[2].sa, pl[3].sa}, sb23 = {pl[2].sb, pl[3].sb};
-    const f32x2 st23 = {pl[2].stm, pl[3].stm}, ns23 = {pl[2].ns, pl[3].ns};
-
-    MAC_WALK_STAMP(1);
-    for (int rb = R.z; rb <= R.w; rb += kPollRB) {
-        const int nr = min(kPollRB, R.w - rb + 1);
-        if (tid < nr) {
-            const int64_t rowbase = (int64_t)(rb + tid) * g.nTx;
-            const int s = off[rowbase + R.x];
-            rs[tid] = s;
-            rpre[tid + 1] = off[rowbase + R.y + 1] - s;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            rpre[0] = 0;
-            for (int r = 0; r < nr; ++r) rpre[r + 1] += rpre[r];
-        }
-        __syncthreads();
-        const int total = rpre[nr];
-#ifdef MAC_DIAG
-        diag_entries += total;
-        if (rb == R.z) MAC_WALK_STAMP(2);
-#endif
-        for (int base = 0; base < total; base += kPollCH) {
-            const int n = min(kPollCH, total - base);
-            bool mixed = false;
-            double wfirst = 0.0;
-            for (int q = tid; q < n; q += kPollThreads) {
-                const int f = base + q;
-                int lo = 0, hi = nr - 1;
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (rpre[mid] <= f) lo = mid; else hi = mid - 1;
+        for (int j = 0; j < kPollPairs; ++j) {
+            PollLane q2[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int u = 2 * j + h;
+                const int p = kb + u * kWave + lane;
+                acc[u] = 0.0;
+                q2[h] = PollLane{0.0f, 0.0f, -1.0f, -1.0f, 0.5f};  // d' < -X' for every entry: inert
+                if (p < ke) {
+                    const DiskRec d = urec[row + p];
+                    int4 sp;
+                    if (disk_span(d, g, sp)) {
+                        live |= 1u << u;
+                        q2[h] = poll_lane(d, ox, oy, Umax);
+                    }
                 }
-                const int j = rs[lo] + (f - rpre[lo]);
-                const double2 p = xy[j];
-                const double wj = w[j];
-                s64[q] = p;
-                sw[q] = wj;
-                const bool shared =
-                    nc > 0 && entry_shared(nc, nbox, tile_of(p.x, g.gx0, g.invS, g.nTx), rb + lo);
-                const float fu = (float)(p.x - ox), fv = (float)(p.y - oy);
-                s32[q] = !shared && __builtin_isfinite(fu) && __builtin_isfinite(fv)
-                             ? make_float4(__builtin_fmaf(fu, fu, fv * fv), fu, fv, 0.0f)
-                             : make_float4(__builtin_inff(), 0.0f, 0.0f, 0.0f);
-                if (q == tid) wfirst = wj;
-                mixed |= __builtin_bit_cast(uint64_t, wj) != __builtin_bit_cast(uint64_t, wfirst);
+                xp[u] = q2[h].xp;
             }
-            // pad to a multiple of 4 entries with inert ones (d' = -inf: never counted, never band)
-            if (tid < ((4 - (n & 3)) & 3)) s32[n + tid] = make_float4(__builtin_inff(), 0.0f, 0.0f, 0.0f);
-            __syncthreads();
-            // weights identical across the chunk? (compare with entry 0 after staging)
-            const uint64_t w0 = __builtin_bit_cast(uint64_t, sw[0]);
-            mixed |= (tid < n) && __builtin_bit_cast(uint64_t, sw[tid]) != w0;
-            const bool uniform = !__syncthreads_or(mixed);
-#ifdef MAC_DIAG
-            if (rb == R.z && base == 0) MAC_WALK_STAMP(3);
-#endif
+            sa[j] = f32x2{q2[0].sa, q2[1].sa};
+            sb[j] = f32x2{q2[0].sb, q2[1].sb};
+            st[j] = f32x2{q2[0].stm, q2[1].stm};
+            ns[j] = f32x2{q2[0].ns, q2[1].ns};
+        }
+        // candidate pairs with a position (block-uniform)
+        const int np = (ke - kb + 2 * kWave - 1) / (2 * kWave);
+        // d' of slot u for a staged entry (the hot loop's arithmetic, one candidate)
+        auto dprime = [&](const float4& e, int u) {
+            const int j = u >> 1;
+            const float a_ = (u & 1) ? sa[j].y : sa[j].x, b_ = (u & 1) ? sb[j].y : sb[j].x;
+            const float t_ = (u & 1) ? st[j].y : st[j].x, n_ = (u & 1) ? ns[j].y : ns[j].x;
+            return __builtin_fmaf(e.x, n_, __builtin_fmaf(e.z, b_, __builtin_fmaf(e.y, a_, t_)));
+        };
+        MAC_WALK_STAMP(1);
 
-            if (pair0 || pair1) {
-                float bmin[kPollKPL];
-#pragma unroll
-                for (int u = 0; u < kPollKPL; ++u) bmin[u] = __builtin_inff();
-                double cw[kPollKPL];   // this chunk's credited weight per candidate
-                if (uniform) {
-                    // hot loop: 2 entries x 2 candidates per step, 3 VALU ops per test
-                    f32x2 h01 = zero2, h23 = zero2;
-                    // entries staged as (Q, U, V, 0); bmin updates chained so they form v_min3
-#define MAC_POLL_PAIR(E0, E1, SA, SB, ST, NS, H, B0, B1)                                       \
-    {                                                                                         \
-        const f32x2 d0 = fma2(E0.x, NS, fma2(E0.z, SB, fma2(E0.y, SA, ST)));                   \
-        const f32x2 d1 = fma2(E1.x, NS, fma2(E1.z, SB, fma2(E1.y, SA, ST)));                   \
-        H += clamp01x2(d0, zero2);                                                            \
-        H += clamp01x2(d1, zero2);                                                            \
-        B0 = __builtin_fminf(__builtin_fminf(B0, __builtin_fabsf(d0.x)), __builtin_fabsf(d1.x)); \
-        B1 = __builtin_fminf(__builtin_fminf(B1, __builtin_fabsf(d0.y)), __builtin_fabsf(d1.y)); \
-    }
-                    if (pair1) {
-                        for (int q = 0; q < n; q += 4) {
-                            const float4 e0 = s32[q], e1 = s32[q + 1], e2 = s32[q + 2], e3 = s32[q + 3];
-                            MAC_POLL_PAIR(e0, e1, sa01, sb01, st01, ns01, h01, bmin[0], bmin[1])
-                            MAC_POLL_PAIR(e0, e1, sa23, sb23, st23, ns23, h23, bmin[2], bmin[3])
-                            MAC_POLL_PAIR(e2, e3, sa01, sb01, st01, ns01, h01, bmin[0], bmin[1])
-                            MAC_POLL_PAIR(e2, e3, sa23, sb23, st23, ns23, h23, bmin[2], bmin[3])
-                        }
-                    } else {
-                        for (int q = 0; q < n; q += 4) {
-                            const float4 e0 = s32[q], e1 = s32[q + 1], e2 = s32[q + 2], e3 = s32[q + 3];
-                            MAC_POLL_PAIR(e0, e1, sa01, sb01, st01, ns01, h01, bmin[0], bmin[1])
-                            MAC_POLL_PAIR(e2, e3, sa01, sb01, st01, ns01, h01, bmin[0], bmin[1])
-                        }
+        for (int rb = R.z; rb <= R.w; rb += kPollRB) {
+            const int nr = min(kPollRB, R.w - rb + 1);
+            if (tid < nr) {
+                const int64_t rowbase = (int64_t)(rb + tid) * g.nTx;
+                const int s0 = off[rowbase + R.x];
+                rs[tid] = s0;
+                rpre[tid + 1] = off[rowbase + R.y + 1] - s0;
+            }
+            __syncthreads();
+            if (tid < kWave) {  // inclusive scan of the row lengths (nr <= 64: one wave)
+                const int v = wave_incl_scan_i32(tid < nr ? rpre[tid + 1] : 0, tid);
+                if (tid < nr) rpre[tid + 1] = v;
+                if (tid == 0) rpre[0] = 0;
+            }
+            __syncthreads();
+            const int total = rpre[nr];
+#ifdef MAC_DIAG
+            diag_entries += total;
+            if (rb == R.z) MAC_WALK_STAMP(2);
+#endif
+            for (int base = 0; base < total; base += kPollCH) {
+                const int n = min(kPollCH, total - base);
+                bool mixed = false;
+                double wfirst = 0.0;
+                for (int q = tid; q < n; q += kPollThreads) {
+                    const int f = base + q;
+                    int lo = 0, hi = nr - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (rpre[mid] <= f) lo = mid; else hi = mid - 1;
                     }
-#undef MAC_POLL_PAIR
-                    // counts < 2^24: exact in fp32 when no entry is in the band
-                    const double wu = sw[0];
-                    cw[0] = (double)h01.x * wu;
-                    cw[1] = (double)h01.y * wu;
-                    cw[2] = (double)h23.x * wu;
-                    cw[3] = (double)h23.y * wu;
-                } else {
-                    // weighted loop: covered entries add their own weight (clamp(d') is 0 or 1
-                    // off the band; a band chunk is recomputed below)
-#pragma unroll
-                    for (int u = 0; u < kPollKPL; ++u) cw[u] = 0.0;
-                    for (int q = 0; q < n; ++q) {
-                        const float4 e = s32[q];
-                        const double wq = sw[q];
-#pragma unroll
-                        for (int u = 0; u < kPollKPL; ++u) {
-                            const float d = poll_dprime(e, pl[u]);
-                            cw[u] += d > 0.0f ? wq : 0.0;
-                            bmin[u] = __builtin_fminf(bmin[u], __builtin_fabsf(d));
-                        }
-                    }
+                    const int j = rs[lo] + (f - rpre[lo]);
+                    const double2 p = xy[j];
+                    const double wj = w[j];
+                    s64[q] = p;
+                    sw[q] = wj;
+                    const bool shared =
+                        nc > 0 && entry_shared(nc, nbox, tile_of(p.x, g.gx0, g.invS, g.nTx), rb + lo);
+                    const float fu = (float)(p.x - ox), fv = (float)(p.y - oy);
+                    s32[q] = !shared && __builtin_isfinite(fu) && __builtin_isfinite(fv)
+                                 ? make_float4(__builtin_fmaf(fu, fu, fv * fv), fu, fv, 0.0f)
+                                 : make_float4(__builtin_inff(), 0.0f, 0.0f, 0.0f);
+                    if (q == tid) wfirst = wj;
+                    mixed |= __builtin_bit_cast(uint64_t, wj) != __builtin_bit_cast(uint64_t, wfirst);
                 }
-                // band: the lane re-decides this chunk; entries with |d'| <= X' in fp64.
-                // Shared entries (q = +inf, d' = -inf) are skipped: the shared kernel owns them;
-                // for a forced lane (X' = +inf) they are told apart from non-finite ones here.
+                // pad to a multiple of 4 entries with inert ones (d' = -inf: never counted, never band)
+                if (tid < ((4 - (n & 3)) & 3)) s32[n + tid] = make_float4(__builtin_inff(), 0.0f, 0.0f, 0.0f);
+                __syncthreads();
+                // weights identical across the chunk? (compare with entry 0 after staging)
+                const uint64_t w0 = __builtin_bit_cast(uint64_t, sw[0]);
+                mixed |= (tid < n) && __builtin_bit_cast(uint64_t, sw[tid]) != w0;
+                const bool uniform = !__syncthreads_or(mixed);
+#ifdef MAC_DIAG
+                if (rb == R.z && base == 0) MAC_WALK_STAMP(3);
+#endif
+                const int ng = (n + 3) >> 2;   // groups of 4 entries; this wave: wid, wid + 4, ...
+                float bmin[kPollSlots];
 #pragma unroll
-                for (int u = 0; u < kPollKPL; ++u) {
-                    if (live[u] && bmin[u] <= pl[u].xp) {
-                        const DiskRec d = urec[row + kk[u]];
-                        double c = 0.0;
-                        for (int q = 0; q < n; ++q) {
+                for (int u = 0; u < kPollSlots; ++u) bmin[u] = __builtin_inff();
+                // band: the lane re-decides this wave's entries of the chunk for slot u; entries
+                // with |d'| <= X' in fp64. Shared entries (q = +inf, d' = -inf) are skipped: the
+                // shared kernel owns them; for a forced lane (X' = +inf) they are told apart from
+                // non-finite ones here.
+                auto band = [&](int u) {
+                    const DiskRec d = urec[row + kb + u * kWave + lane];
+                    double c = 0.0;
+                    for (int q4 = wid; q4 < ng; q4 += kPollWaves)
+                        for (int q = 4 * q4; q < min(4 * q4 + 4, n); ++q) {
                             const float4 e = s32[q];
-                            const float dp = poll_dprime(e, pl[u]);
+                            const float dp = dprime(e, u);
                             bool cov;
-                            if (__builtin_fabsf(dp) <= pl[u].xp) {
+                            if (__builtin_fabsf(dp) <= xp[u]) {
                                 const double2 p = s64[q];
                                 if (e.x == __builtin_inff() && nc > 0 &&
                                     entry_shared(nc, nbox, tile_of(p.x, g.gx0, g.invS, g.nTx),
@@ -405,22 +401,70 @@ __device__ __forceinline__ void coverage_poll_body(
                             }
                             if (cov) c += sw[q];
                         }
-                        cw[u] = c;
+                    return c;
+                };
+                if (uniform) {
+                    f32x2 h[kPollPairs];
+                    switch (np) {   // hot loop: 3 VALU ops per test, np pairs per entry pair
+                    case 1: poll_hot<1>(s32, ng, wid, sa, sb, st, ns, h, bmin); break;
+                    case 2: poll_hot<2>(s32, ng, wid, sa, sb, st, ns, h, bmin); break;
+                    case 3: poll_hot<3>(s32, ng, wid, sa, sb, st, ns, h, bmin); break;
+                    default: poll_hot<4>(s32, ng, wid, sa, sb, st, ns, h, bmin); break;
                     }
-                    if (live[u]) acc[u] += cw[u];
-                }
-            }
-#ifdef MAC_DIAG
-            if (rb == R.z && base == 0) MAC_WALK_STAMP(4);
-#endif
-            __syncthreads();
-        }
-    }
+                    // counts < 2^24: exact in fp32 when no entry is in the band
+                    const double wu = sw[0];
 #pragma unroll
-    for (int u = 0; u < kPollKPL; ++u)
-        if (kk[u] >= 0) partial[row + kk[u]] = acc[u];
-    MAC_WALK_STAMP(5);
-    MAC_DIAG_STAMP(diag_t0, 3, ((uint64_t)nc << 40) | ((uint64_t)(ke - kb) << 20) | (uint64_t)diag_entries);
+                    for (int u = 0; u < kPollSlots; ++u) {
+                        if (!(live & (1u << u))) continue;
+                        const float hc = (u & 1) ? h[u >> 1].y : h[u >> 1].x;
+                        acc[u] += bmin[u] <= xp[u] ? band(u) : (double)hc * wu;
+                    }
+                } else {
+                    // weighted loop: covered entries add their own weight (clamp(d') is 0 or 1
+                    // off the band; a band chunk is recomputed)
+                    double cw[kPollSlots];
+#pragma unroll
+                    for (int u = 0; u < kPollSlots; ++u) cw[u] = 0.0;
+                    for (int q4 = wid; q4 < ng; q4 += kPollWaves) {
+                        for (int e = 0; e < 4; ++e) {
+                            const int q = 4 * q4 + e;
+                            const float4 en = s32[q];
+                            const double wq = q < n ? sw[q] : 0.0;
+#pragma unroll
+                            for (int u = 0; u < kPollSlots; ++u) {
+                                if ((u >> 1) >= np) continue;
+                                const float d = dprime(en, u);
+                                cw[u] += d > 0.0f ? wq : 0.0;
+                                bmin[u] = __builtin_fminf(bmin[u], __builtin_fabsf(d));
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < kPollSlots; ++u) {
+                        if (!(live & (1u << u))) continue;
+                        acc[u] += bmin[u] <= xp[u] ? band(u) : cw[u];
+                    }
+                }
+#ifdef MAC_DIAG
+                if (rb == R.z && base == 0) MAC_WALK_STAMP(4);
+#endif
+                __syncthreads();
+            }
+        }
+        // the slice's credit per position: the four waves' shares, added in wave order
+#pragma unroll
+        for (int u = 0; u < kPollSlots; ++u) red[wid][u * kWave + lane] = acc[u];
+        __syncthreads();
+        for (int p = tid; p < ke - kb; p += kPollThreads) {
+            double a = 0.0;
+#pragma unroll
+            for (int q = 0; q < kPollWaves; ++q) a += red[q][p];
+            partial[row + kb + p] = a;
+        }
+        __syncthreads();
+        MAC_WALK_STAMP(5);
+    }
+    MAC_DIAG_STAMP(diag_t0, 3, ((uint64_t)nc << 40) | ((uint64_t)U << 20) | (uint64_t)diag_entries);
 }
 
 // timed entry point (ts: in-kernel launch timing, k_common.h)

@@ -29,37 +29,15 @@ __device__ __forceinline__ bool box_has(const int4& b, int tx, int ty)
     return b.x <= tx && tx <= b.y && b.z <= ty && ty <= b.w;
 }
 
-// Block i: the disks j < i whose region boxes overlap region i's (at most kPollNbr kept in
-// nbr[i*kPollNbr ...]; ncount[i] is the true count, > kPollNbr meaning "overflowed"). Disks
-// with neighbours are appended to dlist (order irrelevant: each is processed independently);
-// *dcount must be zero on entry (region_kernel clears it).
-// Block 0 also picks the walk: mode[0] = poll when its point-visits (cost[i].x summed) stay
-// within `ratio` x the per-candidate walk's (cost[i].y summed) — its visits are broadcast LDS
-// reads, the other's scattered global loads — or `forced`.
-__global__ __launch_bounds__(kBlock) void neighbors_kernel(const int4* __restrict__ region, int N,
-                                                           uint16_t* __restrict__ nbr,
-                                                           int* __restrict__ ncount,
-                                                           int* __restrict__ dlist,
-                                                           int* __restrict__ dcount,
-                                                           const double2* __restrict__ cost,
-                                                           double ratio, int forced,
-                                                           int* __restrict__ mode)
+// Disk i's lower-index neighbours: the disks j < i whose region boxes overlap region i's (at
+// most kPollNbr kept in nbr[i*kPollNbr ...]; ncount[i] is the true count, > kPollNbr meaning
+// "overflowed"). Disks with neighbours are appended to dlist (order irrelevant: each is processed
+// independently); *dcount must be zero on entry (the index kernel clears it).
+__device__ __forceinline__ void neighbors_block(int i, const int4* __restrict__ region,
+                                                uint16_t* __restrict__ nbr, int* __restrict__ ncount,
+                                                int* __restrict__ dlist, int* __restrict__ dcount)
 {
-    if (blockIdx.x == 0) {
-        __shared__ double red[kWavesPerBlock];
-        double a = 0.0, b = 0.0;
-        for (int j = threadIdx.x; j < N; j += kBlock) {
-            a += cost[j].x;
-            b += cost[j].y;
-        }
-        const double A = block_sum_f64(a, red);
-        __syncthreads();
-        const double B = block_sum_f64(b, red);
-        if (threadIdx.x == 0) mode[0] = forced ? forced : (A <= ratio * B ? kModePoll : kModeTiled);
-        __syncthreads();
-    }
     __shared__ int cnt;
-    const int i = blockIdx.x;
     if (threadIdx.x == 0) cnt = 0;
     __syncthreads();
     const int4 R = region[i];
@@ -77,6 +55,29 @@ __global__ __launch_bounds__(kBlock) void neighbors_kernel(const int4* __restric
         ncount[i] = cnt;
         if (cnt > 0) dlist[atomicAdd(dcount, 1)] = i;
     }
+}
+
+// The device-side walk choice: poll when its point-visits (cost[i].x summed) stay within `ratio`
+// x the per-candidate walk's (cost[i].y summed) — its visits are broadcast LDS reads, the other's
+// scattered global loads — or `forced`. The costs are integer-valued doubles, so the sums are
+// exact and every block that computes the choice gets the same one. Block-uniform result.
+__device__ __forceinline__ int walk_choice(int N, const double2* __restrict__ cost, double ratio,
+                                           int forced)
+{
+    __shared__ double red[kWavesPerBlock];
+    __shared__ int smode;
+    if (forced) return forced;
+    double a = 0.0, b = 0.0;
+    for (int j = threadIdx.x; j < N; j += kBlock) {
+        a += cost[j].x;
+        b += cost[j].y;
+    }
+    const double A = block_sum_f64(a, red);
+    __syncthreads();
+    const double B = block_sum_f64(b, red);
+    if (threadIdx.x == 0) smode = A <= ratio * B ? kModePoll : kModeTiled;
+    __syncthreads();
+    return smode;
 }
 
 // Entry (tile tx, ty) of region i is shared when it lies in a neighbour's box.
@@ -97,7 +98,7 @@ __device__ __forceinline__ bool entry_shared(int nc, const int4* nbox, int tx, i
 // over groups keeps a heavily overlapped disk from serialising one lane per candidate over all
 // of its shared entries. Writes spart[i*K + k] (the finalize kernel adds the rows of the disks
 // with ncount[i] > 0).
-constexpr int kShC = 128;
+constexpr int kShC = 64;
 constexpr int kShG = kPollThreads / kShC;
 __device__ __forceinline__ void poll_shared_job(
     const double2* __restrict__ xy, const double* __restrict__ w,
@@ -148,9 +149,10 @@ __device__ __forceinline__ void poll_shared_job(
             rpre[tid + 1] = off[rowbase + R.y + 1] - s0;
         }
         __syncthreads();
-        if (tid == 0) {
-            rpre[0] = 0;
-            for (int r = 0; r < nr; ++r) rpre[r + 1] += rpre[r];
+        if (tid < kWave) {  // inclusive scan of the row lengths (nr <= 64: one wave)
+            const int v = wave_incl_scan_i32(tid < nr ? rpre[tid + 1] : 0, tid);
+            if (tid < nr) rpre[tid + 1] = v;
+            if (tid == 0) rpre[0] = 0;
         }
         __syncthreads();
         const int total = rpre[nr];

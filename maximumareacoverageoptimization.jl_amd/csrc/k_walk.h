@@ -7,6 +7,7 @@
 #include "predicate.h"
 #include "k_common.h"
 #include "k_index.h"
+#include "k_poll_shared.h"
 
 #pragma clang fp contract(off)
 
@@ -231,6 +232,30 @@ __global__ __launch_bounds__(kBlock) void coverage_tiled_kernel(
 {
     ts_begin(ts);
     coverage_tiled_body(xy, w, off, g, urec, umap, N, K, G, mode, partial);
+    ts_end(ts);
+}
+
+// The walk choice, then its launch-time work, in one launch (k_poll_shared.h walk_choice; every
+// block computes the same choice, block 0 stores it in mode[0] for the kernels that follow):
+// poll: block i < N builds disk i's neighbour list for the poll kernel; per-candidate walk: the
+// blocks grid-stride over its (candidate, slice) units. Dynamic LDS: tiled_lds_bytes(N) whenever
+// the per-candidate walk may be chosen.
+__global__ __launch_bounds__(kBlock) void walk_setup_kernel(
+    uint64_t* ts, const double2* __restrict__ xy, const double* __restrict__ w,
+    const int32_t* __restrict__ off, Grid g, const DiskRec* __restrict__ urec,
+    const int* __restrict__ umap, int N, int K, int G, double* __restrict__ partial,
+    const int4* __restrict__ region, uint16_t* __restrict__ nbr, int* __restrict__ ncount,
+    int* __restrict__ dlist, int* __restrict__ dcount, const double2* __restrict__ cost,
+    double ratio, int forced, int* __restrict__ mode)
+{
+    ts_begin(ts);
+    const int m = walk_choice(N, cost, ratio, forced);
+    if (blockIdx.x == 0 && threadIdx.x == 0) mode[0] = m;
+    if (m == kModePoll) {
+        if ((int)blockIdx.x < N) neighbors_block(blockIdx.x, region, nbr, ncount, dlist, dcount);
+    } else {
+        coverage_tiled_body(xy, w, off, g, urec, umap, N, K, G, nullptr, partial);
+    }
     ts_end(ts);
 }
 

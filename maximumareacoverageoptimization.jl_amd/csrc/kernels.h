@@ -4,15 +4,19 @@
 // (src/TDM_STATIC_opt.jl:82-100 via src/AreaCoverageCalculation.jl:63-78), as a short chain:
 //   disk_prep_kernel      (streaming scan) per (candidate, disk): {cx, cy, T(r), r}, T the exact
 //                         threshold, and the objective-penalty term / cons3 mark
+//   cands_keys_kernel     (matrix source) fp32 keys of every candidate value, variable-major
 //   disk_index_kernel     (tiled / poll walks) per disk over all K candidates: the distinct disks
 //                         (records, penalty terms), the candidate -> distinct map, the region
 //                         and the two walk costs
-//   neighbors_kernel      per disk i: lower-index disks whose regions overlap region i; its
-//                         block 0 picks the poll walk or the per-candidate walk on the device
-//   coverage_poll_kernel  workgroup = (disk i, 1024 candidates): the entries of disk i's region
-//                         staged in LDS once, 4 candidates per lane, exact fp32 filter; leading
-//                         workgroups run the penalty chains and the shared-entry pass
+//   walk_setup_kernel     the walk choice (every block; block 0 stores it), then per disk i the
+//                         lower-index disks whose regions overlap region i (poll walk), or the
+//                         per-candidate walk itself (grid-stride over candidate x slice units)
+//   coverage_poll_kernel  workgroup = disk i: the entries of disk i's region staged in LDS once,
+//                         every wave holding all of the disk's distinct disks (8 per lane) over a
+//                         quarter of the entries, exact fp32 filter; further workgroups run the
+//                         shared-entry pass and the penalty chains
 //   coverage_tiled_kernel workgroup = candidate: each wave walks whole disks over the CSR rows
+//                         (batches too small for the poll walk)
 //   coverage_scan_kernel  streaming brute force (every entry x every disk), the fallback
 //   finalize_kernel       fixed-order sum of per-slice partials -> area, objective
 //   argmin_kernel         lexicographic (objective, index) minimum

@@ -485,41 +485,44 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             1, std::min<int64_t>((target + K - 1) / K, std::max(1, N / kWavesPerBlock)));
         n_other = G;
         L->partial.reserve(sizeof(double) * (size_t)K * std::max(G, poll_possible ? N : 1));
+        const bool run_tiled = ctx->algo != MAC_ALGO_POLL;
+        const int64_t units = (int64_t)K * G;
         if (poll_possible) {
+            // walk choice + neighbour lists (poll) or the per-candidate walk itself, one launch;
+            // when the poll walk is chosen the extra blocks just exit, so the per-candidate walk
+            // gets one workgroup per CU (grid-striding over its units)
             const int forced = ctx->algo == MAC_ALGO_POLL ? kModePoll : 0;
             L->nbr.reserve(sizeof(uint16_t) * (size_t)N * kPollNbr);
             L->ncount.reserve(sizeof(int) * (size_t)N);
             L->dlist.reserve(sizeof(int) * (size_t)N);
-            hipLaunchKernelGGL(neighbors_kernel, dim3(N), dim3(kBlock), 0, s, L->region.as<int4>(),
-                               N, L->nbr.as<uint16_t>(), L->ncount.as<int>(), L->dlist.as<int>(),
-                               L->mode.as<int>() + 1, L->cost.as<double2>(), kPollCostRatio, forced,
-                               L->mode.as<int>());
+            const size_t lds = run_tiled ? tiled_lds_bytes(N) : 0;
+            const unsigned nwg = (unsigned)std::max<int64_t>(
+                N, run_tiled ? std::min<int64_t>(units, ctx->cus) : 0);
+            uint64_t* ts = run_tiled ? take_ts(nwg, ts_a, ts_na) : nullptr;
+            hipLaunchKernelGGL(walk_setup_kernel, dim3(nwg), dim3(kBlock), (uint32_t)lds, s, ts,
+                               ctx->xys.as<double2>(), ctx->ws.as<double>(), ctx->off.as<int32_t>(),
+                               ctx->grid, d_urec, d_map, N, K, G, L->partial.as<double>(),
+                               L->region.as<int4>(), L->nbr.as<uint16_t>(), L->ncount.as<int>(),
+                               L->dlist.as<int>(), L->mode.as<int>() + 1, L->cost.as<double2>(),
+                               kPollCostRatio, forced, L->mode.as<int>());
             HCK(hipGetLastError());
             d_mode = L->mode.as<int>();
             d_umap = d_map;
-        }
-        const bool run_tiled = ctx->algo != MAC_ALGO_POLL;
-        if (run_tiled) {
-            const size_t lds = tiled_lds_bytes(N);
-            const int64_t units = (int64_t)K * G;
-            // when the device may pick the poll walk, this launch usually just exits: one
-            // workgroup per CU keeps that cheap (a chosen tiled walk grid-strides over its units)
-            const int64_t cap = poll_possible ? (int64_t)ctx->cus : units;
-            const unsigned nwg = (unsigned)std::min(units, cap);
-            uint64_t* ts = take_ts(nwg, ts_a, ts_na);
-            hipLaunchKernelGGL(coverage_tiled_kernel, dim3(nwg), dim3(kBlock),
-                               (uint32_t)lds, s, ts, ctx->xys.as<double2>(), ctx->ws.as<double>(),
-                               ctx->off.as<int32_t>(), ctx->grid, d_urec, d_map, N, K, G,
-                               d_mode, L->partial.as<double>());
+        } else {
+            uint64_t* ts = take_ts(units, ts_a, ts_na);
+            hipLaunchKernelGGL(coverage_tiled_kernel, dim3((unsigned)units), dim3(kBlock),
+                               (uint32_t)tiled_lds_bytes(N), s, ts, ctx->xys.as<double2>(),
+                               ctx->ws.as<double>(), ctx->off.as<int32_t>(), ctx->grid, d_urec, d_map,
+                               N, K, G, nullptr, L->partial.as<double>());
             HCK(hipGetLastError());
         }
         if (poll_possible) {
-            const int gy = (K + kPollKPB - 1) / kPollKPB;
-            const int chains = (K + kChainC - 1) / kChainC;          // spread over the gy rows
-            const int n_chain = d_obj ? (chains + gy - 1) / gy : 0;
+            const int gy = 1;   // walk workgroups loop over their disk's position slices
+            const int chains = (K + kChainC - 1) / kChainC;
+            const int n_chain = d_obj ? chains : 0;
             L->spart.reserve(sizeof(double) * (size_t)N * K);
-            const int n_shared = (kSharedWG + gy - 1) / gy;
-            const dim3 pgrid(n_chain + n_shared + N, gy);
+            const int n_shared = kSharedWG;
+            const dim3 pgrid(N + n_shared + n_chain, gy);
             uint64_t* ts = take_ts((int64_t)pgrid.x * pgrid.y, ts_b, ts_nb);
             hipLaunchKernelGGL(coverage_poll_kernel, pgrid, dim3(kPollThreads), 0, s, ts,
                                ctx->xys.as<double2>(), ctx->ws.as<double>(),

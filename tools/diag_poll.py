@@ -17,9 +17,9 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import __graft_entry__ as ge  # noqa: E402
 
-KPB = 1024        # kPollKPB
+KPB = 1 << 30   # one walk workgroup per disk (grid row 0 only)
 THREADS = 256     # kPollThreads
-SHB = 1024        # kSharedWG (shared-entry workgroups, spread over the grid rows)
+SHB = 256         # kSharedWG (shared-entry workgroups, spread over the grid rows)
 CHAINC = 16       # kChainC (candidates per penalty-chain workgroup)
 
 
