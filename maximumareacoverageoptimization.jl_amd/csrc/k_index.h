@@ -31,6 +31,7 @@
 #include "predicate.h"
 #include "k_common.h"
 #include "k_prep.h"
+#include "k_lane.h"
 
 #pragma clang fp contract(off)
 
@@ -70,6 +71,8 @@ __device__ __forceinline__ bool span_of(double x, double y, double r, const Grid
     return true;
 }
 
+constexpr int kRowInfo = 32;   // region rows described per disk (larger regions: walks read off)
+
 struct IndexOut {
     DiskRec* urec;
     double* pen;     // per candidate: pen[i*K + k] (null: no objective)
@@ -78,6 +81,14 @@ struct IndexOut {
     int4* region;
     double2* cost;
     int* dcount;     // the poll walk's disks-with-neighbours counter, cleared here
+    // poll walk inputs (null: not needed): per position the scaled-filter constants (k_lane.h)
+    // {S*2cu, S*2cv, S*(T - C), -S} and X' (-1: inert), relative to the region centre; per disk
+    // kRowInfo + 1 row descriptors of its region {first entry of the row's run, entries before
+    // it} (entry nr = {0, total}), written when the region has at most kRowInfo rows
+    float4* lane4;
+    float* lanexp;
+    int2* rows;
+    const int32_t* off;
 };
 
 // fp32 key of value v relative to the base b: exact when b + (double)key reproduces v bit for bit
@@ -265,13 +276,7 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(8))
             if (o.pen) o.pen[row + k] = pen_term(x, y, r, i, N, pa);
             add_span(x, y, r);
         }
-        // ---- per distinct disk: its record, from the owner's exact key (base + offset)
-        const int U = ucnt;
-        for (int u = tid; u < U; u += kIdxThreads) {
-            const int k = owner_of[u];
-            o.urec[row + u] = make_disk(bx + (double)kx[k], by + (double)ky[k], br + (double)kr[k]);
-        }
-        if (tid == 0) o.ucount[i] = U;
+        if (tid == 0) o.ucount[i] = ucnt;
     }
     MAC_IDX_STAMP(4);
     // ---- region (block min / max) and costs (block sum: exact, integer-valued)
@@ -289,6 +294,7 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(8))
         sred[3][wid] = R.w;
     }
     const double csum = block_sum_f64<kIdxWaves>(span_area, dred);   // (contains a barrier)
+    __shared__ int4 sRg;
     if (tid == 0) {
         int4 Rg = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
         for (int q = 0; q < kIdxWaves; ++q) {
@@ -301,6 +307,50 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(8))
         o.region[i] = Rg;
         const double rc = Rg.x <= Rg.y ? (double)(Rg.y - Rg.x + 1) * (double)(Rg.w - Rg.z + 1) : 0.0;
         o.cost[i] = make_double2(rc * (double)K, csum);
+        sRg = Rg;
+    }
+    __syncthreads();
+    const int4 Rg = sRg;
+    const bool any = Rg.x <= Rg.y;
+    // ---- the region's row descriptors (one wave)
+    if (o.rows && any && Rg.w - Rg.z + 1 <= kRowInfo && tid < kWave) {
+        const int nr = Rg.w - Rg.z + 1;
+        int s0 = 0, len = 0;
+        if (tid < nr) {
+            const int64_t rb = (int64_t)(Rg.z + tid) * g.nTx;
+            s0 = o.off[rb + Rg.x];
+            len = o.off[rb + Rg.y + 1] - s0;
+        }
+        const int incl = wave_incl_scan_i32(len, tid);
+        if (tid <= nr) o.rows[(int64_t)i * (kRowInfo + 1) + tid] = make_int2(s0, incl - len);
+    }
+    // ---- per position: the record (hashed: from the owner's exact key, base + offset; identity:
+    // written above) and the poll walk's lane constants relative to the region centre (the same
+    // origin and bound the walk stages its entries with, k_poll.h)
+    const double ox = g.gx0 + 0.5 * (double)(Rg.x + Rg.y + 1) * g.S;
+    const double oy = g.gy0 + 0.5 * (double)(Rg.z + Rg.w + 1) * g.S;
+    const double Umax = 0.5 * (double)max(Rg.y - Rg.x + 1, Rg.w - Rg.z + 1) * g.S + 2.0 * g.S;
+    const int U = hashed ? ucnt : K;
+    if (hashed || o.lane4) {
+        for (int u = tid; u < U; u += kIdxThreads) {
+            DiskRec d;
+            if (hashed) {
+                const int k = owner_of[u];
+                d = make_disk(bx + (double)kx[k], by + (double)ky[k], br + (double)kr[k]);
+                o.urec[row + u] = d;
+            } else {
+                double x, y, r;
+                get3(u, x, y, r);
+                d = make_disk(x, y, r);
+            }
+            if (o.lane4) {
+                PollLane L = inert_lane();
+                int4 sp;
+                if (any && disk_span(d, g, sp)) L = poll_lane(d, ox, oy, Umax);
+                o.lane4[row + u] = make_float4(L.sa, L.sb, L.stm, L.ns);
+                o.lanexp[row + u] = L.xp;
+            }
+        }
     }
     MAC_IDX_STAMP(5);
 }

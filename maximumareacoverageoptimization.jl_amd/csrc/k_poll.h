@@ -44,6 +44,7 @@
 #include "k_poll_shared.h"
 #include "k_final.h"
 #include "k_index.h"
+#include "k_lane.h"
 
 #pragma clang fp contract(off)
 
@@ -74,91 +75,6 @@ __device__ uint64_t g_diag_walk[8 * 65536];   // walk role, grid row 0: per-disk
 #define MAC_DIAG_STAMP(t0, role, info)
 #define MAC_WALK_STAMP(q)
 #endif
-
-__device__ __forceinline__ float next_down_f32(float f)
-{
-    if (f != f || f == -__builtin_inff()) return f;
-    if (f == 0.0f) return -__builtin_bit_cast(float, 1u);
-    uint32_t b = __builtin_bit_cast(uint32_t, f);
-    b = f > 0.0f ? b - 1 : b + 1;
-    return __builtin_bit_cast(float, b);
-}
-
-__device__ __forceinline__ float next_up_f32(float f)
-{
-    if (f != f || f == __builtin_inff()) return f;
-    if (f == 0.0f) return __builtin_bit_cast(float, 1u);
-    uint32_t b = __builtin_bit_cast(uint32_t, f);
-    b = f > 0.0f ? b + 1 : b - 1;
-    return __builtin_bit_cast(float, b);
-}
-
-// largest float <= v (NaN -> -inf: the fast "covered" test then never fires)
-__device__ __forceinline__ float f32_down(double v)
-{
-    if (!(v == v)) return -__builtin_inff();
-    float f = (float)v;
-    if ((double)f > v) f = next_down_f32(f);
-    return f;
-}
-
-// smallest float >= v (NaN -> +inf: everything not surely covered goes to the exact pass)
-__device__ __forceinline__ float f32_up(double v)
-{
-    if (!(v == v)) return __builtin_inff();
-    float f = (float)v;
-    if ((double)f < v) f = next_up_f32(f);
-    return f;
-}
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-// clamp to [0, 1] of both halves in one packed op (d' > X' >= 1 -> 1, d' < 0 -> 0)
-__device__ __forceinline__ f32x2 clamp01x2(f32x2 x, f32x2 zero)
-{
-    f32x2 r;
-    asm("v_pk_add_f32 %0, %1, %2 clamp" : "=v"(r) : "v"(x), "v"(zero));
-    return r;
-}
-
-__device__ __forceinline__ f32x2 fma2(float a, f32x2 b, f32x2 c)
-{
-    return __builtin_elementwise_fma((f32x2)a, b, c);
-}
-
-// Per-candidate constants of the scaled fp32 filter (see the header comment).
-struct PollLane {
-    float sa, sb, stm, ns, xp;   // S*2cu, S*2cv, S*fl32(T - C), -S, X'
-};
-
-__device__ __forceinline__ PollLane poll_lane(const DiskRec& d, double ox, double oy, double U)
-{
-    PollLane L;
-    const double cu = d.cx - ox, cv = d.cy - oy;
-    const double M = __builtin_fmax(__builtin_fmax(U, d.r),
-                                    __builtin_fmax(__builtin_fabs(cu), __builtin_fabs(cv)));
-    if (!(M <= 0x1p60 && M >= 0x1p-60)) {  // forced: everything to the exact pass
-        L.sa = L.sb = L.stm = 0.0f;
-        L.ns = -1.0f;
-        L.xp = __builtin_inff();
-        return L;
-    }
-    const float X = f32_up(M * M * 0x1p-18 + 0x1p-120);
-    const int ex = (int)((__builtin_bit_cast(uint32_t, X) >> 23) & 0xff) - 127;  // X normal
-    const double S = __builtin_ldexp(1.0, -ex);   // S*X in [1, 2)
-    const double C = cu * cu + cv * cv;
-    L.sa = (float)(2.0 * cu * S);
-    L.sb = (float)(2.0 * cv * S);
-    L.stm = (float)((d.T - C) * S);
-    L.ns = (float)(-S);
-    L.xp = (float)((double)X * S);
-    return L;
-}
-
-__device__ __forceinline__ float poll_dprime(const float4& e, const PollLane& L)
-{
-    return __builtin_fmaf(e.x, L.ns, __builtin_fmaf(e.z, L.sb, __builtin_fmaf(e.y, L.sa, L.stm)));
-}
 
 // Hot loop of the poll walk over this wave's groups of 4 staged entries (q4 = w, w + 4, ...):
 // NP candidate pairs per entry pair, per 2 entries x 2 candidates six packed fmas, two packed
@@ -194,7 +110,7 @@ __device__ __forceinline__ void poll_hot(const float4* __restrict__ s32, int ng,
 #undef MAC_POLL_PAIR
 }
 
-// Grid (N + n_shared + n_chain); roles by x, in dispatch order (the longest first): x < N, when
+// Grid (N + n_shared + n_chain); roles by x, in dispatch order: x < N, when
 // *mode == kModePoll (or mode == null): one workgroup per disk i, over slices of kPollKPB
 // positions of disk i's distinct disks (urec / ucount, k_index.h): partial[i*K + p] = weight of
 // the non-shared entries credited to position p (finalize gathers it for every candidate through
@@ -209,6 +125,8 @@ __device__ __forceinline__ void coverage_poll_body(
     const int32_t* __restrict__ off, Grid g, const DiskRec* __restrict__ urec,
     const int* __restrict__ umap, const int* __restrict__ ucount,
     const int4* __restrict__ region, const uint16_t* __restrict__ nbrT,
+    const int4* __restrict__ nboxT, const float4* __restrict__ lane4,
+    const float* __restrict__ lanexp, const int2* __restrict__ rows,
     const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
     int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
     double* __restrict__ spart, int n_chain, const double* __restrict__ pen, double penalty,
@@ -231,8 +149,8 @@ __device__ __forceinline__ void coverage_poll_body(
         const int nd = *dcount;
         const int nsub = (K + kShC - 1) / kShC;
         for (int job = bx - N; job < nd * nsub; job += n_shared)
-            poll_shared_job(xy, w, off, g, urec, umap, region, nbrT, ncount, dlist[job / nsub], K,
-                            (job % nsub) * kShC, spart);
+            poll_shared_job(xy, w, off, g, urec, umap, region, nbrT, nboxT, rows, ncount,
+                            dlist[job / nsub], K, (job % nsub) * kShC, spart);
         MAC_DIAG_STAMP(diag_t0, 2, (uint64_t)nd);
         return;
     }
@@ -255,57 +173,72 @@ __device__ __forceinline__ void coverage_poll_body(
 
     const int i = bx;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
-    // positions p = distinct disks of disk i (k_index.h; all K candidates without dedup)
+    const int64_t row = (int64_t)i * K;
+    // One memory round trip for everything indexed by disk i, loaded speculatively (bounds are
+    // checked once it has arrived): the position count, region, neighbour count and boxes, the
+    // region's row descriptors and the first slice's lane constants (k_index.h).
     const int U = ucount[i];
     const int4 R = region[i];
     const int nc = ncount[i];
-    const int64_t row = (int64_t)i * K;
+    const int2 rinfo = tid <= kRowInfo ? rows[(int64_t)i * (kRowInfo + 1) + tid] : make_int2(0, 0);
+    const int4 nb = tid < kPollNbr ? nboxT[i * kPollNbr + tid] : make_int4(0, 0, 0, 0);
+    // every wave holds every position of a slice: p = kb + 64 s + lane (slot s); the waves split
+    // the staged entries instead (groups of 4, wave w takes groups w, w + 4, ...). Per slot: the
+    // lane constants as pair vectors (slots 2j, 2j+1) and X'.
+    f32x2 sa[kPollPairs], sb[kPollPairs], st[kPollPairs], ns[kPollPairs];
+    float xp[kPollSlots];
+    auto load_lanes = [&](int kb) {   // speculative: any p < K is allocated
+#pragma unroll
+        for (int u = 0; u < kPollSlots; ++u) {
+            const int p = kb + u * kWave + lane;
+            const float4 c = p < K ? lane4[row + p] : make_float4(0.0f, 0.0f, -1.0f, -1.0f);
+            xp[u] = p < K ? lanexp[row + p] : -1.0f;
+            const int j = u >> 1;
+            if (u & 1) {
+                sa[j].y = c.x;
+                sb[j].y = c.y;
+                st[j].y = c.z;
+                ns[j].y = c.w;
+            } else {
+                sa[j].x = c.x;
+                sb[j].x = c.y;
+                st[j].x = c.z;
+                ns[j].x = c.w;
+            }
+        }
+    };
+    load_lanes(0);
     if (R.x > R.y) {  // disk i covers nothing in any candidate (uniform across the block)
         for (int p = tid; p < U; p += kPollThreads) partial[row + p] = 0.0;
         return;
     }
-    if (tid < min(nc, kPollNbr)) nbox[tid] = region[nbrT[i * kPollNbr + tid]];
+    if (tid < min(nc, kPollNbr)) nbox[tid] = nb;
+    // regions of at most kRowInfo rows (every MADS poll) take their row runs from the index
+    const int nrows = R.w - R.z + 1;
+    const bool fastrows = nrows <= kRowInfo;
+    if (fastrows && tid <= nrows) {
+        rs[tid] = rinfo.x;
+        rpre[tid] = rinfo.y;
+    }
+    __syncthreads();
 
-    // region centre and the bound Umax on every staged offset (entries of tile t satisfy
-    // t <= (p - g0)/S < t + 1 up to rounding; two tiles of slack absorb it)
+    // region centre: the origin of the staged offsets and of the index's lane constants
     const double ox = g.gx0 + 0.5 * (double)(R.x + R.y + 1) * g.S;
     const double oy = g.gy0 + 0.5 * (double)(R.z + R.w + 1) * g.S;
-    const double Umax = 0.5 * (double)max(R.y - R.x + 1, R.w - R.z + 1) * g.S + 2.0 * g.S;
 
     // slices of kPollKPB positions (one for any MADS poll: a few hundred distinct disks)
     for (int kb = 0; kb < U; kb += kPollKPB) {
         const int ke = min(U, kb + kPollKPB);
         MAC_WALK_STAMP(0);
-        // every wave holds every position of the slice: p = kb + 64 s + lane (slot s); the waves
-        // split the staged entries instead (groups of 4, wave w takes groups w, w + 4, ...)
-        // per slot: the lane constants as pair vectors (slots 2j, 2j+1), X', liveness bits
-        f32x2 sa[kPollPairs], sb[kPollPairs], st[kPollPairs], ns[kPollPairs];
-        float xp[kPollSlots];
+        if (kb > 0) load_lanes(kb);
         uint32_t live = 0;
         double acc[kPollSlots];
 #pragma unroll
-        for (int j = 0; j < kPollPairs; ++j) {
-            PollLane q2[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int u = 2 * j + h;
-                const int p = kb + u * kWave + lane;
-                acc[u] = 0.0;
-                q2[h] = PollLane{0.0f, 0.0f, -1.0f, -1.0f, 0.5f};  // d' < -X' for every entry: inert
-                if (p < ke) {
-                    const DiskRec d = urec[row + p];
-                    int4 sp;
-                    if (disk_span(d, g, sp)) {
-                        live |= 1u << u;
-                        q2[h] = poll_lane(d, ox, oy, Umax);
-                    }
-                }
-                xp[u] = q2[h].xp;
-            }
-            sa[j] = f32x2{q2[0].sa, q2[1].sa};
-            sb[j] = f32x2{q2[0].sb, q2[1].sb};
-            st[j] = f32x2{q2[0].stm, q2[1].stm};
-            ns[j] = f32x2{q2[0].ns, q2[1].ns};
+        for (int u = 0; u < kPollSlots; ++u) {
+            acc[u] = 0.0;
+            if (kb + u * kWave + lane < ke) live |= 1u << u;
+            else xp[u] = -1.0f;   // past the slice's last position: never band (its lane
+                                  // constants may be another disk's or stale: never credited)
         }
         // candidate pairs with a position (block-uniform)
         const int np = (ke - kb + 2 * kWave - 1) / (2 * kWave);
@@ -320,19 +253,21 @@ __device__ __forceinline__ void coverage_poll_body(
 
         for (int rb = R.z; rb <= R.w; rb += kPollRB) {
             const int nr = min(kPollRB, R.w - rb + 1);
-            if (tid < nr) {
-                const int64_t rowbase = (int64_t)(rb + tid) * g.nTx;
-                const int s0 = off[rowbase + R.x];
-                rs[tid] = s0;
-                rpre[tid + 1] = off[rowbase + R.y + 1] - s0;
+            if (!fastrows) {  // row runs of this batch from the CSR offsets
+                if (tid < nr) {
+                    const int64_t rowbase = (int64_t)(rb + tid) * g.nTx;
+                    const int s0 = off[rowbase + R.x];
+                    rs[tid] = s0;
+                    rpre[tid + 1] = off[rowbase + R.y + 1] - s0;
+                }
+                __syncthreads();
+                if (tid < kWave) {  // inclusive scan of the row lengths (nr <= 64: one wave)
+                    const int v = wave_incl_scan_i32(tid < nr ? rpre[tid + 1] : 0, tid);
+                    if (tid < nr) rpre[tid + 1] = v;
+                    if (tid == 0) rpre[0] = 0;
+                }
+                __syncthreads();
             }
-            __syncthreads();
-            if (tid < kWave) {  // inclusive scan of the row lengths (nr <= 64: one wave)
-                const int v = wave_incl_scan_i32(tid < nr ? rpre[tid + 1] : 0, tid);
-                if (tid < nr) rpre[tid + 1] = v;
-                if (tid == 0) rpre[0] = 0;
-            }
-            __syncthreads();
             const int total = rpre[nr];
 #ifdef MAC_DIAG
             diag_entries += total;
@@ -468,19 +403,22 @@ __device__ __forceinline__ void coverage_poll_body(
 }
 
 // timed entry point (ts: in-kernel launch timing, k_common.h)
-__global__ __launch_bounds__(kPollThreads) __attribute__((amdgpu_waves_per_eu(4))) void coverage_poll_kernel(
+__global__ __launch_bounds__(kPollThreads) __attribute__((amdgpu_waves_per_eu(3))) void coverage_poll_kernel(
     uint64_t* ts, const double2* __restrict__ xy, const double* __restrict__ w,
     const int32_t* __restrict__ off, Grid g, const DiskRec* __restrict__ urec,
     const int* __restrict__ umap, const int* __restrict__ ucount,
     const int4* __restrict__ region, const uint16_t* __restrict__ nbrT,
+    const int4* __restrict__ nboxT, const float4* __restrict__ lane4,
+    const float* __restrict__ lanexp, const int2* __restrict__ rows,
     const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
     int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
     double* __restrict__ spart, int n_chain, const double* __restrict__ pen, double penalty,
     double* __restrict__ vp, int n_shared)
 {
     ts_begin(ts);
-    coverage_poll_body(xy, w, off, g, urec, umap, ucount, region, nbrT, ncount, dlist, dcount, N, K,
-                       mode, partial, spart, n_chain, pen, penalty, vp, n_shared);
+    coverage_poll_body(xy, w, off, g, urec, umap, ucount, region, nbrT, nboxT, lane4, lanexp, rows,
+                       ncount, dlist, dcount, N, K, mode, partial, spart, n_chain, pen, penalty, vp,
+                       n_shared);
     ts_end(ts);
 }
 

@@ -31,10 +31,11 @@ __device__ __forceinline__ bool box_has(const int4& b, int tx, int ty)
 
 // Disk i's lower-index neighbours: the disks j < i whose region boxes overlap region i's (at
 // most kPollNbr kept in nbr[i*kPollNbr ...]; ncount[i] is the true count, > kPollNbr meaning
-// "overflowed"). Disks with neighbours are appended to dlist (order irrelevant: each is processed
+// "overflowed"), their region boxes in nboxT. Disks with neighbours are appended to dlist (order irrelevant: each is processed
 // independently); *dcount must be zero on entry (the index kernel clears it).
 __device__ __forceinline__ void neighbors_block(int i, const int4* __restrict__ region,
-                                                uint16_t* __restrict__ nbr, int* __restrict__ ncount,
+                                                uint16_t* __restrict__ nbr, int4* __restrict__ nboxT,
+                                                int* __restrict__ ncount,
                                                 int* __restrict__ dlist, int* __restrict__ dcount)
 {
     __shared__ int cnt;
@@ -46,7 +47,10 @@ __device__ __forceinline__ void neighbors_block(int i, const int4* __restrict__ 
             const int4 Q = region[j];
             if (box_overlap(Q, R)) {
                 const int p = atomicAdd(&cnt, 1);  // list order is irrelevant (a boolean OR)
-                if (p < kPollNbr) nbr[i * kPollNbr + p] = (uint16_t)j;
+                if (p < kPollNbr) {
+                    nbr[i * kPollNbr + p] = (uint16_t)j;
+                    nboxT[i * kPollNbr + p] = Q;   // the neighbour's region box
+                }
             }
         }
     }
@@ -104,6 +108,7 @@ __device__ __forceinline__ void poll_shared_job(
     const double2* __restrict__ xy, const double* __restrict__ w,
     const int32_t* __restrict__ off, const Grid& g, const DiskRec* __restrict__ urec,
     const int* __restrict__ umap, const int4* __restrict__ region, const uint16_t* __restrict__ nbrT,
+    const int4* __restrict__ nboxT, const int2* __restrict__ rows,
     const int* __restrict__ ncount, int i, int K, int kb, double* __restrict__ spart)
 {
     __shared__ double2 sp[kPollThreads];
@@ -122,10 +127,17 @@ __device__ __forceinline__ void poll_shared_job(
     const int nc = ncount[i];
     const int ncl = min(nc, kPollNbr);
     const int4 R = region[i];
+    const int2 rinfo = tid <= kRowInfo ? rows[(int64_t)i * (kRowInfo + 1) + tid] : make_int2(0, 0);
+    const int nrows = R.w - R.z + 1;
+    const bool fastrows = nrows <= kRowInfo;   // row runs from the index (k_index.h)
     __syncthreads();  // LDS reuse across jobs
     if (tid < ncl) {
         nbr[tid] = nbrT[i * kPollNbr + tid];
-        nbox[tid] = region[nbr[tid]];
+        nbox[tid] = nboxT[i * kPollNbr + tid];
+    }
+    if (fastrows && tid <= nrows) {
+        rs[tid] = rinfo.x;
+        rpre[tid] = rinfo.y;
     }
     DiskRec d = DiskRec{0.0, 0.0, -1.0, 0.0};
     DiskRec e[4];
@@ -142,19 +154,21 @@ __device__ __forceinline__ void poll_shared_job(
 
     for (int rb = R.z; rb <= R.w; rb += kPollRB) {
         const int nr = min(kPollRB, R.w - rb + 1);
-        if (tid < nr) {
-            const int64_t rowbase = (int64_t)(rb + tid) * g.nTx;
-            const int s0 = off[rowbase + R.x];
-            rs[tid] = s0;
-            rpre[tid + 1] = off[rowbase + R.y + 1] - s0;
+        if (!fastrows) {
+            if (tid < nr) {
+                const int64_t rowbase = (int64_t)(rb + tid) * g.nTx;
+                const int s0 = off[rowbase + R.x];
+                rs[tid] = s0;
+                rpre[tid + 1] = off[rowbase + R.y + 1] - s0;
+            }
+            __syncthreads();
+            if (tid < kWave) {  // inclusive scan of the row lengths (nr <= 64: one wave)
+                const int v = wave_incl_scan_i32(tid < nr ? rpre[tid + 1] : 0, tid);
+                if (tid < nr) rpre[tid + 1] = v;
+                if (tid == 0) rpre[0] = 0;
+            }
+            __syncthreads();
         }
-        __syncthreads();
-        if (tid < kWave) {  // inclusive scan of the row lengths (nr <= 64: one wave)
-            const int v = wave_incl_scan_i32(tid < nr ? rpre[tid + 1] : 0, tid);
-            if (tid < nr) rpre[tid + 1] = v;
-            if (tid == 0) rpre[0] = 0;
-        }
-        __syncthreads();
         const int total = rpre[nr];
         for (int base = 0; base < total; base += kPollThreads) {
             // this round's entries (one per thread), shared ones compacted in list order

@@ -120,7 +120,7 @@ struct Lane {
     hipStream_t last = nullptr;   // stream of the most recent use
     hipEvent_t done = nullptr;
     DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode, pen, nbr,
-        ncount, dlist, spart, vp, xinc, perm, ucount, umap, keysT, kbad;
+        ncount, dlist, spart, vp, xinc, perm, ucount, umap, keysT, kbad, lane4, lanexp, rows, nboxT;
     std::vector<double> h_dlim;
     PinnedBuf h_stage;                         // native MADS driver: best, permutations, incumbent
 };
@@ -455,8 +455,16 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         L->region.reserve(sizeof(int4) * N);
         L->cost.reserve(sizeof(double2) * N);
         L->mode.reserve(2 * sizeof(int));  // [0] walk, [1] disks-with-neighbours count
+        if (poll_possible) {  // the poll walk's lane constants and row descriptors
+            L->lane4.reserve(sizeof(float4) * (size_t)N * K);
+            L->lanexp.reserve(sizeof(float) * (size_t)N * K);
+            L->rows.reserve(sizeof(int2) * (size_t)N * (kRowInfo + 1));
+        }
         const IndexOut io{L->disks.as<DiskRec>(), d_pen, L->umap.as<int>(), L->ucount.as<int>(),
-                          L->region.as<int4>(), L->cost.as<double2>(), L->mode.as<int>() + 1};
+                          L->region.as<int4>(), L->cost.as<double2>(), L->mode.as<int>() + 1,
+                          poll_possible ? L->lane4.as<float4>() : nullptr,
+                          poll_possible ? L->lanexp.as<float>() : nullptr,
+                          poll_possible ? L->rows.as<int2>() : nullptr, ctx->off.as<int32_t>()};
         CandSrc isrc = src;
         if (src.cands && K <= kIndexMaxK + 1) {  // matrix: fp32 keys, variable-major, so each
                                                  // disk's K keys are a row
@@ -495,6 +503,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             L->nbr.reserve(sizeof(uint16_t) * (size_t)N * kPollNbr);
             L->ncount.reserve(sizeof(int) * (size_t)N);
             L->dlist.reserve(sizeof(int) * (size_t)N);
+            L->nboxT.reserve(sizeof(int4) * (size_t)N * kPollNbr);
             const size_t lds = run_tiled ? tiled_lds_bytes(N) : 0;
             const unsigned nwg = (unsigned)std::max<int64_t>(
                 N, run_tiled ? std::min<int64_t>(units, ctx->cus) : 0);
@@ -502,9 +511,9 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             hipLaunchKernelGGL(walk_setup_kernel, dim3(nwg), dim3(kBlock), (uint32_t)lds, s, ts,
                                ctx->xys.as<double2>(), ctx->ws.as<double>(), ctx->off.as<int32_t>(),
                                ctx->grid, d_urec, d_map, N, K, G, L->partial.as<double>(),
-                               L->region.as<int4>(), L->nbr.as<uint16_t>(), L->ncount.as<int>(),
-                               L->dlist.as<int>(), L->mode.as<int>() + 1, L->cost.as<double2>(),
-                               kPollCostRatio, forced, L->mode.as<int>());
+                               L->region.as<int4>(), L->nbr.as<uint16_t>(), L->nboxT.as<int4>(),
+                               L->ncount.as<int>(), L->dlist.as<int>(), L->mode.as<int>() + 1,
+                               L->cost.as<double2>(), kPollCostRatio, forced, L->mode.as<int>());
             HCK(hipGetLastError());
             d_mode = L->mode.as<int>();
             d_umap = d_map;
@@ -528,6 +537,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                                ctx->xys.as<double2>(), ctx->ws.as<double>(),
                                ctx->off.as<int32_t>(), ctx->grid, d_urec, d_map,
                                L->ucount.as<int>(), L->region.as<int4>(), L->nbr.as<uint16_t>(),
+                               L->nboxT.as<int4>(), L->lane4.as<float4>(), L->lanexp.as<float>(),
+                               L->rows.as<int2>(),
                                L->ncount.as<int>(), L->dlist.as<int>(), L->mode.as<int>() + 1, N, K,
                                d_mode, L->partial.as<double>(), L->spart.as<double>(), n_chain, d_pen,
                                penalty, d_vp, n_shared);
@@ -774,7 +785,8 @@ void mac_ctx_destroy(mac_ctx* ctx)
         for (DevBuf* b : {&l->cands, &l->disks, &l->partial, &l->area, &l->obj, &l->best,
                           &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->pen, &l->nbr,
                           &l->ncount, &l->dlist, &l->spart, &l->vp, &l->xinc,
-                          &l->perm, &l->ucount, &l->umap, &l->keysT, &l->kbad})
+                          &l->perm, &l->ucount, &l->umap, &l->keysT, &l->kbad, &l->lane4,
+                          &l->lanexp, &l->rows, &l->nboxT})
             b->release();
         if (l->done) (void)hipEventDestroy(l->done);
         if (l->stream) (void)hipStreamDestroy(l->stream);
