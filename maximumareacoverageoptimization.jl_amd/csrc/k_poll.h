@@ -128,7 +128,7 @@ __device__ __forceinline__ void coverage_poll_body(
     const int4* __restrict__ nboxT, const float4* __restrict__ lane4,
     const float* __restrict__ lanexp, const int2* __restrict__ rows,
     const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
-    int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
+    int* __restrict__ jobctr, int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
     double* __restrict__ spart, int n_chain, const double* __restrict__ pen, double penalty,
     double* __restrict__ vp, int n_shared)
 {
@@ -137,6 +137,30 @@ __device__ __forceinline__ void coverage_poll_body(
     const uint64_t diag_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
     const int bx = blockIdx.x;
+    // The shared-entry jobs (disk with neighbours x kShC-candidate slice, k_poll_shared.h) are
+    // taken from a counter (the index kernel cleared it) by the shared workgroups and by every
+    // walk workgroup once its disk is done: few jobs (separated disks) finish at once, many (a
+    // crowded poll) spread over the whole grid.
+    // Jobs [0, n_shared) go to the shared workgroups one each, without the counter; the rest are
+    // taken as n_shared + counter.
+    auto shared_jobs = [&](int first) {
+        __shared__ int sjob;
+        const int nsub = (K + kShC - 1) / kShC;
+        const int total = *dcount * nsub;
+        int job = first;
+        for (;;) {
+            if (job < 0) {
+                if (threadIdx.x == 0) sjob = n_shared + atomicAdd(jobctr, 1);
+                __syncthreads();
+                job = sjob;
+                __syncthreads();
+            }
+            if (job >= total) break;   // uniform
+            poll_shared_job(xy, w, off, g, urec, umap, region, nbrT, nboxT, rows, ncount,
+                            dlist[job / nsub], K, (job % nsub) * kShC, spart);
+            job = -1;
+        }
+    };
     if (bx >= N + n_shared) {  // last: the objective-penalty chains (whatever the walk)
         static_assert(kPollThreads == kBlock, "penalty_chain_block needs kBlock threads");
         const int k0 = (bx - N - n_shared) * kChainC;
@@ -145,15 +169,12 @@ __device__ __forceinline__ void coverage_poll_body(
         return;
     }
     if (mode && *mode != kModePoll) return;
-    if (bx >= N) {  // then: the shared entries (k_poll_shared.h)
-        const int nd = *dcount;
-        const int nsub = (K + kShC - 1) / kShC;
-        for (int job = bx - N; job < nd * nsub; job += n_shared)
-            poll_shared_job(xy, w, off, g, urec, umap, region, nbrT, nboxT, rows, ncount,
-                            dlist[job / nsub], K, (job % nsub) * kShC, spart);
-        MAC_DIAG_STAMP(diag_t0, 2, (uint64_t)nd);
+    if (bx >= N) {  // then: the shared entries
+        shared_jobs(bx - N);
+        MAC_DIAG_STAMP(diag_t0, 2, (uint64_t)*dcount);
         return;
     }
+    do {  // the walk of disk bx (break: nothing more to credit)
 #ifdef MAC_DIAG
     int diag_entries = 0;
 #endif
@@ -210,7 +231,7 @@ __device__ __forceinline__ void coverage_poll_body(
     load_lanes(0);
     if (R.x > R.y) {  // disk i covers nothing in any candidate (uniform across the block)
         for (int p = tid; p < U; p += kPollThreads) partial[row + p] = 0.0;
-        return;
+        break;
     }
     if (tid < min(nc, kPollNbr)) nbox[tid] = nb;
     // regions of at most kRowInfo rows (every MADS poll) take their row runs from the index
@@ -400,6 +421,8 @@ __device__ __forceinline__ void coverage_poll_body(
         MAC_WALK_STAMP(5);
     }
     MAC_DIAG_STAMP(diag_t0, 3, ((uint64_t)nc << 40) | ((uint64_t)U << 20) | (uint64_t)diag_entries);
+    } while (0);
+    shared_jobs(-1);
 }
 
 // timed entry point (ts: in-kernel launch timing, k_common.h)
@@ -411,13 +434,14 @@ __global__ __launch_bounds__(kPollThreads) __attribute__((amdgpu_waves_per_eu(3)
     const int4* __restrict__ nboxT, const float4* __restrict__ lane4,
     const float* __restrict__ lanexp, const int2* __restrict__ rows,
     const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
-    int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
+    int* __restrict__ jobctr, int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
     double* __restrict__ spart, int n_chain, const double* __restrict__ pen, double penalty,
     double* __restrict__ vp, int n_shared)
 {
     ts_begin(ts);
     coverage_poll_body(xy, w, off, g, urec, umap, ucount, region, nbrT, nboxT, lane4, lanexp, rows,
-                       ncount, dlist, dcount, N, K, mode, partial, spart, n_chain, pen, penalty, vp,
+                       ncount, dlist, dcount, jobctr, N, K, mode, partial, spart, n_chain, pen,
+                       penalty, vp,
                        n_shared);
     ts_end(ts);
 }

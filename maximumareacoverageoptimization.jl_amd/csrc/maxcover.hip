@@ -454,7 +454,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         L->ucount.reserve(sizeof(int) * (size_t)N);
         L->region.reserve(sizeof(int4) * N);
         L->cost.reserve(sizeof(double2) * N);
-        L->mode.reserve(2 * sizeof(int));  // [0] walk, [1] disks-with-neighbours count
+        L->mode.reserve(4 * sizeof(int));  // [0] walk, [1] disks-with-neighbours count, [2] jobs
         if (poll_possible) {  // the poll walk's lane constants and row descriptors
             L->lane4.reserve(sizeof(float4) * (size_t)N * K);
             L->lanexp.reserve(sizeof(float) * (size_t)N * K);
@@ -539,7 +539,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                                L->ucount.as<int>(), L->region.as<int4>(), L->nbr.as<uint16_t>(),
                                L->nboxT.as<int4>(), L->lane4.as<float4>(), L->lanexp.as<float>(),
                                L->rows.as<int2>(),
-                               L->ncount.as<int>(), L->dlist.as<int>(), L->mode.as<int>() + 1, N, K,
+                               L->ncount.as<int>(), L->dlist.as<int>(), L->mode.as<int>() + 1,
+                               L->mode.as<int>() + 2, N, K,
                                d_mode, L->partial.as<double>(), L->spart.as<double>(), n_chain, d_pen,
                                penalty, d_vp, n_shared);
             HCK(hipGetLastError());

@@ -45,6 +45,10 @@ for s in $STEPS; do
         make -s -C maximumareacoverageoptimization.jl_amd/csrc diag
         MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
             run diag 600 python tools/diag_poll.py ; rc=$? ;;
+    diag5)
+        make -s -C maximumareacoverageoptimization.jl_amd/csrc diag
+        MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
+            run diag5 600 python tools/diag_poll.py --config 5 ; rc=$? ;;
     diagidx)
         make -s -C maximumareacoverageoptimization.jl_amd/csrc diag
         MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
@@ -55,6 +59,8 @@ for s in $STEPS; do
             --no-cpu --dist-backend gloo --steps 20 ; rc=$? ;;
     bench3)
         run bench3 600 python bench.py --config 3 --no-cpu ; rc=$? ;;
+    bench5)
+        run bench5 600 python bench.py --config 5 --steps 3 --warmup 1 --no-cpu ; rc=$? ;;
     bench2)
         run bench2 600 python bench.py --config 2 --no-cpu ; rc=$? ;;
     prof)
