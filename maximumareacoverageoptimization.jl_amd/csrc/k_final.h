@@ -84,11 +84,13 @@ __global__ __launch_bounds__(kBlock) void penalty_chain_kernel(const double* __r
 // lower-index neighbours (ncount[g] > 0), its shared-entry row spart[g*K + k] (rows of other
 // disks are never written and never read). Per batch the map and ncount loads go first, then the
 // gathers and shared rows they select: two memory round trips per batch.
-// obj_k = -area_k + vp_k when obj_out != null.
+// obj_k = -area_k + vp_k when obj_out != null. With `counts` (every entry weighs w0) and the poll
+// walk chosen, the rows hold uint32 covered-entry counts per candidate (partial[i][k], and
+// spart[i][k] of the disks with neighbours): area_k = (their integer sum) * w0.
 __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
     const double* __restrict__ partial, const int* __restrict__ mode, int n_poll, int n_other,
     int K, int N, const int* __restrict__ map, const double* __restrict__ spart,
-    const int* __restrict__ ncount,
+    const int* __restrict__ ncount, int counts, double w0,
     const double* __restrict__ vp, double* __restrict__ area_out, double* __restrict__ obj_out)
 {
     __shared__ double red[kFinThreads / kFinC][kFinC];
@@ -98,6 +100,37 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
     const int k = k0 + c;
     const bool poll = mode && *mode == kModePoll;
     const int G = poll ? n_poll : n_other;
+    if (counts && poll && spart) {  // equal weights: integer rows, exact in any order
+        const unsigned* const crow = reinterpret_cast<const unsigned*>(partial);
+        const unsigned* const srow = reinterpret_cast<const unsigned*>(spart);
+        __shared__ uint64_t ired[kFinThreads / kFinC][kFinC];
+        uint64_t a = 0;
+        if (k < K) {
+            constexpr int B = 8;
+            for (int g = sg; g < G; g += B * SG) {
+                unsigned v[B], sv[B];
+#pragma unroll
+                for (int b = 0; b < B; ++b) {
+                    const int gb = g + b * SG;
+                    v[b] = gb < G ? crow[(int64_t)gb * K + k] : 0u;
+                    sv[b] = gb < G && ncount[gb] > 0 ? srow[(int64_t)gb * K + k] : 0u;
+                }
+#pragma unroll
+                for (int b = 0; b < B; ++b) a += (uint64_t)v[b] + sv[b];
+            }
+        }
+        ired[sg][c] = a;
+        __syncthreads();
+        if (sg == 0 && k < K) {
+            uint64_t n = 0;
+#pragma unroll
+            for (int q = 0; q < SG; ++q) n += ired[q][c];
+            const double area = (double)n * w0;
+            if (area_out) area_out[k] = area;
+            if (obj_out) obj_out[k] = -area + vp[k];
+        }
+        return;
+    }
     const bool rows = spart && poll;
     const int* mp = (map && poll) ? map : nullptr;
     constexpr int kFinB = 8;

@@ -130,7 +130,7 @@ __device__ __forceinline__ void coverage_poll_body(
     const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
     int* __restrict__ jobctr, int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
     double* __restrict__ spart, int n_chain, const double* __restrict__ pen, double penalty,
-    double* __restrict__ vp, int n_shared)
+    double* __restrict__ vp, int n_shared, int counts)
 {
     static_assert(kPollSlots == 2 * kPollPairs, "the hot loop pairs candidate slots");
 #ifdef MAC_DIAG
@@ -157,7 +157,7 @@ __device__ __forceinline__ void coverage_poll_body(
             }
             if (job >= total) break;   // uniform
             poll_shared_job(xy, w, off, g, urec, umap, region, nbrT, nboxT, rows, ncount,
-                            dlist[job / nsub], K, (job % nsub) * kShC, spart);
+                            dlist[job / nsub], K, (job % nsub) * kShC, spart, counts);
             job = -1;
         }
     };
@@ -230,7 +230,10 @@ __device__ __forceinline__ void coverage_poll_body(
     };
     load_lanes(0);
     if (R.x > R.y) {  // disk i covers nothing in any candidate (uniform across the block)
-        for (int p = tid; p < U; p += kPollThreads) partial[row + p] = 0.0;
+        if (counts)
+            for (int k = tid; k < K; k += kPollThreads) reinterpret_cast<unsigned*>(partial)[row + k] = 0u;
+        else
+            for (int p = tid; p < U; p += kPollThreads) partial[row + p] = 0.0;
         break;
     }
     if (tid < min(nc, kPollNbr)) nbox[tid] = nb;
@@ -355,7 +358,7 @@ __device__ __forceinline__ void coverage_poll_body(
                             } else {
                                 cov = dp > 0.0f;
                             }
-                            if (cov) c += sw[q];
+                            if (cov) c += counts ? 1.0 : sw[q];
                         }
                     return c;
                 };
@@ -373,7 +376,7 @@ __device__ __forceinline__ void coverage_poll_body(
                     for (int u = 0; u < kPollSlots; ++u) {
                         if (!(live & (1u << u))) continue;
                         const float hc = (u & 1) ? h[u >> 1].y : h[u >> 1].x;
-                        acc[u] += bmin[u] <= xp[u] ? band(u) : (double)hc * wu;
+                        acc[u] += bmin[u] <= xp[u] ? band(u) : (counts ? (double)hc : (double)hc * wu);
                     }
                 } else {
                     // weighted loop: covered entries add their own weight (clamp(d') is 0 or 1
@@ -415,9 +418,19 @@ __device__ __forceinline__ void coverage_poll_body(
             double a = 0.0;
 #pragma unroll
             for (int q = 0; q < kPollWaves; ++q) a += red[q][p];
-            partial[row + kb + p] = a;
+            if (counts) red[0][p] = a;   // column p: this thread's alone
+            else partial[row + kb + p] = a;
         }
         __syncthreads();
+        if (counts) {  // per candidate whose disk i sits at one of this slice's positions: its
+                       // covered-entry count, a uint32 row of partial (finalize adds the rows)
+            unsigned* const crow = reinterpret_cast<unsigned*>(partial) + row;
+            for (int k = tid; k < K; k += kPollThreads) {
+                const int u = umap[row + k] - kb;
+                if (u >= 0 && u < ke - kb) crow[k] = (unsigned)red[0][u];
+            }
+            __syncthreads();
+        }
         MAC_WALK_STAMP(5);
     }
     MAC_DIAG_STAMP(diag_t0, 3, ((uint64_t)nc << 40) | ((uint64_t)U << 20) | (uint64_t)diag_entries);
@@ -436,13 +449,13 @@ __global__ __launch_bounds__(kPollThreads) __attribute__((amdgpu_waves_per_eu(3)
     const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
     int* __restrict__ jobctr, int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
     double* __restrict__ spart, int n_chain, const double* __restrict__ pen, double penalty,
-    double* __restrict__ vp, int n_shared)
+    double* __restrict__ vp, int n_shared, int counts)
 {
     ts_begin(ts);
     coverage_poll_body(xy, w, off, g, urec, umap, ucount, region, nbrT, nboxT, lane4, lanexp, rows,
                        ncount, dlist, dcount, jobctr, N, K, mode, partial, spart, n_chain, pen,
                        penalty, vp,
-                       n_shared);
+                       n_shared, counts);
     ts_end(ts);
 }
 

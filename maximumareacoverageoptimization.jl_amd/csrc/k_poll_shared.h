@@ -109,7 +109,7 @@ __device__ __forceinline__ void poll_shared_job(
     const int32_t* __restrict__ off, const Grid& g, const DiskRec* __restrict__ urec,
     const int* __restrict__ umap, const int4* __restrict__ region, const uint16_t* __restrict__ nbrT,
     const int4* __restrict__ nboxT, const int2* __restrict__ rows,
-    const int* __restrict__ ncount, int i, int K, int kb, double* __restrict__ spart)
+    const int* __restrict__ ncount, int i, int K, int kb, double* __restrict__ spart, int counts)
 {
     __shared__ double2 sp[kPollThreads];
     __shared__ double sw[kPollThreads];
@@ -222,7 +222,7 @@ __device__ __forceinline__ void poll_shared_job(
                             }
                         }
                     }
-                    if (!stolen) acc += sw[s];
+                    if (!stolen) acc += counts ? 1.0 : sw[s];
                 }
             }
             __syncthreads();
@@ -234,7 +234,8 @@ __device__ __forceinline__ void poll_shared_job(
         double t = 0.0;
 #pragma unroll
         for (int q = 0; q < kShG; ++q) t += gsum[q][c];
-        spart[(int64_t)i * K + k] = t;
+        if (counts) reinterpret_cast<unsigned*>(spart)[(int64_t)i * K + k] = (unsigned)t;
+        else spart[(int64_t)i * K + k] = t;
     }
 }
 

@@ -14,18 +14,27 @@ namespace mac {
 // ------------------------------------------------------------------ set-up kernels
 
 // Per-block min/max of finite x and y: out[blk] = {xmin, xmax, ymin, ymax}.
+// Per block: bbox of the finite points, and wmix[b] = 1 when one of its weights differs (bit for
+// bit) from w[0] (equal weights let the poll walk credit integer counts, k_poll.h).
 __global__ __launch_bounds__(kBlock) void bbox_kernel(const double* __restrict__ x,
-                                                      const double* __restrict__ y, int64_t M,
-                                                      double4* __restrict__ out)
+                                                      const double* __restrict__ y,
+                                                      const double* __restrict__ w, int64_t M,
+                                                      double4* __restrict__ out,
+                                                      int* __restrict__ wmix)
 {
     double xmn = __builtin_inf(), xmx = -__builtin_inf();
     double ymn = __builtin_inf(), ymx = -__builtin_inf();
+    const uint64_t w0 = M > 0 ? __builtin_bit_cast(uint64_t, w[0]) : 0;
+    bool mixed = false;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < M;
          i += (int64_t)gridDim.x * kBlock) {
         const double a = x[i], b = y[i];
         if (__builtin_isfinite(a)) { xmn = a < xmn ? a : xmn; xmx = a > xmx ? a : xmx; }
         if (__builtin_isfinite(b)) { ymn = b < ymn ? b : ymn; ymx = b > ymx ? b : ymx; }
+        mixed |= __builtin_bit_cast(uint64_t, w[i]) != w0;
     }
+    const int anym = __syncthreads_or(mixed);
+    if (threadIdx.x == 0) wmix[blockIdx.x] = anym;
     __shared__ double4 sh[kBlock];
     sh[threadIdx.x] = make_double4(xmn, xmx, ymn, ymx);
     __syncthreads();

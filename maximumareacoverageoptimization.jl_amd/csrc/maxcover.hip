@@ -120,7 +120,8 @@ struct Lane {
     hipStream_t last = nullptr;   // stream of the most recent use
     hipEvent_t done = nullptr;
     DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode, pen, nbr,
-        ncount, dlist, spart, vp, xinc, perm, ucount, umap, keysT, kbad, lane4, lanexp, rows, nboxT;
+        ncount, dlist, spart, vp, xinc, perm, ucount, umap, keysT, kbad, lane4, lanexp, rows, nboxT,
+        cnt;
     std::vector<double> h_dlim;
     PinnedBuf h_stage;                         // native MADS driver: best, permutations, incumbent
 };
@@ -160,6 +161,8 @@ struct mac_ctx {
     DevBuf xys, ws, perm, off;
     Grid grid{};
     int64_t nTiles = 1;
+    bool w_uniform = false;   // every entry's weight is bit-identical to w0 (build_index)
+    double w0 = 0.0;
     // setup scratch
     DevBuf keys_in, keys_out, idx_in, tmp, bbox, flags_s, flags_o, keep, sel_count, cx, cy, cw,
         cidx, circ, cdisk;
@@ -279,15 +282,23 @@ static Grid choose_grid(double xmn, double xmx, double ymn, double ymx, int64_t 
 static void build_index(mac_ctx* ctx, hipStream_t s)
 {
     const int64_t M = ctx->M;
-    // bbox
+    // bbox, and whether every entry weighs the same (bit for bit)
     const int nb = (int)std::min<int64_t>(std::max<int64_t>(grid1d(M, kBlock), 1), 1024);
-    ctx->bbox.reserve(sizeof(double4) * nb);
+    ctx->bbox.reserve(sizeof(double4) * nb + sizeof(int) * nb);
+    int* d_wmix = (int*)(ctx->bbox.as<double4>() + nb);
     hipLaunchKernelGGL(bbox_kernel, dim3(nb), dim3(kBlock), 0, s, ctx->x.as<double>(),
-                       ctx->y.as<double>(), M, ctx->bbox.as<double4>());
+                       ctx->y.as<double>(), ctx->w.as<double>(), M, ctx->bbox.as<double4>(), d_wmix);
     HCK(hipGetLastError());
     std::vector<double4> hb(nb);
+    std::vector<int> hw(nb);
+    double w0 = 0.0;
     HCK(hipMemcpyAsync(hb.data(), ctx->bbox.p, sizeof(double4) * nb, hipMemcpyDeviceToHost, s));
+    HCK(hipMemcpyAsync(hw.data(), d_wmix, sizeof(int) * nb, hipMemcpyDeviceToHost, s));
+    if (M > 0) HCK(hipMemcpyAsync(&w0, ctx->w.p, sizeof(double), hipMemcpyDeviceToHost, s));
     HCK(hipStreamSynchronize(s));
+    ctx->w_uniform = M > 0;
+    for (int v : hw) ctx->w_uniform = ctx->w_uniform && v == 0;
+    ctx->w0 = w0;
     double xmn = INFINITY, xmx = -INFINITY, ymn = INFINITY, ymx = -INFINITY;
     for (auto& b : hb) {
         xmn = std::min(xmn, b.x);
@@ -386,6 +397,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
     const double* d_spart = nullptr;   // poll walk: shared-entry rows
     const int* d_umap = nullptr;       // poll walk: candidate -> distinct-disk position
     const int* d_ncount = nullptr;
+    int counts = 0;                    // poll walk with equal weights: integer count rows
     if (d_obj) {
         L->vp.reserve(sizeof(double) * (size_t)std::max(K, 1));
         d_vp = L->vp.as<double>();
@@ -460,6 +472,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             L->lanexp.reserve(sizeof(float) * (size_t)N * K);
             L->rows.reserve(sizeof(int2) * (size_t)N * (kRowInfo + 1));
         }
+        counts = poll_possible && ctx->w_uniform ? 1 : 0;   // equal weights: the walks count
         const IndexOut io{L->disks.as<DiskRec>(), d_pen, L->umap.as<int>(), L->ucount.as<int>(),
                           L->region.as<int4>(), L->cost.as<double2>(), L->mode.as<int>() + 1,
                           poll_possible ? L->lane4.as<float4>() : nullptr,
@@ -542,7 +555,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                                L->ncount.as<int>(), L->dlist.as<int>(), L->mode.as<int>() + 1,
                                L->mode.as<int>() + 2, N, K,
                                d_mode, L->partial.as<double>(), L->spart.as<double>(), n_chain, d_pen,
-                               penalty, d_vp, n_shared);
+                               penalty, d_vp, n_shared, counts);
             HCK(hipGetLastError());
             chain_done = true;
             d_spart = L->spart.as<double>();
@@ -562,7 +575,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
     }
     hipLaunchKernelGGL(finalize_kernel, dim3((K + kFinC - 1) / kFinC), dim3(kFinThreads), 0, s,
                        L->partial.as<double>(), d_mode, n_poll, n_other, K, N, d_umap, d_spart, d_ncount,
-                       d_vp, d_area, d_obj);
+                       counts, ctx->w0, d_vp, d_area, d_obj);
     HCK(hipGetLastError());
     if (d_best) {
         hipLaunchKernelGGL(argmin_kernel, dim3(1), dim3(kArgThreads), 0, s, d_obj, K, idx_base, d_best,
@@ -787,7 +800,7 @@ void mac_ctx_destroy(mac_ctx* ctx)
                           &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->pen, &l->nbr,
                           &l->ncount, &l->dlist, &l->spart, &l->vp, &l->xinc,
                           &l->perm, &l->ucount, &l->umap, &l->keysT, &l->kbad, &l->lane4,
-                          &l->lanexp, &l->rows, &l->nboxT})
+                          &l->lanexp, &l->rows, &l->nboxT, &l->cnt})
             b->release();
         if (l->done) (void)hipEventDestroy(l->done);
         if (l->stream) (void)hipStreamDestroy(l->stream);

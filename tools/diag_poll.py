@@ -109,6 +109,25 @@ def main():
             "max_us": [float(v) for v in ph.max(axis=0)],
             "start_us_pct": [float(v) for v in np.percentile((a[:, 0] - a[:, 0].min()) / 100.0,
                                                             (0, 50, 100))]}
+    bb = (ctypes.c_uint64 * (8 * 4096))()
+    if hasattr(L, "mac_diag_band_read") and L.mac_diag_band_read(bb, 8 * 4096) == 0:
+        a = np.frombuffer(bb, dtype=np.uint64).reshape(4096, 8).astype(np.int64)
+        a = a[a[:, 0] > 0]
+        if a.size:
+            base = a[:, 0].min()
+            full = a[(a[:, 1:7] > 0).all(axis=1)]
+            out["band_jobs"] = {
+                "jobs": int(a.shape[0]), "with_entries": int(full.shape[0]),
+                "end_us_max": float((a[:, 1:7].max() - base) / 100.0)}
+            if full.size:
+                ph = np.diff(full[:, :7], axis=1) / 100.0
+                out["band_jobs"].update({
+                    "names": ["tiles", "stage", "A masks", "neighbours+count", "rest chunks", "atomics"],
+                    "median_us": [float(v) for v in np.median(ph, axis=0)],
+                    "max_us": [float(v) for v in ph.max(axis=0)],
+                    "ns_median": float(np.median(full[:, 7] >> 32)),
+                    "nc_median": float(np.median((full[:, 7] >> 16) & 0xFFFF)),
+                    "U_median": float(np.median(full[:, 7] & 0xFFFF))})
     print(json.dumps(out, indent=1))
 
 
