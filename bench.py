@@ -253,15 +253,19 @@ def main():
     stream = torch.cuda.Stream(dev)
     s_handle = stream.cuda_stream
 
+    # one bound poll per candidate set: the ctypes arguments are built once (Context.poll_step)
+    steps = [ctx.poll_step(d, 3 * N, Kl, d_rmax, d_best, idx_base=idx_base, stream=s_handle)
+             for d in d_polls]
+
     def step(i):
         """One MADS poll. It ends with the best (objective, index) on the host, because the
         next poll's candidates depend on it: polls never overlap."""
-        d = d_polls[i % len(d_polls)]
-        ctx.poll_best_dev(d, 3 * N, Kl, d_rmax, d_best, idx_base=idx_base, stream=s_handle)
         if distributed:
+            d = d_polls[i % len(d_polls)]
+            ctx.poll_best_dev(d, 3 * N, Kl, d_rmax, d_best, idx_base=idx_base, stream=s_handle)
             with torch.cuda.stream(stream):
                 return pdist.gather_best(d_best if coll_dev.type == "cuda" else d_best.cpu())
-        return ctx.best_fetch(d_best, stream=s_handle)   # pinned 16-B copy + stream sync
+        return steps[i % len(steps)]()   # poll + the 16-B result from pinned host memory
 
     for i in range(args.warmup):
         step(i)
@@ -369,10 +373,14 @@ def main():
                 "bytes_per_eval": b_eval,
                 "evals_per_launch": cands_per_launch,
                 "avg_launch_ms": avg_launch_ms,
+                "traffic_frac": (traffic / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                 if traffic and avg_launch_ms else None),
                 "timing": "in-kernel workgroup stamps (s_memrealtime) over the timed steps",
                 "note": "achieved = SURVEY 8(d) algorithmic bytes (24 B x M entries + disks) per "
                         "eval x evals per launch / launch time; the walks read only the "
-                        "entries near the disks, so frac > 1 is by design (see DESIGN.md)",
+                        "entries near the disks, so frac > 1 is by design (see DESIGN.md). "
+                        "traffic_frac = the kernel's measured HBM bytes per launch (PMC, "
+                        "profiles/pmc_traffic_config4.json) / launch time / peak",
             },
             "cpu_baseline": cpu,
             "best": {"objective": result[0], "index": result[1]},

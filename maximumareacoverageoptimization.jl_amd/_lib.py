@@ -402,6 +402,35 @@ class Context:
             _devptr(d_prev), _devptr(d_dlim), float(tan_half_fov), int(idx_base),
             _devptr(d_obj), _devptr(d_best), _devptr(stream)))
 
+    def poll_step(self, d_cands, three_n: int, K: int, d_rmax, d_best, penalty: float = 1e5,
+                  d_prev=None, d_dlim=None, tan_half_fov: float = 1.0, idx_base: int = 0,
+                  d_obj=None, stream=None):
+        """A bound device poll: returns a zero-argument callable that enqueues the poll
+        (mac_poll_best_dev_f64) and returns its (objective, index) (mac_best_fetch). The ctypes
+        arguments are built once, so a step costs two foreign calls and nothing else on the
+        host — the next poll of a MADS loop cannot start before this one's result is known."""
+        h = _vp(self._h.value if isinstance(self._h, _vp) else self._h)
+        poll_args = (h, _vp(_devptr(d_cands)), _i64(int(three_n)), _i64(int(K)),
+                     _vp(_devptr(d_rmax)), ctypes.c_double(float(penalty)),
+                     _vp(_devptr(d_prev)), _vp(_devptr(d_dlim)),
+                     ctypes.c_double(float(tan_half_fov)), _i64(int(idx_base)),
+                     _vp(_devptr(d_obj)), _vp(_devptr(d_best)), _vp(_devptr(stream)))
+        bo, bi = ctypes.c_double(), ctypes.c_int64()
+        fetch_args = (h, _vp(_devptr(d_best)), _vp(_devptr(stream)), ctypes.byref(bo),
+                      ctypes.byref(bi))
+        poll, fetch = self._L.mac_poll_best_dev_f64, self._L.mac_best_fetch
+
+        def step():
+            rc = poll(*poll_args)
+            if rc != MAC_OK:
+                _check(rc)
+            rc = fetch(*fetch_args)
+            if rc != MAC_OK:
+                _check(rc)
+            return bo.value, bi.value
+
+        return step
+
     def best_fetch(self, d_best, stream=None):
         """Wait for ``stream`` and return the (objective, index) a device poll wrote to d_best."""
         self._bo = getattr(self, "_bo", None) or (ctypes.c_double(), ctypes.c_int64())

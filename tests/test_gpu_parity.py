@@ -289,6 +289,13 @@ def test_device_pointer_api(ctx, pkg, orc):
                       stream=s.cuda_stream)
     w2 = wobj[::-1]
     assert ctx.best_fetch(tB, stream=s.cuda_stream) == (w2.min(), int(np.argmin(w2)))
+    # the bound poll step (bench.py's loop): same result, repeatable, alternating sets
+    tC2 = torch.from_numpy(C2).to(dev)
+    st1 = ctx.poll_step(tC, C.shape[1], C.shape[0], tR, tB, idx_base=100, stream=s.cuda_stream)
+    st2 = ctx.poll_step(tC2, C.shape[1], C.shape[0], tR, tB, stream=s.cuda_stream)
+    for _ in range(3):
+        assert st1() == (wobj.min(), 100 + int(np.argmin(wobj)))
+        assert st2() == (w2.min(), int(np.argmin(w2)))
 
 
 # ---------------------------------------------------------------------------- full size
