@@ -145,7 +145,10 @@ __device__ __forceinline__ void coverage_poll_body(
     // taken as n_shared + counter.
     auto shared_jobs = [&](int first) {
         __shared__ int sjob;
-        const int nsub = (K + kShC - 1) / kShC;
+        // candidates per job: 64 while the jobs fill the chip, 256 when the disks with
+        // neighbours alone would (fewer re-stagings of each region)
+        const int C = *dcount * ((K + kShC - 1) / kShC) > 2 * (int)gridDim.x ? kShCWide : kShC;
+        const int nsub = (K + C - 1) / C;
         const int total = *dcount * nsub;
         int job = first;
         for (;;) {
@@ -157,7 +160,7 @@ __device__ __forceinline__ void coverage_poll_body(
             }
             if (job >= total) break;   // uniform
             poll_shared_job(xy, w, off, g, urec, umap, region, nbrT, nboxT, rows, ncount,
-                            dlist[job / nsub], K, (job % nsub) * kShC, spart, counts);
+                            dlist[job / nsub], K, (job % nsub) * C, C, spart, counts);
             job = -1;
         }
     };

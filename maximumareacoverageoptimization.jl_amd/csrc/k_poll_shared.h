@@ -94,22 +94,25 @@ __device__ __forceinline__ bool entry_shared(int nc, const int4* nbox, int tx, i
 }
 
 // Shared-entry pass of the poll kernel (k_poll.h). A job is (disk dlist[job / nsub], candidates
-// [kb, kb + kShC), kb = (job % nsub) * kShC); the workgroup's threads are kShC candidates x kShG
-// entry groups. Shared entries are compacted (in list order) into LDS round by round; thread
-// (c, eg) decides entries eg, eg + kShG, ... of each round in fp64 for candidate kb + c (the
-// neighbour disks of the candidate preloaded — first four — or read once per entry — the rest),
-// and the kShG group sums are added in group order at the end: fixed order. Splitting the entries
-// over groups keeps a heavily overlapped disk from serialising one lane per candidate over all
-// of its shared entries. Writes spart[i*K + k] (the finalize kernel adds the rows of the disks
-// with ncount[i] > 0).
-constexpr int kShC = 64;
-constexpr int kShG = kPollThreads / kShC;
+// [kb, kb + C), kb = (job % nsub) * C), C = kShC or kShCWide (the poll kernel picks); the
+// workgroup's threads are C candidates x G = 256 / C entry groups. Shared entries are compacted (in
+// list order) into LDS round by round; thread (c, eg) decides entries eg, eg + G, ... of each
+// round in fp64 for candidate kb + c (the neighbour disks of the candidate preloaded — first four
+// — or read once per entry — the rest), and the G group sums are added in group order at the end:
+// fixed order. Splitting the entries over groups keeps a heavily overlapped disk from serialising
+// one lane per candidate over all of its shared entries; wide jobs re-stage each region fewer
+// times when many disks share entries. Writes spart[i*K + k] (the finalize kernel adds the rows of
+// the disks with ncount[i] > 0).
+constexpr int kShC = 64;                      // candidates per job when few disks share entries
+constexpr int kShCWide = kPollThreads;        // ... when many do (one entry group per job)
+constexpr int kShG = kPollThreads / kShC;     // the most entry groups
 __device__ __forceinline__ void poll_shared_job(
     const double2* __restrict__ xy, const double* __restrict__ w,
     const int32_t* __restrict__ off, const Grid& g, const DiskRec* __restrict__ urec,
     const int* __restrict__ umap, const int4* __restrict__ region, const uint16_t* __restrict__ nbrT,
     const int4* __restrict__ nboxT, const int2* __restrict__ rows,
-    const int* __restrict__ ncount, int i, int K, int kb, double* __restrict__ spart, int counts)
+    const int* __restrict__ ncount, int i, int K, int kb, int C, double* __restrict__ spart,
+    int counts)
 {
     __shared__ double2 sp[kPollThreads];
     __shared__ double sw[kPollThreads];
@@ -117,10 +120,11 @@ __device__ __forceinline__ void poll_shared_job(
     __shared__ int4 nbox[kPollNbr];
     __shared__ uint16_t nbr[kPollNbr];
     __shared__ int wcount[kPollWaves];
-    __shared__ double gsum[kShG][kShC];
+    __shared__ double gsum[kPollThreads];     // [group][candidate], C candidates x G groups
 
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
-    const int c = tid % kShC, eg = tid / kShC;
+    const int G = kPollThreads / C;
+    const int c = tid % C, eg = tid / C;
     const int k = kb + c;
     const bool valid = k < K;
 
@@ -201,7 +205,7 @@ __device__ __forceinline__ void poll_shared_job(
             }
             __syncthreads();
             if (valid && d.T >= 0.0) {
-                for (int s = eg; s < ns; s += kShG) {
+                for (int s = eg; s < ns; s += G) {
                     const double2 q = sp[s];
                     if (!(sqdist(q.x, q.y, d.cx, d.cy) <= d.T)) continue;
                     bool stolen = false;
@@ -228,12 +232,11 @@ __device__ __forceinline__ void poll_shared_job(
             __syncthreads();
         }
     }
-    gsum[eg][c] = acc;
+    gsum[eg * C + c] = acc;
     __syncthreads();
     if (eg == 0 && valid) {
         double t = 0.0;
-#pragma unroll
-        for (int q = 0; q < kShG; ++q) t += gsum[q][c];
+        for (int q = 0; q < G; ++q) t += gsum[q * C + c];
         if (counts) reinterpret_cast<unsigned*>(spart)[(int64_t)i * K + k] = (unsigned)t;
         else spart[(int64_t)i * K + k] = t;
     }
