@@ -121,6 +121,8 @@ __device__ __forceinline__ void poll_shared_job(
     __shared__ uint16_t nbr[kPollNbr];
     __shared__ int wcount[kPollWaves];
     __shared__ double gsum[kPollThreads];     // [group][candidate], C candidates x G groups
+    __shared__ int run_s[kPollThreads], run_pre[kPollThreads + 1];
+    __shared__ int nruns;
 
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
     const int G = kPollThreads / C;
@@ -156,7 +158,118 @@ __device__ __forceinline__ void poll_shared_job(
     double acc = 0.0;
     __syncthreads();
 
-    for (int rb = R.z; rb <= R.w; rb += kPollRB) {
+    // the fp64 decision of the shared entries in sp/sw[0, ns) for this thread's candidate
+    auto decide = [&](int ns) {
+        if (valid && d.T >= 0.0) {
+            for (int s = eg; s < ns; s += G) {
+                const double2 q = sp[s];
+                if (!(sqdist(q.x, q.y, d.cx, d.cy) <= d.T)) continue;
+                bool stolen = false;
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    if (m < ncl) stolen |= sqdist(q.x, q.y, e[m].cx, e[m].cy) <= e[m].T;
+                if (!stolen && nc > 4) {
+                    if (nc <= kPollNbr) {
+                        for (int m = 4; m < nc && !stolen; ++m) {
+                            const DiskRec x = rec_of(urec, umap, nbr[m], K, k);
+                            stolen = sqdist(q.x, q.y, x.cx, x.cy) <= x.T;
+                        }
+                    } else {  // overflowed list: every lower-index overlapping region
+                        for (int j = 0; j < i && !stolen; ++j) {
+                            if (!box_overlap(region[j], R)) continue;
+                            const DiskRec x = rec_of(urec, umap, j, K, k);
+                            stolen = sqdist(q.x, q.y, x.cx, x.cy) <= x.T;
+                        }
+                    }
+                }
+                if (!stolen) acc += counts ? 1.0 : sw[s];
+            }
+        }
+    };
+
+    // Fast path (regions at most 64 tiles wide and 64 rows high): the shared tiles of each row
+    // are runs of a 64-bit tile mask (the union of the neighbour boxes), and a run of tiles is a
+    // contiguous run of entries; only those entries are staged, in the same (list) order.
+    const int tw = R.y - R.x + 1;
+    bool fast = tw <= kWave && nrows <= kWave;
+    if (fast) {
+        if (tid < kWave) {
+            uint64_t mask = 0;
+            const int r = R.z + tid;
+            if (tid < nrows) {
+                const uint64_t all = tw == 64 ? ~0ull : ((1ull << tw) - 1);
+                if (nc > kPollNbr) {
+                    mask = all;   // overflowed list: every entry is decided here
+                } else {
+                    for (int m = 0; m < ncl; ++m) {
+                        const int4 Q = nbox[m];
+                        if (r < Q.z || r > Q.w) continue;
+                        const int a = max(R.x, Q.x) - R.x, b = min(R.y, Q.y) - R.x;
+                        if (a <= b)   // tiles a..b of the row
+                            mask |= (b - a == 63 ? ~0ull : ((1ull << (b - a + 1)) - 1)) << a;
+                    }
+                }
+            }
+            const uint64_t starts = mask & ~(mask << 1);
+            const int cnt = __popcll(starts);
+            const int incl = wave_incl_scan_i32(cnt, tid);
+            const int tot = __shfl(incl, kWave - 1, kWave);
+            if (tid == 0) nruns = tot;
+            if (tot <= kPollThreads) {
+                int q = incl - cnt;
+                uint64_t m2 = mask;
+                const int64_t rowbase = (int64_t)r * g.nTx + R.x;
+                while (m2) {
+                    const int a = __builtin_ctzll(m2);
+                    const uint64_t from = m2 >> a;
+                    const int len = ~from ? __builtin_ctzll(~from) : 64 - a;   // tiles in the run
+                    const int s0 = off[rowbase + a];
+                    run_s[q] = s0;
+                    run_pre[q + 1] = off[rowbase + a + len] - s0;
+                    ++q;
+                    m2 &= len + a >= 64 ? 0ull : (~0ull << (a + len));
+                }
+            }
+        }
+        __syncthreads();
+        const int nrun = nruns;
+        fast = nrun <= kPollThreads;   // uniform
+        if (fast) {
+            // exclusive prefix of the run lengths (one run per thread)
+            const int len = tid < nrun ? run_pre[tid + 1] : 0;
+            const int incl = wave_incl_scan_i32(len, lane);
+            if (lane == kWave - 1) wcount[wid] = incl;
+            __syncthreads();
+            int pre = incl - len, total = 0;
+            for (int q = 0; q < kPollWaves; ++q) {
+                if (q < wid) pre += wcount[q];
+                total += wcount[q];
+            }
+            __syncthreads();
+            if (tid < nrun) run_pre[tid] = pre;
+            if (tid == 0) run_pre[nrun] = total;
+            __syncthreads();
+            for (int base = 0; base < total; base += kPollThreads) {
+                const int n = min(kPollThreads, total - base);
+                if (tid < n) {
+                    const int f = base + tid;
+                    int lo = 0, hi = nrun - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (run_pre[mid] <= f) lo = mid; else hi = mid - 1;
+                    }
+                    const int j = run_s[lo] + (f - run_pre[lo]);
+                    sp[tid] = xy[j];
+                    sw[tid] = w[j];
+                }
+                __syncthreads();
+                decide(n);
+                __syncthreads();
+            }
+        }
+    }
+
+    for (int rb = R.z; !fast && rb <= R.w; rb += kPollRB) {
         const int nr = min(kPollRB, R.w - rb + 1);
         if (!fastrows) {
             if (tid < nr) {
@@ -204,31 +317,7 @@ __device__ __forceinline__ void poll_shared_job(
                 sw[pos] = ww;
             }
             __syncthreads();
-            if (valid && d.T >= 0.0) {
-                for (int s = eg; s < ns; s += G) {
-                    const double2 q = sp[s];
-                    if (!(sqdist(q.x, q.y, d.cx, d.cy) <= d.T)) continue;
-                    bool stolen = false;
-#pragma unroll
-                    for (int m = 0; m < 4; ++m)
-                        if (m < ncl) stolen |= sqdist(q.x, q.y, e[m].cx, e[m].cy) <= e[m].T;
-                    if (!stolen && nc > 4) {
-                        if (nc <= kPollNbr) {
-                            for (int m = 4; m < nc && !stolen; ++m) {
-                                const DiskRec x = rec_of(urec, umap, nbr[m], K, k);
-                                stolen = sqdist(q.x, q.y, x.cx, x.cy) <= x.T;
-                            }
-                        } else {  // overflowed list: every lower-index overlapping region
-                            for (int j = 0; j < i && !stolen; ++j) {
-                                if (!box_overlap(region[j], R)) continue;
-                                const DiskRec x = rec_of(urec, umap, j, K, k);
-                                stolen = sqdist(q.x, q.y, x.cx, x.cy) <= x.T;
-                            }
-                        }
-                    }
-                    if (!stolen) acc += counts ? 1.0 : sw[s];
-                }
-            }
+            decide(ns);
             __syncthreads();
         }
     }
