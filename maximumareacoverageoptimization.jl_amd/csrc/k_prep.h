@@ -95,44 +95,55 @@ struct CandSrc {
 };
 
 // cands (3N x K column-major) -> keysT (3N x K variable-major: candidates contiguous) of fp32
-// keys, key = fl32(x - x0) with x0 = the variable's value in candidate 0, through 32 x 32 LDS
+// keys, key = fl32(x - x0) with x0 = the variable's value in candidate 0, through 32 x 64 LDS
 // tiles so that both sides are coalesced. A key is exact when x0 + (double)key reproduces x bit
 // for bit (k_index.h "Keys"); kbad[v*nkt + tile] = 1 when some key of variable v in this tile is
 // not (every tile writes its flag, so nothing needs clearing). Half the bytes of a transposed
 // fp64 copy are written here and read by the index.
+constexpr int kKeysK = 64;   // candidates per cands_keys_kernel tile (x 32 variables)
+
 __global__ __launch_bounds__(kBlock) void cands_keys_kernel(const double* __restrict__ cands, int n,
                                                             int K, float* __restrict__ keysT,
                                                             int* __restrict__ kbad, int nkt)
 {
-    __shared__ float t[32][33];
-    __shared__ int sbad[32];
-    const int v0 = blockIdx.x * 32, k0 = blockIdx.y * 32;
+    __shared__ float t[kKeysK][33];
+    __shared__ int sbad[2][32];
+    const int v0 = blockIdx.x * 32, k0 = blockIdx.y * kKeysK;
     const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
-    if (threadIdx.x < 32) sbad[threadIdx.x] = 0;
+    if (threadIdx.x < 64) sbad[threadIdx.x >> 5][threadIdx.x & 31] = 0;
     const int vr = v0 + tx;
     const double base = vr < n ? cands[vr] : 0.0;
-    bool ok = true;
-    double x[4];
+    constexpr int J = kKeysK / 8;
+    double x[J];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < J; ++j) {   // every load in flight at once
         const int k = k0 + ty + 8 * j;
         x[j] = (k < K && vr < n) ? cands[(int64_t)k * n + vr] : base;
     }
+    bool ok[2] = {true, true};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < J; ++j) {
         const float f = (float)(x[j] - base);
-        ok &= __builtin_bit_cast(uint64_t, base + (double)f) == __builtin_bit_cast(uint64_t, x[j]);
+        ok[j >= J / 2] &= __builtin_bit_cast(uint64_t, base + (double)f) == __builtin_bit_cast(uint64_t, x[j]);
         t[ty + 8 * j][tx] = f;
     }
     __syncthreads();
-    if (!ok) atomicOr(&sbad[tx], 1);
+    if (!ok[0]) atomicOr(&sbad[0][tx], 1);
+    if (!ok[1]) atomicOr(&sbad[1][tx], 1);
+    // rows of kKeysK keys per variable: 64 consecutive threads write one row (256 B)
+    const int kk = threadIdx.x & (kKeysK - 1), vq = threadIdx.x / kKeysK;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int v = v0 + ty + 8 * j, k = k0 + tx;
-        if (k < K && v < n) keysT[(int64_t)v * K + k] = t[tx][ty + 8 * j];
+    for (int j = 0; j < 32 / (kBlock / kKeysK); ++j) {
+        const int vv = vq + (kBlock / kKeysK) * j;
+        const int v = v0 + vv, k = k0 + kk;
+        if (k < K && v < n) keysT[(int64_t)v * K + k] = t[kk][vv];
     }
     __syncthreads();
-    if (threadIdx.x < 32 && vr < n) kbad[(int64_t)vr * nkt + blockIdx.y] = sbad[threadIdx.x];
+    if (threadIdx.x < 64) {
+        const int h = threadIdx.x >> 5, vv = threadIdx.x & 31, v = v0 + vv;
+        const int tile = 2 * blockIdx.y + h;
+        if (v < n && tile < nkt) kbad[(int64_t)v * nkt + tile] = sbad[h][vv];
+    }
 }
 
 // cands: see CandSrc. Writes disks[k*N + i] (scan walk) and, when pen != null,

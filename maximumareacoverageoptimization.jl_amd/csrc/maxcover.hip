@@ -484,7 +484,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             const int nkt = (K + 31) / 32;
             L->keysT.reserve(sizeof(float) * (size_t)3 * N * K);
             L->kbad.reserve(sizeof(int) * (size_t)3 * N * nkt);
-            hipLaunchKernelGGL(cands_keys_kernel, dim3((3 * N + 31) / 32, nkt), dim3(kBlock), 0, s,
+            hipLaunchKernelGGL(cands_keys_kernel, dim3((3 * N + 31) / 32, (K + kKeysK - 1) / kKeysK),
+                               dim3(kBlock), 0, s,
                                src.cands, 3 * N, K, L->keysT.as<float>(), L->kbad.as<int>(), nkt);
             HCK(hipGetLastError());
             isrc.keysT = L->keysT.as<float>();
