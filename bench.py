@@ -57,6 +57,92 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
+def floor_bytes(x, y, w, cands, G):
+    """Algorithmic bytes of one poll for an exact culling evaluation: the 3N x K
+    candidate matrix read once (8 B per value), every entry inside the union over disks i of the
+    poll-wide box of disk i's footprints [min(x-r), max(x+r)] x [min(y-r), max(y+r)] read once
+    (16 B of coordinates, + 8 B of weight unless every weight is equal), and the 16-B result.
+    Entries are counted on the G x G createPOI lattice (pitch 5, (i - 1/2) * 5)."""
+    K, n3 = cands.shape
+    N = n3 // 3
+    cx, cy, r = cands[:, :N], cands[:, N:2 * N], cands[:, 2 * N:]
+    good = r > 0
+    lo_x = np.where(good, cx - r, np.inf).min(axis=0)
+    hi_x = np.where(good, cx + r, -np.inf).max(axis=0)
+    lo_y = np.where(good, cy - r, np.inf).min(axis=0)
+    hi_y = np.where(good, cy + r, -np.inf).max(axis=0)
+    mask = np.zeros((G, G), dtype=bool)
+    for i in range(N):
+        if not (lo_x[i] <= hi_x[i]):
+            continue
+        i0 = max(1, int(np.ceil(lo_x[i] / 5.0 + 0.5)))
+        i1 = min(G, int(np.floor(hi_x[i] / 5.0 + 0.5)))
+        j0 = max(1, int(np.ceil(lo_y[i] / 5.0 + 0.5)))
+        j1 = min(G, int(np.floor(hi_y[i] / 5.0 + 0.5)))
+        if i0 <= i1 and j0 <= j1:
+            mask[i0 - 1:i1, j0 - 1:j1] = True
+    E = int(mask.sum())
+    per_entry = 16 if np.all(w == w[0]) else 24
+    cand_b = 8 * n3 * K
+    return {"bytes": cand_b + per_entry * E + 16, "candidate_bytes": cand_b, "entries": E,
+            "bytes_per_entry": per_entry}
+
+
+def src_hash():
+    """sha256 over the library sources (csrc/*.hip, csrc/*.h, include/maxcover.h): stamps the
+    PMC traffic files so that a number measured on another build is never attached."""
+    import hashlib
+    h = hashlib.sha256()
+    d = os.path.join(ROOT, "maximumareacoverageoptimization.jl_amd", "csrc")
+    for name in sorted(os.listdir(d)):
+        if name.endswith((".hip", ".h")):
+            with open(os.path.join(d, name), "rb") as f:
+                h.update(name.encode() + b"\0" + f.read())
+    with open(os.path.join(ROOT, "include", "maxcover.h"), "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(config, disks, world, algo):
+    """(HBM bytes per poll chain, source note) from profiles/pmc_traffic_config{config}.json
+    when it was measured on these sources, this workload and the default walk; else (None, why)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_traffic_config{config}.json")
+    if world != 1 or algo != "auto" or disks != "uniform":
+        return None, "not profiled for this workload"
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, "no PMC file"
+    if d.get("src_sha") != src_hash():
+        return None, f"PMC file is from another build (src_sha {d.get('src_sha')})"
+    return d.get("hbm_bytes_per_poll"), os.path.relpath(path, ROOT) + f" (src_sha {d['src_sha']})"
+
+
+def usable_cpus():
+    """(threads to use, description): the CPUs this process may run on — its affinity mask,
+    capped by a cgroup CPU quota and by OMP_NUM_THREADS (the GPU pool sets it to the CPU share
+    of one GPU: the box's os.cpu_count() is the whole machine, shared with other jobs)."""
+    total = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = total
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        quota = None
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+    n = min(v for v in (aff, quota, omp) if v)
+    info = {"host_logical_cpus": total, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+            "omp_num_threads_env": omp}
+    return max(1, n), info
+
+
 def cpu_baseline(x, y, w, cands, seconds_target: float, threads: int):
     """The oracle's C restatement of calculateArea (pointer-per-entry records, same loop and
     break, -O2 no FMA) on `threads` host threads, one candidate per thread, over a bounded
@@ -124,12 +210,11 @@ def bench_config5(args, pkg, dev_index):
     if not args.no_cpu:
         x, y, w = ctx.get_points()
         polls = wl.poll_candidates(sim.x_prev, wl.SplitMix64(args.seed + 1))
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
-        threads = max(1, min(threads, 16))
+        threads, cinfo = usable_cpus()
         try:
             v, desc = cpu_baseline(x, y, w, polls, args.cpu_seconds, threads)
             cpu = {"value": v, "unit": "evals/s", "cores": threads, "kind": "port",
-                   "sample": desc + " (the final config-5 point list)"}
+                   "sample": desc + " (the final config-5 point list)", **cinfo}
         except Exception as e:  # report, never fake
             log("cpu baseline failed:", e)
     out = {
@@ -179,10 +264,17 @@ def main():
                     help="points per spatial tile of the index (library default when omitted)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the parity guard and the closure timing (profiler passes: only "
+                         "the warmup and timed polls launch kernels after set-up)")
     ap.add_argument("--seed", type=int, default=20250216)
-    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
-                    help="N>1: weak = one full poll set per GPU (P*K candidates per step); "
-                         "strong = the single poll split over the GPUs")
+    ap.add_argument("--scaling", default="strong", choices=("strong", "weak"),
+                    help="N>1: strong (default, the north star's split) = the single poll's "
+                         "candidates sharded over the GPUs; weak = one full poll set per GPU "
+                         "(P*K candidates per step, a wider poll)")
+    ap.add_argument("--disks", default="uniform", choices=("uniform", "clustered"),
+                    help="UAV disks: uniform over the domain (default) or SURVEY 8(d)'s "
+                         "clustered variant (sqrt(N)*40 m around the centre, overlapping)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL on ROCm) for the real multi-GPU run; gloo only to rehearse "
                          "N>1 with several ranks sharing one GPU (MAXCOVER_BENCH_DEVICE)")
@@ -220,7 +312,7 @@ def main():
     G, N = cfg["G"], cfg["N"]
     rng = wl.SplitMix64(args.seed)
     x, y, w = wl.grid_points(G)
-    x0 = wl.uniform_disks(N, G, rng)
+    x0 = (wl.uniform_disks if args.disks == "uniform" else wl.clustered_disks)(N, G, rng)
     if cfg["K"] == 1:
         polls = [x0[None, :].copy() for _ in range(args.polls)]
         for p in polls[1:]:
@@ -250,19 +342,29 @@ def main():
     d_polls = [torch.from_numpy(np.ascontiguousarray(p[lo:hi])).to(dev) for p in polls]
     d_rmax = torch.from_numpy(r_max).to(dev)
     d_best = torch.empty(2, dtype=torch.float64, device=dev)
+    # cons3 (src/TDM_Constraints.jl:54-75) is part of every reference poll (extreme constraints
+    # [cons1, cons3], src/TDM_STATIC_opt.jl:151-153): prev = the incumbent, d_lim = 10 m
+    # (src/FullSimulation.jl:740), FOV = 100 deg (:735)
+    tan_half = float(np.tan(100 / 180 * np.pi / 2))
+    dlim = np.full(N, 10.0)
+    d_dlim = torch.from_numpy(dlim).to(dev)
+    d_prevs = [torch.from_numpy(np.ascontiguousarray(p[0])).to(dev) for p in polls]
     stream = torch.cuda.Stream(dev)
     s_handle = stream.cuda_stream
 
     # one bound poll per candidate set: the ctypes arguments are built once (Context.poll_step)
-    steps = [ctx.poll_step(d, 3 * N, Kl, d_rmax, d_best, idx_base=idx_base, stream=s_handle)
-             for d in d_polls]
+    steps = [ctx.poll_step(d, 3 * N, Kl, d_rmax, d_best, d_prev=pv, d_dlim=d_dlim,
+                           tan_half_fov=tan_half, idx_base=idx_base, stream=s_handle)
+             for d, pv in zip(d_polls, d_prevs)]
 
     def step(i):
         """One MADS poll. It ends with the best (objective, index) on the host, because the
         next poll's candidates depend on it: polls never overlap."""
         if distributed:
             d = d_polls[i % len(d_polls)]
-            ctx.poll_best_dev(d, 3 * N, Kl, d_rmax, d_best, idx_base=idx_base, stream=s_handle)
+            ctx.poll_best_dev(d, 3 * N, Kl, d_rmax, d_best, d_prev=d_prevs[i % len(d_polls)],
+                              d_dlim=d_dlim, tan_half_fov=tan_half, idx_base=idx_base,
+                              stream=s_handle)
             with torch.cuda.stream(stream):
                 return pdist.gather_best(d_best if coll_dev.type == "cuda" else d_best.cpu())
         return steps[i % len(steps)]()   # poll + the 16-B result from pinned host memory
@@ -271,17 +373,29 @@ def main():
         step(i)
     torch.cuda.synchronize(dev)
 
-    # correctness guard on the timed workload: scan kernel vs tiled on poll 0's first entries
+    # correctness guard on the timed workload: the timed poll (this rank's shard, the device's
+    # walk choice, cons3) writes every objective; 16 sampled candidates plus its argmin are
+    # re-evaluated by the streaming scan (an independent kernel) and must agree bit for bit
     check = None
-    if rank == 0:
-        probe = polls[0][: min(8, K)]
+    if K > 1 and not args.no_extras:
+        d_obj = torch.empty(Kl, dtype=torch.float64, device=dev)
+        ctx.poll_best_dev(d_polls[0], 3 * N, Kl, d_rmax, d_best, d_prev=d_prevs[0], d_dlim=d_dlim,
+                          tan_half_fov=tan_half, idx_base=idx_base, d_obj=d_obj, stream=s_handle)
+        got_best = ctx.best_fetch(d_best, stream=s_handle)
+        torch.cuda.synchronize(dev)
+        objs = d_obj.cpu().numpy()
+        pick = np.unique(np.concatenate([
+            np.floor(wl.SplitMix64(args.seed + 7).uniform(16) * Kl).astype(np.int64),
+            [int(np.argmin(objs))]]))
         ctx.set_algo("scan")
-        a_scan = ctx.area_batch(probe)
+        _, _, o_scan = ctx.poll_best(polls[0][lo:hi][pick], r_max, 1e5, prev=polls[0][0],
+                                     d_lim=dlim, tan_half_fov=tan_half, want_all=True)
         ctx.set_algo(args.algo)
-        a_main = ctx.area_batch(probe)
-        check = bool(np.array_equal(a_scan, a_main))
+        kmin = int(np.argmin(objs))
+        check = bool(np.array_equal(o_scan, objs[pick]) and got_best[1] == idx_base + kmin
+                     and got_best[0] == objs[kmin])
         if not check:
-            log("WARNING: scan/tiled disagree on the probe candidates", a_scan, a_main)
+            log("WARNING: timed poll vs scan disagree", pick, o_scan, objs[pick], got_best)
 
     ctx.profile(True)
     ctx.profile_read(reset=True)
@@ -296,6 +410,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    split = ctx.profile_split()
     k_ms, k_launches, k_cands, k_walk = ctx.profile_read(reset=True)
     ctx.profile(False)
     if distributed:
@@ -310,31 +425,42 @@ def main():
     value = total_evals / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
-    # roofline of the dominant kernel (this rank's launches; SURVEY §8(d) algorithmic bytes)
-    s = 8  # fp64
-    b_eval = 3 * M * s + 3 * N * s + 8
+    # roofline. The unit is one poll's device chain (the fused poll: launch 1 +
+    # launch 2; the legacy chain: its coverage kernel), timed live by in-kernel workgroup stamps
+    # over the timed steps. Its algorithmic floor is what any exact culling evaluation must move:
+    # the candidate matrix read once, every entry that lies in some disk's poll-wide footprint
+    # box read once (xy, 16 B; w only when the weights differ), and the 16-B result.
     avg_launch_ms = k_ms / max(k_launches, 1)
     cands_per_launch = k_cands / max(k_launches, 1)
-    achieved = b_eval * cands_per_launch / (avg_launch_ms * 1e-3) / 1e9 if k_launches else None
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_config{args.config}.json")
-    if world == 1 and args.algo == "auto" and os.path.exists(pmc_path):  # the profiled launch
-        try:
-            with open(pmc_path) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    floor = floor_bytes(x, y, w, polls[0][lo:hi], G)
+    achieved = floor["bytes"] / (avg_launch_ms * 1e-3) / 1e9 if k_launches else None
+    b_eval = 3 * M * 8 + 3 * N * 8 + 8     # a brute-force scan per candidate
+    traffic, traffic_src = pmc_traffic(args.config, args.disks, world, args.algo)
+
+    # the single-candidate closure path (src/TDM_STATIC_opt.jl:125: DirectSearch calls the
+    # objective once per trial point): host-pointer mac_area_f64 latency on the timed workload
+    closure = None
+    if rank == 0 and not args.no_extras:
+        c0 = np.ascontiguousarray(polls[0][min(1, K - 1)])
+        for _ in range(20):
+            ctx.area(c0)
+        n_cl = 300
+        t_cl = time.perf_counter()
+        for _ in range(n_cl):
+            a_cl = ctx.area(c0)
+        closure = {"mac_area_f64_us": (time.perf_counter() - t_cl) / n_cl * 1e6, "calls": n_cl,
+                   "area": a_cl, "note": "host candidate in, host double out: copy-in, the walk, "
+                   "copy-out, synchronous (what a Julia ccall per trial point costs)"}
 
     out = None
     if rank == 0:
         cpu = None
         if not args.no_cpu and world == 1:
-            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
-            threads = max(1, min(threads, 16))
+            threads, cinfo = usable_cpus()
             try:
                 v, desc = cpu_baseline(x, y, w, polls[0], args.cpu_seconds, threads)
                 cpu = {"value": v, "unit": "evals/s", "cores": threads, "kind": "port",
-                       "sample": desc}
+                       "sample": desc, **cinfo}
             except Exception as e:  # report, never fake
                 log("cpu baseline failed:", e)
         out = {
@@ -355,7 +481,9 @@ def main():
                 "uavs": N, "cells": M, "grid": f"{G}x{G} @ 5 m", "candidates_per_poll": K,
                 "candidates_per_step": K_step,
                 "poll": "incumbent + 2n LTMADS directions (n=3N), l=2, delta=1",
-                "disks": "integer centres uniform over the domain, R=36",
+                "disks": ("integer centres uniform over the domain, R=36" if args.disks == "uniform"
+                          else "clustered: integer centres within sqrt(N)*40 m of the centre, R=36"),
+                "cons3": "prev = incumbent, d_lim = 10 m, FOV 100 deg (every candidate checked)",
                 "parallelism": (f"{world} GPU(s), one full poll set each, 16-B argmin all-gather"
                                 if args.scaling == "weak" else
                                 f"one poll's candidates sharded over {world} GPU(s), "
@@ -369,22 +497,32 @@ def main():
                 "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "traffic": traffic,
-                "kernel": f"coverage_{k_walk}_kernel",
-                "bytes_per_eval": b_eval,
-                "evals_per_launch": cands_per_launch,
+                "kernel": ("fused poll chain: fused_prep_kernel + fused_walk_kernel"
+                           if k_walk == "fused" else f"coverage_{k_walk}_kernel"),
                 "avg_launch_ms": avg_launch_ms,
+                "evals_per_launch": cands_per_launch,
+                "split_ms_per_poll": ({"prep": split[0] / split[3], "walk": split[1] / split[3],
+                                       "gap": split[2] / split[3]} if split[3] else None),
+                "floor": floor,
+                "traffic_source": traffic_src,
                 "traffic_frac": (traffic / (avg_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
                                  if traffic and avg_launch_ms else None),
+                "brute_force_equiv": {
+                    "bytes_per_eval": b_eval,
+                    "achieved": b_eval * cands_per_launch / (avg_launch_ms * 1e-3) / 1e9
+                    if k_launches else None,
+                    "note": "SURVEY 8(d)'s full-scan bytes per evaluation: what a brute-force "
+                            "scan would have to stream, not a roofline of this algorithm"},
                 "timing": "in-kernel workgroup stamps (s_memrealtime) over the timed steps",
-                "note": "achieved = SURVEY 8(d) algorithmic bytes (24 B x M entries + disks) per "
-                        "eval x evals per launch / launch time; the walks read only the "
-                        "entries near the disks, so frac > 1 is by design (see DESIGN.md). "
-                        "traffic_frac = the kernel's measured HBM bytes per launch (PMC, "
-                        "profiles/pmc_traffic_config4.json) / launch time / peak",
+                "note": "achieved = floor.bytes / chain time (first workgroup start of launch 1 to "
+                        "last workgroup end of launch 2); traffic = PMC-measured HBM bytes of "
+                        "the same chain per poll, attached only when the kernel sources hash "
+                        "to the profiled build",
             },
             "cpu_baseline": cpu,
+            "closure": closure,
             "best": {"objective": result[0], "index": result[1]},
-            "check_scan_vs_main": check,
+            "check_timed_poll_vs_scan": check,
             "setup_s": t_set,
         }
         print(json.dumps(out), flush=True)

@@ -62,7 +62,11 @@ extern "C" {
 #define MAC_ALGO_SCAN   1  /* streaming brute-force scan: every point against every disk     */
 #define MAC_ALGO_TILED  2  /* per-candidate walk over the tile-binned point list (exact culling) */
 #define MAC_ALGO_POLL   3  /* per-disk walk over the whole poll: region entries staged in LDS,
-                              one candidate per lane (AUTO picks it on the device when cheaper) */
+                              one candidate per lane (the six-launch chain; weighted lists) */
+#define MAC_ALGO_FUSED  4  /* the two-launch poll for lists whose entries all weigh the same (every
+                              reference input): disk index + walk + ownership + objective + argmin
+                              (k_fused.h). AUTO takes it whenever the weights are equal; weighted
+                              lists fall back to the AUTO choice of the other walks */
 
 #define MAC_STORE_F64   0
 #define MAC_STORE_F32   1
@@ -185,6 +189,13 @@ int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* b
  * none); reset != 0 clears the record. */
 int32_t mac_profile_read(mac_ctx* ctx, double* kernel_ms, int64_t* launches,
                          int64_t* candidates, int32_t* last_algo, int32_t reset);
+
+/* Per-launch split of the fused polls recorded since the last reset (call before
+ * mac_profile_read with reset): summed in-kernel spans of launch 1 (keys, penalty chains,
+ * neighbour lists) and launch 2 (walk, shared entries, objective, argmin), the summed idle gap
+ * between them, and the number of fused polls. */
+int32_t mac_profile_split(mac_ctx* ctx, double* prep_ms, double* walk_ms, double* gap_ms,
+                          int64_t* polls);
 
 /* ---- fire generator (src/DynamicArea.jl, config 5) ------------------------------ */
 /* Cellular-automaton forest fire on an nx x ny grid of dx x dy cells, cell (i, j) 1-based with

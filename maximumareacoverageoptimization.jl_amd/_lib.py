@@ -32,11 +32,12 @@ MAC_ALGO_AUTO = 0
 MAC_ALGO_SCAN = 1
 MAC_ALGO_TILED = 2
 MAC_ALGO_POLL = 3
+MAC_ALGO_FUSED = 4
 MAC_STORE_F64 = 0
 MAC_STORE_F32 = 1
 
 ALGOS = {"auto": MAC_ALGO_AUTO, "scan": MAC_ALGO_SCAN, "tiled": MAC_ALGO_TILED,
-         "poll": MAC_ALGO_POLL}
+         "poll": MAC_ALGO_POLL, "fused": MAC_ALGO_FUSED}
 
 # Every symbol include/maxcover.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -46,6 +47,7 @@ EXPORTS = (
     "mac_remove_covered_f64", "mac_covered_flags_f64", "mac_area_f64", "mac_area_batch_f64",
     "mac_objective_batch_f64", "mac_poll_best_f64", "mac_area_batch_dev_f64",
     "mac_poll_best_dev_f64", "mac_best_fetch", "mac_cover_threshold", "mac_profile_read",
+    "mac_profile_split",
     "mac_append_points_f64", "mac_append_points_dev_f64", "mac_mads_run",
     "mac_fire_last_error", "mac_fire_thresholds", "mac_fire_create", "mac_fire_destroy",
     "mac_fire_initial_points", "mac_fire_step", "mac_fire_last_points", "mac_fire_get_grid",
@@ -127,6 +129,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mac_best_fetch": ([_vp, _vp, _vp, _dp, _i64p], _i32),
         "mac_cover_threshold": ([ctypes.c_double], ctypes.c_double),
         "mac_profile_read": ([_vp, _dp, _i64p, _i64p, ctypes.POINTER(_i32), _i32], _i32),
+        "mac_profile_split": ([_vp, _dp, _dp, _dp, _i64p], _i32),
         "mac_append_points_f64": ([_vp, _dp, _dp, _dp, _i64], _i32),
         "mac_mads_run": ([_vp, _dp, _i64, _dp, ctypes.c_double, _dp, _dp, ctypes.c_double,
                           ctypes.POINTER(MadsParams), _dp, ctypes.POINTER(MadsStats)], _i32),
@@ -258,8 +261,18 @@ class Context:
         a = _i32()
         _check(self._L.mac_profile_read(self._h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(k),
                                         ctypes.byref(a), 1 if reset else 0))
-        name = {MAC_ALGO_SCAN: "scan", MAC_ALGO_TILED: "tiled", MAC_ALGO_POLL: "poll"}.get(a.value)
+        name = {MAC_ALGO_SCAN: "scan", MAC_ALGO_TILED: "tiled", MAC_ALGO_POLL: "poll",
+                MAC_ALGO_FUSED: "fused"}.get(a.value)
         return ms.value, int(n.value), int(k.value), name
+
+    def profile_split(self):
+        """Fused polls since the last reset: (launch-1 ms, launch-2 ms, gap ms, polls), summed.
+        Call before profile_read(reset=True)."""
+        p1, p2, gap = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        n = _i64()
+        _check(self._L.mac_profile_split(self._h, ctypes.byref(p1), ctypes.byref(p2),
+                                         ctypes.byref(gap), ctypes.byref(n)))
+        return p1.value, p2.value, gap.value, int(n.value)
 
     # -- point list
     def set_points(self, x, y, w) -> None:

@@ -34,3 +34,4 @@
 #include "k_poll.h"
 #include "k_final.h"
 #include "k_setup.h"
+#include "k_fused.h"

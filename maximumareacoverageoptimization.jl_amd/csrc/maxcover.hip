@@ -82,6 +82,13 @@ struct DevBuf {
         HCK(hipMalloc(&p, b));
         cap = b;
     }
+    // reserve(); true when the buffer was (re)allocated (its contents are then undefined)
+    bool grow(size_t bytes)
+    {
+        if (bytes <= cap) return false;
+        reserve(bytes);
+        return true;
+    }
     void release()
     {
         if (p) (void)hipFree(p);
@@ -121,7 +128,12 @@ struct Lane {
     hipEvent_t done = nullptr;
     DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode, pen, nbr,
         ncount, dlist, spart, vp, xinc, perm, ucount, umap, keysT, kbad, lane4, lanexp, rows, nboxT,
-        cnt;
+        cnt, dlimraw;
+    // the fused equal-weight poll (k_fused.h): keys, regions (generation-tagged), chains, counts,
+    // neighbour lists, hand-off counters
+    DevBuf f_keys, f_kbad, f_rlo, f_rhi, f_spanA, f_vp, f_cnt, f_region, f_nbr, f_nboxT, f_ncount,
+        f_dlist, f_ctl;
+    uint32_t gen = 0;
     std::vector<double> h_dlim;
     PinnedBuf h_stage;                         // native MADS driver: best, permutations, incumbent
 };
@@ -146,6 +158,8 @@ struct mac_ctx {
     // In-kernel launch timing (k_common.h ts_begin / ts_end): each profiled walk launch takes
     // nwg consecutive {start, end} slots of `stamps`. a: the scan / tiled launch, b: the poll
     // launch when the device picks the walk (mode != null): the launch that ran is read.
+    // fused polls: a = launch 1, b = launch 2, mode = null, algo = MAC_ALGO_FUSED (the span is
+    // taken over both launches)
     struct Prof { int64_t a, na, b, nb; int64_t K; const int* mode; int algo; };
     std::vector<Prof> prof;                          // recorded launches (guarded by mu)
     DevBuf stamps;
@@ -377,14 +391,124 @@ static bool use_tiled(mac_ctx* ctx, int N, const double* h_cands, int64_t three_
     return visits < 0.5 * (double)ctx->M * (double)N;
 }
 
+// The fused equal-weight poll (k_fused.h) runs for AUTO and FUSED whenever every entry weighs
+// the same (all reference inputs); weighted lists and the forced walks take the legacy chain.
+static bool use_fused(const mac_ctx* ctx, int N, int64_t K)
+{
+    return (ctx->algo == MAC_ALGO_AUTO || ctx->algo == MAC_ALGO_FUSED) && ctx->w_uniform &&
+           ctx->M > 0 && N > 0 && K > 0;
+}
+
+// Two launches (k_fused.h): fused_prep_kernel, fused_walk_kernel. d_dlim: raw d_lim per UAV.
+static void enqueue_fused(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& src, int N, int K,
+                          const double* d_rmax, double penalty, const double* d_prev,
+                          const double* d_dlim, double tan_half_fov, double* d_area, double* d_obj,
+                          double* d_best, int64_t idx_base, double* d_mirror, uint64_t mirror_seq)
+{
+    FusedArgs a{};
+    a.src = src;
+    a.N = N;
+    a.K = K;
+    a.ndt = (N + kFD - 1) / kFD;
+    a.nct = (K + kFC - 1) / kFC;
+    a.Kp = a.nct * kFC;
+    const bool objective = d_obj != nullptr || d_best != nullptr;
+    a.n_chain = objective ? (K + kChainC - 1) / kChainC : 0;
+    a.n_shared = kSharedWG;
+    a.g = ctx->grid;
+    a.rmax = objective ? d_rmax : nullptr;
+    a.prev = objective ? d_prev : nullptr;
+    a.dlim = d_dlim;
+    a.tan_half_fov = tan_half_fov;
+    a.penalty = penalty;
+    a.w0 = ctx->w0;
+    const size_t n = (size_t)N;
+    L->f_keys.reserve(sizeof(int16_t) * 3 * n * (size_t)a.Kp);
+    L->f_kbad.reserve(n * (size_t)a.nct);
+    bool fresh = L->f_rlo.grow(sizeof(unsigned long long) * 2 * n);
+    fresh |= L->f_rhi.grow(sizeof(unsigned long long) * 2 * n);
+    L->f_spanA.reserve(sizeof(double) * (size_t)a.ndt * a.nct);
+    L->f_vp.reserve(sizeof(double) * (size_t)K);
+    L->f_cnt.reserve(sizeof(unsigned) * (size_t)K);
+    L->f_region.reserve(sizeof(int4) * n);
+    L->f_nbr.reserve(sizeof(uint16_t) * n * kPollNbr);
+    L->f_nboxT.reserve(sizeof(int4) * n * kPollNbr);
+    L->f_ncount.reserve(sizeof(int) * n);
+    L->f_dlist.reserve(sizeof(int) * n);
+    const bool fresh_ctl = L->f_ctl.grow(sizeof(int) * kCtlWords);
+    if (++L->gen == 0) {   // 2^32 polls: restart the tags
+        L->gen = 1;
+        fresh = true;
+    }
+    if (fresh) {   // no tag of these words may look current: lo words +inf, hi words 0
+        HCK(hipMemsetAsync(L->f_rlo.p, 0xff, L->f_rlo.cap, s));
+        HCK(hipMemsetAsync(L->f_rhi.p, 0x00, L->f_rhi.cap, s));
+    }
+    if (fresh_ctl) HCK(hipMemsetAsync(L->f_ctl.p, 0, L->f_ctl.cap, s));
+    a.gen = L->gen;
+    a.keys = L->f_keys.as<int16_t>();
+    a.kbad = L->f_kbad.as<uint8_t>();
+    a.rlo = L->f_rlo.as<unsigned long long>();
+    a.rhi = L->f_rhi.as<unsigned long long>();
+    a.spanA = L->f_spanA.as<double>();
+    a.vp = L->f_vp.as<double>();
+    a.cnt = L->f_cnt.as<unsigned>();
+    a.region = L->f_region.as<int4>();
+    a.nbr = L->f_nbr.as<uint16_t>();
+    a.nboxT = L->f_nboxT.as<int4>();
+    a.ncount = L->f_ncount.as<int>();
+    a.dlist = L->f_dlist.as<int>();
+    a.ctl = L->f_ctl.as<int>();
+    a.xy = ctx->xys.as<double2>();
+    a.off = ctx->off.as<int32_t>();
+    a.area_out = d_area;
+    a.obj_out = d_obj;
+    a.best = d_best;
+    a.mirror = d_mirror;
+    a.seq = mirror_seq;
+    a.idx_base = idx_base;
+
+    const unsigned n1 = (unsigned)(a.n_chain + a.ndt * a.nct);
+    const unsigned n2 = (unsigned)(N + a.n_shared);
+    int64_t ts_a = -1, ts_na = 0, ts_b = -1, ts_nb = 0;
+    uint64_t* ts1 = nullptr;
+    uint64_t* ts2 = nullptr;
+    if (ctx->profile) {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        if (ctx->stamp_used + n1 + n2 <= ctx->stamp_cap) {
+            ts_a = ctx->stamp_used;
+            ts_na = n1;
+            ts_b = ts_a + n1;
+            ts_nb = n2;
+            ctx->stamp_used += n1 + n2;
+            ts1 = ctx->stamps.as<uint64_t>() + 2 * ts_a;
+            ts2 = ctx->stamps.as<uint64_t>() + 2 * ts_b;
+        }
+    }
+    hipLaunchKernelGGL(fused_prep_kernel, dim3(n1), dim3(kBlock), 0, s, ts1, a);
+    HCK(hipGetLastError());
+    hipLaunchKernelGGL(fused_walk_kernel, dim3(n2), dim3(kPollThreads), 0, s, ts2, a);
+    HCK(hipGetLastError());
+    if (ts1) {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        ctx->prof.push_back({ts_a, ts_na, ts_b, ts_nb, (int64_t)K, nullptr, MAC_ALGO_FUSED});
+    }
+}
+
 // Enqueue disk prep + coverage + finalize (+ argmin) on stream s. All pointers device.
 // area_out/obj_out may be null; best may be null.
+// d_dlimT: cons3 thresholds per UAV (legacy chain); d_dlim_raw: the raw d_lim (fused poll).
 static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& src, int N,
                          int K, bool tiled, const double* d_rmax, double penalty,
-                         const double* d_prev, const double* d_dlimT, double tan_half_fov,
-                         double* d_area, double* d_obj, double* d_best, int64_t idx_base,
-                         double* d_mirror = nullptr, uint64_t mirror_seq = 0)
+                         const double* d_prev, const double* d_dlimT, const double* d_dlim_raw,
+                         double tan_half_fov, double* d_area, double* d_obj, double* d_best,
+                         int64_t idx_base, double* d_mirror = nullptr, uint64_t mirror_seq = 0)
 {
+    if (use_fused(ctx, N, K)) {
+        enqueue_fused(ctx, L, s, src, N, K, d_rmax, penalty, d_prev, d_dlim_raw, tan_half_fov,
+                      d_area, d_obj, d_best, idx_base, d_mirror, mirror_seq);
+        return;
+    }
     const int64_t M = ctx->M;
     int n_poll = N, n_other = 1;
     const int* d_mode = nullptr;
@@ -638,17 +762,20 @@ static int32_t host_eval(mac_ctx* ctx, const double* cands, int64_t three_n, int
         if (!d_lim) return fail(MAC_E_INVAL, "prev given without d_lim");
         L->prev.reserve(sizeof(double) * three_n);
         L->dlim.reserve(sizeof(double) * N);
+        L->dlimraw.reserve(sizeof(double) * N);
         L->h_dlim.resize(N);
         for (int i = 0; i < N; ++i) L->h_dlim[i] = dlim_threshold(d_lim[i]);
         HCK(hipMemcpyAsync(L->prev.p, prev, sizeof(double) * three_n, hipMemcpyHostToDevice, s));
         HCK(hipMemcpyAsync(L->dlim.p, L->h_dlim.data(), sizeof(double) * N, hipMemcpyHostToDevice,
                            s));
+        HCK(hipMemcpyAsync(L->dlimraw.p, d_lim, sizeof(double) * N, hipMemcpyHostToDevice, s));
         d_prev = L->prev.as<double>();
         d_dlimT = L->dlim.as<double>();
     }
     const bool tiled = use_tiled(ctx, N, cands, three_n);
     enqueue_eval(ctx, L, s, matrix_src(L->cands.as<double>(), N), N, (int)K, tiled, d_rmax, penalty, d_prev,
-                 d_dlimT, tan_half_fov, L->area.as<double>(), want_obj ? L->obj.as<double>() : nullptr,
+                 d_dlimT, d_prev ? L->dlimraw.as<double>() : nullptr, tan_half_fov, L->area.as<double>(),
+                 want_obj ? L->obj.as<double>() : nullptr,
                  (best_obj || best_idx) ? L->best.as<double>() : nullptr, 0);
     if (area_out)
         HCK(hipMemcpyAsync(area_out, L->area.p, sizeof(double) * K, hipMemcpyDeviceToHost, s));
@@ -683,6 +810,20 @@ int32_t mac_diag_walk_read(uint64_t* out, int64_t n)
     if (n > (int64_t)(8 * 65536)) n = 8 * 65536;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_walk), sizeof(uint64_t) * n, 0,
                             hipMemcpyDeviceToHost) != hipSuccess)
+        return MAC_E_HIP;
+    return MAC_OK;
+}
+
+// diagnostic build only: the raw profiling stamps ({start, end} per workgroup slot, in launch
+// order) and how many slots are used
+int32_t mac_diag_stamps(mac_ctx* ctx, uint64_t* out, int64_t n, int64_t* used)
+{
+    if (!ctx) return MAC_E_INVAL;
+    if (hipDeviceSynchronize() != hipSuccess) return MAC_E_HIP;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    *used = ctx->stamp_used;
+    n = std::min<int64_t>(n, 2 * ctx->stamp_used);
+    if (n > 0 && hipMemcpy(out, ctx->stamps.p, sizeof(uint64_t) * n, hipMemcpyDeviceToHost) != hipSuccess)
         return MAC_E_HIP;
     return MAC_OK;
 }
@@ -727,6 +868,17 @@ int32_t mac_profile_read(mac_ctx* ctx, double* kernel_ms, int64_t* launches,
     };
     for (auto& p : ctx->prof) {
         algo = p.algo;
+        if (p.algo == MAC_ALGO_FUSED) {   // the chain: first start of launch 1 .. last end of launch 2
+            uint64_t t0 = ~(uint64_t)0, t1 = 0;
+            for (int64_t q = p.a; q < p.b + p.nb; ++q) {
+                t0 = std::min(t0, st[(size_t)(2 * q)]);
+                t1 = std::max(t1, st[(size_t)(2 * q + 1)]);
+            }
+            ms += t1 > t0 ? (double)(t1 - t0) / kRealtimeHz * 1e3 : 0.0;
+            ++n;
+            kc += p.K;
+            continue;
+        }
         int64_t a = p.a, na = p.na;
         if (p.mode) {  // the device's choice (the lane's mode word holds its latest decision)
             int m = 0;
@@ -751,6 +903,43 @@ int32_t mac_profile_read(mac_ctx* ctx, double* kernel_ms, int64_t* launches,
         if (ctx->stamp_used) HCK(hipMemset(ctx->stamps.p, 0, sizeof(uint64_t) * 2 * ctx->stamp_used));
         ctx->stamp_used = 0;
     }
+    return MAC_OK;
+    ABI_END
+}
+
+int32_t mac_profile_split(mac_ctx* ctx, double* prep_ms, double* walk_ms, double* gap_ms,
+                          int64_t* polls)
+{
+    ABI_BEGIN
+    if (!ctx) return fail(MAC_E_INVAL, "null context");
+    set_device(ctx);
+    HCK(hipDeviceSynchronize());
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::vector<uint64_t> st((size_t)(2 * ctx->stamp_used));
+    if (!st.empty())
+        HCK(hipMemcpy(st.data(), ctx->stamps.p, sizeof(uint64_t) * st.size(), hipMemcpyDeviceToHost));
+    double a1 = 0.0, a2 = 0.0, gap = 0.0;
+    int64_t n = 0;
+    for (auto& p : ctx->prof) {
+        if (p.algo != MAC_ALGO_FUSED) continue;
+        uint64_t s1 = ~(uint64_t)0, e1 = 0, s2 = ~(uint64_t)0, e2 = 0;
+        for (int64_t q = p.a; q < p.a + p.na; ++q) {
+            s1 = std::min(s1, st[(size_t)(2 * q)]);
+            e1 = std::max(e1, st[(size_t)(2 * q + 1)]);
+        }
+        for (int64_t q = p.b; q < p.b + p.nb; ++q) {
+            s2 = std::min(s2, st[(size_t)(2 * q)]);
+            e2 = std::max(e2, st[(size_t)(2 * q + 1)]);
+        }
+        if (e1 > s1) a1 += (double)(e1 - s1) / kRealtimeHz * 1e3;
+        if (e2 > s2) a2 += (double)(e2 - s2) / kRealtimeHz * 1e3;
+        if (s2 > e1 && e1 > 0) gap += (double)(s2 - e1) / kRealtimeHz * 1e3;
+        ++n;
+    }
+    if (prep_ms) *prep_ms = a1;
+    if (walk_ms) *walk_ms = a2;
+    if (gap_ms) *gap_ms = gap;
+    if (polls) *polls = n;
     return MAC_OK;
     ABI_END
 }
@@ -801,7 +990,9 @@ void mac_ctx_destroy(mac_ctx* ctx)
                           &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->pen, &l->nbr,
                           &l->ncount, &l->dlist, &l->spart, &l->vp, &l->xinc,
                           &l->perm, &l->ucount, &l->umap, &l->keysT, &l->kbad, &l->lane4,
-                          &l->lanexp, &l->rows, &l->nboxT, &l->cnt})
+                          &l->lanexp, &l->rows, &l->nboxT, &l->cnt, &l->dlimraw, &l->f_keys,
+                          &l->f_kbad, &l->f_rlo, &l->f_rhi, &l->f_spanA, &l->f_vp, &l->f_cnt,
+                          &l->f_region, &l->f_nbr, &l->f_nboxT, &l->f_ncount, &l->f_dlist, &l->f_ctl})
             b->release();
         if (l->done) (void)hipEventDestroy(l->done);
         if (l->stream) (void)hipStreamDestroy(l->stream);
@@ -823,7 +1014,7 @@ int32_t mac_set_option(mac_ctx* ctx, int32_t option, int64_t value)
     if (!ctx) return fail(MAC_E_INVAL, "null context");
     switch (option) {
     case MAC_OPT_ALGO:
-        if (value < MAC_ALGO_AUTO || value > MAC_ALGO_POLL) return fail(MAC_E_INVAL, "bad algo");
+        if (value < MAC_ALGO_AUTO || value > MAC_ALGO_FUSED) return fail(MAC_E_INVAL, "bad algo");
         ctx->algo = (int)value;
         return MAC_OK;
     case MAC_OPT_STORAGE:
@@ -1177,10 +1368,12 @@ int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const doub
     if (prev) {
         L->prev.reserve(sizeof(double) * three_n);
         L->dlim.reserve(sizeof(double) * N);
+        L->dlimraw.reserve(sizeof(double) * N);
         L->h_dlim.resize(N);
         for (int i = 0; i < N; ++i) L->h_dlim[i] = dlim_threshold(d_lim[i]);
         HCK(hipMemcpyAsync(L->prev.p, prev, sizeof(double) * three_n, hipMemcpyHostToDevice, s));
         HCK(hipMemcpyAsync(L->dlim.p, L->h_dlim.data(), sizeof(double) * N, hipMemcpyHostToDevice, s));
+        HCK(hipMemcpyAsync(L->dlimraw.p, d_lim, sizeof(double) * N, hipMemcpyHostToDevice, s));
         d_prev = L->prev.as<double>();
         d_dlimT = L->dlim.as<double>();
     }
@@ -1192,8 +1385,8 @@ int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const doub
     int* hperm = (int*)(hx + three_n);
     auto best_of = [&](const CandSrc& src, int Kc) {
         enqueue_eval(ctx, L, s, src, N, Kc, use_tiled(ctx, N, nullptr, three_n), L->rmax.as<double>(),
-                     penalty, d_prev, d_dlimT, tan_half_fov, L->area.as<double>(), L->obj.as<double>(),
-                     L->best.as<double>(), 0);
+                     penalty, d_prev, d_dlimT, d_prev ? L->dlimraw.as<double>() : nullptr, tan_half_fov,
+                     L->area.as<double>(), L->obj.as<double>(), L->best.as<double>(), 0);
         HCK(hipMemcpyAsync(hb, L->best.p, 16, hipMemcpyDeviceToHost, s));
     };
     // f(x0): the objective, +inf when x0 itself violates cons3 (mads: obj(x) if feasible(x))
@@ -1336,7 +1529,7 @@ int32_t mac_area_batch_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t thre
     LaneGuard lg(ctx, s);
     const int N = (int)(three_n / 3);
     enqueue_eval(ctx, lg.lane, s, matrix_src(d_cands, N), N, (int)K, use_tiled(ctx, N, nullptr, three_n), nullptr,
-                 0.0, nullptr, nullptr, 1.0, d_area, nullptr, nullptr, 0);
+                 0.0, nullptr, nullptr, nullptr, 1.0, d_area, nullptr, nullptr, 0);
     return MAC_OK;
     ABI_END
 }
@@ -1368,8 +1561,8 @@ int32_t mac_poll_best_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three
         return MAC_OK;
     }
     double* d_dlimT = nullptr;
-    if (d_prev) {
-        if (!d_dlim) return fail(MAC_E_INVAL, "d_prev given without d_dlim");
+    if (d_prev && !d_dlim) return fail(MAC_E_INVAL, "d_prev given without d_dlim");
+    if (d_prev && !use_fused(ctx, N, K)) {   // the legacy chain takes thresholds
         L->dlim.reserve(sizeof(double) * std::max(N, 1));
         hipLaunchKernelGGL(dlim_threshold_kernel, dim3(grid1d(std::max(N, 1), 256)), dim3(256), 0,
                            s, d_dlim, N, L->dlim.as<double>());
@@ -1397,7 +1590,7 @@ int32_t mac_poll_best_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three
         ctx->mirror_for = d_best;
     }
     enqueue_eval(ctx, L, s, matrix_src(d_cands, N), N, (int)K, use_tiled(ctx, N, nullptr, three_n), d_rmax,
-                 penalty, d_prev, d_dlimT, tan_half_fov, nullptr, d_o, (double*)d_best, idx_base,
+                 penalty, d_prev, d_dlimT, d_dlim, tan_half_fov, nullptr, d_o, (double*)d_best, idx_base,
                  d_mirror, seq);
     return MAC_OK;
     ABI_END

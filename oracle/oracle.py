@@ -90,6 +90,14 @@ def lib() -> ctypes.CDLL:
                                     ctypes.c_double, ctypes.c_uint64, ctypes.c_uint64, _dp,
                                     ctypes.c_int64]
         L.ref_fire_step.restype = ctypes.c_int64
+        L.ref_lattice_count_batch.argtypes = [_dp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                              ctypes.c_int64, _i64p, ctypes.c_int]
+        L.ref_lattice_count_batch.restype = ctypes.c_int
+        L.ref_violation_batch.argtypes = [_dp, ctypes.c_int64, ctypes.c_int64, _dp, _dp]
+        L.ref_violation_batch.restype = None
+        L.ref_cons3_batch.argtypes = [_dp, _dp, ctypes.c_int64, ctypes.c_int64, _dp, ctypes.c_double,
+                                      ctypes.POINTER(ctypes.c_uint8)]
+        L.ref_cons3_batch.restype = None
         _LIB = L
     return _LIB
 
@@ -292,6 +300,39 @@ def exact_threshold(r: float) -> float:
     if math.isinf(t):
         t = float(np.finfo(np.float64).max)
     return t
+
+
+def lattice_count_batch(cands, G: int, pitch: int = 5, nthreads: int = 0) -> np.ndarray:
+    """lattice_count for every row of cands (K x 3N integer-valued disks) on the G x G lattice of
+    pitch `pitch`: the exact number of covered entries (C, ref_lattice_count_batch, OpenMP)."""
+    c = _f64(np.atleast_2d(cands))
+    out = np.zeros(c.shape[0], dtype=np.int64)
+    rc = lib().ref_lattice_count_batch(_p(c), c.shape[1], c.shape[0], int(G), int(pitch),
+                                       out.ctypes.data_as(_i64p), int(nthreads))
+    if rc == 2:
+        raise InexactError("three_n not a multiple of 3")
+    if rc != 0:
+        raise MemoryError("ref_lattice_count_batch: mask allocation failed")
+    return out
+
+
+def violation_batch(cands, r_max) -> np.ndarray:
+    """sum_i |x[2N+i] - r_max[i]| per row, accumulated sequentially (src/TDM_STATIC_opt.jl:89-93)."""
+    c = _f64(np.atleast_2d(cands))
+    rm = _f64(r_max)
+    out = np.zeros(c.shape[0])
+    lib().ref_violation_batch(_p(c), c.shape[1], c.shape[0], _p(rm), _p(out))
+    return out
+
+
+def cons3_batch(prev, cands, d_lim, tan_half_fov: float) -> np.ndarray:
+    """ref_cons3 per row (src/TDM_Constraints.jl:54-75): True = feasible."""
+    c = _f64(np.atleast_2d(cands))
+    pv, dl = _f64(prev), _f64(d_lim)
+    out = np.zeros(c.shape[0], dtype=np.uint8)
+    lib().ref_cons3_batch(_p(pv), _p(c), c.shape[1], c.shape[0], _p(dl), float(tan_half_fov),
+                          out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+    return out.astype(bool)
 
 
 def lattice_count_fast(circles_int, G: int, pitch: int = 5) -> int:

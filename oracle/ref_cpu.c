@@ -286,3 +286,83 @@ int64_t ref_fire_step(const uint8_t* g, uint8_t* gn, int64_t nx, int64_t ny, con
     }
     return n;
 }
+
+/* ---------------------------------------------------------------------------------------
+ * Known-answer counts (independent of floating point), for full-size parity checks.
+ * On the half-integer lattice of createPOI(pitch, pitch, G, G) (src/AreaCoverageCalculation.jl
+ * :11-21: entry (i - 1/2)*pitch, (j - 1/2)*pitch) with integer disk centres and radii, entry
+ * (i, j) lies strictly inside disk (cx, cy, R) iff ((2i-1)p - 2cx)^2 + ((2j-1)p - 2cy)^2 < 4R^2
+ * in exact int64 arithmetic. out[k] = number of entries covered by the union of candidate k's
+ * disks (cands: K x 3N, integer-valued doubles; R <= 0 covers nothing). One G x G byte mask per
+ * thread; only the disks' bounding windows are touched and cleared. */
+int ref_lattice_count_batch(const double* cands, int64_t three_n, int64_t K, int64_t G,
+                            int64_t pitch, int64_t* out, int nthreads)
+{
+    if (three_n % 3 != 0) return REF_E_SIZE;
+    const int64_t N = three_n / 3;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+    int rc = REF_OK;
+#ifdef _OPENMP
+#pragma omp parallel
+#endif
+    {
+        uint8_t* cov = (uint8_t*)calloc((size_t)(G * G), 1);
+        if (!cov) rc = -1;
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 4)
+#endif
+        for (int64_t k = 0; k < K; ++k) {
+            if (!cov) continue;
+            const double* c = cands + k * three_n;
+            int64_t n = 0;
+            for (int pass = 0; pass < 2; ++pass) {   /* 0: mark and count, 1: clear windows */
+                for (int64_t d = 0; d < N; ++d) {
+                    const int64_t cx = (int64_t)c[d], cy = (int64_t)c[N + d], R = (int64_t)c[2 * N + d];
+                    if (R <= 0) continue;
+                    int64_t i0 = (2 * (cx - R)) / (2 * pitch) - 1, i1 = (2 * (cx + R)) / (2 * pitch) + 2;
+                    int64_t j0 = (2 * (cy - R)) / (2 * pitch) - 1, j1 = (2 * (cy + R)) / (2 * pitch) + 2;
+                    if (i0 < 1) i0 = 1;
+                    if (j0 < 1) j0 = 1;
+                    if (i1 > G) i1 = G;
+                    if (j1 > G) j1 = G;
+                    for (int64_t i = i0; i <= i1; ++i) {
+                        const int64_t dx = (2 * i - 1) * pitch - 2 * cx;
+                        for (int64_t j = j0; j <= j1; ++j) {
+                            uint8_t* m = cov + (i - 1) * G + (j - 1);
+                            if (pass) { *m = 0; continue; }
+                            const int64_t dy = (2 * j - 1) * pitch - 2 * cy;
+                            if (dx * dx + dy * dy < 4 * R * R && !*m) { *m = 1; ++n; }
+                        }
+                    }
+                }
+            }
+            out[k] = n;
+        }
+        free(cov);
+    }
+    return rc;
+}
+
+/* The objective penalty of src/TDM_STATIC_opt.jl:89-93 for K candidates (K x 3N rows):
+ * violation_k = sum_{i=1..N} abs(x[i+2N] - r_max[i]) accumulated sequentially from 0.0. */
+void ref_violation_batch(const double* cands, int64_t three_n, int64_t K, const double* r_max,
+                         double* out)
+{
+    const int64_t N = three_n / 3;
+    for (int64_t k = 0; k < K; ++k) {
+        const double* x = cands + k * three_n;
+        double v = 0.0;
+        for (int64_t i = 0; i < N; ++i) v += fabs(x[i + 2 * N] - r_max[i]);
+        out[k] = v;
+    }
+}
+
+/* cons3 (ref_cons3) for K candidates: feas[k] = 1 feasible, 0 infeasible. */
+void ref_cons3_batch(const double* prev, const double* cands, int64_t three_n, int64_t K,
+                     const double* d_lim, double tan_half_fov, uint8_t* feas)
+{
+    for (int64_t k = 0; k < K; ++k)
+        feas[k] = (uint8_t)ref_cons3(prev, cands + k * three_n, three_n, d_lim, tan_half_fov);
+}

@@ -14,7 +14,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-ALGOS = ("tiled", "scan", "poll")
+ALGOS = ("tiled", "scan", "poll", "fused")
 TAN50 = math.tan(100 / 180 * math.pi / 2)
 
 
@@ -335,20 +335,60 @@ def test_config3_full_poll(ctx, pkg, orc):
         assert np.array_equal(objs, wbar) and bi == int(np.argmin(wbar)) and bo == wbar[bi], a
 
 
-def test_config4_full_poll(ctx, pkg, orc):
-    """512 UAVs x 16.8M cells, K=3073 (the bench workload): every candidate's area equals the
-    exact integer lattice count; the scan kernel agrees on a sample."""
+def _full_poll_check(ctx, orc, C, rmax, G, algos, tag):
+    """Every candidate of a full poll against the exact integer lattice count, through every
+    listed walk; objectives (-25*count + 1e5*sequential violation) and the argmin bit-exact,
+    without and with cons3 (d_lim = 10 m around the incumbent, src/FullSimulation.jl:740)."""
+    cnt = orc.lattice_count_batch(C, G)
+    want_area = 25.0 * cnt.astype(np.float64)
+    want_obj = -want_area + orc.violation_batch(C, rmax) * 1e5
+    tan = float(np.tan(100 / 180 * np.pi / 2))
+    dlim = np.full(C.shape[1] // 3, 10.0)
+    feas = orc.cons3_batch(C[0], C, dlim, tan)
+    want_bar = np.where(feas, want_obj, np.inf)
+    for a in algos:
+        ctx.set_algo(a)
+        got = ctx.area_batch(C)
+        bad = np.flatnonzero(got != want_area)
+        assert bad.size == 0, (tag, a, bad[:5], got[bad[:5]], want_area[bad[:5]])
+        bo, bi, objs = ctx.poll_best(C, rmax, want_all=True)
+        assert np.array_equal(objs, want_obj), (tag, a, np.flatnonzero(objs != want_obj)[:5])
+        k = int(np.argmin(want_obj))
+        assert bi == k and bo == want_obj[k], (tag, a, bi, k)
+        bo, bi, objs = ctx.poll_best(C, rmax, 1e5, prev=C[0], d_lim=dlim, tan_half_fov=tan,
+                                     want_all=True)
+        assert np.array_equal(objs, want_bar), (tag, a)
+        k = int(np.argmin(want_bar))
+        assert bi == k and bo == want_bar[k], (tag, a, bi, k)
+    ctx.set_algo("auto")
+    return cnt
+
+
+@pytest.mark.parametrize("algo", ["auto", "fused", "poll", "tiled"])
+def test_config4_full_poll(ctx, pkg, orc, algo):
+    """512 UAVs x 16.8M cells, K=3073 — the bench workload, through the walk the bench times
+    (auto = the poll walk for K >= 64) and the others: all 3073 areas == 25 x the exact integer
+    lattice count, objectives and argmin bit-exact (with and without cons3); the streaming scan
+    agrees on a sample."""
     x, y, w, C, rmax = pkg.workloads.make_config(4)
     ctx.set_points(x, y, w)
-    ctx.set_algo("tiled")
-    got = ctx.area_batch(C)
-    ctx.set_algo("scan")
-    sample = C[::256]
-    got_scan = ctx.area_batch(sample)
-    ctx.set_algo("auto")
-    assert np.array_equal(got[::256], got_scan)
-    want = np.array([25.0 * orc.lattice_count_fast(c.astype(np.int64), 4096) for c in C])
-    assert np.array_equal(got, want)
+    cnt = _full_poll_check(ctx, orc, C, rmax, 4096, [algo], "config4")
+    if algo == "auto":
+        ctx.set_algo("scan")
+        got_scan = ctx.area_batch(C[::384])
+        ctx.set_algo("auto")
+        assert np.array_equal(got_scan, 25.0 * cnt[::384])
+
+
+@pytest.mark.parametrize("algo", ["auto", "fused", "poll"])
+def test_config4_clustered_full_poll(ctx, pkg, orc, algo):
+    """SURVEY 8(d)'s "clustered" variant at full size: 512 R=36 disks within sqrt(N)*40 m of the
+    centre of the 16.8M-cell grid, so most disks overlap lower-index ones and the shared-entry
+    pass (ownership between overlapping disks) carries a large part of every candidate's area.
+    Every candidate == exact lattice count; objectives, cons3 and argmin bit-exact."""
+    x, y, w, C, rmax = pkg.workloads.make_config(4, disks="clustered")
+    ctx.set_points(x, y, w)
+    _full_poll_check(ctx, orc, C, rmax, 4096, [algo], "config4-clustered")
 
 
 @pytest.mark.parametrize("case", ["real_clustered", "big_radius", "mixed_weights", "pythagorean",

@@ -45,6 +45,12 @@ for s in $STEPS; do
         make -s -C maximumareacoverageoptimization.jl_amd/csrc diag
         MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
             run diag 600 python tools/diag_poll.py ; rc=$? ;;
+    dfused)
+        make -s -C maximumareacoverageoptimization.jl_amd/csrc diag
+        MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
+            run dfused 300 python tools/diag_fused.py ; rc=$?
+        fatal $rc || MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
+            run dfusedc 300 python tools/diag_fused.py --disks clustered ; rc=$? ;;
     diag5)
         make -s -C maximumareacoverageoptimization.jl_amd/csrc diag
         MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
@@ -57,6 +63,13 @@ for s in $STEPS; do
         MAXCOVER_BENCH_DEVICE=0 run weak2 300 python -m torch.distributed.run --nnodes=1 \
             --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 \
             --no-cpu --dist-backend gloo --steps 20 ; rc=$? ;;
+    probe)
+        { nproc; python3 -c "import os; print(os.cpu_count(), len(os.sched_getaffinity(0)))";
+          cat /sys/fs/cgroup/cpu.max 2>/dev/null; lscpu | grep -E 'Model name|Socket|Core|Thread'; 
+          echo OMP=$OMP_NUM_THREADS; } > gpurun_out/probe.log 2>&1; cat gpurun_out/probe.log; rc=0 ;;
+    benchc)
+        run benchc 400 python bench.py --disks clustered --no-cpu ; rc=$?
+        grep '^{' gpurun_out/benchc.log > gpurun_out/benchc_${TAG}.json ;;
     bench3)
         run bench3 600 python bench.py --config 3 --no-cpu ; rc=$? ;;
     bench5)
@@ -66,16 +79,18 @@ for s in $STEPS; do
     prof)
         rm -rf gpurun_out/prof
         run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
-            -- python3 bench.py --steps 10 --warmup 2 --no-cpu ; rc=$?
+            -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-extras ; rc=$?
         find gpurun_out/prof -name '*stats*' | head ;;
     pmc)
         rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
         run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run \
-            -- python3 bench.py --steps 5 --warmup 1 --no-cpu ; rc=$?
+            -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-extras ; rc=$?
         if ! fatal $rc; then
             run pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run \
-                -- python3 bench.py --steps 5 --warmup 1 --no-cpu ; rc=$?
-        fi ;;
+                -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-extras ; rc=$?
+        fi
+        fatal $rc || python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write --config 4 \
+            --out gpurun_out/pmc_traffic_config4.json ;;
     *) echo "unknown step $s"; rc=0 ;;
     esac
     if fatal $rc; then echo "=== stopping: $s exited $rc"; exit $rc; fi

@@ -9,9 +9,11 @@ pass) with --kernel-trace-free counter collection only. Corrections, per
   * the counters are in KiB (rocprofv3 derived metrics: TCC_EA0_*REQ x 64 B / 1024);
   * on gfx950 FETCH_SIZE reports 1/2 of the bytes of wide coalesced reads, so it is doubled;
   * Infinity-Cache hits are counted by the memory-side counters, not excluded.
-The dominant kernel is coverage_poll_kernel (the bench's walk); the value stored as
-"hbm_bytes_per_launch" is 2 * FETCH + WRITE averaged over its launches, which bench.py reports
-as roofline.traffic.
+Per kernel: 2 * FETCH + WRITE averaged over its launches. "hbm_bytes_per_poll" sums the kernels
+of one poll chain (--chain; the fused poll by default), which bench.py reports as
+roofline.traffic — only while the library sources hash to "src_sha" (bench.src_hash), i.e. the
+build that was profiled. Run the passes with `bench.py --no-extras` so that only the poll chain
+launches after set-up.
 """
 from __future__ import annotations
 
@@ -43,7 +45,8 @@ def main():
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("--config", type=int, default=4)
-    ap.add_argument("--kernel", default="mac::coverage_poll_kernel")
+    ap.add_argument("--chain", default="mac::fused_prep_kernel,mac::fused_walk_kernel",
+                    help="comma-separated kernels of one poll")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     fetch = load(a.fetch_dir, "FETCH_SIZE")
@@ -62,15 +65,23 @@ def main():
             "write_kib_raw": wk,
             "hbm_bytes_per_launch": 2.0 * fk * 1024.0 + wk * 1024.0,
         }
-    if a.kernel not in kernels:
-        raise SystemExit(f"{a.kernel} not found; have {list(kernels)}")
+    chain = a.chain.split(",")
+    missing = [k for k in chain if k not in kernels]
+    if missing:
+        raise SystemExit(f"{missing} not found; have {list(kernels)}")
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
     out = {
         "config": a.config,
-        "kernel": a.kernel,
-        "hbm_bytes_per_launch": kernels[a.kernel]["hbm_bytes_per_launch"],
+        "workload": "bench.py default (uniform disks, cons3, algo auto)",
+        "src_sha": bench.src_hash(),
+        "chain": chain,
+        "hbm_bytes_per_poll": sum(kernels[k]["hbm_bytes_per_launch"] for k in chain),
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
-                  "`python3 bench.py --steps 5 --warmup 1 --no-cpu`; bytes = 2*FETCH_SIZE*1024 "
-                  "+ WRITE_SIZE*1024 (gfx950 FETCH correction, MI355X_MICROARCH.md)",
+                  "`python3 bench.py --steps 5 --warmup 1 --no-cpu --no-extras`; bytes = "
+                  "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH correction, "
+                  "MI355X_MICROARCH.md)",
         "kernels": kernels,
     }
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
