@@ -61,7 +61,9 @@ constexpr int kFSlots = 4096;      // walk: LDS hash table (uint64 packed keys)
 constexpr int kFMaxU = 3072;       // walk: distinct disks hashed at most (load <= 3/4)
 constexpr int kFMaxK = 8192;       // walk: candidates whose table slot is kept in LDS (uint16)
 constexpr int kFRegTile = 1024;    // prep (last workgroup): regions per LDS tile
-constexpr int kFChainSeg = 16;     // chain: consecutive disks per thread and round
+constexpr int kFChainCands = 64;   // chain: candidates per workgroup (4 threads each)
+constexpr int kFChainU = 4;        // chain: rounds of 16 disks per batch of loads
+constexpr int kFChainThr = 256;    // chain: cons3 thresholds per LDS chunk
 
 enum { kCtlDone1 = 0, kCtlDone2 = 1, kCtlDcount = 2, kCtlJobs = 3, kCtlWords = 8 };
 
@@ -71,7 +73,6 @@ struct FusedArgs {
     int ndt, nct;                  // key tiles: ceil(N / kFD) x ceil(K / kFC)
     int n_chain, n_shared;
     Grid g;
-    uint32_t gen;                  // this poll's generation (tags of the region words, >= 1)
     // objective: rmax == null -> areas only (no chains)
     const double* rmax;
     const double* prev;            // cons3 around prev (null: no cons3), raw d_lim per UAV
@@ -80,12 +81,11 @@ struct FusedArgs {
     // lane scratch
     int16_t* keys;                 // [3][N][Kp]
     uint8_t* kbad;                 // [N][nct]
-    unsigned long long* rlo;       // [N][2] tagged min tile x, y
-    unsigned long long* rhi;       // [N][2] tagged max tile x, y
-    double* spanA;                 // [ndt * nct]
+    int4* part;                    // [ndt][nct][kFD] partial regions (sc1)
+    unsigned* dtctr;               // [ndt] per disk tile arrival counters (self-resetting)
     double* vp;                    // [K]
     unsigned* cnt;                 // [K]
-    int4* region;                  // [N]
+    int4* region;                  // [N] (sc1)
     uint16_t* nbr;                 // [N][kPollNbr]
     int4* nboxT;                   // [N][kPollNbr]
     int* ncount;                   // [N]
@@ -103,19 +103,33 @@ struct FusedArgs {
     int64_t idx_base;
 };
 
-__device__ __forceinline__ unsigned long long tag_lo(uint32_t gen, int v)
-{
-    return ((unsigned long long)(0xffffffffu - gen) << 32) | (uint32_t)v;
-}
-__device__ __forceinline__ unsigned long long tag_hi(uint32_t gen, int v)
-{
-    return ((unsigned long long)gen << 32) | (uint32_t)v;
-}
-__device__ __forceinline__ unsigned long long atomic_read_u64(unsigned long long* p)
-{
-    return __hip_atomic_fetch_or(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// int4 through two 8-B agent-scope (sc1) accesses: the cross-workgroup hand-offs of launch 1
+__device__ __forceinline__ void st_sc1(int4* p, const int4& v)
+{
+    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+    __hip_atomic_store(q, (unsigned long long)(uint32_t)v.x | ((unsigned long long)(uint32_t)v.y << 32),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, (unsigned long long)(uint32_t)v.z | ((unsigned long long)(uint32_t)v.w << 32),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int4 ld_sc1(const int4* p)
+{
+    const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
+    const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_int4((int)(uint32_t)a, (int)(uint32_t)(a >> 32), (int)(uint32_t)b, (int)(uint32_t)(b >> 32));
+}
+
+__device__ __forceinline__ int4 empty_box() { return make_int4(0x7fffffff, -1, 0x7fffffff, -1); }
+__device__ __forceinline__ void box_join(int4& R, const int4& P)
+{
+    R.x = min(R.x, P.x);
+    R.y = max(R.y, P.y);
+    R.z = min(R.z, P.z);
+    R.w = max(R.w, P.w);
+}
 
 // exact int16 offset of v from b: b + (double)key reproduces v bit for bit, else ok = false
 __device__ __forceinline__ int key16(double v, double b, bool& ok)
@@ -144,69 +158,83 @@ __device__ __forceinline__ uint32_t hash_key(unsigned long long key)
 
 // ================================================================== launch 1
 
-// Penalty chain of candidates [k0, k0 + kChainC) (k_final.h penalty_chain_block), its terms
-// |R_i - r_max_i| and cons3 marks computed from the source in place (pen_term, k_prep.h).
+// Penalty chains of candidates [k0, k0 + 64): violation_k = sum_{i=0..N-1} |R_i - r_max_i|
+// accumulated IN ORDER from 0.0 (src/TDM_STATIC_opt.jl:89-93), +inf when cons3 rejects a UAV's
+// move (pen_term, k_prep.h). Thread t: candidate k0 + t/4, quarter t%4. A round covers 16
+// disks: the quarter loads disks [4q, 4q + 4) of the round from its candidate's contiguous
+// column (one 128-B line per candidate and section, shared by its four lanes), and the running
+// sum is relayed through the four lanes in quarter order by shuffles: the additions stay in
+// disk order without a barrier. kFChainU rounds of loads are in flight at once.
 __device__ __forceinline__ void fused_chain_block(const FusedArgs& a, int k0, unsigned char* lds)
 {
-    double* carry = (double*)lds;                       // [kChainC]
-    double* thr = carry + kChainC;                      // [kChainG * kFChainSeg]
-    int* bad = (int*)(thr + kChainG * kFChainSeg);      // [kChainC]
-    const int t = threadIdx.x, c = t % kChainC, grp = t / kChainC;
+    double* thr = (double*)lds;   // [kFChainThr] cons3 thresholds of the chunk
+    const int t = threadIdx.x, lane = t & (kWave - 1), c = t >> 2, qq = t & 3;
     const int k = k0 + c, N = a.N;
-    if (t < kChainC) {
-        carry[t] = 0.0;
-        bad[t] = 0;
-    }
-    constexpr int R = kChainG * kFChainSeg;
-    for (int base = 0; base < N; base += R) {
-        if (a.prev)
-            for (int q = t; q < R; q += kBlock) thr[q] = base + q < N ? dlim_threshold(a.dlim[base + q]) : 0.0;
+    const bool kv = k < a.K;
+    double carry = 0.0;
+    bool bad = false;
+    for (int c0 = 0; c0 < N; c0 += kFChainThr) {
+        const int c1 = min(N, c0 + kFChainThr);
         __syncthreads();
-        const int i0 = base + grp * kFChainSeg;
-        double v[kFChainSeg];
+        if (a.prev)
+            for (int q = t; q < kFChainThr; q += kBlock) thr[q] = c0 + q < N ? dlim_threshold(a.dlim[c0 + q]) : 0.0;
+        __syncthreads();
+        for (int base = c0; base < c1; base += 16 * kFChainU) {
+            double R[kFChainU][4], X[kFChainU][4], Y[kFChainU][4];
 #pragma unroll
-        for (int j = 0; j < kFChainSeg; ++j) {
-            const int ii = i0 + j;
-            double term = 0.0;   // pad: + 0.0, exact
-            if (k < a.K && ii < N) {
-                const double R2 = a.src.get(k, 2 * N + ii, N);
-                term = __builtin_fabs(R2 - a.rmax[ii]);
-                if (a.prev) {
-                    const double x2 = a.src.get(k, ii, N), y2 = a.src.get(k, N + ii, N);
-                    const double x1 = a.prev[ii], y1 = a.prev[N + ii];
-                    const double z1 = a.prev[2 * N + ii] / a.tan_half_fov, z2 = R2 / a.tan_half_fov;
-                    const double ddx = x1 - x2, ddy = y1 - y2, ddz = z1 - z2;
-                    if (ddx * ddx + ddy * ddy + ddz * ddz > thr[ii - base]) term = -1.0;
+            for (int u = 0; u < kFChainU; ++u)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int ii = base + 16 * u + 4 * qq + e;
+                    const bool v = kv && ii < c1;
+                    R[u][e] = v ? a.src.get(k, 2 * N + ii, N) : 0.0;
+                    X[u][e] = (v && a.prev) ? a.src.get(k, ii, N) : 0.0;
+                    Y[u][e] = (v && a.prev) ? a.src.get(k, N + ii, N) : 0.0;
+                }
+#pragma unroll
+            for (int u = 0; u < kFChainU; ++u) {
+                double term[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int ii = base + 16 * u + 4 * qq + e;
+                    term[e] = 0.0;   // pad: + 0.0, exact
+                    if (kv && ii < c1) {
+                        term[e] = __builtin_fabs(R[u][e] - a.rmax[ii]);
+                        if (a.prev) {
+                            const double x1 = a.prev[ii], y1 = a.prev[N + ii];
+                            const double z1 = a.prev[2 * N + ii] / a.tan_half_fov;
+                            const double z2 = R[u][e] / a.tan_half_fov;
+                            const double ddx = x1 - X[u][e], ddy = y1 - Y[u][e], ddz = z1 - z2;
+                            if (ddx * ddx + ddy * ddy + ddz * ddz > thr[ii - c0]) bad = true;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int step = 0; step < 4; ++step) {
+                    if (qq == step) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) carry += term[e];
+                    }
+                    carry = __shfl(carry, (lane & ~3) | step, kWave);
                 }
             }
-            v[j] = term;
-        }
-        for (int sgrp = 0; sgrp < kChainG; ++sgrp) {
-            if (grp == sgrp) {
-                double acc = carry[c];
-                bool neg = false;
-#pragma unroll
-                for (int j = 0; j < kFChainSeg; ++j) {
-                    neg |= v[j] < 0.0;
-                    acc += v[j];
-                }
-                carry[c] = acc;
-                if (neg) bad[c] = 1;
-            }
-            __syncthreads();
         }
     }
-    if (t < kChainC && k < a.K) a.vp[k] = bad[t] ? __builtin_inf() : carry[t] * a.penalty;
+    // a cons3 failure anywhere in the candidate's four quarters bars it
+    const bool anybad = __shfl_xor((int)bad, 1, kWave) | __shfl_xor((int)bad, 2, kWave) |
+                        __shfl_xor((int)bad, 3, kWave) | (int)bad;
+    if (qq == 0 && kv) a.vp[k] = anybad ? __builtin_inf() : carry * a.penalty;
 }
 
-// Key tile (disk tile dt, candidate tile ct).
-__device__ __forceinline__ void fused_key_tile(const FusedArgs& a, int tile, unsigned char* lds)
+// Key tile (disk tile dt, candidate tile ct): keys, exactness flags, the tile's partial regions.
+// Returns true on the workgroup that arrives last among its disk tile's nct tiles.
+__device__ __forceinline__ bool fused_key_tile(const FusedArgs& a, int tile, unsigned char* lds)
 {
     typedef int16_t KRow[kFC + 4];
     KRow* ks = (KRow*)lds;                                             // [3 * kFD] rows
     int4* rr = (int4*)(lds + 3 * kFD * sizeof(KRow));                  // [8][kFD]
     int* okv = (int*)(rr + 8 * kFD);                                   // [8][kFD]
-    double* red = (double*)(okv + 8 * kFD);                            // [kWavesPerBlock]
+    int* flag = okv + 8 * kFD;
     const int dt = tile % a.ndt, ct = tile / a.ndt;
     const int t = threadIdx.x, l = t & (kFD - 1), q = t / kFD;         // 32 disks x 8
     const int N = a.N, K = a.K;
@@ -228,8 +256,7 @@ __device__ __forceinline__ void fused_key_tile(const FusedArgs& a, int tile, uns
         r[j] = v ? a.src.get(k, 2 * N + i, N) : br;
     }
     bool ok = true;
-    int4 R = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
-    double area = 0.0;
+    int4 R = empty_box();
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int kk = q + 8 * j, k = ct * kFC + kk;
@@ -239,13 +266,7 @@ __device__ __forceinline__ void fused_key_tile(const FusedArgs& a, int tile, uns
             ky = key16(y[j], by, ok);
             kr = key16(r[j], br, ok);
             int4 sp;
-            if (span_of(x[j], y[j], r[j], a.g, sp)) {
-                R.x = min(R.x, sp.x);
-                R.y = max(R.y, sp.y);
-                R.z = min(R.z, sp.z);
-                R.w = max(R.w, sp.w);
-                area += (double)(sp.y - sp.x + 1) * (double)(sp.w - sp.z + 1);
-            }
+            if (span_of(x[j], y[j], r[j], a.g, sp)) box_join(R, sp);
         }
         ks[l][kk] = (int16_t)kx;
         ks[kFD + l][kk] = (int16_t)ky;
@@ -253,28 +274,17 @@ __device__ __forceinline__ void fused_key_tile(const FusedArgs& a, int tile, uns
     }
     rr[q * kFD + l] = R;
     okv[q * kFD + l] = ok ? 1 : 0;
-    const double s = block_sum_f64(area, red);   // (contains a barrier)
-    if (t == 0) __hip_atomic_store(&a.spanA[tile], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    if (t < kFD && di) {
-        int4 Q = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
+    if (t < kFD) {
+        int4 Q = empty_box();
         int okall = 1;
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
-            const int4 P = rr[g * kFD + t];
-            Q.x = min(Q.x, P.x);
-            Q.y = max(Q.y, P.y);
-            Q.z = min(Q.z, P.z);
-            Q.w = max(Q.w, P.w);
+            box_join(Q, rr[g * kFD + t]);
             okall &= okv[g * kFD + t];
         }
-        a.kbad[(int64_t)i * a.nct + ct] = okall ? 0 : 1;
-        if (Q.x <= Q.y) {
-            atomicMin(&a.rlo[2 * i], tag_lo(a.gen, Q.x));
-            atomicMin(&a.rlo[2 * i + 1], tag_lo(a.gen, Q.z));
-            atomicMax(&a.rhi[2 * i], tag_hi(a.gen, Q.y));
-            atomicMax(&a.rhi[2 * i + 1], tag_hi(a.gen, Q.w));
-        }
+        if (di) a.kbad[(int64_t)i * a.nct + ct] = okall ? 0 : 1;
+        st_sc1(&a.part[((int64_t)dt * a.nct + ct) * kFD + t], Q);
     }
     // key rows: 3 x 32 rows of 64 int16 (128 B each), 8-B stores (Kp is a multiple of kFC)
 #pragma unroll
@@ -291,47 +301,59 @@ __device__ __forceinline__ void fused_key_tile(const FusedArgs& a, int tile, uns
     }
     if (dt == 0 && t < kFC && ct * kFC + t < K) a.cnt[ct * kFC + t] = 0u;
     if (tile == 0 && t == 0) a.ctl[kCtlJobs] = 0;
+    vm_drain();          // this wave's stores are complete ...
+    __syncthreads();     // ... and every other wave's
+    if (t == 0) *flag = atomicInc(&a.dtctr[dt], a.nct - 1) == (unsigned)(a.nct - 1);
+    __syncthreads();
+    return *flag != 0;
 }
 
-// The last arriver of launch 1: regions, neighbour lists, disks with neighbours.
+// The last tile of disk tile dt: the regions of its 32 disks from the nct partials.
+__device__ __forceinline__ void fused_dt_regions(const FusedArgs& a, int dt, unsigned char* lds)
+{
+    int4* rr = (int4*)lds;   // [8][kFD]
+    const int t = threadIdx.x, l = t & (kFD - 1), g = t / kFD;
+    int4 R = empty_box();
+    for (int c = g; c < a.nct; c += 8) box_join(R, ld_sc1(&a.part[((int64_t)dt * a.nct + c) * kFD + l]));
+    rr[g * kFD + l] = R;
+    __syncthreads();
+    const int i = dt * kFD + t;
+    if (t < kFD && i < a.N) {
+        int4 Q = empty_box();
+#pragma unroll
+        for (int q = 0; q < 8; ++q) box_join(Q, rr[q * kFD + t]);
+        if (Q.x > Q.y || Q.z > Q.w) Q = empty_box();
+        st_sc1(&a.region[i], Q);
+    }
+    vm_drain();
+    __syncthreads();
+}
+
+// The last disk tile's last tile: every disk's lower-index neighbour list (all pairs, the
+// regions through LDS in tiles of kFRegTile) and the list of disks with neighbours.
 __device__ __forceinline__ void fused_prep_last(const FusedArgs& a, unsigned char* lds)
 {
     int4* sreg = (int4*)lds;                         // [kFRegTile]
     int* sd = (int*)(sreg + kFRegTile);
     const int t = threadIdx.x, N = a.N;
-    const unsigned long long want_lo = (unsigned long long)(0xffffffffu - a.gen);
-    const unsigned long long want_hi = (unsigned long long)a.gen;
     if (t == 0) *sd = 0;
-    for (int i = t; i < N; i += kBlock) {
-        const unsigned long long x0 = atomic_read_u64(&a.rlo[2 * i]), y0 = atomic_read_u64(&a.rlo[2 * i + 1]);
-        const unsigned long long x1 = atomic_read_u64(&a.rhi[2 * i]), y1 = atomic_read_u64(&a.rhi[2 * i + 1]);
-        int4 R = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
-        if ((x0 >> 32) == want_lo && (y0 >> 32) == want_lo && (x1 >> 32) == want_hi && (y1 >> 32) == want_hi)
-            R = make_int4((int)(uint32_t)x0, (int)(uint32_t)x1, (int)(uint32_t)y0, (int)(uint32_t)y1);
-        __hip_atomic_store(&a.region[i].x, R.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&a.region[i].y, R.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&a.region[i].z, R.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&a.region[i].w, R.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    vm_drain();
-    __syncthreads();
-    auto reg_ld = [&](int j) {
-        int4 R;
-        R.x = __hip_atomic_load(&a.region[j].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        R.y = __hip_atomic_load(&a.region[j].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        R.z = __hip_atomic_load(&a.region[j].z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        R.w = __hip_atomic_load(&a.region[j].w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return R;
-    };
-    for (int ib = 0; ib < N; ib += kBlock) {
-        const int i = ib + t;
-        const int4 Ri = i < N ? reg_ld(i) : make_int4(0x7fffffff, -1, 0x7fffffff, -1);
+    // snake order over rounds of 256 disks: every thread walks about the same number of pairs
+    for (int m = 0; m * kBlock < N; ++m) {
+        const int i = m * kBlock + ((m & 1) ? kBlock - 1 - t : t);
+        const int4 Ri = i < N ? ld_sc1(&a.region[i]) : empty_box();
         int cnt = 0;
-        const int jend = min(N, ib + kBlock);
+        const int jend = min(N, (m + 1) * kBlock);
         for (int jb = 0; jb < jend; jb += kFRegTile) {
             __syncthreads();
-            for (int q = t; q < kFRegTile; q += kBlock)
-                sreg[q] = jb + q < jend ? reg_ld(jb + q) : make_int4(0x7fffffff, -1, 0x7fffffff, -1);
+            constexpr int PT = kFRegTile / kBlock;
+            int4 v[PT];
+#pragma unroll
+            for (int q = 0; q < PT; ++q) {   // every load in flight at once
+                const int j = jb + t + q * kBlock;
+                v[q] = j < jend ? ld_sc1(&a.region[j]) : empty_box();
+            }
+#pragma unroll
+            for (int q = 0; q < PT; ++q) sreg[t + q * kBlock] = v[q];
             __syncthreads();
             if (i < N && Ri.x <= Ri.y) {
                 const int je = min(i, jb + kFRegTile);
@@ -358,21 +380,27 @@ __device__ __forceinline__ void fused_prep_last(const FusedArgs& a, unsigned cha
 
 constexpr int kPrepLds = 3 * kFD * (kFC + 4) * 2 + 8 * kFD * 16 + 8 * kFD * 4 + 64;
 static_assert(kPrepLds >= kFRegTile * 16 + 16, "the last workgroup's region tile fits");
+static_assert(kPrepLds >= kFChainThr * 8, "the chain's thresholds fit");
 
+// Grid: n_chain chain workgroups, then ndt * nct key tiles.
 __global__ __launch_bounds__(kBlock) void fused_prep_kernel(uint64_t* ts, FusedArgs a)
 {
     ts_begin(ts);
     __shared__ __attribute__((aligned(16))) unsigned char lds[kPrepLds];
     __shared__ int last;
     const int b = blockIdx.x;
-    if (b < a.n_chain) fused_chain_block(a, b * kChainC, lds);
-    else fused_key_tile(a, b - a.n_chain, lds);
-    vm_drain();          // this wave's stores and atomics are complete ...
-    __syncthreads();     // ... and every other wave's
-    if (threadIdx.x == 0)
-        last = atomicInc((unsigned*)&a.ctl[kCtlDone1], gridDim.x - 1) == gridDim.x - 1;
-    __syncthreads();
-    if (last) fused_prep_last(a, lds);
+    if (b < a.n_chain) {
+        fused_chain_block(a, b * kFChainCands, lds);
+    } else {
+        const int tile = b - a.n_chain;
+        if (fused_key_tile(a, tile, lds)) {   // the last of its disk tile
+            fused_dt_regions(a, tile % a.ndt, lds);
+            if (threadIdx.x == 0)
+                last = atomicInc((unsigned*)&a.ctl[kCtlDone1], a.ndt - 1) == (unsigned)(a.ndt - 1);
+            __syncthreads();
+            if (last) fused_prep_last(a, lds);
+        }
+    }
     ts_end(ts);
 }
 
@@ -429,32 +457,52 @@ __device__ __forceinline__ void fused_shared_job(const FusedArgs& a, int i, int 
     unsigned acc = 0;
     __syncthreads();
 
+    // the exact decision of this round's staged entries sp[0, ns) for this thread's candidate:
+    // its entries s = eg + G*j (j < 256 / G) as a 256-bit mask of those disk i covers, then each
+    // lower-index neighbour strips the entries it covers — a neighbour disk is read once per
+    // round, not once per entry
     auto decide = [&](int ns) {
-        if (valid && d.T >= 0.0) {
-            for (int s = eg; s < ns; s += G) {
-                const double2 q = sp[s];
-                if (!(sqdist(q.x, q.y, d.cx, d.cy) <= d.T)) continue;
-                bool stolen = false;
-#pragma unroll
-                for (int m = 0; m < 4; ++m)
-                    if (m < ncl) stolen |= sqdist(q.x, q.y, e[m].cx, e[m].cy) <= e[m].T;
-                if (!stolen && nc > 4) {
-                    if (nc <= kPollNbr) {
-                        for (int m = 4; m < nc && !stolen; ++m) {
-                            const DiskRec x = src_disk(a.src, N, nbr[m], k);
-                            stolen = sqdist(q.x, q.y, x.cx, x.cy) <= x.T;
-                        }
-                    } else {  // overflowed list: every lower-index overlapping region
-                        for (int j = 0; j < i && !stolen; ++j) {
-                            if (!box_overlap(a.region[j], R)) continue;
-                            const DiskRec x = src_disk(a.src, N, j, k);
-                            stolen = sqdist(q.x, q.y, x.cx, x.cy) <= x.T;
-                        }
-                    }
-                }
-                if (!stolen) ++acc;
+        if (!(valid && d.T >= 0.0) || ns <= eg) return;
+        const int nj = (ns - eg + G - 1) / G;
+        uint64_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
+        for (int j = 0; j < nj; ++j) {
+            const double2 q = sp[eg + G * j];
+            if (sqdist(q.x, q.y, d.cx, d.cy) <= d.T) {
+                const uint64_t bit = 1ull << (j & 63);
+                const int w = j >> 6;
+                m0 |= w == 0 ? bit : 0ull;
+                m1 |= w == 1 ? bit : 0ull;
+                m2 |= w == 2 ? bit : 0ull;
+                m3 |= w == 3 ? bit : 0ull;
             }
         }
+        auto strip_word = [&](uint64_t& mw, int w, const DiskRec& x) {
+            uint64_t m = mw;
+            while (m) {
+                const int b = __builtin_ctzll(m);
+                m &= m - 1;
+                const double2 q = sp[eg + G * (64 * w + b)];
+                if (sqdist(q.x, q.y, x.cx, x.cy) <= x.T) mw &= ~(1ull << b);
+            }
+        };
+        auto strip = [&](const DiskRec& x) {
+            strip_word(m0, 0, x);
+            strip_word(m1, 1, x);
+            strip_word(m2, 2, x);
+            strip_word(m3, 3, x);
+        };
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            if (m < ncl && (m0 | m1 | m2 | m3)) strip(e[m]);
+        if (nc > 4 && (m0 | m1 | m2 | m3)) {
+            if (nc <= kPollNbr) {
+                for (int m = 4; m < nc && (m0 | m1 | m2 | m3); ++m) strip(src_disk(a.src, N, nbr[m], k));
+            } else {  // overflowed list: every lower-index overlapping region
+                for (int j = 0; j < i && (m0 | m1 | m2 | m3); ++j)
+                    if (box_overlap(a.region[j], R)) strip(src_disk(a.src, N, j, k));
+            }
+        }
+        acc += (unsigned)(__popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3));
     };
 
     // shared tiles of each row: runs of a 64-bit tile mask (the union of the neighbour boxes);
@@ -591,8 +639,15 @@ constexpr int kFWalkLds = kFSlots * 8 + kFMaxK * 2 + kFMaxU * 2 + kFStage +
                           (kPollRB + kPollRB + 4) * 4 + kPollNbr * 16 + 64;
 static_assert(kPollWaves * kPollKPB * 4 + kPollKPB * 4 <= kFStage, "counts alias the staging");
 
+#ifdef MAC_DIAG
+#define MAC_FW_STAMP(q) if (threadIdx.x == 0 && i < 65536) g_diag_walk[8 * i + (q)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define MAC_FW_STAMP(q)
+#endif
+
 __device__ __forceinline__ void fused_walk_disk(const FusedArgs& a, int i, unsigned char* lds)
 {
+    MAC_FW_STAMP(0);
     unsigned long long* table = (unsigned long long*)lds;                 // [kFSlots]
     uint16_t* cslot = (uint16_t*)(table + kFSlots);                       // [kFMaxK]
     uint16_t* pslot = cslot + kFMaxK;                                     // [kFMaxU]
@@ -678,6 +733,7 @@ __device__ __forceinline__ void fused_walk_disk(const FusedArgs& a, int i, unsig
         }
     }
     __syncthreads();
+    MAC_FW_STAMP(1);
     const bool hashed = hashed0 && misc[0] <= kFMaxU && misc[1] == 0;
     int U = K;
     if (hashed) {
@@ -705,6 +761,7 @@ __device__ __forceinline__ void fused_walk_disk(const FusedArgs& a, int i, unsig
         U = wsum[0] + wsum[1] + wsum[2] + wsum[3];
         __syncthreads();
     }
+    MAC_FW_STAMP(2);
     // position p -> its disk (hashed: candidate 0's disk + the exact key; identity: candidate p)
     auto pos_disk = [&](int p) {
         if (hashed) {
@@ -750,6 +807,7 @@ __device__ __forceinline__ void fused_walk_disk(const FusedArgs& a, int i, unsig
                 sa[j].x = L.sa; sb[j].x = L.sb; st[j].x = L.stm; ns[j].x = L.ns;
             }
         }
+        if (kb == 0) MAC_FW_STAMP(3);
         const int np = (ke - kb + 2 * kWave - 1) / (2 * kWave);
         auto dprime = [&](const float4& e, int u) {
             const int j = u >> 1;
@@ -836,6 +894,7 @@ __device__ __forceinline__ void fused_walk_disk(const FusedArgs& a, int i, unsig
                 __syncthreads();
             }
         }
+        if (kb == 0) MAC_FW_STAMP(4);
         // the slice's count per position: the four waves' shares (integers: any order)
 #pragma unroll
         for (int u = 0; u < kPollSlots; ++u) red[wid][u * kWave + lane] = (unsigned)acc[u];
@@ -851,6 +910,7 @@ __device__ __forceinline__ void fused_walk_disk(const FusedArgs& a, int i, unsig
                 if (v) atomicAdd(&a.cnt[k], v);
             }
         }
+        if (kb == 0) MAC_FW_STAMP(5);
     }
 }
 
@@ -927,6 +987,11 @@ __global__ __launch_bounds__(kPollThreads) void fused_walk_kernel(uint64_t* ts, 
         const int x = bx % 8, r = bx / 8, fl = N / 8, rem = N % 8;
         const int i = x < rem ? x * (fl + 1) + r : rem * (fl + 1) + (x - rem) * fl + r;
         fused_walk_disk(a, i, lds);
+#ifdef MAC_DIAG
+        vm_drain();
+        __syncthreads();
+        if (threadIdx.x == 0 && i < 65536) g_diag_walk[8 * i + 6] = __builtin_amdgcn_s_memrealtime();
+#endif
     }
     // shared-entry jobs: [0, n_shared) one each to the shared workgroups, the rest from the
     // counter (walk workgroups join once their disk is done)

@@ -131,9 +131,8 @@ struct Lane {
         cnt, dlimraw;
     // the fused equal-weight poll (k_fused.h): keys, regions (generation-tagged), chains, counts,
     // neighbour lists, hand-off counters
-    DevBuf f_keys, f_kbad, f_rlo, f_rhi, f_spanA, f_vp, f_cnt, f_region, f_nbr, f_nboxT, f_ncount,
+    DevBuf f_keys, f_kbad, f_part, f_dtctr, f_vp, f_cnt, f_region, f_nbr, f_nboxT, f_ncount,
         f_dlist, f_ctl;
-    uint32_t gen = 0;
     std::vector<double> h_dlim;
     PinnedBuf h_stage;                         // native MADS driver: best, permutations, incumbent
 };
@@ -413,7 +412,7 @@ static void enqueue_fused(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& s
     a.nct = (K + kFC - 1) / kFC;
     a.Kp = a.nct * kFC;
     const bool objective = d_obj != nullptr || d_best != nullptr;
-    a.n_chain = objective ? (K + kChainC - 1) / kChainC : 0;
+    a.n_chain = objective ? (K + kFChainCands - 1) / kFChainCands : 0;
     a.n_shared = kSharedWG;
     a.g = ctx->grid;
     a.rmax = objective ? d_rmax : nullptr;
@@ -425,9 +424,8 @@ static void enqueue_fused(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& s
     const size_t n = (size_t)N;
     L->f_keys.reserve(sizeof(int16_t) * 3 * n * (size_t)a.Kp);
     L->f_kbad.reserve(n * (size_t)a.nct);
-    bool fresh = L->f_rlo.grow(sizeof(unsigned long long) * 2 * n);
-    fresh |= L->f_rhi.grow(sizeof(unsigned long long) * 2 * n);
-    L->f_spanA.reserve(sizeof(double) * (size_t)a.ndt * a.nct);
+    L->f_part.reserve(sizeof(int4) * (size_t)a.ndt * a.nct * kFD);
+    const bool fresh_dt = L->f_dtctr.grow(sizeof(unsigned) * (size_t)a.ndt);
     L->f_vp.reserve(sizeof(double) * (size_t)K);
     L->f_cnt.reserve(sizeof(unsigned) * (size_t)K);
     L->f_region.reserve(sizeof(int4) * n);
@@ -436,21 +434,14 @@ static void enqueue_fused(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& s
     L->f_ncount.reserve(sizeof(int) * n);
     L->f_dlist.reserve(sizeof(int) * n);
     const bool fresh_ctl = L->f_ctl.grow(sizeof(int) * kCtlWords);
-    if (++L->gen == 0) {   // 2^32 polls: restart the tags
-        L->gen = 1;
-        fresh = true;
-    }
-    if (fresh) {   // no tag of these words may look current: lo words +inf, hi words 0
-        HCK(hipMemsetAsync(L->f_rlo.p, 0xff, L->f_rlo.cap, s));
-        HCK(hipMemsetAsync(L->f_rhi.p, 0x00, L->f_rhi.cap, s));
-    }
+    // the arrival counters reset themselves (atomicInc wraps at the last arrival): zero only
+    // when (re)allocated
+    if (fresh_dt) HCK(hipMemsetAsync(L->f_dtctr.p, 0, L->f_dtctr.cap, s));
     if (fresh_ctl) HCK(hipMemsetAsync(L->f_ctl.p, 0, L->f_ctl.cap, s));
-    a.gen = L->gen;
     a.keys = L->f_keys.as<int16_t>();
     a.kbad = L->f_kbad.as<uint8_t>();
-    a.rlo = L->f_rlo.as<unsigned long long>();
-    a.rhi = L->f_rhi.as<unsigned long long>();
-    a.spanA = L->f_spanA.as<double>();
+    a.part = L->f_part.as<int4>();
+    a.dtctr = L->f_dtctr.as<unsigned>();
     a.vp = L->f_vp.as<double>();
     a.cnt = L->f_cnt.as<unsigned>();
     a.region = L->f_region.as<int4>();
@@ -991,7 +982,7 @@ void mac_ctx_destroy(mac_ctx* ctx)
                           &l->ncount, &l->dlist, &l->spart, &l->vp, &l->xinc,
                           &l->perm, &l->ucount, &l->umap, &l->keysT, &l->kbad, &l->lane4,
                           &l->lanexp, &l->rows, &l->nboxT, &l->cnt, &l->dlimraw, &l->f_keys,
-                          &l->f_kbad, &l->f_rlo, &l->f_rhi, &l->f_spanA, &l->f_vp, &l->f_cnt,
+                          &l->f_kbad, &l->f_part, &l->f_dtctr, &l->f_vp, &l->f_cnt,
                           &l->f_region, &l->f_nbr, &l->f_nboxT, &l->f_ncount, &l->f_dlist, &l->f_ctl})
             b->release();
         if (l->done) (void)hipEventDestroy(l->done);

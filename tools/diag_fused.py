@@ -32,7 +32,7 @@ ctx.profile(True)
 ctx.profile_read(reset=True)
 for _ in range(args.polls):
     ctx.poll_best(C, rmax, 1e5, prev=C[0], d_lim=dl, tan_half_fov=tan)
-n_chain = (K + 15) // 16
+n_chain = (K + 63) // 64
 ndt, nct = (N + 31) // 32, (K + 63) // 64
 n1 = n_chain + ndt * nct
 n2 = N + 256
@@ -63,4 +63,14 @@ for p in range(args.polls):
         "launch2_start_pct": [us(np.percentile(b[:, 0] - b[:, 0].min(), q)) for q in (50, 90, 100)],
         "launch2_last_wg_extra": us(np.sort(b[:, 1])[-1] - np.sort(b[:, 1])[-2]),
     })
-print(json.dumps({"config": args.config, "disks": args.disks, "polls": res[-2:]}, indent=1))
+L.mac_diag_walk_read.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int64]
+wb = (ctypes.c_uint64 * (8 * N))()
+assert L.mac_diag_walk_read(wb, 8 * N) == 0
+ws = np.frombuffer(wb, dtype=np.uint64).astype(np.int64).reshape(N, 8)[:, :7]
+ok = np.all(ws[:, :7] > 0, axis=1)
+ph = np.diff(ws[ok], axis=1) / 100.0
+names = ["prologue+insert", "ids", "lane constants", "staging+tests (slice 0)", "atomics issue",
+         "drain"]
+walk = {n: [float(np.median(ph[:, q])), float(ph[:, q].max())] for q, n in enumerate(names)}
+print(json.dumps({"config": args.config, "disks": args.disks, "polls": res[-2:],
+                  "walk_phases_med_max_us": walk, "walk_disks_timed": int(ok.sum())}, indent=1))
