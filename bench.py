@@ -258,7 +258,7 @@ def main():
                     help="4 (default): one MADS poll per step; 5: one end-to-end MPC step "
                          "(CA fire stream + rmvCoveredPOI + a MADS run) per step")
     ap.add_argument("--mads-iters", type=int, default=100, help="config 5: N_iter per MPC step")
-    ap.add_argument("--algo", default="auto", choices=("auto", "tiled", "scan", "poll"))
+    ap.add_argument("--algo", default="auto", choices=("auto", "tiled", "scan", "poll", "fused"))
     ap.add_argument("--polls", type=int, default=4, help="distinct poll sets cycled over steps")
     ap.add_argument("--tile-points", type=int, default=None,
                     help="points per spatial tile of the index (library default when omitted)")

@@ -65,8 +65,8 @@ extern "C" {
                               one candidate per lane (the six-launch chain; weighted lists) */
 #define MAC_ALGO_FUSED  4  /* the two-launch poll for lists whose entries all weigh the same (every
                               reference input): disk index + walk + ownership + objective + argmin
-                              (k_fused.h). AUTO takes it whenever the weights are equal; weighted
-                              lists fall back to the AUTO choice of the other walks */
+                              (k_fused.h). Opt-in (slower than the chain AUTO picks, DESIGN.md
+                              section 4); weighted lists fall back to the AUTO choice */
 
 #define MAC_STORE_F64   0
 #define MAC_STORE_F32   1

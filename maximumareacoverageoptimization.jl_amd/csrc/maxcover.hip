@@ -390,12 +390,12 @@ static bool use_tiled(mac_ctx* ctx, int N, const double* h_cands, int64_t three_
     return visits < 0.5 * (double)ctx->M * (double)N;
 }
 
-// The fused equal-weight poll (k_fused.h) runs for AUTO and FUSED whenever every entry weighs
-// the same (all reference inputs); weighted lists and the forced walks take the legacy chain.
+// The fused equal-weight poll (k_fused.h) runs only when asked for (MAC_ALGO_FUSED) and every
+// entry weighs the same. Measured on the MI355X (profiles/r02a_*), its two launches take 0.19 ms
+// per config-4 poll against the six-launch chain's 0.087 ms, so AUTO keeps the chain.
 static bool use_fused(const mac_ctx* ctx, int N, int64_t K)
 {
-    return (ctx->algo == MAC_ALGO_AUTO || ctx->algo == MAC_ALGO_FUSED) && ctx->w_uniform &&
-           ctx->M > 0 && N > 0 && K > 0;
+    return ctx->algo == MAC_ALGO_FUSED && ctx->w_uniform && ctx->M > 0 && N > 0 && K > 0;
 }
 
 // Two launches (k_fused.h): fused_prep_kernel, fused_walk_kernel. d_dlim: raw d_lim per UAV.
