@@ -87,12 +87,91 @@ __global__ __launch_bounds__(kBlock) void penalty_chain_kernel(const double* __r
 // obj_k = -area_k + vp_k when obj_out != null. With `counts` (every entry weighs w0) and the poll
 // walk chosen, the rows hold uint32 covered-entry counts per candidate (partial[i][k], and
 // spart[i][k] of the disks with neighbours): area_k = (their integer sum) * w0.
+// The poll argmin (fb.best != null) is taken here too, with no launch of its own: every block
+// publishes the lexicographic minimum of its kFinC candidates and the block that arrives last
+// reduces the published minima (finalize_argmin below).
+struct FinBest {
+    double* best;          // {objective, index bits} (null: no argmin)
+    double* mirror;        // mapped pinned host words {obj, idx, seq} (may be null)
+    uint64_t seq;
+    int64_t idx_base;
+    unsigned long long* blk;   // [gridDim.x][2] per-block minima {obj bits, index}
+    unsigned* arrive;          // arrival counter, zero between launches (the last block resets it)
+};
+
+__device__ __forceinline__ void argmin_take(double& v1, int& i1, double v2, int i2)
+{
+    if ((i2 >= 0) && (i1 < 0 || v2 < v1 || (v2 == v1 && i2 < i1))) {
+        v1 = v2;
+        i1 = i2;
+    }
+}
+
+// Wave 0 of every finalize block, lanes 0..kFinC-1 holding (o, k) of the block's candidates
+// (have: k < K). Cross-workgroup hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first
+// row of the sc1 table): lane 0 alone stores its block's minimum with 8-B agent-scope (sc1) stores,
+// waits for them (vmcnt(0)), then adds to ONE counter; the block whose add returns the last count
+// loads every minimum with sc1 loads, in the same wave. The lexicographic (objective, index)
+// minimum is order-independent, so the result equals argmin_kernel's; NaN / +inf never selected.
+__device__ __forceinline__ void finalize_argmin(const FinBest& fb, double o, int k, bool have)
+{
+    const int lane = threadIdx.x & (kWave - 1);
+    double bv = __builtin_inf();
+    int bi = -1;
+    if (have && lane < kFinC && o < bv) {
+        bv = o;
+        bi = k;
+    }
+#pragma unroll
+    for (int off = kFinC / 2; off >= 1; off >>= 1)
+        argmin_take(bv, bi, __shfl_xor(bv, off, kWave), __shfl_xor(bi, off, kWave));
+    unsigned old = 0;
+    if (lane == 0) {
+        __hip_atomic_store(fb.blk + 2 * blockIdx.x, __builtin_bit_cast(unsigned long long, bv),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(fb.blk + 2 * blockIdx.x + 1, (unsigned long long)(long long)bi,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        old = __hip_atomic_fetch_add(fb.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    old = __shfl(old, 0, kWave);
+    if (old != gridDim.x - 1) return;   // wave-uniform: not the last block
+    bv = __builtin_inf();
+    bi = -1;
+    for (unsigned q = lane; q < gridDim.x; q += kWave) {
+        const unsigned long long v = __hip_atomic_load(fb.blk + 2 * q, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long ix = __hip_atomic_load(fb.blk + 2 * q + 1, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+        argmin_take(bv, bi, __builtin_bit_cast(double, v), (int)(long long)ix);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+        argmin_take(bv, bi, __shfl_xor(bv, off, kWave), __shfl_xor(bi, off, kWave));
+    if (lane == 0) {
+        fb.best[0] = bi >= 0 ? bv : __builtin_inf();
+        const int64_t gidx = bi >= 0 ? fb.idx_base + bi : (int64_t)-1;
+        fb.best[1] = __builtin_bit_cast(double, gidx);
+        __hip_atomic_store(fb.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (fb.mirror) {  // pinned coherent host words: the result, then (released) its sequence
+            fb.mirror[0] = fb.best[0];
+            fb.mirror[1] = fb.best[1];
+            __threadfence_system();
+            __hip_atomic_store(reinterpret_cast<uint64_t*>(fb.mirror + 2), fb.seq, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
     const double* __restrict__ partial, const int* __restrict__ mode, int n_poll, int n_other,
     int K, int N, const int* __restrict__ map, const double* __restrict__ spart,
     const int* __restrict__ ncount, int counts, double w0,
-    const double* __restrict__ vp, double* __restrict__ area_out, double* __restrict__ obj_out)
+    const double* __restrict__ vp, double* __restrict__ area_out, double* __restrict__ obj_out,
+    FinBest fb, uint64_t* ts)
 {
+    ts_begin(ts);   // profiling only: the chain's last launch (k_common.h)
+    double o = __builtin_inf();   // lanes sg == 0: candidate k's objective (for the argmin)
     __shared__ double red[kFinThreads / kFinC][kFinC];
     const int t = threadIdx.x, c = t % kFinC, sg = t / kFinC;
     constexpr int SG = kFinThreads / kFinC;
@@ -127,8 +206,11 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
             for (int q = 0; q < SG; ++q) n += ired[q][c];
             const double area = (double)n * w0;
             if (area_out) area_out[k] = area;
-            if (obj_out) obj_out[k] = -area + vp[k];
+            if (vp) o = -area + vp[k];
+            if (obj_out) obj_out[k] = o;
         }
+        if (fb.best && t < kWave) finalize_argmin(fb, o, k, k < K);
+        ts_end(ts);
         return;
     }
     const bool rows = spart && poll;
@@ -166,8 +248,11 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
 #pragma unroll
         for (int q = 0; q < SG; ++q) area += red[q][c];
         if (area_out) area_out[k] = area;
-        if (obj_out) obj_out[k] = -area + vp[k];
+        if (vp) o = -area + vp[k];
+        if (obj_out) obj_out[k] = o;
     }
+    if (fb.best && t < kWave) finalize_argmin(fb, o, k, k < K);
+    ts_end(ts);
 }
 
 // Single block: lexicographic minimum over (obj, index); NaN / +inf never selected.
@@ -177,14 +262,6 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
 // 16 waves; each thread keeps its first minimum over k = t, t + 1024, ... (4 loads in flight),
 // then wave butterflies and one pass over the 16 wave results.
 constexpr int kArgThreads = 1024;
-
-__device__ __forceinline__ void argmin_take(double& v1, int& i1, double v2, int i2)
-{
-    if ((i2 >= 0) && (i1 < 0 || v2 < v1 || (v2 == v1 && i2 < i1))) {
-        v1 = v2;
-        i1 = i2;
-    }
-}
 
 __global__ __launch_bounds__(kArgThreads) void argmin_kernel(const double* __restrict__ obj, int K,
                                                              int64_t idx_base, double* __restrict__ best,

@@ -111,8 +111,9 @@ __device__ __forceinline__ float key_of(double v, double b, bool& ok)
 // (src.keysT, src.kbad; exact doubles from src.cands); else the generator (src.get), keyed here.
 template <bool kKeys>
 __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(8))) void disk_index_kernel(
-    CandSrc src, int N, int K, Grid g, PenArgs pa, int dedup, IndexOut o)
+    uint64_t* ts, CandSrc src, int N, int K, Grid g, PenArgs pa, int dedup, IndexOut o)
 {
+    ts_begin(ts);   // profiling only, when the index opens the chain (k_common.h)
     __shared__ float kx[kIndexMaxK + 1], ky[kIndexMaxK + 1], kr[kIndexMaxK + 1];
     __shared__ int table[kIndexSlots];       // owner candidate, then (owner << 12 | id)
     __shared__ uint16_t owner_of[kIndexMaxK + 1];
@@ -133,6 +134,7 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(8))
     // candidates of this thread: k = tid + j * kIdxThreads (j < kIdxPer), and thread 0 also
     // takes k = kIndexMaxK (a full MADS poll is 2n + 1 = kIndexMaxK + 1 candidates at most here)
     const bool fits = dedup && K > 0 && K <= kIndexMaxK + 1;
+    const double T3 = o.pen ? pen_threshold(pa, i) : 0.0;   // cons3 threshold of UAV i
 
     int4 R = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
     double span_area = 0.0;
@@ -224,7 +226,7 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(8))
             get3(k, x, y, r);
             add_span(x, y, r);
             o.urec[row + k] = make_disk(x, y, r);
-            if (o.pen) o.pen[row + k] = pen_term(x, y, r, i, N, pa);
+            if (o.pen) o.pen[row + k] = pen_term(x, y, r, i, N, pa, T3);
             o.umap[row + k] = k;
         }
         if (tid == 0) o.ucount[i] = K;
@@ -276,7 +278,7 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(8))
             const int u = table[slot[j]] & 0xfff;
             const double x = bx + (double)kx[k], y = by + (double)ky[k], r = br + (double)kr[k];
             o.umap[row + k] = u;
-            if (o.pen) o.pen[row + k] = pen_term(x, y, r, i, N, pa);
+            if (o.pen) o.pen[row + k] = pen_term(x, y, r, i, N, pa, T3);
             add_span(x, y, r);
         }
         if (tid == 0) o.ucount[i] = ucnt;
@@ -356,6 +358,7 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(8))
         }
     }
     MAC_IDX_STAMP(5);
+    ts_end(ts);
 }
 
 // disk i of candidate k through the index

@@ -19,22 +19,31 @@ struct PenArgs {
     const double* rmax;
     const double* prev;
     const double* dlimT;   // per UAV: cons3 holds iff s <= dlimT[i] (predicate.h dlim_threshold)
+    const double* dlim;    // ... or the raw d_lim[i], thresholded where it is read (dlimT == null)
     double tan_half_fov;
 };
 
+// UAV i's cons3 threshold: dlimT[i], or dlim_threshold(d_lim[i]) (evaluated once per disk by the
+// callers that loop over candidates, so the device API needs no threshold launch of its own)
+__device__ __forceinline__ double pen_threshold(const PenArgs& pa, int i)
+{
+    if (!pa.prev) return 0.0;
+    return pa.dlimT ? pa.dlimT[i] : dlim_threshold(pa.dlim[i]);
+}
+
 // Term i of candidate (x_i, y_i, R_i): |R_i - rmax_i| (0 without rmax), or -1 when UAV i's move
 // violates cons3 (sqrt(dx^2 + dy^2 + dz^2) > d_lim[i], z = R / tan(FOV/2), evaluated exactly as
-// s > dlimT[i]). A negative term marks the candidate infeasible; the finalize chain sums the
-// others sequentially in i (bit-exact with the reference's loop).
+// s > T3 = pen_threshold(pa, i)). A negative term marks the candidate infeasible; the finalize
+// chain sums the others sequentially in i (bit-exact with the reference's loop).
 __device__ __forceinline__ double pen_term(double x2, double y2, double R2, int i, int N,
-                                           const PenArgs& pa)
+                                           const PenArgs& pa, double T3)
 {
     if (pa.prev) {
         const double x1 = pa.prev[i], y1 = pa.prev[N + i], z1 = pa.prev[2 * N + i] / pa.tan_half_fov;
         const double z2 = R2 / pa.tan_half_fov;
         const double ddx = x1 - x2, ddy = y1 - y2, ddz = z1 - z2;
         const double s = ddx * ddx + ddy * ddy + ddz * ddz;
-        if (s > pa.dlimT[i]) return -1.0;
+        if (s > T3) return -1.0;
     }
     return pa.rmax ? __builtin_fabs(R2 - pa.rmax[i]) : 0.0;
 }
@@ -102,10 +111,11 @@ struct CandSrc {
 // fp64 copy are written here and read by the index.
 constexpr int kKeysK = 64;   // candidates per cands_keys_kernel tile (x 32 variables)
 
-__global__ __launch_bounds__(kBlock) void cands_keys_kernel(const double* __restrict__ cands, int n,
-                                                            int K, float* __restrict__ keysT,
+__global__ __launch_bounds__(kBlock) void cands_keys_kernel(uint64_t* ts, const double* __restrict__ cands,
+                                                            int n, int K, float* __restrict__ keysT,
                                                             int* __restrict__ kbad, int nkt)
 {
+    ts_begin(ts);   // profiling only (the chain's first launch: k_common.h)
     __shared__ float t[kKeysK][33];
     __shared__ int sbad[2][32];
     const int v0 = blockIdx.x * 32, k0 = blockIdx.y * kKeysK;
@@ -144,6 +154,7 @@ __global__ __launch_bounds__(kBlock) void cands_keys_kernel(const double* __rest
         const int tile = 2 * blockIdx.y + h;
         if (v < n && tile < nkt) kbad[(int64_t)v * nkt + tile] = sbad[h][vv];
     }
+    ts_end(ts);
 }
 
 // cands: see CandSrc. Writes disks[k*N + i] (scan walk) and, when pen != null,
@@ -156,7 +167,7 @@ __global__ void disk_prep_kernel(CandSrc src, int N, int K, DiskRec* __restrict_
     const int k = (int)(t / N), i = (int)(t % N);
     const double x = src.get(k, i, N), y = src.get(k, N + i, N), r = src.get(k, 2 * N + i, N);
     disks[t] = make_disk(x, y, r);
-    if (pen) pen[(int64_t)i * K + k] = pen_term(x, y, r, i, N, pa);
+    if (pen) pen[(int64_t)i * K + k] = pen_term(x, y, r, i, N, pa, pen_threshold(pa, i));
 }
 
 }  // namespace mac

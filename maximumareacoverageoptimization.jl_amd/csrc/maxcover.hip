@@ -128,7 +128,7 @@ struct Lane {
     hipEvent_t done = nullptr;
     DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode, pen, nbr,
         ncount, dlist, spart, vp, xinc, perm, ucount, umap, keysT, kbad, lane4, lanexp, rows, nboxT,
-        cnt, dlimraw;
+        cnt, dlimraw, finblk, finarrive;
     // the fused equal-weight poll (k_fused.h): keys, regions (generation-tagged), chains, counts,
     // neighbour lists, hand-off counters
     DevBuf f_keys, f_kbad, f_part, f_dtctr, f_vp, f_cnt, f_region, f_nbr, f_nboxT, f_ncount,
@@ -159,7 +159,10 @@ struct mac_ctx {
     // launch when the device picks the walk (mode != null): the launch that ran is read.
     // fused polls: a = launch 1, b = launch 2, mode = null, algo = MAC_ALGO_FUSED (the span is
     // taken over both launches)
-    struct Prof { int64_t a, na, b, nb; int64_t K; const int* mode; int algo; };
+    // c / f: the chain's first launch (cands_keys or the index) and its last (finalize), whose
+    // stamps give the whole poll chain's device span (-1: not stamped)
+    struct Prof { int64_t a, na, b, nb; int64_t K; const int* mode; int algo;
+                  int64_t c = -1, nc = 0, f = -1, nf = 0; };
     std::vector<Prof> prof;                          // recorded launches (guarded by mu)
     DevBuf stamps;
     int64_t stamp_cap = 0, stamp_used = 0;           // in workgroup slots (guarded by mu)
@@ -505,7 +508,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
     const int* d_mode = nullptr;
     // objective penalty terms + cons3 marks are written by the prep kernels (one term per disk
     // and candidate); the finalize kernel runs the sequential violation chain
-    const PenArgs pa{d_rmax, d_prev, d_dlimT, tan_half_fov};
+    const PenArgs pa{d_rmax, d_prev, d_dlimT, d_dlim_raw, tan_half_fov};
     double* d_pen = nullptr;           // penalty terms, pen[i*K + k]
     double* d_vp = nullptr;            // per-candidate penalty (or +inf: cons3)
     bool chain_done = false;           // the poll kernel ran the chains
@@ -523,7 +526,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
     }
     // Profiling: the measured walk launches stamp their own workgroups' start / end times
     // (k_common.h), so measuring adds no packet, event or dependency to the stream.
-    int64_t ts_a = -1, ts_na = 0, ts_b = -1, ts_nb = 0;
+    int64_t ts_a = -1, ts_na = 0, ts_b = -1, ts_nb = 0, ts_c = -1, ts_nc = 0, ts_f = -1, ts_nf = 0;
     auto take_ts = [&](int64_t nwg, int64_t& base, int64_t& n) -> uint64_t* {
         if (!ctx->profile) return nullptr;
         std::lock_guard<std::mutex> lk(ctx->mu);
@@ -537,7 +540,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         if (!ctx->profile || (ts_a < 0 && ts_b < 0)) return;
         std::lock_guard<std::mutex> lk(ctx->mu);
         ctx->prof.push_back({ts_a, ts_na, ts_b, ts_nb, (int64_t)K, d_mode,
-                             tiled ? MAC_ALGO_TILED : MAC_ALGO_SCAN});
+                             tiled ? MAC_ALGO_TILED : MAC_ALGO_SCAN, ts_c, ts_nc, ts_f, ts_nf});
     };
 
     if (N == 0 || M == 0) {  // no UAV or no entry: every area is 0 (the loops never run)
@@ -570,7 +573,6 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                            dim3(kBlock), 0, s, ts, ctx->xys.as<double2>(), ctx->ws.as<double>(), M,
                            L->disks.as<DiskRec>(), N, K, chunk, L->partial.as<double>());
         HCK(hipGetLastError());
-        prof_end();
     } else {
         const bool poll_possible = ctx->algo == MAC_ALGO_POLL ||
                                    (ctx->algo == MAC_ALGO_AUTO && K >= kPollMinK);
@@ -599,20 +601,23 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             const int nkt = (K + 31) / 32;
             L->keysT.reserve(sizeof(float) * (size_t)3 * N * K);
             L->kbad.reserve(sizeof(int) * (size_t)3 * N * nkt);
-            hipLaunchKernelGGL(cands_keys_kernel, dim3((3 * N + 31) / 32, (K + kKeysK - 1) / kKeysK),
-                               dim3(kBlock), 0, s,
+            const dim3 kgrid((3 * N + 31) / 32, (K + kKeysK - 1) / kKeysK);
+            uint64_t* tsk = take_ts((int64_t)kgrid.x * kgrid.y, ts_c, ts_nc);
+            hipLaunchKernelGGL(cands_keys_kernel, kgrid, dim3(kBlock), 0, s, tsk,
                                src.cands, 3 * N, K, L->keysT.as<float>(), L->kbad.as<int>(), nkt);
             HCK(hipGetLastError());
             isrc.keysT = L->keysT.as<float>();
             isrc.kbad = L->kbad.as<int>();
             isrc.nkt = nkt;
         }
+        const unsigned nidx = 8 * ((N + 7) / 8);
+        uint64_t* tsi = ts_c < 0 ? take_ts(nidx, ts_c, ts_nc) : nullptr;   // the index opens the chain
         if (isrc.cands)
-            hipLaunchKernelGGL(disk_index_kernel<true>, dim3(8 * ((N + 7) / 8)), dim3(kIdxThreads), 0, s,
-                               isrc, N, K, ctx->grid, pa, 1, io);
+            hipLaunchKernelGGL(disk_index_kernel<true>, dim3(nidx), dim3(kIdxThreads), 0, s,
+                               tsi, isrc, N, K, ctx->grid, pa, 1, io);
         else
-            hipLaunchKernelGGL(disk_index_kernel<false>, dim3(8 * ((N + 7) / 8)), dim3(kIdxThreads), 0, s,
-                               isrc, N, K, ctx->grid, pa, 1, io);
+            hipLaunchKernelGGL(disk_index_kernel<false>, dim3(nidx), dim3(kIdxThreads), 0, s,
+                               tsi, isrc, N, K, ctx->grid, pa, 1, io);
         HCK(hipGetLastError());
         const DiskRec* d_urec = L->disks.as<DiskRec>();
         const int* d_map = L->umap.as<int>();
@@ -682,22 +687,28 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             HCK(hipGetLastError());
             chain_done = true;
         }
-        prof_end();
     }
     if (d_obj && !chain_done) {
         hipLaunchKernelGGL(penalty_chain_kernel, dim3((K + kChainC - 1) / kChainC), dim3(kBlock), 0, s,
                            d_pen, K, N, penalty, d_vp);
         HCK(hipGetLastError());
     }
-    hipLaunchKernelGGL(finalize_kernel, dim3((K + kFinC - 1) / kFinC), dim3(kFinThreads), 0, s,
-                       L->partial.as<double>(), d_mode, n_poll, n_other, K, N, d_umap, d_spart, d_ncount,
-                       counts, ctx->w0, d_vp, d_area, d_obj);
-    HCK(hipGetLastError());
+    // finalize, with the poll argmin taken by its last-arriving block (k_final.h)
+    const unsigned nfin = (unsigned)((K + kFinC - 1) / kFinC);
+    FinBest fb{};
     if (d_best) {
-        hipLaunchKernelGGL(argmin_kernel, dim3(1), dim3(kArgThreads), 0, s, d_obj, K, idx_base, d_best,
-                           d_mirror, mirror_seq);
-        HCK(hipGetLastError());
+        L->finblk.reserve(2 * sizeof(unsigned long long) * nfin);
+        if (L->finarrive.grow(sizeof(unsigned)))   // zero once; the last block of each launch resets it
+            HCK(hipMemsetAsync(L->finarrive.p, 0, L->finarrive.cap, s));
+        fb = FinBest{d_best, d_mirror, mirror_seq, idx_base, L->finblk.as<unsigned long long>(),
+                     L->finarrive.as<unsigned>()};
     }
+    uint64_t* tsf = ts_c >= 0 ? take_ts(nfin, ts_f, ts_nf) : nullptr;
+    hipLaunchKernelGGL(finalize_kernel, dim3(nfin), dim3(kFinThreads), 0, s,
+                       L->partial.as<double>(), d_mode, n_poll, n_other, K, N, d_umap, d_spart, d_ncount,
+                       counts, ctx->w0, d_vp, d_area, d_obj, fb, tsf);
+    HCK(hipGetLastError());
+    prof_end();
 }
 
 static double dlim_threshold(double d) { return mac::dlim_threshold(d); }
@@ -912,7 +923,33 @@ int32_t mac_profile_split(mac_ctx* ctx, double* prep_ms, double* walk_ms, double
     double a1 = 0.0, a2 = 0.0, gap = 0.0;
     int64_t n = 0;
     for (auto& p : ctx->prof) {
-        if (p.algo != MAC_ALGO_FUSED) continue;
+        if (p.algo != MAC_ALGO_FUSED) {
+            // the launch chain: prep = first launch's start .. the walk's start, walk = the walk
+            // launch, gap = the walk's end .. finalize's end (the argmin included)
+            if (p.c < 0 || p.f < 0) continue;
+            int64_t wa = p.a, wn = p.na;
+            if (p.mode) {
+                int m = 0;
+                HCK(hipMemcpy(&m, p.mode, sizeof(int), hipMemcpyDeviceToHost));
+                if (m == kModePoll) {
+                    wa = p.b;
+                    wn = p.nb;
+                }
+            }
+            uint64_t s0 = ~(uint64_t)0, sw = ~(uint64_t)0, ew = 0, ef = 0;
+            for (int64_t q = p.c; q < p.c + p.nc; ++q) s0 = std::min(s0, st[(size_t)(2 * q)]);
+            for (int64_t q = wa; wa >= 0 && q < wa + wn; ++q) {
+                sw = std::min(sw, st[(size_t)(2 * q)]);
+                ew = std::max(ew, st[(size_t)(2 * q + 1)]);
+            }
+            for (int64_t q = p.f; q < p.f + p.nf; ++q) ef = std::max(ef, st[(size_t)(2 * q + 1)]);
+            if (!(ef > s0) || !(ew > sw) || sw < s0) continue;
+            a1 += (double)(sw - s0) / kRealtimeHz * 1e3;
+            a2 += (double)(ew - sw) / kRealtimeHz * 1e3;
+            gap += (double)(ef - ew) / kRealtimeHz * 1e3;
+            ++n;
+            continue;
+        }
         uint64_t s1 = ~(uint64_t)0, e1 = 0, s2 = ~(uint64_t)0, e2 = 0;
         for (int64_t q = p.a; q < p.a + p.na; ++q) {
             s1 = std::min(s1, st[(size_t)(2 * q)]);
@@ -981,7 +1018,7 @@ void mac_ctx_destroy(mac_ctx* ctx)
                           &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->pen, &l->nbr,
                           &l->ncount, &l->dlist, &l->spart, &l->vp, &l->xinc,
                           &l->perm, &l->ucount, &l->umap, &l->keysT, &l->kbad, &l->lane4,
-                          &l->lanexp, &l->rows, &l->nboxT, &l->cnt, &l->dlimraw, &l->f_keys,
+                          &l->lanexp, &l->rows, &l->nboxT, &l->cnt, &l->dlimraw, &l->finblk, &l->finarrive, &l->f_keys,
                           &l->f_kbad, &l->f_part, &l->f_dtctr, &l->f_vp, &l->f_cnt,
                           &l->f_region, &l->f_nbr, &l->f_nboxT, &l->f_ncount, &l->f_dlist, &l->f_ctl})
             b->release();
@@ -1019,7 +1056,7 @@ int32_t mac_set_option(mac_ctx* ctx, int32_t option, int64_t value)
         std::lock_guard<std::mutex> lk(ctx->mu);
         if (value && !ctx->profile) {  // fresh, zeroed stamp slots (outside any timed region)
             set_device(ctx);
-            constexpr int64_t kSlots = (int64_t)1 << 20;   // 16 MB: ~600 config-4 poll launches
+            constexpr int64_t kSlots = (int64_t)1 << 21;   // 32 MB: ~800 config-4 poll chains
             ctx->stamps.reserve(sizeof(uint64_t) * 2 * kSlots);
             HCK(hipDeviceSynchronize());
             HCK(hipMemset(ctx->stamps.p, 0, sizeof(uint64_t) * 2 * kSlots));
@@ -1200,7 +1237,7 @@ static void compute_flags(mac_ctx* ctx, hipStream_t s, const double* circles, in
         HCK(hipMemcpyAsync(ctx->circ.p, circles, sizeof(double) * 3 * N, hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(disk_prep_kernel, dim3(grid1d(N, 256)), dim3(256), 0, s,
                            matrix_src(ctx->circ.as<double>(), N), N, 1, ctx->cdisk.as<DiskRec>(),
-                           PenArgs{nullptr, nullptr, nullptr, 1.0}, nullptr);
+                           PenArgs{nullptr, nullptr, nullptr, nullptr, 1.0}, nullptr);
         HCK(hipGetLastError());
         const unsigned nb = (unsigned)std::max(1, std::min((N + kWavesPerBlock - 1) / kWavesPerBlock,
                                                            8 * ctx->cus));
@@ -1551,15 +1588,10 @@ int32_t mac_poll_best_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three
         HCK(hipStreamSynchronize(s));
         return MAC_OK;
     }
-    double* d_dlimT = nullptr;
+    // cons3: the raw d_lim goes down the chain; the kernels that read it threshold it once per
+    // UAV (k_prep.h pen_threshold)
+    const double* d_dlimT = nullptr;
     if (d_prev && !d_dlim) return fail(MAC_E_INVAL, "d_prev given without d_dlim");
-    if (d_prev && !use_fused(ctx, N, K)) {   // the legacy chain takes thresholds
-        L->dlim.reserve(sizeof(double) * std::max(N, 1));
-        hipLaunchKernelGGL(dlim_threshold_kernel, dim3(grid1d(std::max(N, 1), 256)), dim3(256), 0,
-                           s, d_dlim, N, L->dlim.as<double>());
-        HCK(hipGetLastError());
-        d_dlimT = L->dlim.as<double>();
-    }
     double* d_o = d_obj;
     if (!d_o) {
         L->obj.reserve(sizeof(double) * K);

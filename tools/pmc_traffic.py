@@ -10,7 +10,7 @@ pass) with --kernel-trace-free counter collection only. Corrections, per
   * on gfx950 FETCH_SIZE reports 1/2 of the bytes of wide coalesced reads, so it is doubled;
   * Infinity-Cache hits are counted by the memory-side counters, not excluded.
 Per kernel: 2 * FETCH + WRITE averaged over its launches. "hbm_bytes_per_poll" sums the kernels
-of one poll chain (--chain; the fused poll by default), which bench.py reports as
+of one poll chain (--chain; the default launch chain by default), which bench.py reports as
 roofline.traffic — only while the library sources hash to "src_sha" (bench.src_hash), i.e. the
 build that was profiled. Run the passes with `bench.py --no-extras` so that only the poll chain
 launches after set-up.
@@ -45,7 +45,8 @@ def main():
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("--config", type=int, default=4)
-    ap.add_argument("--chain", default="mac::fused_prep_kernel,mac::fused_walk_kernel",
+    ap.add_argument("--chain", default="mac::cands_keys_kernel,mac::disk_index_kernel<true>,"
+                    "mac::walk_setup_kernel,mac::coverage_poll_kernel,mac::finalize_kernel",
                     help="comma-separated kernels of one poll")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
