@@ -49,14 +49,15 @@ extern "C" {
 #define MAC_E_NOPOINTS    3  /* no point list set on the context                             */
 #define MAC_E_HIP         4  /* a HIP runtime call failed (see mac_last_error)               */
 #define MAC_E_NOMEM       5  /* device allocation failed                                     */
-#define MAC_E_LOSSY       6  /* f32 storage requested but a coordinate/weight is not exact   */
+#define MAC_E_LOSSY       6  /* reserved                                                      */
 #define MAC_E_NODEVICE    7  /* no HIP device / bad device index                             */
 
 /* ---- options (mac_set_option) --------------------------------------------------- */
 #define MAC_OPT_ALGO         1  /* MAC_ALGO_AUTO (default) | _SCAN | _TILED | _POLL             */
-#define MAC_OPT_STORAGE      2  /* MAC_STORE_F64 (default) | MAC_STORE_F32 (lossless coords)   */
+#define MAC_OPT_STORAGE      2  /* MAC_STORE_F64 only: the list is kept in fp64 (fp32 inputs go
+                                   through the *_f32 entry points, widened exactly); _F32 fails */
 #define MAC_OPT_TILE_POINTS  3  /* target points per spatial tile (default 4), set before points */
-#define MAC_OPT_PROFILE      4  /* 1: bracket every coverage-kernel launch with HIP events       */
+#define MAC_OPT_PROFILE      4  /* 1: the timed launches stamp their workgroups' start / end     */
 
 #define MAC_ALGO_AUTO   0
 #define MAC_ALGO_SCAN   1  /* streaming brute-force scan: every point against every disk     */
@@ -93,6 +94,13 @@ int32_t mac_set_points_records_f64(mac_ctx* ctx, const double* rec, int64_t M, i
 /* Same, from device-resident SoA arrays (borrowed for the call, copied). */
 int32_t mac_set_points_dev_f64(mac_ctx* ctx, const double* d_x, const double* d_y,
                                const double* d_w, int64_t M);
+/* fp32 point lists (SURVEY 8(b) *_f32): each float is widened to the double of the same value
+ * on the device and the list is then exactly the fp64 list of those values (the reference's
+ * Vector{Float64} would hold the same doubles after Float64(::Float32)). */
+int32_t mac_set_points_f32(mac_ctx* ctx, const float* x, const float* y, const float* w,
+                           int64_t M);
+int32_t mac_set_points_dev_f32(mac_ctx* ctx, const float* d_x, const float* d_y, const float* d_w,
+                               int64_t M);
 int32_t mac_num_points(mac_ctx* ctx, int64_t* M_out);
 /* Copy the current list (original order) back to host SoA arrays (each M_out entries). */
 int32_t mac_get_points_f64(mac_ctx* ctx, double* x, double* y, double* w);
@@ -165,6 +173,19 @@ int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const doub
                      double penalty, const double* prev, const double* d_lim, double tan_half_fov,
                      const mac_mads_params* params, double* x_out, mac_mads_stats* stats);
 
+/* fp32 candidates (config 3's "fp32" caller path; SURVEY 8(b) "*_f32: coords f32, accum f64"):
+ * the candidate matrix (and prev) are uploaded as floats and widened exactly on the device;
+ * coverage is then the reference's fp64 predicate on those doubles, areas accumulate in fp64 /
+ * integer counts, and the outputs equal the *_f64 calls on the widened inputs bit for bit.
+ * r_max and d_lim stay fp64 (model parameters, not coordinates). */
+int32_t mac_area_f32(mac_ctx* ctx, const float* circles, int64_t three_n, double* area_out);
+int32_t mac_area_batch_f32(mac_ctx* ctx, const float* cands, int64_t three_n, int64_t K,
+                           double* area_out);
+int32_t mac_poll_best_f32(mac_ctx* ctx, const float* cands, int64_t three_n, int64_t K,
+                          const double* r_max, double penalty, const float* prev,
+                          const double* d_lim, double tan_half_fov, double* obj_out,
+                          double* best_obj, int64_t* best_idx);
+
 /* ---- device-pointer, stream-ordered variants (inputs already resident in HBM) ----- */
 /* d_cands: 3N x K column-major on the context's device; d_area: K doubles. `stream` is a
  * hipStream_t (NULL = the context's own stream). Returns after enqueueing. */
@@ -176,24 +197,30 @@ int32_t mac_poll_best_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three
                               const double* d_rmax, double penalty,
                               const double* d_prev, const double* d_dlim, double tan_half_fov,
                               int64_t idx_base, double* d_obj, void* d_best, void* stream);
+/* Same with fp32 d_cands / d_prev (widened into the call's scratch on `stream` first). */
+int32_t mac_poll_best_dev_f32(mac_ctx* ctx, const float* d_cands, int64_t three_n, int64_t K,
+                              const double* d_rmax, double penalty,
+                              const float* d_prev, const double* d_dlim, double tan_half_fov,
+                              int64_t idx_base, double* d_obj, void* d_best, void* stream);
 /* Waits for `stream` (NULL = the context's own stream) and returns the 16 bytes a device poll
  * wrote to d_best, through a pinned staging buffer: the host side of one MADS poll step. */
 int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* best_obj,
                        int64_t* best_idx);
 
 /* ---- measurement ----------------------------------------------------------------- */
-/* With MAC_OPT_PROFILE = 1, every coverage-kernel launch (tiled walk or streaming scan) is
- * bracketed by HIP events recorded on the stream it runs on. Reads (waiting for the recorded
- * events) the summed kernel time in ms, the launch count and the candidates evaluated by
- * those launches, and the walk the LAST of them used (MAC_ALGO_SCAN / _TILED / _POLL, 0 =
- * none); reset != 0 clears the record. */
+/* With MAC_OPT_PROFILE = 1, the coverage-kernel launches (and the first and last launch of
+ * each poll chain) stamp their workgroups' start / end times (s_memrealtime, k_common.h): no
+ * packet or dependency is added to the stream. Reads (after a device sync) the summed coverage-
+ * kernel time in ms (last end - first start per launch), the launch count and the candidates
+ * evaluated by those launches, and the walk the LAST of them used (MAC_ALGO_SCAN / _TILED /
+ * _POLL / _FUSED, 0 = none); reset != 0 clears the record. */
 int32_t mac_profile_read(mac_ctx* ctx, double* kernel_ms, int64_t* launches,
                          int64_t* candidates, int32_t* last_algo, int32_t reset);
 
-/* Per-launch split of the fused polls recorded since the last reset (call before
- * mac_profile_read with reset): summed in-kernel spans of launch 1 (keys, penalty chains,
- * neighbour lists) and launch 2 (walk, shared entries, objective, argmin), the summed idle gap
- * between them, and the number of fused polls. */
+/* Split of the poll chains recorded since the last reset (call before mac_profile_read with
+ * reset), summed: launch chain: prep = first launch's first start .. the walk's first start,
+ * walk = the walk launch, gap = the walk's last end .. finalize's (+ argmin) last end; fused
+ * polls: launch 1, launch 2, the idle gap between them. polls = chains counted. */
 int32_t mac_profile_split(mac_ctx* ctx, double* prep_ms, double* walk_ms, double* gap_ms,
                           int64_t* polls);
 

@@ -52,6 +52,8 @@ EXPORTS = (
     "mac_fire_last_error", "mac_fire_thresholds", "mac_fire_create", "mac_fire_destroy",
     "mac_fire_initial_points", "mac_fire_step", "mac_fire_last_points", "mac_fire_get_grid",
     "mac_fire_set_grid",
+    "mac_set_points_f32", "mac_set_points_dev_f32", "mac_area_f32", "mac_area_batch_f32",
+    "mac_poll_best_f32", "mac_poll_best_dev_f32",
 )
 
 
@@ -93,6 +95,7 @@ class InexactError(MaxCoverError, ValueError):
 
 
 _dp = ctypes.POINTER(ctypes.c_double)
+_fp = ctypes.POINTER(ctypes.c_float)
 _i64p = ctypes.POINTER(ctypes.c_int64)
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _vp = ctypes.c_void_p
@@ -143,6 +146,14 @@ def _declare(L: ctypes.CDLL) -> None:
         "mac_fire_last_points": ([_vp, _dp, _i64, _i64p], _i32),
         "mac_fire_get_grid": ([_vp, _u8p], _i32),
         "mac_fire_set_grid": ([_vp, _u8p], _i32),
+        "mac_set_points_f32": ([_vp, _fp, _fp, _fp, _i64], _i32),
+        "mac_set_points_dev_f32": ([_vp, _vp, _vp, _vp, _i64], _i32),
+        "mac_area_f32": ([_vp, _fp, _i64, _dp], _i32),
+        "mac_area_batch_f32": ([_vp, _fp, _i64, _i64, _dp], _i32),
+        "mac_poll_best_f32": ([_vp, _fp, _i64, _i64, _dp, ctypes.c_double, _fp, _dp,
+                               ctypes.c_double, _dp, _dp, _i64p], _i32),
+        "mac_poll_best_dev_f32": ([_vp, _vp, _i64, _i64, _vp, ctypes.c_double, _vp, _vp,
+                                   ctypes.c_double, _i64, _vp, _vp, _vp], _i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -197,6 +208,14 @@ def _f64(a) -> np.ndarray:
 
 def _ptr(a: np.ndarray):
     return a.ctypes.data_as(_dp)
+
+
+def _f32(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+
+
+def _fptr(a: np.ndarray):
+    return a.ctypes.data_as(_fp)
 
 
 def _devptr(t) -> int:
@@ -280,6 +299,18 @@ class Context:
         if not (x.shape == y.shape == w.shape) or x.ndim != 1:
             raise ValueError("x, y, w must be 1-D arrays of equal length")
         _check(self._L.mac_set_points_f64(self._h, _ptr(x), _ptr(y), _ptr(w), x.size))
+
+    def set_points_f32(self, x, y, w) -> None:
+        """fp32 SoA arrays (mac_set_points_f32): widened exactly to the fp64 list."""
+        x, y, w = _f32(x), _f32(y), _f32(w)
+        if not (x.shape == y.shape == w.shape) or x.ndim != 1:
+            raise ValueError("x, y, w must be 1-D arrays of equal length")
+        _check(self._L.mac_set_points_f32(self._h, _fptr(x), _fptr(y), _fptr(w), x.size))
+
+    def set_points_device_f32(self, x, y, w, M: int | None = None) -> None:
+        """x, y, w: torch float32 tensors on this context's device (widened copies)."""
+        n = int(M if M is not None else x.numel())
+        _check(self._L.mac_set_points_dev_f32(self._h, _devptr(x), _devptr(y), _devptr(w), n))
 
     def set_points_records(self, rec) -> None:
         r = _f64(rec)
@@ -382,6 +413,49 @@ class Context:
         if want_all:
             return bo.value, int(bi.value), objs
         return bo.value, int(bi.value)
+
+    # -- fp32 candidates (*_f32: widened exactly on the device, fp64 decisions)
+    def area_f32(self, circles) -> float:
+        c = _f32(circles)
+        out = ctypes.c_double()
+        _check(self._L.mac_area_f32(self._h, _fptr(c), c.size, ctypes.byref(out)))
+        return out.value
+
+    def area_batch_f32(self, cands) -> np.ndarray:
+        c = _f32(cands)
+        if c.ndim != 2:
+            raise ValueError("cands must be K x 3N")
+        K, three_n = c.shape
+        out = np.empty(K)
+        _check(self._L.mac_area_batch_f32(self._h, _fptr(c), three_n, K, _ptr(out)))
+        return out
+
+    def poll_best_f32(self, cands, r_max, penalty: float = 1e5, prev=None, d_lim=None,
+                      tan_half_fov: float = 1.0, want_all: bool = False):
+        c = _f32(cands)
+        K, three_n = c.shape
+        rm = _f64(r_max)
+        pv = _f32(prev) if prev is not None else None
+        dl = _f64(d_lim) if d_lim is not None else None
+        objs = np.empty(K) if want_all else None
+        bo = ctypes.c_double()
+        bi = _i64()
+        _check(self._L.mac_poll_best_f32(
+            self._h, _fptr(c), three_n, K, _ptr(rm), float(penalty),
+            _fptr(pv) if pv is not None else None, _ptr(dl) if dl is not None else None,
+            float(tan_half_fov), _ptr(objs) if objs is not None else None,
+            ctypes.byref(bo), ctypes.byref(bi)))
+        if want_all:
+            return bo.value, int(bi.value), objs
+        return bo.value, int(bi.value)
+
+    def poll_best_dev_f32(self, d_cands, three_n: int, K: int, d_rmax, d_best,
+                          penalty: float = 1e5, d_prev=None, d_dlim=None, tan_half_fov: float = 1.0,
+                          idx_base: int = 0, d_obj=None, stream=None) -> None:
+        _check(self._L.mac_poll_best_dev_f32(
+            self._h, _devptr(d_cands), int(three_n), int(K), _devptr(d_rmax), float(penalty),
+            _devptr(d_prev), _devptr(d_dlim), float(tan_half_fov), int(idx_base),
+            _devptr(d_obj), _devptr(d_best), _devptr(stream)))
 
     # -- native MADS driver
     def mads_run(self, x0, r_max, penalty: float = 1e5, prev=None, d_lim=None,

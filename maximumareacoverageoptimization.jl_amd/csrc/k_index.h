@@ -37,7 +37,6 @@
 
 namespace mac {
 
-constexpr int kIndexSlots = 4096;            // LDS hash table (int32 slots)
 #ifdef MAC_DIAG
 __device__ uint64_t g_diag_index[8 * 65536];  // diagnostic build only: per-disk phase stamps
 #define MAC_IDX_STAMP(q) if (threadIdx.x == 0 && i < 65536) g_diag_index[8 * i + (q)] = __builtin_amdgcn_s_memrealtime()
@@ -46,9 +45,18 @@ __device__ uint64_t g_diag_index[8 * 65536];  // diagnostic build only: per-disk
 #endif
 constexpr int kIdxThreads = 1024;            // 16 waves: the phases are latency-bound
 constexpr int kIdxWaves = kIdxThreads / kWave;
-constexpr int kIdxPer = 3;                   // candidates per thread, held in registers
-constexpr int kIndexMaxK = kIdxThreads * kIdxPer;   // 3072 + 1 (below): larger polls use the
-                                                    // identity map (table load <= 3/4)
+// candidates per thread, held in registers: 3 up to K = 3073 (N <= 512: two workgroups per CU,
+// ~60 KB LDS), 6 up to K = 6145 (N <= 1024: one per CU, ~118 KB LDS); larger polls use the
+// identity map (one position per candidate: exact, only slower walks)
+constexpr int kIdxPer = 3;
+constexpr int kIdxPerWide = 6;
+constexpr int kIndexMaxK = kIdxThreads * kIdxPer;          // 3072 (+ 1, below)
+constexpr int kIndexMaxKWide = kIdxThreads * kIdxPerWide;  // 6144 (+ 1)
+template <int P> struct IdxShape {
+    static constexpr int MaxK = kIdxThreads * P;          // + 1: thread 0 takes k = MaxK
+    static constexpr int Slots = P <= 3 ? 4096 : 8192;    // table load <= 3/4
+    static constexpr int IdBits = P <= 3 ? 12 : 13;       // table word = owner << IdBits | id
+};
 
 __device__ __forceinline__ uint32_t key_hash(uint32_t a, uint32_t b, uint32_t c)
 {
@@ -109,13 +117,17 @@ __device__ __forceinline__ float key_of(double v, double b, bool& ok)
 // workgroups fit a CU and the whole index runs in one round at N = 512.
 // kKeys: a candidate matrix, whose fp32 keys and exactness flags cands_keys_kernel wrote
 // (src.keysT, src.kbad; exact doubles from src.cands); else the generator (src.get), keyed here.
-template <bool kKeys>
-__global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(8))) void disk_index_kernel(
+template <bool kKeys, int kPer>
+__global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPer <= 3 ? 8 : 4))) void disk_index_kernel(
     uint64_t* ts, CandSrc src, int N, int K, Grid g, PenArgs pa, int dedup, IndexOut o)
 {
+    constexpr int kIdxPer = kPer;
+    constexpr int kIndexMaxK = IdxShape<kPer>::MaxK;
+    constexpr int kIndexSlots = IdxShape<kPer>::Slots;
+    constexpr int kIdBits = IdxShape<kPer>::IdBits;
     ts_begin(ts);   // profiling only, when the index opens the chain (k_common.h)
     __shared__ float kx[kIndexMaxK + 1], ky[kIndexMaxK + 1], kr[kIndexMaxK + 1];
-    __shared__ int table[kIndexSlots];       // owner candidate, then (owner << 12 | id)
+    __shared__ int table[kIndexSlots];       // owner candidate, then (owner << kIdBits | id)
     __shared__ uint16_t owner_of[kIndexMaxK + 1];
     __shared__ int ucnt;
     __shared__ int sred[4][kIdxWaves];
@@ -264,7 +276,7 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(8))
             if (owner >= 0) {
                 const int u = atomicAdd(&ucnt, 1);
                 owner_of[u] = (uint16_t)owner;
-                table[q] = (owner << 12) | u;
+                table[q] = (owner << kIdBits) | u;
             }
         }
         __syncthreads();
@@ -275,7 +287,7 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(8))
         for (int j = 0; j < P; ++j) {
             const int k = j < kIdxPer ? tid + j * kIdxThreads : (tid == 0 ? kIndexMaxK : K);
             if (k >= K) continue;
-            const int u = table[slot[j]] & 0xfff;
+            const int u = table[slot[j]] & ((1 << kIdBits) - 1);
             const double x = bx + (double)kx[k], y = by + (double)ky[k], r = br + (double)kr[k];
             o.umap[row + k] = u;
             if (o.pen) o.pen[row + k] = pen_term(x, y, r, i, N, pa, T3);

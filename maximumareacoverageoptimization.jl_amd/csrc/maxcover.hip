@@ -16,6 +16,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "kernels.h"
@@ -26,6 +27,9 @@
 using namespace mac;
 
 static constexpr int kPollMinK = 64;          // below this the per-candidate walk always wins
+static constexpr int kTiledMaxN = 2048;       // the per-candidate walk keeps all N disks in LDS;
+                                              // more UAVs take the poll walk at any K (one
+                                              // workgroup per disk: a per-disk walk for K = 1)
 static constexpr double kPollCostRatio = 4.0; // poll walk if its visits <= 4x the other's
 
 // ------------------------------------------------------------------ errors
@@ -128,7 +132,7 @@ struct Lane {
     hipEvent_t done = nullptr;
     DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode, pen, nbr,
         ncount, dlist, spart, vp, xinc, perm, ucount, umap, keysT, kbad, lane4, lanexp, rows, nboxT,
-        cnt, dlimraw, finblk, finarrive;
+        cnt, dlimraw, finblk, finarrive, c32, p32;
     // the fused equal-weight poll (k_fused.h): keys, regions (generation-tagged), chains, counts,
     // neighbour lists, hand-off counters
     DevBuf f_keys, f_kbad, f_part, f_dtctr, f_vp, f_cnt, f_region, f_nbr, f_nboxT, f_ncount,
@@ -239,6 +243,30 @@ struct LaneGuard {
 };
 
 static inline unsigned grid1d(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
+
+// fp32 entry points (*_f32): every float is widened to the double of the same value (exact), and
+// the fp64 path then evaluates the reference predicate on those doubles.
+__global__ void widen_f32_kernel(const float* __restrict__ in, int64_t n, double* __restrict__ out)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) out[t] = (double)in[t];
+}
+
+static void widen_async(const float* d_in, int64_t n, double* d_out, hipStream_t s)
+{
+    if (n <= 0) return;
+    hipLaunchKernelGGL(widen_f32_kernel, dim3(grid1d(n, 256)), dim3(256), 0, s, d_in, n, d_out);
+    HCK(hipGetLastError());
+}
+
+// host floats -> device doubles through the device scratch `stage`
+static void upload_widen(const float* h, int64_t n, DevBuf& stage, double* d_out, hipStream_t s)
+{
+    if (n <= 0) return;
+    stage.reserve(sizeof(float) * (size_t)n);
+    HCK(hipMemcpyAsync(stage.p, h, sizeof(float) * (size_t)n, hipMemcpyHostToDevice, s));
+    widen_async(stage.as<float>(), n, d_out, s);
+}
 
 static inline CandSrc matrix_src(const double* d_cands, int N)
 {
@@ -374,7 +402,7 @@ static bool use_tiled(mac_ctx* ctx, int N, const double* h_cands, int64_t three_
 {
     if (N <= 0 || ctx->algo == MAC_ALGO_SCAN) return false;
     if (ctx->algo == MAC_ALGO_POLL) return true;        // no N limit: fixed LDS footprint
-    if (N > 2048) return false;                          // per-candidate walk keeps N disks in LDS
+    if (N > kTiledMaxN) return true;                     // the poll walk, whatever K (enqueue_eval)
     if (ctx->algo == MAC_ALGO_TILED) return true;
     if (!h_cands) return true;
     // AUTO with host candidates: compare the tiled walk's point visits for candidate 0 with
@@ -574,7 +602,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                            L->disks.as<DiskRec>(), N, K, chunk, L->partial.as<double>());
         HCK(hipGetLastError());
     } else {
-        const bool poll_possible = ctx->algo == MAC_ALGO_POLL ||
+        const bool big = N > kTiledMaxN;
+        const bool poll_possible = ctx->algo == MAC_ALGO_POLL || big ||
                                    (ctx->algo == MAC_ALGO_AUTO && K >= kPollMinK);
         // the disk index: distinct disks per UAV, their records / penalty terms, the map, and
         // each disk's region and walk costs (k_index.h)
@@ -596,7 +625,9 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                           poll_possible ? L->lanexp.as<float>() : nullptr,
                           poll_possible ? L->rows.as<int2>() : nullptr, ctx->off.as<int32_t>()};
         CandSrc isrc = src;
-        if (src.cands && K <= kIndexMaxK + 1) {  // matrix: fp32 keys, variable-major, so each
+        // candidates per index thread: 3 (K <= 3073), 6 (K <= 6145); larger: identity map
+        const int iper = K <= kIndexMaxK + 1 ? kIdxPer : K <= kIndexMaxKWide + 1 ? kIdxPerWide : 0;
+        if (src.cands && iper) {  // matrix: fp32 keys, variable-major, so each
                                                  // disk's K keys are a row
             const int nkt = (K + 31) / 32;
             L->keysT.reserve(sizeof(float) * (size_t)3 * N * K);
@@ -612,12 +643,19 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         }
         const unsigned nidx = 8 * ((N + 7) / 8);
         uint64_t* tsi = ts_c < 0 ? take_ts(nidx, ts_c, ts_nc) : nullptr;   // the index opens the chain
-        if (isrc.cands)
-            hipLaunchKernelGGL(disk_index_kernel<true>, dim3(nidx), dim3(kIdxThreads), 0, s,
-                               tsi, isrc, N, K, ctx->grid, pa, 1, io);
+        const int dedup = iper ? 1 : 0;
+        if (isrc.cands && iper == kIdxPerWide)
+            hipLaunchKernelGGL((disk_index_kernel<true, kIdxPerWide>), dim3(nidx), dim3(kIdxThreads), 0,
+                               s, tsi, isrc, N, K, ctx->grid, pa, dedup, io);
+        else if (isrc.cands)
+            hipLaunchKernelGGL((disk_index_kernel<true, kIdxPer>), dim3(nidx), dim3(kIdxThreads), 0, s,
+                               tsi, isrc, N, K, ctx->grid, pa, dedup, io);
+        else if (iper == kIdxPerWide)
+            hipLaunchKernelGGL((disk_index_kernel<false, kIdxPerWide>), dim3(nidx), dim3(kIdxThreads), 0,
+                               s, tsi, isrc, N, K, ctx->grid, pa, dedup, io);
         else
-            hipLaunchKernelGGL(disk_index_kernel<false>, dim3(nidx), dim3(kIdxThreads), 0, s,
-                               tsi, isrc, N, K, ctx->grid, pa, 1, io);
+            hipLaunchKernelGGL((disk_index_kernel<false, kIdxPer>), dim3(nidx), dim3(kIdxThreads), 0, s,
+                               tsi, isrc, N, K, ctx->grid, pa, dedup, io);
         HCK(hipGetLastError());
         const DiskRec* d_urec = L->disks.as<DiskRec>();
         const int* d_map = L->umap.as<int>();
@@ -627,13 +665,13 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             1, std::min<int64_t>((target + K - 1) / K, std::max(1, N / kWavesPerBlock)));
         n_other = G;
         L->partial.reserve(sizeof(double) * (size_t)K * std::max(G, poll_possible ? N : 1));
-        const bool run_tiled = ctx->algo != MAC_ALGO_POLL;
+        const bool run_tiled = ctx->algo != MAC_ALGO_POLL && !big;
         const int64_t units = (int64_t)K * G;
         if (poll_possible) {
             // walk choice + neighbour lists (poll) or the per-candidate walk itself, one launch;
             // when the poll walk is chosen the extra blocks just exit, so the per-candidate walk
             // gets one workgroup per CU (grid-striding over its units)
-            const int forced = ctx->algo == MAC_ALGO_POLL ? kModePoll : 0;
+            const int forced = (ctx->algo == MAC_ALGO_POLL || big) ? kModePoll : 0;
             L->nbr.reserve(sizeof(uint16_t) * (size_t)N * kPollNbr);
             L->ncount.reserve(sizeof(int) * (size_t)N);
             L->dlist.reserve(sizeof(int) * (size_t)N);
@@ -726,11 +764,13 @@ static int32_t check_common(mac_ctx* ctx, int64_t three_n, int64_t K)
 }
 
 // Host-pointer batch: upload, evaluate, download.
-static int32_t host_eval(mac_ctx* ctx, const double* cands, int64_t three_n, int64_t K,
-                         const double* r_max, double penalty, const double* prev,
+template <class T>
+static int32_t host_eval(mac_ctx* ctx, const T* cands, int64_t three_n, int64_t K,
+                         const double* r_max, double penalty, const T* prev,
                          const double* d_lim, double tan_half_fov, double* area_out,
                          double* obj_out, double* best_obj, int64_t* best_idx)
 {
+    constexpr bool f32 = std::is_same<T, float>::value;
     int32_t rc = check_common(ctx, three_n, K);
     if (rc) return rc;
     if (K == 0) {
@@ -748,9 +788,13 @@ static int32_t host_eval(mac_ctx* ctx, const double* cands, int64_t three_n, int
     L->area.reserve(sizeof(double) * K);
     L->obj.reserve(sizeof(double) * K);
     L->best.reserve(16);
-    if (three_n * K > 0)
-        HCK(hipMemcpyAsync(L->cands.p, cands, sizeof(double) * three_n * K, hipMemcpyHostToDevice,
-                           s));
+    if (three_n * K > 0) {
+        if constexpr (f32)
+            upload_widen(cands, three_n * K, L->c32, L->cands.as<double>(), s);
+        else
+            HCK(hipMemcpyAsync(L->cands.p, cands, sizeof(double) * three_n * K,
+                               hipMemcpyHostToDevice, s));
+    }
     const bool want_obj = obj_out || best_obj || best_idx;
     double* d_rmax = nullptr;
     if (want_obj && r_max && N > 0) {
@@ -767,14 +811,19 @@ static int32_t host_eval(mac_ctx* ctx, const double* cands, int64_t three_n, int
         L->dlimraw.reserve(sizeof(double) * N);
         L->h_dlim.resize(N);
         for (int i = 0; i < N; ++i) L->h_dlim[i] = dlim_threshold(d_lim[i]);
-        HCK(hipMemcpyAsync(L->prev.p, prev, sizeof(double) * three_n, hipMemcpyHostToDevice, s));
+        if constexpr (f32)
+            upload_widen(prev, three_n, L->p32, L->prev.as<double>(), s);
+        else
+            HCK(hipMemcpyAsync(L->prev.p, prev, sizeof(double) * three_n, hipMemcpyHostToDevice, s));
         HCK(hipMemcpyAsync(L->dlim.p, L->h_dlim.data(), sizeof(double) * N, hipMemcpyHostToDevice,
                            s));
         HCK(hipMemcpyAsync(L->dlimraw.p, d_lim, sizeof(double) * N, hipMemcpyHostToDevice, s));
         d_prev = L->prev.as<double>();
         d_dlimT = L->dlim.as<double>();
     }
-    const bool tiled = use_tiled(ctx, N, cands, three_n);
+    const double* hc = nullptr;
+    if constexpr (!f32) hc = cands;   // (AUTO's host-side walk estimate reads fp64 candidates)
+    const bool tiled = use_tiled(ctx, N, hc, three_n);
     enqueue_eval(ctx, L, s, matrix_src(L->cands.as<double>(), N), N, (int)K, tiled, d_rmax, penalty, d_prev,
                  d_dlimT, d_prev ? L->dlimraw.as<double>() : nullptr, tan_half_fov, L->area.as<double>(),
                  want_obj ? L->obj.as<double>() : nullptr,
@@ -1018,7 +1067,7 @@ void mac_ctx_destroy(mac_ctx* ctx)
                           &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->pen, &l->nbr,
                           &l->ncount, &l->dlist, &l->spart, &l->vp, &l->xinc,
                           &l->perm, &l->ucount, &l->umap, &l->keysT, &l->kbad, &l->lane4,
-                          &l->lanexp, &l->rows, &l->nboxT, &l->cnt, &l->dlimraw, &l->finblk, &l->finarrive, &l->f_keys,
+                          &l->lanexp, &l->rows, &l->nboxT, &l->cnt, &l->dlimraw, &l->finblk, &l->finarrive, &l->c32, &l->p32, &l->f_keys,
                           &l->f_kbad, &l->f_part, &l->f_dtctr, &l->f_vp, &l->f_cnt,
                           &l->f_region, &l->f_nbr, &l->f_nboxT, &l->f_ncount, &l->f_dlist, &l->f_ctl})
             b->release();
@@ -1048,7 +1097,9 @@ int32_t mac_set_option(mac_ctx* ctx, int32_t option, int64_t value)
     case MAC_OPT_STORAGE:
         if (value != MAC_STORE_F64 && value != MAC_STORE_F32)
             return fail(MAC_E_INVAL, "bad storage");
-        if (value == MAC_STORE_F32) return fail(MAC_E_INVAL, "f32 storage not available yet");
+        // the list stays fp64 in HBM: the walks' band decisions re-read exact coordinates, and
+        // fp32 inputs arrive through the *_f32 entry points, widened losslessly
+        if (value == MAC_STORE_F32) return fail(MAC_E_INVAL, "storage is fp64 (use the *_f32 entry points)");
         ctx->storage = (int)value;
         return MAC_OK;
     case MAC_OPT_PROFILE: {
@@ -1106,6 +1157,39 @@ int32_t mac_set_points_f64(mac_ctx* ctx, const double* x, const double* y, const
         HCK(hipMemcpyAsync(ctx->y.p, y, sizeof(double) * M, hipMemcpyHostToDevice, s));
         HCK(hipMemcpyAsync(ctx->w.p, w, sizeof(double) * M, hipMemcpyHostToDevice, s));
     }
+    build_index(ctx, s);
+    return MAC_OK;
+    ABI_END
+}
+
+int32_t mac_set_points_f32(mac_ctx* ctx, const float* x, const float* y, const float* w, int64_t M)
+{
+    ABI_BEGIN
+    if (M > 0 && (!x || !y || !w)) return fail(MAC_E_INVAL, "null point array");
+    int32_t rc = set_points_common(ctx, M);
+    if (rc) return rc;
+    hipStream_t s = ctx->setup_stream;
+    upload_widen(x, M, ctx->tmp, ctx->x.as<double>(), s);
+    HCK(hipStreamSynchronize(s));   // (one staging buffer, reused per coordinate)
+    upload_widen(y, M, ctx->tmp, ctx->y.as<double>(), s);
+    HCK(hipStreamSynchronize(s));
+    upload_widen(w, M, ctx->tmp, ctx->w.as<double>(), s);
+    build_index(ctx, s);
+    return MAC_OK;
+    ABI_END
+}
+
+int32_t mac_set_points_dev_f32(mac_ctx* ctx, const float* d_x, const float* d_y, const float* d_w,
+                               int64_t M)
+{
+    ABI_BEGIN
+    if (M > 0 && (!d_x || !d_y || !d_w)) return fail(MAC_E_INVAL, "null point array");
+    int32_t rc = set_points_common(ctx, M);
+    if (rc) return rc;
+    hipStream_t s = ctx->setup_stream;
+    widen_async(d_x, M, ctx->x.as<double>(), s);
+    widen_async(d_y, M, ctx->y.as<double>(), s);
+    widen_async(d_w, M, ctx->w.as<double>(), s);
     build_index(ctx, s);
     return MAC_OK;
     ABI_END
@@ -1505,7 +1589,7 @@ int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, doubl
 {
     ABI_BEGIN
     if (!area_out) return fail(MAC_E_INVAL, "null area_out");
-    return host_eval(ctx, circles, three_n, 1, nullptr, 0.0, nullptr, nullptr, 1.0, area_out,
+    return host_eval<double>(ctx, circles, three_n, 1, nullptr, 0.0, nullptr, nullptr, 1.0, area_out,
                      nullptr, nullptr, nullptr);
     ABI_END
 }
@@ -1515,7 +1599,7 @@ int32_t mac_area_batch_f64(mac_ctx* ctx, const double* cands, int64_t three_n, i
 {
     ABI_BEGIN
     if (!area_out && K > 0) return fail(MAC_E_INVAL, "null area_out");
-    return host_eval(ctx, cands, three_n, K, nullptr, 0.0, nullptr, nullptr, 1.0, area_out,
+    return host_eval<double>(ctx, cands, three_n, K, nullptr, 0.0, nullptr, nullptr, 1.0, area_out,
                      nullptr, nullptr, nullptr);
     ABI_END
 }
@@ -1526,7 +1610,7 @@ int32_t mac_objective_batch_f64(mac_ctx* ctx, const double* cands, int64_t three
     ABI_BEGIN
     if (!obj_out && K > 0) return fail(MAC_E_INVAL, "null obj_out");
     if (!r_max && three_n > 0) return fail(MAC_E_INVAL, "null r_max");
-    return host_eval(ctx, cands, three_n, K, r_max, penalty, nullptr, nullptr, 1.0, nullptr,
+    return host_eval<double>(ctx, cands, three_n, K, r_max, penalty, nullptr, nullptr, 1.0, nullptr,
                      obj_out, nullptr, nullptr);
     ABI_END
 }
@@ -1539,8 +1623,40 @@ int32_t mac_poll_best_f64(mac_ctx* ctx, const double* cands, int64_t three_n, in
     ABI_BEGIN
     if (!best_obj || !best_idx) return fail(MAC_E_INVAL, "null best output");
     if (!r_max && three_n > 0) return fail(MAC_E_INVAL, "null r_max");
-    return host_eval(ctx, cands, three_n, K, r_max, penalty, prev, d_lim, tan_half_fov, nullptr,
+    return host_eval<double>(ctx, cands, three_n, K, r_max, penalty, prev, d_lim, tan_half_fov, nullptr,
                      obj_out, best_obj, best_idx);
+    ABI_END
+}
+
+int32_t mac_area_f32(mac_ctx* ctx, const float* circles, int64_t three_n, double* area_out)
+{
+    ABI_BEGIN
+    if (!area_out) return fail(MAC_E_INVAL, "null area_out");
+    return host_eval<float>(ctx, circles, three_n, 1, nullptr, 0.0, nullptr, nullptr, 1.0, area_out,
+                            nullptr, nullptr, nullptr);
+    ABI_END
+}
+
+int32_t mac_area_batch_f32(mac_ctx* ctx, const float* cands, int64_t three_n, int64_t K,
+                           double* area_out)
+{
+    ABI_BEGIN
+    if (!area_out && K > 0) return fail(MAC_E_INVAL, "null area_out");
+    return host_eval<float>(ctx, cands, three_n, K, nullptr, 0.0, nullptr, nullptr, 1.0, area_out,
+                            nullptr, nullptr, nullptr);
+    ABI_END
+}
+
+int32_t mac_poll_best_f32(mac_ctx* ctx, const float* cands, int64_t three_n, int64_t K,
+                          const double* r_max, double penalty, const float* prev,
+                          const double* d_lim, double tan_half_fov, double* obj_out,
+                          double* best_obj, int64_t* best_idx)
+{
+    ABI_BEGIN
+    if (!best_obj || !best_idx) return fail(MAC_E_INVAL, "null best output");
+    if (!r_max && three_n > 0) return fail(MAC_E_INVAL, "null r_max");
+    return host_eval<float>(ctx, cands, three_n, K, r_max, penalty, prev, d_lim, tan_half_fov,
+                            nullptr, obj_out, best_obj, best_idx);
     ABI_END
 }
 
@@ -1562,21 +1678,40 @@ int32_t mac_area_batch_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t thre
     ABI_END
 }
 
-int32_t mac_poll_best_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three_n, int64_t K,
-                              const double* d_rmax, double penalty, const double* d_prev,
-                              const double* d_dlim, double tan_half_fov, int64_t idx_base,
-                              double* d_obj, void* d_best, void* stream)
+}  // extern "C" (the template below has C++ linkage)
+
+template <class T>
+static int32_t poll_best_dev(mac_ctx* ctx, const T* d_cands_in, int64_t three_n, int64_t K,
+                             const double* d_rmax, double penalty, const T* d_prev_in,
+                             const double* d_dlim, double tan_half_fov, int64_t idx_base,
+                             double* d_obj, void* d_best, void* stream)
 {
-    ABI_BEGIN
+    constexpr bool f32 = std::is_same<T, float>::value;
     int32_t rc = check_common(ctx, three_n, K);
     if (rc) return rc;
     if (!d_best) return fail(MAC_E_INVAL, "null d_best");
-    if (K > 0 && !d_cands) return fail(MAC_E_INVAL, "null d_cands");
+    if (K > 0 && !d_cands_in) return fail(MAC_E_INVAL, "null d_cands");
     set_device(ctx);
     hipStream_t s = stream ? (hipStream_t)stream : ctx->dev_stream;
     LaneGuard lg(ctx, s);
     Lane* L = lg.lane;
     const int N = (int)(three_n / 3);
+    const double* d_cands;
+    const double* d_prev;
+    if constexpr (f32) {   // widened into the lane's scratch, stream-ordered before the chain
+        L->cands.reserve(sizeof(double) * (size_t)std::max<int64_t>(three_n * K, 1));
+        widen_async(d_cands_in, three_n * K, L->cands.as<double>(), s);
+        d_cands = L->cands.as<double>();
+        d_prev = nullptr;
+        if (d_prev_in) {
+            L->prev.reserve(sizeof(double) * (size_t)std::max<int64_t>(three_n, 1));
+            widen_async(d_prev_in, three_n, L->prev.as<double>(), s);
+            d_prev = L->prev.as<double>();
+        }
+    } else {
+        d_cands = d_cands_in;
+        d_prev = d_prev_in;
+    }
     if (K == 0) {
         {
             std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1616,6 +1751,29 @@ int32_t mac_poll_best_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three
                  penalty, d_prev, d_dlimT, d_dlim, tan_half_fov, nullptr, d_o, (double*)d_best, idx_base,
                  d_mirror, seq);
     return MAC_OK;
+}
+
+extern "C" {
+
+int32_t mac_poll_best_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three_n, int64_t K,
+                              const double* d_rmax, double penalty, const double* d_prev,
+                              const double* d_dlim, double tan_half_fov, int64_t idx_base,
+                              double* d_obj, void* d_best, void* stream)
+{
+    ABI_BEGIN
+    return poll_best_dev<double>(ctx, d_cands, three_n, K, d_rmax, penalty, d_prev, d_dlim,
+                                 tan_half_fov, idx_base, d_obj, d_best, stream);
+    ABI_END
+}
+
+int32_t mac_poll_best_dev_f32(mac_ctx* ctx, const float* d_cands, int64_t three_n, int64_t K,
+                              const double* d_rmax, double penalty, const float* d_prev,
+                              const double* d_dlim, double tan_half_fov, int64_t idx_base,
+                              double* d_obj, void* d_best, void* stream)
+{
+    ABI_BEGIN
+    return poll_best_dev<float>(ctx, d_cands, three_n, K, d_rmax, penalty, d_prev, d_dlim,
+                                tan_half_fov, idx_base, d_obj, d_best, stream);
     ABI_END
 }
 

@@ -196,7 +196,9 @@ def test_fuzz_vs_oracle(ctx, pkg, orc, seed):
         assert np.array_equal(got, want), (a, seed, np.flatnonzero(got != want)[:5])
 
 
-def test_many_uavs_falls_back_to_scan(ctx, pkg, orc):
+def test_many_uavs_single_candidate(ctx, pkg, orc):
+    """N = 2100 UAVs, above the per-candidate walk's LDS limit (2048 disks): AUTO and 'tiled' take
+    the poll walk (one workgroup per disk; K = 1), 'scan' the brute force; all == the oracle."""
     wl = pkg.workloads
     rng = wl.SplitMix64(55)
     x, y, w = wl.grid_points(60)
@@ -378,6 +380,35 @@ def test_config4_full_poll(ctx, pkg, orc, algo):
         got_scan = ctx.area_batch(C[::384])
         ctx.set_algo("auto")
         assert np.array_equal(got_scan, 25.0 * cnt[::384])
+
+
+@pytest.mark.parametrize("N", [600, 2100])
+def test_many_uav_full_poll_auto(ctx, pkg, orc, N):
+    """Polls past config 4's shape (src/TDM_STATIC_opt.jl:123: n = 3N, no cap). N = 600: K = 3601
+    takes the wide disk index (6 candidates per thread, K <= 6145); N = 2100: K = 12601 takes the
+    identity map and the poll walk (more disks than the per-candidate walk holds). AUTO through
+    the device poll: sampled candidates == 25 x the exact lattice count; every objective ==
+    -area + 1e5 x the sequential violation of the reported area; the argmin of those."""
+    wl = pkg.workloads
+    rng = wl.SplitMix64(600 + N)
+    G = 1024
+    x, y, w = wl.grid_points(G)
+    ctx.set_points(x, y, w)
+    x0 = wl.uniform_disks(N, G, rng)
+    C = wl.poll_candidates(x0, rng)
+    K = C.shape[0]
+    assert K == 6 * N + 1
+    rmax = np.full(N, 30.0 * TAN50)
+    ctx.set_algo("auto")
+    area = ctx.area_batch(C)
+    pick = np.unique(np.concatenate([[0, K - 1], np.floor(rng.uniform(24) * K).astype(np.int64)]))
+    cnt = orc.lattice_count_batch(C[pick], G)
+    assert np.array_equal(area[pick], 25.0 * cnt.astype(np.float64)), (N, pick)
+    bo, bi, objs = ctx.poll_best(C, rmax, want_all=True)
+    want = -area + orc.violation_batch(C, rmax) * 1e5
+    assert np.array_equal(objs, want)
+    k = int(np.argmin(want))
+    assert bi == k and bo == want[k]
 
 
 @pytest.mark.parametrize("algo", ["auto", "fused", "poll"])
