@@ -171,13 +171,18 @@ def cpu_baseline(x, y, w, cands, seconds_target: float, threads: int):
     return n / dt, desc
 
 
-def bench_config5(args, pkg, dev_index):
+def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
     """Config 5: src/FullSimulation.jl's optimisation loop with the CA fire (src/DynamicArea.jl)
     streamed into the device list. One step = one MPC timestep: fire step + append/re-index,
     rmvCoveredPOI by the previous circles, and a native MADS run (mac_mads_run, N_iter
     iterations of a complete 2n-candidate poll). value = candidates evaluated / second over the
-    timed MPC steps, everything inside the step included."""
+    timed MPC steps, everything inside the step included. On P GPUs every rank regenerates the
+    deterministic fire stream on its own GPU (no point transfer) and polls its shard of every
+    LTMADS poll, one 16-B all-gather per MADS iteration (strong scaling: the same polls)."""
     import torch
+    import torch.distributed as dist
+    from importlib import import_module
+    pdist = import_module(pkg.__name__ + ".dist")
     wl = pkg.workloads
     cfg = wl.CONFIGS[5]
     rng = wl.SplitMix64(args.seed)
@@ -185,7 +190,10 @@ def bench_config5(args, pkg, dev_index):
     ctx = pkg.Context(dev_index)
     t_set = time.perf_counter()
     D = pkg.DynamicArea.DynamicArea(**fire_kw, seed=args.seed, device=dev_index)
-    sim = pkg.FullSimulation.Simulation(ctx, x0, fire=D, N_iter=args.mads_iters, seed=args.seed)
+    shard = (rank, world) if world > 1 else None
+    gather = pdist.make_gather(coll_dev) if world > 1 else None
+    sim = pkg.FullSimulation.Simulation(ctx, x0, fire=D, N_iter=args.mads_iters, seed=args.seed,
+                                        shard=shard, gather=gather)
     t_set = time.perf_counter() - t_set
     for _ in range(args.warmup):
         sim.step()
@@ -193,13 +201,34 @@ def bench_config5(args, pkg, dev_index):
     ctx.profile(True)
     ctx.profile_read(reset=True)
     recs = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         recs.append(sim.step())
+    if world > 1:
+        dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     k_ms, k_launches, k_cands, k_walk = ctx.profile_read(reset=True)
     ctx.profile(False)
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        # every rank must hold the same iterates (lock-step check, 8 B per rank)
+        h = torch.tensor([float(np.sum(sim.outputs[-1] * np.arange(1, sim.outputs[-1].size + 1)))],
+                         dtype=torch.float64, device=coll_dev)
+        hs = [torch.empty_like(h) for _ in range(world)]
+        dist.all_gather(hs, h)
+        lockstep = len({float(v.item()) for v in hs}) == 1
+    else:
+        lockstep = None
+    if rank != 0:
+        D.close()
+        ctx.close()
+        return
     evals = sum(r["evaluations"] for r in recs)
     M_avg = float(np.mean([r["points"] for r in recs]))
     b_eval = 24 * M_avg + 24 * cfg["N"] + 8
@@ -207,7 +236,7 @@ def bench_config5(args, pkg, dev_index):
     cands_per_launch = k_cands / max(k_launches, 1)
     achieved = b_eval * cands_per_launch / (avg_launch_ms * 1e-3) / 1e9 if k_launches else None
     cpu = None
-    if not args.no_cpu:
+    if not args.no_cpu and world == 1:
         x, y, w = ctx.get_points()
         polls = wl.poll_candidates(sim.x_prev, wl.SplitMix64(args.seed + 1))
         threads, cinfo = usable_cpus()
@@ -218,7 +247,7 @@ def bench_config5(args, pkg, dev_index):
         except Exception as e:  # report, never fake
             log("cpu baseline failed:", e)
     out = {
-        "metric": METRIC, "value": evals / elapsed, "unit": "evals/s", "n_gpus": 1,
+        "metric": METRIC, "value": evals / elapsed, "unit": "evals/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (seeded CA fire)",
@@ -232,7 +261,10 @@ def bench_config5(args, pkg, dev_index):
             "evaluations": evals,
             "time_split_s": {k: float(np.sum([r[k] for r in recs]))
                              for k in ("fire_s", "remove_s", "mads_s")},
-            "parallelism": "1 GPU",
+            "parallelism": ("1 GPU" if world == 1 else
+                            f"{world} GPUs: every poll's 2n candidates sharded, 16-B all-gather "
+                            f"per MADS iteration; fire stream regenerated per GPU"),
+            "ranks_in_lockstep": lockstep,
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -304,9 +336,11 @@ def main():
     pdist = import_module(pkg.__name__ + ".dist")
     wl = pkg.workloads
     if args.config == 5:
-        if world != 1:
-            raise SystemExit("config 5 runs on one GPU (the native MADS loop is not sharded yet)")
-        return bench_config5(args, pkg, dev_index)
+        bench_config5(args, pkg, dev_index, rank, world, coll_dev)
+        if distributed:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     cfg = wl.CONFIGS[args.config]
     G, N = cfg["G"], cfg["N"]

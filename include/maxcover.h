@@ -173,6 +173,28 @@ int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const doub
                      double penalty, const double* prev, const double* d_lim, double tan_half_fov,
                      const mac_mads_params* params, double* x_out, mac_mads_stats* stats);
 
+/* The same loop one iteration at a time, for the multi-GPU poll (BASELINE config 5 "8 GPUs";
+ * src/TDM_STATIC_opt.jl:129, SetMaxEvals's poll-level parallelism). A stepper owns the shard
+ * [shard_lo, shard_hi) of every poll's 2n candidates (0, 2n: the whole poll, as mac_mads_run):
+ *   mac_mads_poll    done = 1 once the iteration limit or ell < 0 is reached; otherwise evaluates
+ *                    this iteration's shard (generated on the device) and returns its best
+ *                    (objective, poll-wide index) (+inf, -1 for an empty shard or no feasible
+ *                    candidate);
+ *   mac_mads_update  applies the poll's best over ALL shards (the lexicographic (objective,
+ *                    index) minimum of the ranks' results, e.g. a 16-B all-gather): the
+ *                    incumbent, ell and the stream position advance exactly as in mac_mads_run,
+ *                    so every rank stays in lock step with the single-GPU loop;
+ *   mac_mads_result  x and the statistics (evaluations count whole polls). */
+typedef struct mac_mads mac_mads;
+int32_t mac_mads_begin(mac_ctx* ctx, const double* x0, int64_t three_n, const double* r_max,
+                       double penalty, const double* prev, const double* d_lim, double tan_half_fov,
+                       const mac_mads_params* params, int64_t shard_lo, int64_t shard_hi,
+                       mac_mads** out);
+int32_t mac_mads_poll(mac_mads* m, int32_t* done, double* best_obj, int64_t* best_idx);
+int32_t mac_mads_update(mac_mads* m, double best_obj, int64_t best_idx);
+int32_t mac_mads_result(mac_mads* m, double* x_out, mac_mads_stats* stats);
+void mac_mads_destroy(mac_mads* m);
+
 /* fp32 candidates (config 3's "fp32" caller path; SURVEY 8(b) "*_f32: coords f32, accum f64"):
  * the candidate matrix (and prev) are uploaded as floats and widened exactly on the device;
  * coverage is then the reference's fp64 predicate on those doubles, areas accumulate in fp64 /

@@ -11,7 +11,11 @@ Per timestep t (:42-100):
   5. The MADS input is drone_locs for t < 3, else the previous MADS output, unless it violates
      cons3 (:82-93).
   6. MADS (N_iter iterations) on the device: mac_mads_run, one complete LTMADS poll per
-     iteration (:84-95).
+     iteration (:84-95). On P GPUs (``shard = (rank, P)``, config 5 "8 GPUs") every rank runs
+     steps 1-5 itself — the fire CA is deterministic, so each GPU regenerates the same point
+     list with no transfer — and polls its shard of every LTMADS poll (mac_mads_begin / _poll /
+     _update); ``gather`` (dist.make_gather: a 16-B all-gather) combines the ranks' bests, so
+     every rank holds the single-GPU iterates.
 The trajectory stage (ALTRO, :107-251) is out of scope. The next step's circles are taken to be
 the MADS output, i.e. perfect tracking, which the reference's trajectory stage aims at.
 """
@@ -62,7 +66,8 @@ class Simulation:
 
     def __init__(self, ctx: Context, starting_circles, *, fire: DynamicArea | None = None,
                  firepoints=None, initial_points=None, N_iter: int = N_iter, d_lim=None,
-                 r_max=None, seed: int = 20250216, ell0: int = 2, ell_max: int = 6):
+                 r_max=None, seed: int = 20250216, ell0: int = 2, ell_max: int = 6,
+                 shard=None, gather=None):
         self.ctx = ctx
         self.x_prev = np.asarray(starting_circles, dtype=np.float64).copy()
         self.N = N = self.x_prev.size // 3
@@ -72,6 +77,8 @@ class Simulation:
                       else np.asarray(r_max, dtype=np.float64).copy())
         self.fire, self.firepoints = fire, firepoints
         self.N_iter, self.seed, self.ell0, self.ell_max = N_iter, seed, ell0, ell_max
+        self.shard = shard          # (rank, world) or None: the whole poll on this GPU
+        self.gather = gather
         if fire is not None:
             ctx.set_points_records(fire.initial_points())
         elif firepoints is not None:
@@ -108,9 +115,18 @@ class Simulation:
             single_input = self.outputs[-1]
             if not cons3_ok(self.x_prev, single_input, self.d_lim):     # :88-90
                 single_input = drone_locs
-        x_out, st = ctx.mads_run(single_input, self.r_max, 1e5, prev=self.x_prev,
-                                 d_lim=self.d_lim, tan_half_fov=self.tan, n_iter=self.N_iter,
-                                 ell0=self.ell0, ell_max=self.ell_max, seed=self.seed + t)
+        kw = dict(prev=self.x_prev, d_lim=self.d_lim, tan_half_fov=self.tan, n_iter=self.N_iter,
+                  ell0=self.ell0, ell_max=self.ell_max, seed=self.seed + t)
+        if self.shard is None or self.shard[1] == 1:
+            x_out, st = ctx.mads_run(single_input, self.r_max, 1e5, **kw)
+        else:
+            from .dist import mads_loop, shard_range
+            lo, hi = shard_range(2 * single_input.size, *self.shard)
+            stepper = ctx.mads_stepper(single_input, self.r_max, 1e5, shard=(lo, hi), **kw)
+            try:
+                x_out, st = mads_loop(stepper, self.gather)
+            finally:
+                stepper.close()
         t3 = time.perf_counter()
         self.outputs.append(x_out)
         rec = dict(t=t, points=int(ctx.num_points), added=int(added), kept=int(kept.size),

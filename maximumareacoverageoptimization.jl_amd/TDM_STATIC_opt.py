@@ -144,6 +144,52 @@ def mads(input, obj, cons_ext=(), N_iter: int = 100, ell0: int = 2, ell_max: int
     return res
 
 
+class PollStepper:
+    """Host mirror of the native stepper (mac_mads_begin / _poll / _update, include/maxcover.h),
+    driven by ``dist.mads_loop``: the poll sequence of ``mads`` (same stream, same update rule),
+    of which this stepper evaluates only the shard [lo, hi) of every poll's 2n candidates, through
+    ``poll_fn(X_shard) -> (best_obj, best_local_index)`` (index -1: nothing feasible). Every rank
+    draws the whole basis, so all ranks stay at the same stream position."""
+
+    def __init__(self, x0, f0: float, poll_fn, N_iter: int = 100, ell0: int = 2,
+                 ell_max: int = 6, seed: int = 20250216, shard=None):
+        self.x = np.asarray(x0, dtype=np.float64).copy()
+        self.n = self.x.size
+        self.f = float(f0)
+        self.poll_fn = poll_fn
+        self.N_iter, self.ell, self.ell_max = N_iter, ell0, ell_max
+        self.rng = SplitMix64(seed)
+        self.it = 0
+        self.evals = 1
+        self.lo, self.hi = (0, 2 * self.n) if shard is None else (int(shard[0]), int(shard[1]))
+        self._X = None
+
+    def poll(self):
+        if self.it >= self.N_iter or self.ell < 0:
+            return True, np.inf, -1
+        self.it += 1
+        B = ltmads_basis(self.n, self.ell, self.rng).astype(np.float64)
+        self._X = np.concatenate([self.x[None, :] + B.T, self.x[None, :] - B.T], axis=0)
+        Xs = self._X[self.lo:self.hi]
+        if Xs.shape[0] == 0:
+            return False, np.inf, -1
+        bo, bi = self.poll_fn(Xs)
+        return False, float(bo), (self.lo + int(bi) if bi >= 0 else -1)
+
+    def update(self, best_obj: float, best_idx: int) -> None:
+        self.evals += 2 * self.n
+        if best_idx >= 0 and best_obj < self.f:
+            self.x = self._X[best_idx].copy()
+            self.f = float(best_obj)
+            self.ell = min(self.ell + 1, self.ell_max)
+        else:
+            self.ell -= 1
+
+    def result(self):
+        return self.x.copy(), {"f": self.f, "iterations": self.it, "evaluations": self.evals,
+                               "status": 0 if self.ell < 0 else 1}
+
+
 def optimize(input, obj, cons_ext, cons_prog, N_iter: int):
     """src/TDM_STATIC_opt.jl:118-222: returns (p.x if feasible else p.i, runtime_total)."""
     p = mads(input, obj, cons_ext, N_iter)

@@ -54,6 +54,7 @@ EXPORTS = (
     "mac_fire_set_grid",
     "mac_set_points_f32", "mac_set_points_dev_f32", "mac_area_f32", "mac_area_batch_f32",
     "mac_poll_best_f32", "mac_poll_best_dev_f32",
+    "mac_mads_begin", "mac_mads_poll", "mac_mads_update", "mac_mads_result", "mac_mads_destroy",
 )
 
 
@@ -146,6 +147,12 @@ def _declare(L: ctypes.CDLL) -> None:
         "mac_fire_last_points": ([_vp, _dp, _i64, _i64p], _i32),
         "mac_fire_get_grid": ([_vp, _u8p], _i32),
         "mac_fire_set_grid": ([_vp, _u8p], _i32),
+        "mac_mads_begin": ([_vp, _dp, _i64, _dp, ctypes.c_double, _dp, _dp, ctypes.c_double,
+                            ctypes.POINTER(MadsParams), _i64, _i64, ctypes.POINTER(_vp)], _i32),
+        "mac_mads_poll": ([_vp, ctypes.POINTER(_i32), _dp, _i64p], _i32),
+        "mac_mads_update": ([_vp, ctypes.c_double, _i64], _i32),
+        "mac_mads_result": ([_vp, _dp, ctypes.POINTER(MadsStats)], _i32),
+        "mac_mads_destroy": ([_vp], None),
         "mac_set_points_f32": ([_vp, _fp, _fp, _fp, _i64], _i32),
         "mac_set_points_dev_f32": ([_vp, _vp, _vp, _vp, _i64], _i32),
         "mac_area_f32": ([_vp, _fp, _i64, _dp], _i32),
@@ -476,6 +483,14 @@ class Context:
                                     ctypes.byref(prm), _ptr(out), ctypes.byref(st)))
         return out, {k: getattr(st, k) for k, _ in MadsStats._fields_}
 
+    def mads_stepper(self, x0, r_max, penalty: float = 1e5, prev=None, d_lim=None,
+                     tan_half_fov: float = 1.0, n_iter: int = 100, ell0: int = 2,
+                     ell_max: int = 6, seed: int = 20250216, shard=None) -> "MadsStepper":
+        """mac_mads_begin: the native loop one poll at a time over the candidate shard
+        ``shard`` = (lo, hi) of each poll's 2n candidates (None: the whole poll)."""
+        return MadsStepper(self, x0, r_max, penalty, prev, d_lim, tan_half_fov, n_iter, ell0,
+                           ell_max, seed, shard)
+
     # -- device-resident, stream-ordered
     def area_batch_dev(self, d_cands, three_n: int, K: int, d_area, stream=None) -> None:
         _check(self._L.mac_area_batch_dev_f64(self._h, _devptr(d_cands), int(three_n), int(K),
@@ -525,6 +540,57 @@ class Context:
         _check(self._L.mac_best_fetch(self._h, _devptr(d_best), _devptr(stream),
                                       ctypes.byref(bo), ctypes.byref(bi)))
         return bo.value, bi.value
+
+
+class MadsStepper:
+    """mac_mads_begin / _poll / _update / _result (include/maxcover.h): poll() -> (done,
+    best_obj, best_idx) over this stepper's shard; update(obj, idx) with the best over all
+    shards; result() -> (x, stats). dist.mads_loop drives it."""
+
+    def __init__(self, ctx: Context, x0, r_max, penalty, prev, d_lim, tan_half_fov, n_iter,
+                 ell0, ell_max, seed, shard):
+        self._L = ctx._L
+        self._ctx = ctx   # keeps the context alive while the stepper lives
+        x = _f64(x0)
+        rm = _f64(r_max)
+        pv = _f64(prev) if prev is not None else None
+        dl = _f64(d_lim) if d_lim is not None else None
+        self.n = x.size
+        lo, hi = (0, 2 * x.size) if shard is None else (int(shard[0]), int(shard[1]))
+        self.shard = (lo, hi)
+        prm = MadsParams(int(n_iter), int(ell0), int(ell_max), int(seed) & (2**64 - 1))
+        h = _vp()
+        _check(self._L.mac_mads_begin(ctx._h, _ptr(x), x.size, _ptr(rm), float(penalty),
+                                      _ptr(pv) if pv is not None else None,
+                                      _ptr(dl) if dl is not None else None, float(tan_half_fov),
+                                      ctypes.byref(prm), lo, hi, ctypes.byref(h)))
+        self._h = h
+        self._done, self._bo, self._bi = _i32(), ctypes.c_double(), _i64()
+
+    def poll(self):
+        _check(self._L.mac_mads_poll(self._h, ctypes.byref(self._done), ctypes.byref(self._bo),
+                                     ctypes.byref(self._bi)))
+        return bool(self._done.value), self._bo.value, int(self._bi.value)
+
+    def update(self, best_obj: float, best_idx: int) -> None:
+        _check(self._L.mac_mads_update(self._h, float(best_obj), int(best_idx)))
+
+    def result(self):
+        out = np.empty(self.n)
+        st = MadsStats()
+        _check(self._L.mac_mads_result(self._h, _ptr(out), ctypes.byref(st)))
+        return out, {k: getattr(st, k) for k, _ in MadsStats._fields_}
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.mac_mads_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def _fcheck(rc: int) -> None:

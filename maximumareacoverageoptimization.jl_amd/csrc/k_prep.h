@@ -93,10 +93,13 @@ struct CandSrc {
     const int* cp;
     uint64_t state;
     int64_t b;             // 2^ell
-    __device__ __forceinline__ double get(int k, int v, int N) const
+    int k0;                // generator: candidate k of this source is candidate k0 + k of the poll
+                           // (a rank's shard of it)
+    __device__ __forceinline__ double get(int kl, int v, int N) const
     {
-        if (cands) return cands[(int64_t)k * ldc + v];
+        if (cands) return cands[(int64_t)kl * ldc + v];
         const int n = 3 * N;
+        const int k = kl + k0;
         const int kk = k < n ? k : k - n;
         const double d = ltmads_entry(state, n, b, rp[v], cp[kk]);
         return k < n ? xinc[v] + d : xinc[v] - d;

@@ -1447,141 +1447,277 @@ static void stream_permutation(uint64_t state, uint64_t first, int n, std::vecto
 
 
 
+// The native MADS loop as a stepper (mac_mads_begin / _poll / _update / _result): one
+// iteration = one complete LTMADS poll generated on the device. A stepper may own a shard
+// [lo, hi) of every poll's 2n candidates: the ranks of a multi-GPU run poll their shards, combine
+// their local bests (16 B each, lexicographic (objective, index) minimum) and all apply the same
+// update, so they stay in lock step with the single-GPU loop (mac_mads_run = one stepper owning
+// the whole poll).
+struct mac_mads {
+    mac_ctx* ctx = nullptr;
+    Lane* L = nullptr;
+    hipStream_t s = nullptr;
+    int N = 0, n = 0, K = 0;
+    int64_t lo = 0, hi = 0;
+    mac_mads_params prm{};
+    double penalty = 1e5, tan_half_fov = 1.0;
+    const double* d_prev = nullptr;
+    const double* d_dlimT = nullptr;
+    std::vector<double> x;
+    double f = INFINITY;
+    int64_t evals = 0, it = 0;
+    int ell = 0;
+    uint64_t state = 0, T = 0, per_iter = 0;
+    std::vector<int> rp, cp, rp_next, cp_next;
+    double* hb = nullptr;
+    double* hx = nullptr;
+    int* hperm = nullptr;
+    int64_t polled_b = 0;        // 2^ell of the poll awaiting its update (0: none)
+    double h_enq = 0, h_perm = 0, h_wait = 0, h_post = 0;
+    std::chrono::steady_clock::time_point t0;
+};
+
+static void mads_best_of(mac_mads* m, const CandSrc& src, int Kc, int64_t idx_base)
+{
+    enqueue_eval(m->ctx, m->L, m->s, src, m->N, Kc, use_tiled(m->ctx, m->N, nullptr, m->n),
+                 m->L->rmax.as<double>(), m->penalty, m->d_prev, m->d_dlimT,
+                 m->d_prev ? m->L->dlimraw.as<double>() : nullptr, m->tan_half_fov,
+                 m->L->area.as<double>(), m->L->obj.as<double>(), m->L->best.as<double>(), idx_base);
+    HCK(hipMemcpyAsync(m->hb, m->L->best.p, 16, hipMemcpyDeviceToHost, m->s));
+}
+
+static void mads_free(mac_mads* m)
+{
+    if (!m) return;
+    if (m->L) release_lane(m->ctx, m->L, m->s);
+    delete m;
+}
+
+int32_t mac_mads_begin(mac_ctx* ctx, const double* x0, int64_t three_n, const double* r_max,
+                       double penalty, const double* prev, const double* d_lim, double tan_half_fov,
+                       const mac_mads_params* prm, int64_t shard_lo, int64_t shard_hi,
+                       mac_mads** out)
+{
+    ABI_BEGIN
+    if (!out) return fail(MAC_E_INVAL, "null out");
+    *out = nullptr;
+    int32_t rc = check_common(ctx, three_n, 1);
+    if (rc) return rc;
+    if (!x0 || !r_max || !prm) return fail(MAC_E_INVAL, "null argument");
+    if (prev && !d_lim) return fail(MAC_E_INVAL, "prev given without d_lim");
+    if (prm->ell0 < 0 || prm->ell_max < prm->ell0 || prm->ell_max > 52)
+        return fail(MAC_E_INVAL, "need 0 <= ell0 <= ell_max <= 52");
+    const int N = (int)(three_n / 3);
+    if (N == 0) return fail(MAC_E_INVAL, "no UAV");
+    const int n = (int)three_n, K = 2 * n;
+    if (shard_lo < 0 || shard_hi > K || shard_lo > shard_hi)
+        return fail(MAC_E_INVAL, "shard outside [0, 2n)");
+    set_device(ctx);
+    mac_mads* m = new mac_mads();
+    m->t0 = std::chrono::steady_clock::now();
+    m->ctx = ctx;
+    try {
+        m->L = acquire_lane(ctx, nullptr);
+        m->s = m->L->stream;
+        Lane* L = m->L;
+        hipStream_t s = m->s;
+        m->N = N;
+        m->n = n;
+        m->K = K;
+        m->lo = shard_lo;
+        m->hi = shard_hi;
+        m->prm = *prm;
+        m->penalty = penalty;
+        m->tan_half_fov = tan_half_fov;
+        L->cands.reserve(sizeof(double) * three_n);
+        L->xinc.reserve(sizeof(double) * three_n);
+        L->perm.reserve(sizeof(int) * 2 * n);
+        L->area.reserve(sizeof(double) * K);
+        L->obj.reserve(sizeof(double) * K);
+        L->best.reserve(16);
+        L->rmax.reserve(sizeof(double) * N);
+        HCK(hipMemcpyAsync(L->rmax.p, r_max, sizeof(double) * N, hipMemcpyHostToDevice, s));
+        if (prev) {
+            L->prev.reserve(sizeof(double) * three_n);
+            L->dlim.reserve(sizeof(double) * N);
+            L->dlimraw.reserve(sizeof(double) * N);
+            L->h_dlim.resize(N);
+            for (int i = 0; i < N; ++i) L->h_dlim[i] = dlim_threshold(d_lim[i]);
+            HCK(hipMemcpyAsync(L->prev.p, prev, sizeof(double) * three_n, hipMemcpyHostToDevice, s));
+            HCK(hipMemcpyAsync(L->dlim.p, L->h_dlim.data(), sizeof(double) * N,
+                               hipMemcpyHostToDevice, s));
+            HCK(hipMemcpyAsync(L->dlimraw.p, d_lim, sizeof(double) * N, hipMemcpyHostToDevice, s));
+            m->d_prev = L->prev.as<double>();
+            m->d_dlimT = L->dlim.as<double>();
+        }
+        m->x.assign(x0, x0 + three_n);
+        // pinned staging: [best 16 B][incumbent 8*3N][permutations 4*2n]
+        L->h_stage.reserve(16 + sizeof(double) * three_n + sizeof(int) * 2 * n);
+        m->hb = (double*)L->h_stage.p;
+        m->hx = m->hb + 2;
+        m->hperm = (int*)(m->hx + three_n);
+        // f(x0): the objective, +inf when x0 itself violates cons3 (every rank evaluates it)
+        std::copy(m->x.begin(), m->x.end(), m->hx);
+        HCK(hipMemcpyAsync(L->cands.p, m->hx, sizeof(double) * three_n, hipMemcpyHostToDevice, s));
+        mads_best_of(m, matrix_src(L->cands.as<double>(), N), 1, 0);
+        HCK(hipStreamSynchronize(s));
+        m->f = __builtin_bit_cast(int64_t, m->hb[1]) >= 0 ? m->hb[0] : INFINITY;
+        m->evals = 1;
+        m->ell = prm->ell0;
+        m->state = prm->seed;
+        m->T = (uint64_t)n * (uint64_t)(n - 1) / 2;
+        m->per_iter = (uint64_t)n + m->T + 2 * (uint64_t)n;   // ltmads_basis's draws
+        // the permutations do not depend on the poll outcomes: the next iteration's are
+        // computed on the host while the device evaluates the current poll
+        stream_permutation(m->state, (uint64_t)n + m->T + 1, n, m->rp_next);
+        stream_permutation(m->state, (uint64_t)n + m->T + n + 1, n, m->cp_next);
+    } catch (...) {
+        mads_free(m);
+        throw;
+    }
+    *out = m;
+    return MAC_OK;
+    ABI_END
+}
+
+int32_t mac_mads_poll(mac_mads* m, int32_t* done, double* best_obj, int64_t* best_idx)
+{
+    ABI_BEGIN
+    if (!m || !done || !best_obj || !best_idx) return fail(MAC_E_INVAL, "null argument");
+    if (m->polled_b) return fail(MAC_E_INVAL, "mac_mads_poll twice without mac_mads_update");
+    *done = 0;
+    if (m->it >= m->prm.n_iter || m->ell < 0) {
+        *done = 1;
+        return MAC_OK;
+    }
+    set_device(m->ctx);
+    using clk = std::chrono::steady_clock;
+    const auto ta = clk::now();
+    ++m->it;
+    const int n = m->n;
+    const int64_t b = (int64_t)1 << m->ell;
+    m->rp.swap(m->rp_next);
+    m->cp.swap(m->cp_next);
+    const int Kc = (int)(m->hi - m->lo);
+    if (Kc > 0) {
+        // (the staging is free: the previous iteration's copies completed at its sync)
+        std::copy(m->rp.begin(), m->rp.end(), m->hperm);
+        std::copy(m->cp.begin(), m->cp.end(), m->hperm + n);
+        std::copy(m->x.begin(), m->x.end(), m->hx);
+        HCK(hipMemcpyAsync(m->L->perm.p, m->hperm, sizeof(int) * 2 * n, hipMemcpyHostToDevice, m->s));
+        HCK(hipMemcpyAsync(m->L->xinc.p, m->hx, sizeof(double) * n, hipMemcpyHostToDevice, m->s));
+        CandSrc src{};
+        src.xinc = m->L->xinc.as<double>();
+        src.rp = m->L->perm.as<int>();
+        src.cp = m->L->perm.as<int>() + n;
+        src.state = m->state;
+        src.b = b;
+        src.k0 = (int)m->lo;
+        mads_best_of(m, src, Kc, m->lo);
+    }
+    const auto tb = clk::now();
+    if (m->it < m->prm.n_iter) {
+        const uint64_t ns = m->state + m->per_iter * 0x9E3779B97F4A7C15ull;
+        stream_permutation(ns, (uint64_t)n + m->T + 1, n, m->rp_next);
+        stream_permutation(ns, (uint64_t)n + m->T + n + 1, n, m->cp_next);
+    }
+    const auto tc = clk::now();
+    if (Kc > 0) {
+        HCK(hipStreamSynchronize(m->s));
+        *best_obj = m->hb[0];
+        *best_idx = __builtin_bit_cast(int64_t, m->hb[1]);
+    } else {
+        *best_obj = INFINITY;
+        *best_idx = -1;
+    }
+    const auto td = clk::now();
+    m->polled_b = b;
+    m->h_enq += std::chrono::duration<double>(tb - ta).count();
+    m->h_perm += std::chrono::duration<double>(tc - tb).count();
+    m->h_wait += std::chrono::duration<double>(td - tc).count();
+    return MAC_OK;
+    ABI_END
+}
+
+int32_t mac_mads_update(mac_mads* m, double best_obj, int64_t best_idx)
+{
+    ABI_BEGIN
+    if (!m) return fail(MAC_E_INVAL, "null stepper");
+    if (!m->polled_b) return fail(MAC_E_INVAL, "mac_mads_update without a poll");
+    if (best_idx >= m->K) return fail(MAC_E_INVAL, "best index outside the poll");
+    const auto te0 = std::chrono::steady_clock::now();
+    const int n = m->n;
+    const int64_t b = m->polled_b;
+    m->polled_b = 0;
+    m->evals += m->K;
+    if (best_idx >= 0 && best_obj < m->f) {
+        const int kk = best_idx < n ? (int)best_idx : (int)best_idx - n;
+        for (int v = 0; v < n; ++v) {
+            const double d = ltmads_entry(m->state, n, b, m->rp[v], m->cp[kk]);
+            m->x[v] = best_idx < n ? m->x[v] + d : m->x[v] - d;
+        }
+        m->f = best_obj;
+        m->ell = std::min(m->ell + 1, (int)m->prm.ell_max);
+    } else {
+        --m->ell;
+    }
+    m->state += m->per_iter * 0x9E3779B97F4A7C15ull;
+    m->h_post += std::chrono::duration<double>(std::chrono::steady_clock::now() - te0).count();
+    return MAC_OK;
+    ABI_END
+}
+
+int32_t mac_mads_result(mac_mads* m, double* x_out, mac_mads_stats* st)
+{
+    ABI_BEGIN
+    if (!m) return fail(MAC_E_INVAL, "null stepper");
+    if (x_out) std::copy(m->x.begin(), m->x.end(), x_out);
+    if (st) {
+        st->f = m->f;
+        st->iterations = m->it;
+        st->evaluations = m->evals;
+        st->status = m->ell < 0 ? 0 : 1;
+        st->feasible = std::isfinite(m->f) ? 1 : 0;
+        st->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - m->t0).count();
+        st->host_enqueue_s = m->h_enq;
+        st->host_perm_s = m->h_perm;
+        st->wait_s = m->h_wait;
+        st->host_post_s = m->h_post;
+    }
+    return MAC_OK;
+    ABI_END
+}
+
+void mac_mads_destroy(mac_mads* m)
+{
+    if (!m) return;
+    (void)hipSetDevice(m->ctx->device);
+    (void)hipStreamSynchronize(m->s);
+    mads_free(m);
+}
+
 int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const double* r_max,
                      double penalty, const double* prev, const double* d_lim, double tan_half_fov,
                      const mac_mads_params* prm, double* x_out, mac_mads_stats* st)
 {
     ABI_BEGIN
-    int32_t rc = check_common(ctx, three_n, 1);
+    if (!x_out) return fail(MAC_E_INVAL, "null argument");
+    mac_mads* m = nullptr;
+    int32_t rc = mac_mads_begin(ctx, x0, three_n, r_max, penalty, prev, d_lim, tan_half_fov, prm,
+                                0, 2 * three_n, &m);
     if (rc) return rc;
-    if (!x0 || !r_max || !prm || !x_out) return fail(MAC_E_INVAL, "null argument");
-    if (prev && !d_lim) return fail(MAC_E_INVAL, "prev given without d_lim");
-    if (prm->ell0 < 0 || prm->ell_max < prm->ell0 || prm->ell_max > 52)
-        return fail(MAC_E_INVAL, "need 0 <= ell0 <= ell_max <= 52");
-    const int N = (int)(three_n / 3);
-    const int n = (int)three_n;
-    if (N == 0) return fail(MAC_E_INVAL, "no UAV");
-    const auto t0 = std::chrono::steady_clock::now();
-    set_device(ctx);
-    LaneGuard lg(ctx);
-    Lane* L = lg.lane;
-    hipStream_t s = L->stream;
-    const int K = 2 * n;
-    L->cands.reserve(sizeof(double) * three_n);
-    L->xinc.reserve(sizeof(double) * three_n);
-    L->perm.reserve(sizeof(int) * 2 * n);
-    L->area.reserve(sizeof(double) * K);
-    L->obj.reserve(sizeof(double) * K);
-    L->best.reserve(16);
-    L->rmax.reserve(sizeof(double) * N);
-    HCK(hipMemcpyAsync(L->rmax.p, r_max, sizeof(double) * N, hipMemcpyHostToDevice, s));
-    double* d_prev = nullptr;
-    double* d_dlimT = nullptr;
-    if (prev) {
-        L->prev.reserve(sizeof(double) * three_n);
-        L->dlim.reserve(sizeof(double) * N);
-        L->dlimraw.reserve(sizeof(double) * N);
-        L->h_dlim.resize(N);
-        for (int i = 0; i < N; ++i) L->h_dlim[i] = dlim_threshold(d_lim[i]);
-        HCK(hipMemcpyAsync(L->prev.p, prev, sizeof(double) * three_n, hipMemcpyHostToDevice, s));
-        HCK(hipMemcpyAsync(L->dlim.p, L->h_dlim.data(), sizeof(double) * N, hipMemcpyHostToDevice, s));
-        HCK(hipMemcpyAsync(L->dlimraw.p, d_lim, sizeof(double) * N, hipMemcpyHostToDevice, s));
-        d_prev = L->prev.as<double>();
-        d_dlimT = L->dlim.as<double>();
+    for (;;) {
+        int32_t done = 0;
+        double bo = 0.0;
+        int64_t bi = -1;
+        rc = mac_mads_poll(m, &done, &bo, &bi);
+        if (rc || done) break;
+        rc = mac_mads_update(m, bo, bi);
+        if (rc) break;
     }
-    std::vector<double> x(x0, x0 + three_n);
-    // pinned staging: [best 16 B][incumbent 8*3N][permutations 4*2n]
-    L->h_stage.reserve(16 + sizeof(double) * three_n + sizeof(int) * 2 * n);
-    double* hb = (double*)L->h_stage.p;
-    double* hx = hb + 2;
-    int* hperm = (int*)(hx + three_n);
-    auto best_of = [&](const CandSrc& src, int Kc) {
-        enqueue_eval(ctx, L, s, src, N, Kc, use_tiled(ctx, N, nullptr, three_n), L->rmax.as<double>(),
-                     penalty, d_prev, d_dlimT, d_prev ? L->dlimraw.as<double>() : nullptr, tan_half_fov,
-                     L->area.as<double>(), L->obj.as<double>(), L->best.as<double>(), 0);
-        HCK(hipMemcpyAsync(hb, L->best.p, 16, hipMemcpyDeviceToHost, s));
-    };
-    // f(x0): the objective, +inf when x0 itself violates cons3 (mads: obj(x) if feasible(x))
-    std::copy(x.begin(), x.end(), hx);
-    HCK(hipMemcpyAsync(L->cands.p, hx, sizeof(double) * three_n, hipMemcpyHostToDevice, s));
-    best_of(matrix_src(L->cands.as<double>(), N), 1);
-    HCK(hipStreamSynchronize(s));
-    double f = __builtin_bit_cast(int64_t, hb[1]) >= 0 ? hb[0] : INFINITY;
-    int64_t evals = 1, it = 0;
-    int ell = prm->ell0;
-    uint64_t state = prm->seed;
-    const uint64_t T = (uint64_t)n * (uint64_t)(n - 1) / 2;
-    const uint64_t per_iter = (uint64_t)n + T + 2 * (uint64_t)n;   // ltmads_basis's draws
-    // the permutations do not depend on the poll outcomes: the next iteration's are computed
-    // on the host while the device evaluates the current poll
-    std::vector<int> rp, cp, rp_next, cp_next;
-    stream_permutation(state, (uint64_t)n + T + 1, n, rp_next);
-    stream_permutation(state, (uint64_t)n + T + n + 1, n, cp_next);
-    using clk = std::chrono::steady_clock;
-    double h_enq = 0, h_perm = 0, h_wait = 0, h_post = 0;
-    while (it < prm->n_iter && ell >= 0) {
-        ++it;
-        const auto ta = clk::now();
-        const int64_t b = (int64_t)1 << ell;
-        rp.swap(rp_next);
-        cp.swap(cp_next);
-        // (the staging is free: the previous iteration's copies completed at its sync)
-        std::copy(rp.begin(), rp.end(), hperm);
-        std::copy(cp.begin(), cp.end(), hperm + n);
-        std::copy(x.begin(), x.end(), hx);
-        HCK(hipMemcpyAsync(L->perm.p, hperm, sizeof(int) * 2 * n, hipMemcpyHostToDevice, s));
-        HCK(hipMemcpyAsync(L->xinc.p, hx, sizeof(double) * three_n, hipMemcpyHostToDevice, s));
-        CandSrc src{};
-        src.xinc = L->xinc.as<double>();
-        src.rp = L->perm.as<int>();
-        src.cp = L->perm.as<int>() + n;
-        src.state = state;
-        src.b = b;
-        best_of(src, K);
-        const auto tb = clk::now();
-        if (it < prm->n_iter) {
-            const uint64_t ns = state + per_iter * 0x9E3779B97F4A7C15ull;
-            stream_permutation(ns, (uint64_t)n + T + 1, n, rp_next);
-            stream_permutation(ns, (uint64_t)n + T + n + 1, n, cp_next);
-        }
-        const auto tc = clk::now();
-        HCK(hipStreamSynchronize(s));
-        const auto td = clk::now();
-        evals += K;
-        const double bo = hb[0];
-        const int64_t bi = __builtin_bit_cast(int64_t, hb[1]);
-        if (bi >= 0 && bo < f) {
-            const int kk = bi < n ? (int)bi : (int)bi - n;
-            for (int v = 0; v < n; ++v) {
-                const double d = ltmads_entry(state, n, b, rp[v], cp[kk]);
-                x[v] = bi < n ? x[v] + d : x[v] - d;
-            }
-            f = bo;
-            ell = std::min(ell + 1, (int)prm->ell_max);
-        } else {
-            --ell;
-        }
-        state += per_iter * 0x9E3779B97F4A7C15ull;
-        const auto te = clk::now();
-        h_enq += std::chrono::duration<double>(tb - ta).count();
-        h_perm += std::chrono::duration<double>(tc - tb).count();
-        h_wait += std::chrono::duration<double>(td - tc).count();
-        h_post += std::chrono::duration<double>(te - td).count();
-    }
-    std::copy(x.begin(), x.end(), x_out);
-    if (st) {
-        st->f = f;
-        st->iterations = it;
-        st->evaluations = evals;
-        st->status = ell < 0 ? 0 : 1;
-        st->feasible = std::isfinite(f) ? 1 : 0;
-        st->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        st->host_enqueue_s = h_enq;
-        st->host_perm_s = h_perm;
-        st->wait_s = h_wait;
-        st->host_post_s = h_post;
-    }
-    return MAC_OK;
+    if (!rc) rc = mac_mads_result(m, x_out, st);
+    mac_mads_destroy(m);
+    return rc;
     ABI_END
 }
 

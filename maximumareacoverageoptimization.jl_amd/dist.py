@@ -7,6 +7,11 @@ writes {best objective (f64), best global index (i64 bits)} into a 16-byte devic
 all_gather of those 16 B per rank (latency-bound, tens of microseconds) is the only data-path
 collective, after which every rank takes the lexicographic minimum (objective, index): the
 lowest index wins ties, the order in which a sequential poll keeps its first best.
+
+The same exchange drives the multi-GPU MADS loop (config 5, `mads_loop`): every rank steps the
+same LTMADS sequence over its shard of each poll and applies the same global best, so all ranks
+hold the single-GPU loop's iterates. The point list needs no transfer either: the fire stream is
+a deterministic counter-based CA, so every rank regenerates it on its own GPU (DynamicArea).
 """
 from __future__ import annotations
 
@@ -56,3 +61,31 @@ def pack_best(obj: float, idx: int, device="cpu"):
     t[0] = float(obj)
     t.view(torch.int64)[1] = int(idx)
     return t
+
+
+def make_gather(device="cpu", group=None):
+    """(obj, idx) -> the lexicographic minimum over all ranks' (obj, idx): one 16-byte all_gather
+    per call (RCCL for a device tensor, gloo for a CPU one). Identity for a single process."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return lambda obj, idx: (obj, idx)
+
+    def gather(obj, idx):
+        return gather_best(pack_best(obj, idx, device), group)
+
+    return gather
+
+
+def mads_loop(stepper, gather=None):
+    """The sharded MADS loop's host side (mac_mads_poll / mac_mads_update, include/maxcover.h):
+    per iteration the stepper polls its shard, ``gather`` combines the ranks' local bests and
+    every rank applies the same global best. Returns stepper.result()."""
+    while True:
+        done, obj, idx = stepper.poll()
+        if done:
+            break
+        if gather is not None:
+            obj, idx = gather(obj, idx)
+        stepper.update(obj, idx)
+    return stepper.result()

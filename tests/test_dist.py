@@ -77,3 +77,68 @@ def test_gloo_world2_poll_argmin(mode):
         assert p.exitcode == 0
     for rank, got, want in res:
         assert got == want, (rank, got, want)
+
+
+def _mads_worker(rank, world, port, q):
+    """The sharded MADS loop (dist.mads_loop over a PollStepper shard, 16-B gloo all-gather per
+    iteration) against the single-process mads() on the same problem: the oracle evaluates."""
+    import sys
+    import torch.distributed as dist
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    orc = ge.load_oracle()
+    from importlib import import_module
+    d = import_module(pkg.__name__ + ".dist")
+    TS, TC = pkg.TDM_STATIC_opt, pkg.TDM_Constraints
+    if world > 1:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    wl = pkg.workloads
+    rng = wl.SplitMix64(515)
+    x, y, w = wl.grid_points(48)
+    rec = np.stack([x, y, w, w, np.zeros_like(x)], axis=1)
+    N = 5
+    x0 = np.concatenate([np.round(60 + rng.uniform(N) * 120), np.round(60 + rng.uniform(N) * 120),
+                         np.full(N, 20.0)])
+    rmax = np.full(N, 22.0)
+    c3 = TC.create_cons3(x0, 100 / 180 * np.pi, np.full(N, 6.0))
+
+    def obj(v):
+        return orc.ref_objective(v, rec, rmax)
+
+    def poll_fn(X):
+        f = np.array([obj(v) if c3(v) else np.inf for v in X])
+        k = int(np.argmin(f))
+        return (f[k], k) if np.isfinite(f[k]) else (np.inf, -1)
+
+    f0 = obj(x0) if c3(x0) else np.inf
+    n = x0.size
+    lo, hi = d.shard_range(2 * n, rank, world)
+    st = TS.PollStepper(x0, f0, poll_fn, N_iter=25, ell0=2, ell_max=4, seed=99, shard=(lo, hi))
+    xs, info = d.mads_loop(st, d.make_gather("cpu"))
+    ref = TS.mads(x0, obj, [c3], N_iter=25, ell0=2, ell_max=4, seed=99)
+    want_x = ref.x if ref.x is not None else ref.i
+    q.put((rank, xs.tolist(), info["f"], info["iterations"], want_x.tolist(), ref.x_cost,
+           ref.status.iteration))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_sharded_mads_loop():
+    """World size 2: each rank polls half of every LTMADS poll; after the all-gather both hold
+    the single-process MADS iterate, objective and iteration count."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mads_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, xs, f, it, want_x, want_f, want_it in res:
+        assert xs == want_x and f == want_f and it == want_it, rank
+    assert res[0][1] == res[1][1]

@@ -189,3 +189,40 @@ def test_full_simulation_dynamic_matches_replay(ctx, pkg, orc):
         x_prev = sim.outputs[-1]
     ctx2.close()
     D.close()
+
+
+@pytest.mark.gpu
+def test_config5_full_size_mpc_step(ctx, pkg, orc):
+    """Config 5 at full size (512 UAVs over the 512^2-cell ignition block of a 4096^2 CA fire):
+    one MPC step (fire step + append, rmvCoveredPOI, native MADS), then a complete 2n + 1 poll
+    around its output through AUTO (the device index, the poll walk and the shared-entry jobs:
+    the clustered disks overlap heavily) against the C oracle on the device's final list, on
+    sampled candidates and the poll's argmin; the MADS objective against the oracle too."""
+    wl = pkg.workloads
+    cfg = wl.CONFIGS[5]
+    rng = wl.SplitMix64(5555)
+    fire_kw, x0 = wl.config5_setup(rng, cfg["G"], cfg["N"], cfg["ignition"])
+    D = pkg.DynamicArea.DynamicArea(**fire_kw, seed=5555, device=0)
+    sim = pkg.FullSimulation.Simulation(ctx, x0, fire=D, N_iter=4, seed=5555)
+    rec = sim.step()
+    x, y, w = ctx.get_points()
+    assert x.size == rec["points"] > 100000
+    lst = np.stack([x, y, w, w, np.zeros_like(x)], axis=1)
+    N = cfg["N"]
+    xo = sim.outputs[-1]
+    # many overlapping disk pairs: the shared-entry jobs carry part of every candidate's area
+    cx, cy = xo[:N], xo[N:2 * N]
+    d2 = (cx[:, None] - cx[None, :]) ** 2 + (cy[:, None] - cy[None, :]) ** 2
+    assert int(np.sum(np.triu(d2 < (2 * 36.0) ** 2, 1))) > 200
+    if np.isfinite(rec["f"]):
+        assert rec["f"] == orc.ref_objective(xo, lst, sim.r_max)
+    C = wl.poll_candidates(xo, rng)
+    ctx.set_algo("auto")
+    bo, bi, objs = ctx.poll_best(C, sim.r_max, 1e5, want_all=True)
+    pick = np.unique(np.concatenate([[0, bi], np.floor(rng.uniform(10) * C.shape[0]).astype(np.int64)]))
+    pl = orc.PointerList(lst)
+    area = pl.area_batch(C[pick], 16)
+    viol = orc.violation_batch(C[pick], sim.r_max)
+    assert np.array_equal(objs[pick], -area + viol * 1e5), pick
+    assert bi == int(np.argmin(objs)) and bo == objs[bi]
+    D.close()

@@ -559,3 +559,45 @@ def test_native_mads_matches_python_driver(ctx, pkg, with_cons3):
     assert st["iterations"] == res.status.iteration
     assert st["evaluations"] == res.status.function_evaluations
     assert (st["status"] == 0) == (res.status.optimization_status == "MeshPrecisionLimit")
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_native_mads_sharded_steppers(ctx, pkg, world):
+    """The multi-GPU MADS loop's native side in one process: `world` steppers (mac_mads_begin with
+    candidate shards [floor(rK/P), floor((r+1)K/P)) of every poll), each poll's local bests
+    combined by dist.reduce_best (what the 16-B all-gather computes on P GPUs) and applied to
+    every stepper: every stepper ends on mac_mads_run's iterate, objective, iteration and
+    evaluation counts, with cons3."""
+    from importlib import import_module
+    d = import_module(pkg.__name__ + ".dist")
+    wl = pkg.workloads
+    x, y, w = wl.grid_points(200)
+    ctx.set_points(x, y, w)
+    rng = wl.SplitMix64(303)
+    N = 9
+    x0 = np.concatenate([np.round(250 + rng.uniform(N) * 400), np.round(250 + rng.uniform(N) * 400),
+                         np.full(N, 30.0)])
+    r_max = np.full(N, 30.0 * TAN50)
+    kw = dict(prev=x0, d_lim=np.full(N, 10.0), tan_half_fov=TAN50, n_iter=30, ell0=2, ell_max=5,
+              seed=777)
+    want_x, want = ctx.mads_run(x0, r_max, 1e5, **kw)
+    K = 2 * x0.size
+    steppers = [ctx.mads_stepper(x0, r_max, 1e5, shard=d.shard_range(K, r, world), **kw)
+                for r in range(world)]
+    polls = 0
+    while True:
+        res = [s_.poll() for s_ in steppers]
+        assert len({r[0] for r in res}) == 1
+        if res[0][0]:
+            break
+        polls += 1
+        bo, bi = d.reduce_best([r[1] for r in res], [r[2] for r in res])
+        for s_ in steppers:
+            s_.update(bo, bi)
+    assert polls == want["iterations"] > 5
+    for s_ in steppers:
+        xs, st = s_.result()
+        s_.close()
+        assert np.array_equal(xs, want_x)
+        assert st["f"] == want["f"] and st["iterations"] == want["iterations"]
+        assert st["evaluations"] == want["evaluations"]

@@ -63,6 +63,10 @@ for s in $STEPS; do
         MAXCOVER_BENCH_DEVICE=0 run weak2 300 python -m torch.distributed.run --nnodes=1 \
             --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 \
             --no-cpu --dist-backend gloo --steps 20 ; rc=$? ;;
+    c5x2)    # rehearsal of the N=2 config-5 path (sharded MADS) on one GPU (gloo; both ranks on device 0)
+        MAXCOVER_BENCH_DEVICE=0 run c5x2 400 python -m torch.distributed.run --nnodes=1 \
+            --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 \
+            --config 5 --no-cpu --dist-backend gloo --steps 2 --warmup 1 ; rc=$? ;;
     probe)
         { nproc; python3 -c "import os; print(os.cpu_count(), len(os.sched_getaffinity(0)))";
           cat /sys/fs/cgroup/cpu.max 2>/dev/null; lscpu | grep -E 'Model name|Socket|Core|Thread'; 
