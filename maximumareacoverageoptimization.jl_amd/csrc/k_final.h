@@ -175,7 +175,14 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
     __shared__ double red[kFinThreads / kFinC][kFinC];
     const int t = threadIdx.x, c = t % kFinC, sg = t / kFinC;
     constexpr int SG = kFinThreads / kFinC;
-    const int k0 = blockIdx.x * kFinC;
+    // XCD-aware: blocks b and b + 8 share an XCD (round-robin dispatch), so candidate block
+    // (b % 8) * per + b / 8 puts neighbouring candidate blocks — the two halves of each 128-B
+    // line of every count row — on one L2. The grid is 8 * per blocks; the ones past K only
+    // take part in the argmin's arrival count.
+    const int per = (int)(gridDim.x / 8);
+    const int cb = per > 0 && gridDim.x % 8 == 0 ? (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8)
+                                                 : (int)blockIdx.x;
+    const int k0 = cb * kFinC;
     const int k = k0 + c;
     const bool poll = mode && *mode == kModePoll;
     const int G = poll ? n_poll : n_other;

@@ -373,6 +373,23 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
     ts_end(ts);
 }
 
+// Small batches (K < 64 under AUTO: the per-candidate walk, which shares nothing between
+// candidates): the identity map built with one thread per (disk, candidate) instead of a
+// workgroup per disk, and no key pass. urec[i*K + k], umap[i*K + k] = k, pen[i*K + k].
+__global__ __launch_bounds__(256) void disk_index_identity_kernel(CandSrc src, int N, int K,
+                                                                  PenArgs pa, DiskRec* __restrict__ urec,
+                                                                  int* __restrict__ umap,
+                                                                  double* __restrict__ pen)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)N * K) return;
+    const int i = (int)(t / K), k = (int)(t % K);
+    const double x = src.get(k, i, N), y = src.get(k, N + i, N), r = src.get(k, 2 * N + i, N);
+    urec[t] = make_disk(x, y, r);
+    umap[t] = k;
+    if (pen) pen[t] = pen_term(x, y, r, i, N, pa, pen_threshold(pa, i));
+}
+
 // disk i of candidate k through the index
 __device__ __forceinline__ DiskRec rec_of(const DiskRec* __restrict__ urec,
                                           const int* __restrict__ umap, int i, int K, int k)

@@ -81,13 +81,14 @@ __device__ __forceinline__ void coverage_scan_body(
 // ------------------------------------------------------------------ per-candidate tiled walk
 
 // LDS layout, N disks (dynamic shared memory, 16-B aligned carve):
-//   double cx[N], cy[N], T[N], r[N]; int4 span[N]; uint16 ncnt[N]; uint16 nbr[N][kNbrCap];
+//   double cx[N], cy[N], T[N], r[N]; int4 span[N]; int ncnt[N]; uint16 nbr[N][kNbrCap];
 //   per wave: int rowStart[64], rowPre[64]
 __host__ __device__ inline size_t tiled_lds_head(int N)
 {
     size_t b = (size_t)N * 4 * sizeof(double);
     b += (size_t)N * 4 * sizeof(int);
-    b += (size_t)N * sizeof(uint16_t) * (1 + kNbrCap);
+    b += (size_t)N * sizeof(int);
+    b += (size_t)N * sizeof(uint16_t) * kNbrCap;
     return (b + 15) & ~(size_t)15;
 }
 __host__ __device__ inline size_t tiled_lds_bytes(int N)
@@ -115,8 +116,8 @@ __device__ __forceinline__ void coverage_tiled_body(
     double* sT = sy + N;
     double* sR = sT + N;
     int4* span = (int4*)(sR + N);
-    uint16_t* ncnt = (uint16_t*)(span + N);
-    uint16_t* nbr = ncnt + N;
+    int* ncnt = (int*)(span + N);
+    uint16_t* nbr = (uint16_t*)(ncnt + N);
     const int lane = threadIdx.x & (kWave - 1);
     const int wid = threadIdx.x / kWave;
     int* rowStart = (int*)(lds + tiled_lds_head(N)) + wid * 2 * kWave;
@@ -139,23 +140,23 @@ __device__ __forceinline__ void coverage_tiled_body(
         sR[c] = d.r;
         int4 sp;
         span[c] = disk_span(d, g, sp) ? sp : make_int4(1, 0, 1, 0);
+        ncnt[c] = 0;
     }
     __syncthreads();
 
-    // 2. lower-index overlap lists for this slice's disks (disk c belongs to slice c % G)
-    for (int c = gi + G * threadIdx.x; c < N; c += G * kBlock) {
-        int cnt = 0;
-        if (span[c].x <= span[c].y) {
-            const double cx = sx[c], cy = sy[c], r = sR[c];
-            for (int c2 = 0; c2 < c; ++c2) {
-                if (span[c2].x > span[c2].y) continue;  // covers nothing
-                if (disks_may_overlap(cx, cy, r, sx[c2], sy[c2], sR[c2])) {
-                    if (cnt < kNbrCap) nbr[c * kNbrCap + cnt] = (uint16_t)c2;
-                    ++cnt;
-                }
+    // 2. lower-index overlap lists for this slice's disks (disk c belongs to slice c % G): the
+    // pairs (c, c2 < c) spread over the whole workgroup (c2 = tid, tid + kBlock, ...), appended
+    // with LDS atomics — the list order is irrelevant, ownership below is an OR over it
+    for (int c = gi; c < N; c += G) {
+        if (span[c].x > span[c].y) continue;   // uniform
+        const double cx = sx[c], cy = sy[c], r = sR[c];
+        for (int c2 = threadIdx.x; c2 < c; c2 += kBlock) {
+            if (span[c2].x > span[c2].y) continue;  // covers nothing
+            if (disks_may_overlap(cx, cy, r, sx[c2], sy[c2], sR[c2])) {
+                const int q = atomicAdd(&ncnt[c], 1);
+                if (q < kNbrCap) nbr[c * kNbrCap + q] = (uint16_t)c2;
             }
         }
-        ncnt[c] = (uint16_t)(cnt > kNbrCap ? 0xffff : cnt);
     }
     __syncthreads();
 
@@ -166,7 +167,7 @@ __device__ __forceinline__ void coverage_tiled_body(
         const int4 sp = span[c];
         if (sp.x > sp.y) continue;
         const double cx = sx[c], cy = sy[c], T = sT[c];
-        const int nc = ncnt[c];
+        const int nc = ncnt[c] > kNbrCap ? 0xffff : ncnt[c];   // overflow: every lower disk
         for (int rb = sp.z; rb <= sp.w; rb += kWave) {
             const int nr = (sp.w - rb + 1) < kWave ? (sp.w - rb + 1) : kWave;
             int s = 0, len = 0;

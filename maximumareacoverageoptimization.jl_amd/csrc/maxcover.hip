@@ -139,6 +139,7 @@ struct Lane {
         f_dlist, f_ctl;
     std::vector<double> h_dlim;
     PinnedBuf h_stage;                         // native MADS driver: best, permutations, incumbent
+    PinnedBuf h_io;                            // host-pointer calls: candidates in, results out
 };
 
 struct mac_ctx {
@@ -627,7 +628,15 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         CandSrc isrc = src;
         // candidates per index thread: 3 (K <= 3073), 6 (K <= 6145); larger: identity map
         const int iper = K <= kIndexMaxK + 1 ? kIdxPer : K <= kIndexMaxKWide + 1 ? kIdxPerWide : 0;
-        if (src.cands && iper) {  // matrix: fp32 keys, variable-major, so each
+        if (!poll_possible) {
+            // the per-candidate walk alone (small batches, the single-candidate closure): the
+            // identity map, one thread per (disk, candidate), no key pass
+            const int64_t nk = (int64_t)N * K;
+            hipLaunchKernelGGL(disk_index_identity_kernel, dim3(grid1d(nk, 256)), dim3(256), 0, s,
+                               src, N, K, pa, L->disks.as<DiskRec>(), L->umap.as<int>(), d_pen);
+            HCK(hipGetLastError());
+        }
+        if (poll_possible && src.cands && iper) {  // matrix: fp32 keys, variable-major, so each
                                                  // disk's K keys are a row
             const int nkt = (K + 31) / 32;
             L->keysT.reserve(sizeof(float) * (size_t)3 * N * K);
@@ -642,9 +651,11 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             isrc.nkt = nkt;
         }
         const unsigned nidx = 8 * ((N + 7) / 8);
-        uint64_t* tsi = ts_c < 0 ? take_ts(nidx, ts_c, ts_nc) : nullptr;   // the index opens the chain
+        uint64_t* tsi = (poll_possible && ts_c < 0) ? take_ts(nidx, ts_c, ts_nc) : nullptr;
         const int dedup = iper ? 1 : 0;
-        if (isrc.cands && iper == kIdxPerWide)
+        if (!poll_possible)
+            ;   // indexed above
+        else if (isrc.cands && iper == kIdxPerWide)
             hipLaunchKernelGGL((disk_index_kernel<true, kIdxPerWide>), dim3(nidx), dim3(kIdxThreads), 0,
                                s, tsi, isrc, N, K, ctx->grid, pa, dedup, io);
         else if (isrc.cands)
@@ -732,7 +743,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         HCK(hipGetLastError());
     }
     // finalize, with the poll argmin taken by its last-arriving block (k_final.h)
-    const unsigned nfin = (unsigned)((K + kFinC - 1) / kFinC);
+    const unsigned nfin = 8 * (unsigned)((K + 8 * kFinC - 1) / (8 * kFinC));   // k_final.h: XCD map
     FinBest fb{};
     if (d_best) {
         L->finblk.reserve(2 * sizeof(unsigned long long) * nfin);
@@ -788,12 +799,22 @@ static int32_t host_eval(mac_ctx* ctx, const T* cands, int64_t three_n, int64_t 
     L->area.reserve(sizeof(double) * K);
     L->obj.reserve(sizeof(double) * K);
     L->best.reserve(16);
+    // pinned staging (up to 64 MB): from pageable memory HIP would stage each copy
+    // synchronously; one host memcpy into the lane's pinned buffer keeps the copies async
+    const size_t in_bytes = sizeof(T) * (size_t)(three_n * K);
+    const size_t out_bytes = sizeof(double) * (size_t)K * ((area_out ? 1 : 0) + (obj_out ? 1 : 0)) + 16;
+    const bool staged = std::max(in_bytes, out_bytes) <= ((size_t)64 << 20);
+    if (staged) L->h_io.reserve(std::max<size_t>(std::max(in_bytes, out_bytes), 64));
+    const T* src_in = cands;
+    if (staged && in_bytes) {
+        std::memcpy(L->h_io.p, cands, in_bytes);
+        src_in = (const T*)L->h_io.p;
+    }
     if (three_n * K > 0) {
         if constexpr (f32)
-            upload_widen(cands, three_n * K, L->c32, L->cands.as<double>(), s);
+            upload_widen(src_in, three_n * K, L->c32, L->cands.as<double>(), s);
         else
-            HCK(hipMemcpyAsync(L->cands.p, cands, sizeof(double) * three_n * K,
-                               hipMemcpyHostToDevice, s));
+            HCK(hipMemcpyAsync(L->cands.p, src_in, in_bytes, hipMemcpyHostToDevice, s));
     }
     const bool want_obj = obj_out || best_obj || best_idx;
     double* d_rmax = nullptr;
@@ -828,14 +849,19 @@ static int32_t host_eval(mac_ctx* ctx, const T* cands, int64_t three_n, int64_t 
                  d_dlimT, d_prev ? L->dlimraw.as<double>() : nullptr, tan_half_fov, L->area.as<double>(),
                  want_obj ? L->obj.as<double>() : nullptr,
                  (best_obj || best_idx) ? L->best.as<double>() : nullptr, 0);
-    if (area_out)
-        HCK(hipMemcpyAsync(area_out, L->area.p, sizeof(double) * K, hipMemcpyDeviceToHost, s));
-    if (obj_out)
-        HCK(hipMemcpyAsync(obj_out, L->obj.p, sizeof(double) * K, hipMemcpyDeviceToHost, s));
-    double hb[2] = {0, 0};
-    if (best_obj || best_idx)
-        HCK(hipMemcpyAsync(hb, L->best.p, 16, hipMemcpyDeviceToHost, s));
+    // results: into the pinned buffer (the upload has completed before the kernels ran), then
+    // one host copy each after the sync
+    double* ho = staged ? (double*)L->h_io.p : nullptr;
+    double* h_area = area_out ? (staged ? ho : area_out) : nullptr;
+    double* h_obj = obj_out ? (staged ? ho + (area_out ? K : 0) : obj_out) : nullptr;
+    double hb_local[2] = {0, 0};
+    double* hb = staged ? ho + (size_t)K * ((area_out ? 1 : 0) + (obj_out ? 1 : 0)) : hb_local;
+    if (h_area) HCK(hipMemcpyAsync(h_area, L->area.p, sizeof(double) * K, hipMemcpyDeviceToHost, s));
+    if (h_obj) HCK(hipMemcpyAsync(h_obj, L->obj.p, sizeof(double) * K, hipMemcpyDeviceToHost, s));
+    if (best_obj || best_idx) HCK(hipMemcpyAsync(hb, L->best.p, 16, hipMemcpyDeviceToHost, s));
     HCK(hipStreamSynchronize(s));
+    if (staged && area_out) std::memcpy(area_out, h_area, sizeof(double) * K);
+    if (staged && obj_out) std::memcpy(obj_out, h_obj, sizeof(double) * K);
     if (best_obj) *best_obj = hb[0];
     if (best_idx) *best_idx = __builtin_bit_cast(int64_t, hb[1]);
     return MAC_OK;
@@ -1063,6 +1089,7 @@ void mac_ctx_destroy(mac_ctx* ctx)
     ctx->h_best.release();
     for (Lane* l : ctx->lanes_all) {
         l->h_stage.release();
+        l->h_io.release();
         for (DevBuf* b : {&l->cands, &l->disks, &l->partial, &l->area, &l->obj, &l->best,
                           &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->pen, &l->nbr,
                           &l->ncount, &l->dlist, &l->spart, &l->vp, &l->xinc,
