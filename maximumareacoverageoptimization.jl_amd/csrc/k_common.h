@@ -23,6 +23,12 @@ constexpr int kPollThreads = 256;  // poll walk: workgroup size (4 waves share o
 constexpr int kPollWaves = kPollThreads / kWave;
 constexpr int kPollKPB = kWave * kPollSlots;  // poll walk: positions per slice
 constexpr int kSharedWG = 256;     // poll walk: shared-entry workgroups (grid-stride over jobs)
+constexpr int kBitsTab = 2048;     // bit-word kernel: positions per table group (k_bits.h)
+constexpr int kBitsMinDisks = 16;  // bit-word kernel: used above this many disks with neighbours
+// poll walk counters (dcount[]): [0] disks with neighbours the bit-word kernel can take (dlist
+// from the front), [1] poll-kernel jobs taken, [2] the other disks with neighbours (dlist from the
+// back), [3] bit-word jobs taken; cleared by the index kernel
+constexpr int kDcBits = 0, kDcPollJobs = 1, kDcOther = 2, kDcBitsJobs = 3;
 
 constexpr int kModePoll = 1;
 constexpr int kModeTiled = 2;

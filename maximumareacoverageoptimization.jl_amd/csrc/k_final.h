@@ -186,6 +186,8 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
     const int k = k0 + c;
     const bool poll = mode && *mode == kModePoll;
     const int G = poll ? n_poll : n_other;
+    // the candidate's penalty, loaded with the first batch of rows (one round trip fewer)
+    const double vpk = (vp && sg == 0 && k < K) ? vp[k] : 0.0;
     if (counts && poll && spart) {  // equal weights: integer rows, exact in any order
         const unsigned* const crow = reinterpret_cast<const unsigned*>(partial);
         const unsigned* const srow = reinterpret_cast<const unsigned*>(spart);
@@ -213,7 +215,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
             for (int q = 0; q < SG; ++q) n += ired[q][c];
             const double area = (double)n * w0;
             if (area_out) area_out[k] = area;
-            if (vp) o = -area + vp[k];
+            if (vp) o = -area + vpk;
             if (obj_out) obj_out[k] = o;
         }
         if (fb.best && t < kWave) finalize_argmin(fb, o, k, k < K);
@@ -255,7 +257,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
 #pragma unroll
         for (int q = 0; q < SG; ++q) area += red[q][c];
         if (area_out) area_out[k] = area;
-        if (vp) o = -area + vp[k];
+        if (vp) o = -area + vpk;
         if (obj_out) obj_out[k] = o;
     }
     if (fb.best && t < kWave) finalize_argmin(fb, o, k, k < K);

@@ -88,7 +88,7 @@ struct IndexOut {
     int* ucount;
     int4* region;
     double2* cost;
-    int* dcount;     // the poll walk's counters, cleared here: [0] disks with neighbours, [1] jobs
+    int* dcount;     // the poll walk's counters (k_common.h kDc*), cleared here
     // poll walk inputs (null: not needed): per position the scaled-filter constants (k_lane.h)
     // {S*2cu, S*2cv, S*(T - C), -S} and X' (-1: inert), relative to the region centre; per disk
     // kRowInfo + 1 row descriptors of its region {first entry of the row's run, entries before
@@ -138,8 +138,7 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
     if (i >= N) return;                                   // uniform
     MAC_IDX_STAMP(0);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        o.dcount[0] = 0;   // disks with neighbours (walk_setup_kernel)
-        o.dcount[1] = 0;   // shared-entry jobs taken (coverage_poll_kernel)
+        for (int q = 0; q < 4; ++q) o.dcount[q] = 0;   // the poll walk's counters (k_common.h)
     }
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
     const int64_t row = (int64_t)i * K;

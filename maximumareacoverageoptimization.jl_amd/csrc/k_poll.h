@@ -42,6 +42,7 @@
 #include "predicate.h"
 #include "k_common.h"
 #include "k_poll_shared.h"
+#include "k_bits.h"
 #include "k_final.h"
 #include "k_index.h"
 #include "k_lane.h"
@@ -137,6 +138,7 @@ __device__ __forceinline__ void coverage_poll_body(
     const uint64_t diag_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
     const int bx = blockIdx.x;
+
     // The shared-entry jobs (disk with neighbours x kShC-candidate slice, k_poll_shared.h) are
     // taken from a counter (the index kernel cleared it) by the shared workgroups and by every
     // walk workgroup once its disk is done: few jobs (separated disks) finish at once, many (a
@@ -145,11 +147,16 @@ __device__ __forceinline__ void coverage_poll_body(
     // taken as n_shared + counter.
     auto shared_jobs = [&](int first) {
         __shared__ int sjob;
-        // candidates per job: 64 while the jobs fill the chip, 256 when the disks with
-        // neighbours alone would (fewer re-stagings of each region)
-        const int C = *dcount * ((K + kShC - 1) / kShC) > 2 * (int)gridDim.x ? kShCWide : kShC;
+        // fp64 jobs of 64 candidates while the jobs fill the chip, 256 when the disks with
+        // neighbours alone would (fewer re-stagings of each region). With more than
+        // kBitsMinDisks disks with neighbours the bit-word kernel (k_bits.h, launched next) takes
+        // every disk it qualifies for; the jobs of those disks return at once here.
+        const int nA = dcount[kDcBits], nB = dcount[kDcOther];
+        const bool bits = lane4 != nullptr && nA + nB > kBitsMinDisks;
+        const int nlist = bits ? nB : nA + nB;   // list position q: dlist[N-1-q], then dlist[q-nB]
+        const int C = nlist * ((K + kShC - 1) / kShC) > 2 * (int)gridDim.x ? kShCWide : kShC;
         const int nsub = (K + C - 1) / C;
-        const int total = *dcount * nsub;
+        const int total = nlist * nsub;
         int job = first;
         for (;;) {
             if (job < 0) {
@@ -159,8 +166,10 @@ __device__ __forceinline__ void coverage_poll_body(
                 __syncthreads();
             }
             if (job >= total) break;   // uniform
-            poll_shared_job(xy, w, off, g, urec, umap, region, nbrT, nboxT, rows, ncount,
-                            dlist[job / nsub], K, (job % nsub) * C, C, spart, counts);
+            const int ql = job / nsub;
+            const int di = ql < nB ? dlist[N - 1 - ql] : dlist[ql - nB];
+                poll_shared_job(xy, w, off, g, urec, umap, region, nbrT, nboxT, rows, ncount,
+                                di, K, (job % nsub) * C, C, spart, counts);
             job = -1;
         }
     };
@@ -174,7 +183,7 @@ __device__ __forceinline__ void coverage_poll_body(
     if (mode && *mode != kModePoll) return;
     if (bx >= N) {  // then: the shared entries
         shared_jobs(bx - N);
-        MAC_DIAG_STAMP(diag_t0, 2, (uint64_t)*dcount);
+        MAC_DIAG_STAMP(diag_t0, 2, (uint64_t)(dcount[kDcBits] + dcount[kDcOther]));
         return;
     }
     do {  // the walk of disk bx (break: nothing more to credit)

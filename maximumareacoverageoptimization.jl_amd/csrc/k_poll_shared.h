@@ -33,10 +33,14 @@ __device__ __forceinline__ bool box_has(const int4& b, int tx, int ty)
 // most kPollNbr kept in nbr[i*kPollNbr ...]; ncount[i] is the true count, > kPollNbr meaning
 // "overflowed"), their region boxes in nboxT. Disks with neighbours are appended to dlist (order irrelevant: each is processed
 // independently); *dcount must be zero on entry (the index kernel clears it).
-__device__ __forceinline__ void neighbors_block(int i, const int4* __restrict__ region,
+// A disk with neighbours goes to the bit-word kernel's list (front of dlist, k_bits.h) when its
+// list did not overflow, its region is at most 64 x 64 tiles and it and every neighbour have at
+// most kBitsTab positions; otherwise to the back of dlist (the poll kernel's fp64 jobs).
+__device__ __forceinline__ void neighbors_block(int i, int N, const int4* __restrict__ region,
                                                 uint16_t* __restrict__ nbr, int4* __restrict__ nboxT,
                                                 int* __restrict__ ncount,
-                                                int* __restrict__ dlist, int* __restrict__ dcount)
+                                                int* __restrict__ dlist, int* __restrict__ dcount,
+                                                const int* __restrict__ ucount, int* __restrict__ qual)
 {
     __shared__ int cnt;
     if (threadIdx.x == 0) cnt = 0;
@@ -55,9 +59,22 @@ __device__ __forceinline__ void neighbors_block(int i, const int4* __restrict__ 
         }
     }
     __syncthreads();
+    const int nc = cnt;
+    bool bad = false;
+    if (nc > 0) {
+        bad = nc > kPollNbr || R.y - R.x + 1 > 64 || R.w - R.z + 1 > 64;
+        if (!bad)
+            for (int m = threadIdx.x; m <= nc; m += blockDim.x)
+                bad |= ucount[m == 0 ? i : (int)nbr[i * kPollNbr + m - 1]] > kBitsTab;
+    }
+    bad = __syncthreads_or(bad);
     if (threadIdx.x == 0) {
-        ncount[i] = cnt;
-        if (cnt > 0) dlist[atomicAdd(dcount, 1)] = i;
+        ncount[i] = nc;
+        qual[i] = nc > 0 && !bad ? 1 : 0;
+        if (nc > 0) {
+            if (!bad) dlist[atomicAdd(dcount + kDcBits, 1)] = i;
+            else dlist[N - 1 - atomicAdd(dcount + kDcOther, 1)] = i;
+        }
     }
 }
 

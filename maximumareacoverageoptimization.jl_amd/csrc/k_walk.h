@@ -248,13 +248,15 @@ __global__ __launch_bounds__(kBlock) void walk_setup_kernel(
     const int4* __restrict__ region, uint16_t* __restrict__ nbr, int4* __restrict__ nboxT,
     int* __restrict__ ncount, int* __restrict__ dlist, int* __restrict__ dcount,
     const double2* __restrict__ cost,
-    double ratio, int forced, int* __restrict__ mode)
+    double ratio, int forced, int* __restrict__ mode, const int* __restrict__ ucount,
+    int* __restrict__ qual)
 {
     ts_begin(ts);
     const int m = walk_choice(N, cost, ratio, forced);
     if (blockIdx.x == 0 && threadIdx.x == 0) mode[0] = m;
     if (m == kModePoll) {
-        if ((int)blockIdx.x < N) neighbors_block(blockIdx.x, region, nbr, nboxT, ncount, dlist, dcount);
+        if ((int)blockIdx.x < N)
+            neighbors_block(blockIdx.x, N, region, nbr, nboxT, ncount, dlist, dcount, ucount, qual);
     } else {
         coverage_tiled_body(xy, w, off, g, urec, umap, N, K, G, nullptr, partial);
     }

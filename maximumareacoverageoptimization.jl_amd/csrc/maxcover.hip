@@ -132,7 +132,7 @@ struct Lane {
     hipEvent_t done = nullptr;
     DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode, pen, nbr,
         ncount, dlist, spart, vp, xinc, perm, ucount, umap, keysT, kbad, lane4, lanexp, rows, nboxT,
-        cnt, dlimraw, finblk, finarrive, c32, p32;
+        cnt, dlimraw, finblk, finarrive, c32, p32, qual;
     // the fused equal-weight poll (k_fused.h): keys, regions (generation-tagged), chains, counts,
     // neighbour lists, hand-off counters
     DevBuf f_keys, f_kbad, f_part, f_dtctr, f_vp, f_cnt, f_region, f_nbr, f_nboxT, f_ncount,
@@ -613,7 +613,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         L->ucount.reserve(sizeof(int) * (size_t)N);
         L->region.reserve(sizeof(int4) * N);
         L->cost.reserve(sizeof(double2) * N);
-        L->mode.reserve(4 * sizeof(int));  // [0] walk, [1] disks-with-neighbours count, [2] jobs
+        L->mode.reserve(8 * sizeof(int));  // [0] walk, [1..4] the poll walk's counters (k_common.h)
         if (poll_possible) {  // the poll walk's lane constants and row descriptors
             L->lane4.reserve(sizeof(float4) * (size_t)N * K);
             L->lanexp.reserve(sizeof(float) * (size_t)N * K);
@@ -686,6 +686,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             L->nbr.reserve(sizeof(uint16_t) * (size_t)N * kPollNbr);
             L->ncount.reserve(sizeof(int) * (size_t)N);
             L->dlist.reserve(sizeof(int) * (size_t)N);
+            L->qual.reserve(sizeof(int) * (size_t)N);
             L->nboxT.reserve(sizeof(int4) * (size_t)N * kPollNbr);
             const size_t lds = run_tiled ? tiled_lds_bytes(N) : 0;
             const unsigned nwg = (unsigned)std::max<int64_t>(
@@ -696,7 +697,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                                ctx->grid, d_urec, d_map, N, K, G, L->partial.as<double>(),
                                L->region.as<int4>(), L->nbr.as<uint16_t>(), L->nboxT.as<int4>(),
                                L->ncount.as<int>(), L->dlist.as<int>(), L->mode.as<int>() + 1,
-                               L->cost.as<double2>(), kPollCostRatio, forced, L->mode.as<int>());
+                               L->cost.as<double2>(), kPollCostRatio, forced, L->mode.as<int>(),
+                               L->ucount.as<int>(), L->qual.as<int>());
             HCK(hipGetLastError());
             d_mode = L->mode.as<int>();
             d_umap = d_map;
@@ -726,6 +728,24 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                                L->mode.as<int>() + 2, N, K,
                                d_mode, L->partial.as<double>(), L->spart.as<double>(), n_chain, d_pen,
                                penalty, d_vp, n_shared, counts);
+            HCK(hipGetLastError());
+            // the shared entries of crowded polls: bit-words per distinct position (k_bits.h);
+            // returns at once when few disks have neighbours (the poll kernel took them)
+            const unsigned nbits = (unsigned)std::max(1, std::min(N, ctx->cus));
+            if (counts)
+                hipLaunchKernelGGL(shared_bits_kernel<true>, dim3(nbits), dim3(kBitsThreads), 0, s,
+                                   ctx->xys.as<double2>(), ctx->ws.as<double>(), ctx->off.as<int32_t>(),
+                                   ctx->grid, d_urec, d_map, L->ucount.as<int>(), L->region.as<int4>(),
+                                   L->nbr.as<uint16_t>(), L->lane4.as<float4>(), L->lanexp.as<float>(),
+                                   L->ncount.as<int>(), L->qual.as<int>(), L->mode.as<int>() + 1, d_mode,
+                                   N, K, L->spart.as<double>());
+            else
+                hipLaunchKernelGGL(shared_bits_kernel<false>, dim3(nbits), dim3(kBitsThreads), 0, s,
+                                   ctx->xys.as<double2>(), ctx->ws.as<double>(), ctx->off.as<int32_t>(),
+                                   ctx->grid, d_urec, d_map, L->ucount.as<int>(), L->region.as<int4>(),
+                                   L->nbr.as<uint16_t>(), L->lane4.as<float4>(), L->lanexp.as<float>(),
+                                   L->ncount.as<int>(), L->qual.as<int>(), L->mode.as<int>() + 1, d_mode,
+                                   N, K, L->spart.as<double>());
             HCK(hipGetLastError());
             chain_done = true;
             d_spart = L->spart.as<double>();
@@ -886,6 +906,16 @@ int32_t mac_diag_walk_read(uint64_t* out, int64_t n)
 {
     if (n > (int64_t)(8 * 65536)) n = 8 * 65536;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_walk), sizeof(uint64_t) * n, 0,
+                            hipMemcpyDeviceToHost) != hipSuccess)
+        return MAC_E_HIP;
+    return MAC_OK;
+}
+
+// diagnostic build only: per-workgroup phase ticks of shared_bits_kernel (k_bits.h)
+int32_t mac_diag_bits_read(uint64_t* out, int64_t n)
+{
+    if (n > 256 * 16) n = 256 * 16;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_bits), sizeof(uint64_t) * n, 0,
                             hipMemcpyDeviceToHost) != hipSuccess)
         return MAC_E_HIP;
     return MAC_OK;
@@ -1092,7 +1122,7 @@ void mac_ctx_destroy(mac_ctx* ctx)
         l->h_io.release();
         for (DevBuf* b : {&l->cands, &l->disks, &l->partial, &l->area, &l->obj, &l->best,
                           &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->pen, &l->nbr,
-                          &l->ncount, &l->dlist, &l->spart, &l->vp, &l->xinc,
+                          &l->ncount, &l->dlist, &l->qual, &l->spart, &l->vp, &l->xinc,
                           &l->perm, &l->ucount, &l->umap, &l->keysT, &l->kbad, &l->lane4,
                           &l->lanexp, &l->rows, &l->nboxT, &l->cnt, &l->dlimraw, &l->finblk, &l->finarrive, &l->c32, &l->p32, &l->f_keys,
                           &l->f_kbad, &l->f_part, &l->f_dtctr, &l->f_vp, &l->f_cnt,
