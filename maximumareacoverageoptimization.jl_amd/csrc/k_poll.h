@@ -131,13 +131,16 @@ __device__ __forceinline__ void coverage_poll_body(
     const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
     int* __restrict__ jobctr, int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
     double* __restrict__ spart, int n_chain, const double* __restrict__ pen, double penalty,
-    double* __restrict__ vp, int n_shared, int counts)
+    double* __restrict__ vp, int n_shared, int counts, int bits_on, int* __restrict__ dc_out)
 {
     static_assert(kPollSlots == 2 * kPollPairs, "the hot loop pairs candidate slots");
 #ifdef MAC_DIAG
     const uint64_t diag_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
     const int bx = blockIdx.x;
+    // the launch hint for the next poll's bit-word kernel (mapped host memory, maxcover.hip)
+    if (bx == 0 && threadIdx.x == 0 && dc_out && (!mode || *mode == kModePoll))
+        *(volatile int*)dc_out = dcount[kDcBits] + dcount[kDcOther];
 
     // The shared-entry jobs (disk with neighbours x kShC-candidate slice, k_poll_shared.h) are
     // taken from a counter (the index kernel cleared it) by the shared workgroups and by every
@@ -152,7 +155,7 @@ __device__ __forceinline__ void coverage_poll_body(
         // kBitsMinDisks disks with neighbours the bit-word kernel (k_bits.h, launched next) takes
         // every disk it qualifies for; the jobs of those disks return at once here.
         const int nA = dcount[kDcBits], nB = dcount[kDcOther];
-        const bool bits = lane4 != nullptr && nA + nB > kBitsMinDisks;
+        const bool bits = bits_on && lane4 != nullptr && nA + nB > kBitsMinDisks;
         const int nlist = bits ? nB : nA + nB;   // list position q: dlist[N-1-q], then dlist[q-nB]
         const int C = nlist * ((K + kShC - 1) / kShC) > 2 * (int)gridDim.x ? kShCWide : kShC;
         const int nsub = (K + C - 1) / C;
@@ -310,36 +313,66 @@ __device__ __forceinline__ void coverage_poll_body(
             if (rb == R.z) MAC_WALK_STAMP(2);
 #endif
             for (int base = 0; base < total; base += kPollCH) {
-                const int n = min(kPollCH, total - base);
-                bool mixed = false;
-                double wfirst = 0.0;
-                for (int q = tid; q < n; q += kPollThreads) {
-                    const int f = base + q;
-                    int lo = 0, hi = nr - 1;
-                    while (lo < hi) {
-                        const int mid = (lo + hi + 1) >> 1;
-                        if (rpre[mid] <= f) lo = mid; else hi = mid - 1;
+                const int nraw = min(kPollCH, total - base);
+                // the chunk's entries disk i may own: shared ones (the shared-entry pass decides
+                // them) and non-finite ones (never covered) are left out, the rest compacted in a
+                // fixed order (round, wave, lane) so the walk only tests what it can credit
+                constexpr int kR = kPollCH / kPollThreads;
+                __shared__ int wkeep[kR][kPollWaves];
+                double2 pr[kR];
+                double wr[kR];
+                uint64_t bal[kR];
+#pragma unroll
+                for (int r = 0; r < kR; ++r) {
+                    const int q = tid + r * kPollThreads;
+                    bool keep = false;
+                    pr[r] = make_double2(0.0, 0.0);
+                    wr[r] = 0.0;
+                    if (q < nraw) {
+                        const int f = base + q;
+                        int lo = 0, hi = nr - 1;
+                        while (lo < hi) {
+                            const int mid = (lo + hi + 1) >> 1;
+                            if (rpre[mid] <= f) lo = mid; else hi = mid - 1;
+                        }
+                        const int j = rs[lo] + (f - rpre[lo]);
+                        pr[r] = xy[j];
+                        wr[r] = w[j];
+                        const bool shared =
+                            nc > 0 && entry_shared(nc, nbox, tile_of(pr[r].x, g.gx0, g.invS, g.nTx), rb + lo);
+                        // (an entry whose fp32 offset overflows stays: inert for the filter, a
+                        // forced lane decides it in fp64)
+                        keep = !shared && __builtin_isfinite(pr[r].x) && __builtin_isfinite(pr[r].y);
                     }
-                    const int j = rs[lo] + (f - rpre[lo]);
-                    const double2 p = xy[j];
-                    const double wj = w[j];
-                    s64[q] = p;
-                    sw[q] = wj;
-                    const bool shared =
-                        nc > 0 && entry_shared(nc, nbox, tile_of(p.x, g.gx0, g.invS, g.nTx), rb + lo);
-                    const float fu = (float)(p.x - ox), fv = (float)(p.y - oy);
-                    s32[q] = !shared && __builtin_isfinite(fu) && __builtin_isfinite(fv)
-                                 ? make_float4(__builtin_fmaf(fu, fu, fv * fv), fu, fv, 0.0f)
-                                 : make_float4(__builtin_inff(), 0.0f, 0.0f, 0.0f);
-                    if (q == tid) wfirst = wj;
-                    mixed |= __builtin_bit_cast(uint64_t, wj) != __builtin_bit_cast(uint64_t, wfirst);
+                    bal[r] = __ballot(keep);
+                    if (lane == 0) wkeep[r][wid] = __popcll(bal[r]);
+                }
+                __syncthreads();
+                int n = 0;
+#pragma unroll
+                for (int r = 0; r < kR; ++r) {
+                    int dst = n + __popcll(bal[r] & ((1ull << lane) - 1));
+                    for (int q = 0; q < kPollWaves; ++q) {
+                        if (q < wid) dst += wkeep[r][q];
+                        n += wkeep[r][q];
+                    }
+                    if ((bal[r] >> lane) & 1) {
+                        s64[dst] = pr[r];
+                        sw[dst] = wr[r];
+                        const float fu = (float)(pr[r].x - ox), fv = (float)(pr[r].y - oy);
+                        s32[dst] = __builtin_isfinite(fu) && __builtin_isfinite(fv)
+                                       ? make_float4(__builtin_fmaf(fu, fu, fv * fv), fu, fv, 0.0f)
+                                       : make_float4(__builtin_inff(), 0.0f, 0.0f, 0.0f);
+                    }
                 }
                 // pad to a multiple of 4 entries with inert ones (d' = -inf: never counted, never band)
                 if (tid < ((4 - (n & 3)) & 3)) s32[n + tid] = make_float4(__builtin_inff(), 0.0f, 0.0f, 0.0f);
                 __syncthreads();
-                // weights identical across the chunk? (compare with entry 0 after staging)
+                // weights identical across the chunk?
                 const uint64_t w0 = __builtin_bit_cast(uint64_t, sw[0]);
-                mixed |= (tid < n) && __builtin_bit_cast(uint64_t, sw[tid]) != w0;
+                bool mixed = false;
+                for (int q = tid; q < n; q += kPollThreads)
+                    mixed |= __builtin_bit_cast(uint64_t, sw[q]) != w0;
                 const bool uniform = !__syncthreads_or(mixed);
 #ifdef MAC_DIAG
                 if (rb == R.z && base == 0) MAC_WALK_STAMP(3);
@@ -461,13 +494,13 @@ __global__ __launch_bounds__(kPollThreads) __attribute__((amdgpu_waves_per_eu(3)
     const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
     int* __restrict__ jobctr, int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
     double* __restrict__ spart, int n_chain, const double* __restrict__ pen, double penalty,
-    double* __restrict__ vp, int n_shared, int counts)
+    double* __restrict__ vp, int n_shared, int counts, int bits_on, int* __restrict__ dc_out)
 {
     ts_begin(ts);
     coverage_poll_body(xy, w, off, g, urec, umap, ucount, region, nbrT, nboxT, lane4, lanexp, rows,
                        ncount, dlist, dcount, jobctr, N, K, mode, partial, spart, n_chain, pen,
                        penalty, vp,
-                       n_shared, counts);
+                       n_shared, counts, bits_on, dc_out);
     ts_end(ts);
 }
 

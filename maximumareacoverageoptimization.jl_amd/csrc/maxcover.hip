@@ -140,6 +140,8 @@ struct Lane {
     std::vector<double> h_dlim;
     PinnedBuf h_stage;                         // native MADS driver: best, permutations, incumbent
     PinnedBuf h_io;                            // host-pointer calls: candidates in, results out
+    PinnedBuf h_dc;                            // disks with neighbours of the last poll (mapped)
+    int* d_dc = nullptr;                       // ... its device address
 };
 
 struct mac_ctx {
@@ -655,10 +657,10 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         const int dedup = iper ? 1 : 0;
         if (!poll_possible)
             ;   // indexed above
-        else if (isrc.cands && iper == kIdxPerWide)
+        else if (isrc.keysT && iper == kIdxPerWide)
             hipLaunchKernelGGL((disk_index_kernel<true, kIdxPerWide>), dim3(nidx), dim3(kIdxThreads), 0,
                                s, tsi, isrc, N, K, ctx->grid, pa, dedup, io);
-        else if (isrc.cands)
+        else if (isrc.keysT)
             hipLaunchKernelGGL((disk_index_kernel<true, kIdxPer>), dim3(nidx), dim3(kIdxThreads), 0, s,
                                tsi, isrc, N, K, ctx->grid, pa, dedup, io);
         else if (iper == kIdxPerWide)
@@ -711,6 +713,17 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             HCK(hipGetLastError());
         }
         if (poll_possible) {
+            // the bit-word kernel runs when the previous poll on this lane had more than
+            // kBitsMinDisks disks with neighbours (the poll kernel writes the count to mapped host
+            // memory): a hint only, the poll kernel takes every disk when it is not launched
+            if (!L->h_dc.p) {
+                L->h_dc.reserve(64, hipHostMallocMapped | hipHostMallocCoherent);
+                *(volatile int*)L->h_dc.p = 1 << 30;   // first poll: launch
+                void* dp = nullptr;
+                HCK(hipHostGetDevicePointer(&dp, L->h_dc.p, 0));
+                L->d_dc = (int*)dp;
+            }
+            const int bits_on = *(volatile int*)L->h_dc.p > kBitsMinDisks ? 1 : 0;
             const int gy = 1;   // walk workgroups loop over their disk's position slices
             const int chains = (K + kChainC - 1) / kChainC;
             const int n_chain = d_obj ? chains : 0;
@@ -727,12 +740,14 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                                L->ncount.as<int>(), L->dlist.as<int>(), L->mode.as<int>() + 1,
                                L->mode.as<int>() + 2, N, K,
                                d_mode, L->partial.as<double>(), L->spart.as<double>(), n_chain, d_pen,
-                               penalty, d_vp, n_shared, counts);
+                               penalty, d_vp, n_shared, counts, bits_on, L->d_dc);
             HCK(hipGetLastError());
             // the shared entries of crowded polls: bit-words per distinct position (k_bits.h);
             // returns at once when few disks have neighbours (the poll kernel took them)
             const unsigned nbits = (unsigned)std::max(1, std::min(N, ctx->cus));
-            if (counts)
+            if (!bits_on)
+                ;
+            else if (counts)
                 hipLaunchKernelGGL(shared_bits_kernel<true>, dim3(nbits), dim3(kBitsThreads), 0, s,
                                    ctx->xys.as<double2>(), ctx->ws.as<double>(), ctx->off.as<int32_t>(),
                                    ctx->grid, d_urec, d_map, L->ucount.as<int>(), L->region.as<int4>(),
@@ -1120,6 +1135,7 @@ void mac_ctx_destroy(mac_ctx* ctx)
     for (Lane* l : ctx->lanes_all) {
         l->h_stage.release();
         l->h_io.release();
+        l->h_dc.release();
         for (DevBuf* b : {&l->cands, &l->disks, &l->partial, &l->area, &l->obj, &l->best,
                           &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->pen, &l->nbr,
                           &l->ncount, &l->dlist, &l->qual, &l->spart, &l->vp, &l->xinc,
