@@ -168,7 +168,8 @@ __global__ __launch_bounds__(kBitsThreads) void shared_bits_kernel(
     __shared__ uint16_t ucache[kBitsUC]; // map values of the job's disks, [m][k - kb] (when they fit)
     __shared__ float4 ent[kBitsGrp][kWave * kBitsWP / 2];   // {U0, U1, V0, V1} per entry pair
     __shared__ f32x2 entq[kBitsGrp][kWave * kBitsWP / 2];   // {Q0, Q1}
-    __shared__ int slive[kBitsGrp], sg_toff[kBitsGrp], sg_bp[kBitsGrp + 1], sg_m1;
+    __shared__ int slive[kBitsGrp], sg_toff[kBitsGrp], sg_bp[kBitsGrp + 1], sg_np, sg_next[2];
+    __shared__ int sg_m[kBitsGrp], sg_lo[kBitsGrp], sg_hi[kBitsGrp];
 
     if (mode && *mode != kModePoll) return;                     // uniform
     if (dcount[kDcBits] + dcount[kDcOther] <= kBitsMinDisks) return;   // the poll kernel's jobs
@@ -244,29 +245,46 @@ __global__ __launch_bounds__(kBitsThreads) void shared_bits_kernel(
                 const int2* const stile = stilea + pb % kBitsE;
                 const double* const sw = swa + pb % kBitsE;
                 uint64_t W0[kBitsPT], W1[kBitsPT];
+#pragma unroll
+                for (int c = 0; c < kBitsPT; ++c) W0[c] = W1[c] = 0;
                 MAC_BITS_N(9);
-                for (int m0 = 0; m0 < nd;) {
-                    // the group: consecutive disks while their positions fit the table
+                // groups of at most kBitsGrp pieces = (disk m, position range [lo, hi)) of at most
+                // kBitsTab positions in all, in disk order then position order: disk i's pieces come
+                // first (W |= its word: each candidate's position lies in exactly one piece), then
+                // the neighbours' (W &= ~word)
+                for (int gm = 0, gu = 0; gm < nd;) {
                     if (tid == 0) {
-                        int m1 = m0, used = 0;
-                        while (m1 < nd && m1 - m0 < kBitsGrp && used + sU[m1] <= kBitsTab) {
-                            sg_toff[m1 - m0] = used;
-                            used += sU[m1];
-                            ++m1;
+                        int m = gm, u = gu, used = 0, np = 0;
+                        while (m < nd && np < kBitsGrp && used < kBitsTab) {
+                            const int take = min(sU[m] - u, kBitsTab - used);
+                            sg_m[np] = m;
+                            sg_lo[np] = u;
+                            sg_hi[np] = u + take;
+                            sg_toff[np] = used;
+                            used += take;
+                            ++np;
+                            u += take;
+                            if (u == sU[m]) {
+                                ++m;
+                                u = 0;
+                            }
                         }
-                        sg_m1 = m1;
+                        sg_np = np;
+                        sg_next[0] = m;
+                        sg_next[1] = u;
                     }
                     if (tid < kBitsGrp) slive[tid] = 0;
                     __syncthreads();
                     MAC_BITS_T(1);
                     MAC_BITS_N(10);
-                    const int m1 = sg_m1;
-                    // the group's entries relative to each disk's region centre, as the walk
+                    const int np = sg_np;
+                    // the pieces' entries relative to their disk's region centre, as the walk
                     // stages them (k_poll.h), in pairs {U0, U1, V0, V1}, {Q0, Q1}; entries outside
                     // region d's box, past the list or non-finite are inert: Q = +inf (d' = -inf)
                     for (int t = tid; t < kBitsGrp * kPass; t += kBitsThreads) {
-                        const int q = t / kPass, e = t - q * kPass, m = m0 + q;
-                        if (m >= m1) continue;
+                        const int q = t / kPass, e = t - q * kPass;
+                        if (q >= np) continue;
+                        const int m = sg_m[q];
                         const double2 p = s64[e];
                         const int2 tl = stile[e];
                         const int4 bx = sbox[m];
@@ -282,11 +300,11 @@ __global__ __launch_bounds__(kBitsThreads) void shared_bits_kernel(
                         if (in) slive[q] = 1;
                     }
                     __syncthreads();
-                    if (tid == 0) {   // kBitsPL * 64-position blocks of the live disks, flattened
+                    if (tid == 0) {   // kBitsPL * 64-position blocks of the live pieces, flattened
                         int nb = 0;
                         for (int q = 0; q < kBitsGrp; ++q) {
                             sg_bp[q] = nb;
-                            if (m0 + q < m1 && slive[q]) nb += (sU[m0 + q] + kBitsBlk - 1) / kBitsBlk;
+                            if (q < np && slive[q]) nb += (sg_hi[q] - sg_lo[q] + kBitsBlk - 1) / kBitsBlk;
                         }
                         sg_bp[kBitsGrp] = nb;
                     }
@@ -302,9 +320,9 @@ __global__ __launch_bounds__(kBitsThreads) void shared_bits_kernel(
                         int q = 0;
 #pragma unroll
                         for (int z = 1; z < kBitsGrp; ++z) q += b >= sg_bp[z] ? 1 : 0;
-                        const int m = m0 + q, d = sd[m], U = sU[m];
+                        const int m = sg_m[q], d = sd[m], U = sg_hi[q], lo = sg_lo[q];
                         const int64_t row = (int64_t)d * K;
-                        const int p0 = (b - sg_bp[q]) * kBitsBlk + lane;
+                        const int p0 = lo + (b - sg_bp[q]) * kBitsBlk + lane;
                         float4 c[kBitsPL];
                         float xp[kBitsPL];
                         f32x2 sa[kBitsPL], sb[kBitsPL], st[kBitsPL], ns[kBitsPL], xp2[kBitsPL];
@@ -379,7 +397,7 @@ __global__ __launch_bounds__(kBitsThreads) void shared_bits_kernel(
                                 }
                                 t4 = make_uint4(t[0], t[1], t[2], t[3]);
                             }
-                            tab[sg_toff[q] + pp] = t4;
+                            tab[sg_toff[q] + pp - lo] = t4;
                         }
                     }
                     __syncthreads();
@@ -391,26 +409,26 @@ __global__ __launch_bounds__(kBitsThreads) void shared_bits_kernel(
                     for (int c = 0; c < kBitsPT; ++c) {
                         const int k = kb + tid + c * kBitsThreads;
 #pragma unroll
-                        for (int q = 0; q < kBitsGrp; ++q)
-                            um[c][q] = (k < kend && m0 + q < m1 && slive[q])
-                                           ? (cached ? (int)ucache[(m0 + q) * kc + k - kb]
-                                                     : umap[(int64_t)sd[m0 + q] * K + k])
-                                           : 0;
+                        for (int q = 0; q < kBitsGrp; ++q) {
+                            const int m = sg_m[q];
+                            um[c][q] = (k < kend && q < np && slive[q])
+                                           ? (cached ? (int)ucache[m * kc + k - kb]
+                                                     : umap[(int64_t)sd[m] * K + k])
+                                           : -1;
+                        }
                     }
 #pragma unroll
                     for (int c = 0; c < kBitsPT; ++c) {
 #pragma unroll
                         for (int q = 0; q < kBitsGrp; ++q) {
-                            if (m0 + q >= m1) continue;
-                            uint64_t a0 = 0, a1 = 0;
-                            if (slive[q]) {
-                                const uint4 t = tab[sg_toff[q] + um[c][q]];
-                                a0 = (uint64_t)t.x | ((uint64_t)t.y << 32);
-                                a1 = (uint64_t)t.z | ((uint64_t)t.w << 32);
-                            }
-                            if (m0 + q == 0) {
-                                W0[c] = a0;
-                                W1[c] = a1;
+                            const int u = um[c][q] - sg_lo[q];
+                            if (um[c][q] < 0 || u < 0 || um[c][q] >= sg_hi[q]) continue;
+                            const uint4 t = tab[sg_toff[q] + u];
+                            const uint64_t a0 = (uint64_t)t.x | ((uint64_t)t.y << 32);
+                            const uint64_t a1 = (uint64_t)t.z | ((uint64_t)t.w << 32);
+                            if (sg_m[q] == 0) {
+                                W0[c] |= a0;
+                                W1[c] |= a1;
                             } else {
                                 W0[c] &= ~a0;
                                 W1[c] &= ~a1;
@@ -419,7 +437,8 @@ __global__ __launch_bounds__(kBitsThreads) void shared_bits_kernel(
                     }
                     __syncthreads();   // the next group overwrites the tables and its info
                     MAC_BITS_T(4);
-                    m0 = m1;
+                    gm = sg_next[0];
+                    gu = sg_next[1];
                 }
 #pragma unroll
                 for (int c = 0; c < kBitsPT; ++c) {

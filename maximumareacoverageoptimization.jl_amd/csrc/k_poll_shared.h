@@ -34,8 +34,8 @@ __device__ __forceinline__ bool box_has(const int4& b, int tx, int ty)
 // "overflowed"), their region boxes in nboxT. Disks with neighbours are appended to dlist (order irrelevant: each is processed
 // independently); *dcount must be zero on entry (the index kernel clears it).
 // A disk with neighbours goes to the bit-word kernel's list (front of dlist, k_bits.h) when its
-// list did not overflow, its region is at most 64 x 64 tiles and it and every neighbour have at
-// most kBitsTab positions; otherwise to the back of dlist (the poll kernel's fp64 jobs).
+// list did not overflow and its region is at most 64 x 64 tiles; otherwise to the back of dlist
+// (the poll kernel's fp64 jobs).
 __device__ __forceinline__ void neighbors_block(int i, int N, const int4* __restrict__ region,
                                                 uint16_t* __restrict__ nbr, int4* __restrict__ nboxT,
                                                 int* __restrict__ ncount,
@@ -63,9 +63,6 @@ __device__ __forceinline__ void neighbors_block(int i, int N, const int4* __rest
     bool bad = false;
     if (nc > 0) {
         bad = nc > kPollNbr || R.y - R.x + 1 > 64 || R.w - R.z + 1 > 64;
-        if (!bad)
-            for (int m = threadIdx.x; m <= nc; m += blockDim.x)
-                bad |= ucount[m == 0 ? i : (int)nbr[i * kPollNbr + m - 1]] > kBitsTab;
     }
     bad = __syncthreads_or(bad);
     if (threadIdx.x == 0) {

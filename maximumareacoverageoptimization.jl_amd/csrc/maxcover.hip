@@ -142,6 +142,7 @@ struct Lane {
     PinnedBuf h_io;                            // host-pointer calls: candidates in, results out
     PinnedBuf h_dc;                            // disks with neighbours of the last poll (mapped)
     int* d_dc = nullptr;                       // ... its device address
+    int dc_hist[8] = {};                       // ... as read at the last 8 poll enqueues
 };
 
 struct mac_ctx {
@@ -723,7 +724,15 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                 HCK(hipHostGetDevicePointer(&dp, L->h_dc.p, 0));
                 L->d_dc = (int*)dp;
             }
-            const int bits_on = *(volatile int*)L->h_dc.p > kBitsMinDisks ? 1 : 0;
+            // (the maximum over the last 8 polls: MADS alternates crowded and quiet polls, and a
+            // crowded poll without the bit-word kernel costs several times its launch)
+            int dc_max = *(volatile int*)L->h_dc.p;
+            for (int q = 7; q > 0; --q) {
+                L->dc_hist[q] = L->dc_hist[q - 1];
+                dc_max = std::max(dc_max, L->dc_hist[q]);
+            }
+            L->dc_hist[0] = *(volatile int*)L->h_dc.p;
+            const int bits_on = dc_max > kBitsMinDisks ? 1 : 0;
             const int gy = 1;   // walk workgroups loop over their disk's position slices
             const int chains = (K + kChainC - 1) / kChainC;
             const int n_chain = d_obj ? chains : 0;
