@@ -12,6 +12,7 @@
 namespace mac {
 
 constexpr int kFinC = 16;   // candidates per finalize block (x 64 slice groups)
+constexpr int kFinMaxBlk = 256;   // finalize blocks whose minima the last block loads at once
 constexpr int kFinThreads = 1024;
 
 // Sequential objective penalty (src/TDM_STATIC_opt.jl:88-92): violation_k = sum over i = 0..N-1
@@ -138,12 +139,26 @@ __device__ __forceinline__ void finalize_argmin(const FinBest& fb, double o, int
     if (old != gridDim.x - 1) return;   // wave-uniform: not the last block
     bv = __builtin_inf();
     bi = -1;
-    for (unsigned q = lane; q < gridDim.x; q += kWave) {
-        const unsigned long long v = __hip_atomic_load(fb.blk + 2 * q, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long ix = __hip_atomic_load(fb.blk + 2 * q + 1, __ATOMIC_RELAXED,
+    // every block's minimum in flight at once (kFinMaxBlk / 64 per lane), then the reduction
+    constexpr int kPer = kFinMaxBlk / kWave;
+    unsigned long long v[kPer], ix[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+        const unsigned q = lane + r * kWave;
+        v[r] = q < gridDim.x ? __hip_atomic_load(fb.blk + 2 * q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : __builtin_bit_cast(unsigned long long, __builtin_inf());
+        ix[r] = q < gridDim.x ? __hip_atomic_load(fb.blk + 2 * q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : ~0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < kPer; ++r)
+        if ((long long)ix[r] >= 0) argmin_take(bv, bi, __builtin_bit_cast(double, v[r]), (int)(long long)ix[r]);
+    for (unsigned q = lane + kFinMaxBlk; q < gridDim.x; q += kWave) {   // grids past kFinMaxBlk
+        const unsigned long long vv = __hip_atomic_load(fb.blk + 2 * q, __ATOMIC_RELAXED,
                                                         __HIP_MEMORY_SCOPE_AGENT);
-        argmin_take(bv, bi, __builtin_bit_cast(double, v), (int)(long long)ix);
+        const unsigned long long xx = __hip_atomic_load(fb.blk + 2 * q + 1, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+        argmin_take(bv, bi, __builtin_bit_cast(double, vv), (int)(long long)xx);
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1)
@@ -156,7 +171,6 @@ __device__ __forceinline__ void finalize_argmin(const FinBest& fb, double o, int
         if (fb.mirror) {  // pinned coherent host words: the result, then (released) its sequence
             fb.mirror[0] = fb.best[0];
             fb.mirror[1] = fb.best[1];
-            __threadfence_system();
             __hip_atomic_store(reinterpret_cast<uint64_t*>(fb.mirror + 2), fb.seq, __ATOMIC_RELEASE,
                                __HIP_MEMORY_SCOPE_SYSTEM);
         }
