@@ -726,12 +726,13 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             }
             // (the maximum over the last 8 polls: MADS alternates crowded and quiet polls, and a
             // crowded poll without the bit-word kernel costs several times its launch)
-            int dc_max = *(volatile int*)L->h_dc.p;
-            for (int q = 7; q > 0; --q) {
-                L->dc_hist[q] = L->dc_hist[q - 1];
-                dc_max = std::max(dc_max, L->dc_hist[q]);
+            const int dc_now = *(volatile int*)L->h_dc.p;   // 1 << 30 until a poll wrote it
+            int dc_max = dc_now;
+            if (dc_now < (1 << 30)) {
+                for (int q = 7; q > 0; --q) L->dc_hist[q] = L->dc_hist[q - 1];
+                L->dc_hist[0] = dc_now;
+                for (int q = 0; q < 8; ++q) dc_max = std::max(dc_max, L->dc_hist[q]);
             }
-            L->dc_hist[0] = *(volatile int*)L->h_dc.p;
             const int bits_on = dc_max > kBitsMinDisks ? 1 : 0;
             const int gy = 1;   // walk workgroups loop over their disk's position slices
             const int chains = (K + kChainC - 1) / kChainC;

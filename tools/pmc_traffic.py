@@ -45,9 +45,9 @@ def main():
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("--config", type=int, default=4)
-    ap.add_argument("--chain", default="mac::cands_keys_kernel,mac::disk_index_kernel<true>,"
-                    "mac::walk_setup_kernel,mac::coverage_poll_kernel,mac::finalize_kernel",
-                    help="comma-separated kernels of one poll")
+    ap.add_argument("--chain", default="mac::cands_keys_kernel;mac::disk_index_kernel<true, 3>;"
+                    "mac::walk_setup_kernel;mac::coverage_poll_kernel;mac::finalize_kernel",
+                    help="semicolon-separated kernels of one poll")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     fetch = load(a.fetch_dir, "FETCH_SIZE")
@@ -66,7 +66,7 @@ def main():
             "write_kib_raw": wk,
             "hbm_bytes_per_launch": 2.0 * fk * 1024.0 + wk * 1024.0,
         }
-    chain = a.chain.split(",")
+    chain = a.chain.split(";")
     missing = [k for k in chain if k not in kernels]
     if missing:
         raise SystemExit(f"{missing} not found; have {list(kernels)}")
