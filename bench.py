@@ -6,11 +6,14 @@ One step = one complete MADS poll over a synthetic fire grid: K = 6N+1 candidate
 rank holds a full replica of the point list in HBM; inputs are resident before timing starts.
 
 Multi-GPU (`--scaling`):
-  weak (default)  every rank evaluates a complete K-candidate poll set of its own (independent
+  strong (default) the single K-candidate poll is split into P contiguous candidate shards (the
+                  north star's split); value = K candidates per step / the max-over-ranks time;
+  weak            every rank evaluates a complete K-candidate poll set of its own (independent
                   LTMADS bases around the same incumbent, rank 0's being the single-GPU poll), so
                   one step polls P*K candidates and the all-gather picks the best of all of
-                  them: per-GPU work fixed as P grows;
-  strong          the single K-candidate poll is split into P contiguous candidate shards.
+                  them: per-GPU work fixed as P grows (a secondary, labelled line).
+`--shard-of P` times rank 0's shard of a P-way split alone on one GPU (no collective): the
+per-rank chain floor that bounds strong scaling.
 
 Default workload: BASELINE config 4 (512 UAVs, 4096 x 4096 = 16.8M-cell grid, K = 3073, fp64),
 the configuration the north-star targets are quoted on and the one the 1/2/4/8-GPU scaling
@@ -304,6 +307,9 @@ def main():
                     help="N>1: strong (default, the north star's split) = the single poll's "
                          "candidates sharded over the GPUs; weak = one full poll set per GPU "
                          "(P*K candidates per step, a wider poll)")
+    ap.add_argument("--shard-of", type=int, default=1,
+                    help="time rank 0's shard of a P-way strong split alone on one GPU (no "
+                         "collective; value = shard candidates / time)")
     ap.add_argument("--disks", default="uniform", choices=("uniform", "clustered"),
                     help="UAV disks: uniform over the domain (default) or SURVEY 8(d)'s "
                          "clustered variant (sqrt(N)*40 m around the centre, overlapping)")
@@ -363,6 +369,10 @@ def main():
         lo, hi = 0, K                      # a whole poll set per rank
         idx_base = rank * K                # global candidate index = rank * K + k
         K_step = K * world                 # candidates evaluated per step, all ranks
+    elif args.shard_of > 1 and not distributed:
+        lo, hi = pdist.shard_range(K, 0, args.shard_of)   # rank 0's shard, timed alone
+        idx_base = lo
+        K_step = hi - lo
     else:
         lo, hi = pdist.shard_range(K, rank, world)
         idx_base = lo
@@ -522,7 +532,9 @@ def main():
                 "disks": ("integer centres uniform over the domain, R=36" if args.disks == "uniform"
                           else "clustered: integer centres within sqrt(N)*40 m of the centre, R=36"),
                 "cons3": "prev = incumbent, d_lim = 10 m, FOV 100 deg (every candidate checked)",
-                "parallelism": (f"{world} GPU(s), one full poll set each, 16-B argmin all-gather"
+                "parallelism": (f"rank 0 of a {args.shard_of}-way candidate split, timed alone on "
+                                f"1 GPU (no collective)" if args.shard_of > 1 and not distributed else
+                                f"{world} GPU(s), one full poll set each, 16-B argmin all-gather"
                                 if args.scaling == "weak" else
                                 f"one poll's candidates sharded over {world} GPU(s), "
                                 f"16-B argmin all-gather"),
