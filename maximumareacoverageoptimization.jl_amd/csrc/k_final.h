@@ -98,6 +98,9 @@ struct FinBest {
     int64_t idx_base;
     unsigned long long* blk;   // [gridDim.x][2] per-block minima {obj bits, index}
     unsigned* arrive;          // arrival counter, zero between launches (the last block resets it)
+    uint64_t* hblk;            // mapped host words, [block][4] = {obj bits, local index, seq, -}:
+                               // the host reduces them without waiting for the last block (may
+                               // be null)
 };
 
 __device__ __forceinline__ void argmin_take(double& v1, int& i1, double v2, int i2)
@@ -127,6 +130,12 @@ __device__ __forceinline__ void finalize_argmin(const FinBest& fb, double o, int
     for (int off = kFinC / 2; off >= 1; off >>= 1)
         argmin_take(bv, bi, __shfl_xor(bv, off, kWave), __shfl_xor(bi, off, kWave));
     unsigned old = 0;
+    if (lane == 0 && fb.hblk) {   // this block's minimum to the host, then (released) its sequence
+        uint64_t* const h = fb.hblk + 4 * blockIdx.x;
+        h[0] = __builtin_bit_cast(uint64_t, bv);
+        h[1] = (uint64_t)(int64_t)bi;
+        __hip_atomic_store(h + 2, fb.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     if (lane == 0) {
         __hip_atomic_store(fb.blk + 2 * blockIdx.x, __builtin_bit_cast(unsigned long long, bv),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

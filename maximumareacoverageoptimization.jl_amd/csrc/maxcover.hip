@@ -158,6 +158,12 @@ struct mac_ctx {
     double* d_mirror = nullptr;
     uint64_t mirror_seq = 0;
     const void* mirror_for = nullptr;
+    // ... and the per-block minima of the latest such poll's finalize (k_final.h FinBest.hblk):
+    // the host reduces them as soon as every block has written its own
+    PinnedBuf h_blk;
+    uint64_t* d_blk = nullptr;
+    int mirror_nblk = 0;
+    int64_t mirror_base = 0;
     hipStream_t dev_stream = nullptr;   // ordered stream for *_dev calls passed stream = NULL
 
     int algo = MAC_ALGO_AUTO;
@@ -795,7 +801,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         if (L->finarrive.grow(sizeof(unsigned)))   // zero once; the last block of each launch resets it
             HCK(hipMemsetAsync(L->finarrive.p, 0, L->finarrive.cap, s));
         fb = FinBest{d_best, d_mirror, mirror_seq, idx_base, L->finblk.as<unsigned long long>(),
-                     L->finarrive.as<unsigned>()};
+                     L->finarrive.as<unsigned>(),
+                     d_mirror && nfin <= (unsigned)kFinMaxBlk ? ctx->d_blk : nullptr};
     }
     uint64_t* tsf = ts_c >= 0 ? take_ts(nfin, ts_f, ts_nf) : nullptr;
     hipLaunchKernelGGL(finalize_kernel, dim3(nfin), dim3(kFinThreads), 0, s,
@@ -1962,9 +1969,20 @@ static int32_t poll_best_dev(mac_ctx* ctx, const T* d_cands_in, int64_t three_n,
             HCK(hipHostGetDevicePointer(&dp, ctx->h_best.p, 0));
             ctx->d_mirror = (double*)dp;
         }
+        if (!ctx->d_blk) {
+            ctx->h_blk.reserve(sizeof(uint64_t) * 4 * kFinMaxBlk, hipHostMallocMapped | hipHostMallocCoherent);
+            std::memset(ctx->h_blk.p, 0, sizeof(uint64_t) * 4 * kFinMaxBlk);
+            void* dp = nullptr;
+            HCK(hipHostGetDevicePointer(&dp, ctx->h_blk.p, 0));
+            ctx->d_blk = (uint64_t*)dp;
+        }
         d_mirror = ctx->d_mirror;
         seq = ++ctx->mirror_seq;
         ctx->mirror_for = d_best;
+        // finalize's grid (enqueue_eval): its blocks mirror their minima when it fits h_blk
+        const int nfin = 8 * (int)((K + 8 * kFinC - 1) / (8 * kFinC));
+        ctx->mirror_nblk = nfin <= kFinMaxBlk ? nfin : 0;
+        ctx->mirror_base = idx_base;
     }
     enqueue_eval(ctx, L, s, matrix_src(d_cands, N), N, (int)K, use_tiled(ctx, N, nullptr, three_n), d_rmax,
                  penalty, d_prev, d_dlimT, d_dlim, tan_half_fov, nullptr, d_o, (double*)d_best, idx_base,
@@ -2011,6 +2029,34 @@ int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* b
         // poll takes ~0.1 ms), and after 2 ms wait for the stream instead (which also reports a
         // failed launch)
         const uint64_t want = ctx->mirror_seq;
+        if (ctx->mirror_nblk > 0) {
+            // every finalize block's minimum, reduced here (lexicographic (obj, index), as the
+            // device's last block does) as soon as the last one lands
+            const uint64_t* hk = (const uint64_t*)ctx->h_blk.p;
+            const auto t0 = std::chrono::steady_clock::now();
+            int b = 0;
+            for (int spin = 0; b < ctx->mirror_nblk; ++spin) {
+                while (b < ctx->mirror_nblk && __atomic_load_n(hk + 4 * b + 2, __ATOMIC_ACQUIRE) == want) ++b;
+                if (b < ctx->mirror_nblk && (spin & 1023) == 1023 &&
+                    std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2))
+                    break;   // slow or failed: the single-word mirror / the stream below
+            }
+            if (b == ctx->mirror_nblk) {
+                double bv = INFINITY;
+                int64_t bi = -1;
+                for (int q = 0; q < ctx->mirror_nblk; ++q) {
+                    const double v = __builtin_bit_cast(double, hk[4 * q]);
+                    const int64_t i = (int64_t)hk[4 * q + 1];
+                    if (i >= 0 && (bi < 0 || v < bv || (v == bv && i < bi))) {
+                        bv = v;
+                        bi = i;
+                    }
+                }
+                if (best_obj) *best_obj = bi >= 0 ? bv : INFINITY;
+                if (best_idx) *best_idx = bi >= 0 ? ctx->mirror_base + bi : -1;
+                return MAC_OK;
+            }
+        }
         const uint64_t* flag = (const uint64_t*)(hb + 2);
         const auto t0 = std::chrono::steady_clock::now();
         bool ready = false;
