@@ -112,18 +112,19 @@ struct CandSrc {
 // for bit (k_index.h "Keys"); kbad[v*nkt + tile] = 1 when some key of variable v in this tile is
 // not (every tile writes its flag, so nothing needs clearing). Half the bytes of a transposed
 // fp64 copy are written here and read by the index.
-constexpr int kKeysK = 64;   // candidates per cands_keys_kernel tile (x 32 variables)
+constexpr int kKeysK = 128;  // candidates per cands_keys_kernel tile (x 32 variables)
 
 __global__ __launch_bounds__(kBlock) void cands_keys_kernel(uint64_t* ts, const double* __restrict__ cands,
                                                             int n, int K, float* __restrict__ keysT,
                                                             int* __restrict__ kbad, int nkt)
 {
     ts_begin(ts);   // profiling only (the chain's first launch: k_common.h)
+    constexpr int NB = kKeysK / 32;   // 32-candidate flag tiles per workgroup tile
     __shared__ float t[kKeysK][33];
-    __shared__ int sbad[2][32];
+    __shared__ int sbad[NB][32];
     const int v0 = blockIdx.x * 32, k0 = blockIdx.y * kKeysK;
     const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
-    if (threadIdx.x < 64) sbad[threadIdx.x >> 5][threadIdx.x & 31] = 0;
+    if (threadIdx.x < 32 * NB) sbad[threadIdx.x >> 5][threadIdx.x & 31] = 0;
     const int vr = v0 + tx;
     const double base = vr < n ? cands[vr] : 0.0;
     constexpr int J = kKeysK / 8;
@@ -133,16 +134,19 @@ __global__ __launch_bounds__(kBlock) void cands_keys_kernel(uint64_t* ts, const 
         const int k = k0 + ty + 8 * j;
         x[j] = (k < K && vr < n) ? cands[(int64_t)k * n + vr] : base;
     }
-    bool ok[2] = {true, true};
+    bool ok[NB];
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
+    for (int b = 0; b < NB; ++b) ok[b] = true;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {   // candidate ty + 8j lies in flag tile (8j) / 32 = j / 4
         const float f = (float)(x[j] - base);
-        ok[j >= J / 2] &= __builtin_bit_cast(uint64_t, base + (double)f) == __builtin_bit_cast(uint64_t, x[j]);
+        ok[j / 4] &= __builtin_bit_cast(uint64_t, base + (double)f) == __builtin_bit_cast(uint64_t, x[j]);
         t[ty + 8 * j][tx] = f;
     }
     __syncthreads();
-    if (!ok[0]) atomicOr(&sbad[0][tx], 1);
-    if (!ok[1]) atomicOr(&sbad[1][tx], 1);
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+        if (!ok[b]) atomicOr(&sbad[b][tx], 1);
     // rows of kKeysK keys per variable: 64 consecutive threads write one row (256 B)
     const int kk = threadIdx.x & (kKeysK - 1), vq = threadIdx.x / kKeysK;
 #pragma unroll
@@ -152,9 +156,9 @@ __global__ __launch_bounds__(kBlock) void cands_keys_kernel(uint64_t* ts, const 
         if (k < K && v < n) keysT[(int64_t)v * K + k] = t[kk][vv];
     }
     __syncthreads();
-    if (threadIdx.x < 64) {
+    if (threadIdx.x < 32 * NB) {
         const int h = threadIdx.x >> 5, vv = threadIdx.x & 31, v = v0 + vv;
-        const int tile = 2 * blockIdx.y + h;
+        const int tile = NB * blockIdx.y + h;
         if (v < n && tile < nkt) kbad[(int64_t)v * nkt + tile] = sbad[h][vv];
     }
     ts_end(ts);
