@@ -36,20 +36,31 @@ def reduce_best(objs: np.ndarray, idxs: np.ndarray) -> tuple[float, int]:
     return best_o, best_i
 
 
+_GATHER_OUT = {}
+
+
 def gather_best(best16, group=None):
     """all_gather of the 16-byte {obj f64, idx i64} record; returns (obj, idx) lexicographic min.
 
     ``best16``: torch tensor of 2 float64 (the poll's d_best; the index is stored as raw int64
-    bits). Works on any backend: RCCL for device tensors, gloo for CPU tensors."""
+    bits). Works on any backend: RCCL for device tensors, gloo for CPU tensors. One collective
+    into a preallocated (world x 2) buffer per (device, group), one 16*world-byte copy to the
+    host: the per-poll cost is the collective's latency, not allocations."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
-    out = [torch.empty_like(best16) for _ in range(world)]
-    dist.all_gather(out, best16, group=group)
-    stacked = torch.stack(out).cpu()
-    objs = stacked[:, 0].numpy().copy()
-    idxs = stacked.view(torch.int64)[:, 1].numpy().copy()
+    key = (best16.device, id(group), world)
+    out = _GATHER_OUT.get(key)
+    if out is None:
+        out = _GATHER_OUT[key] = torch.empty((world, 2), dtype=torch.float64, device=best16.device)
+    if hasattr(dist, "all_gather_into_tensor"):
+        dist.all_gather_into_tensor(out, best16.reshape(1, 2), group=group)
+    else:   # pragma: no cover - older torch
+        dist.all_gather(list(out.unbind(0)), best16, group=group)
+    h = out.cpu()
+    objs = h[:, 0].numpy().copy()
+    idxs = h.view(torch.int64)[:, 1].numpy().copy()
     return reduce_best(objs, idxs)
 
 
