@@ -58,6 +58,13 @@ extern "C" {
                                    through the *_f32 entry points, widened exactly); _F32 fails */
 #define MAC_OPT_TILE_POINTS  3  /* target points per spatial tile (default 4), set before points */
 #define MAC_OPT_PROFILE      4  /* 1: the timed launches stamp their workgroups' start / end     */
+#define MAC_OPT_SHARED       5  /* poll walk, entries two disks' regions share:
+                                   MAC_SHARED_AUTO (default) | _FP64 | _BITS                      */
+
+#define MAC_SHARED_AUTO  0  /* bit-word kernel when one of the lane's last 8 polls had more than 16
+                               disks with neighbours, else fp64 jobs in the poll kernel         */
+#define MAC_SHARED_FP64  1  /* always the poll kernel's fp64 jobs                                */
+#define MAC_SHARED_BITS  2  /* always the bit-word kernel (every disk it takes, any count)       */
 
 #define MAC_ALGO_AUTO   0
 #define MAC_ALGO_SCAN   1  /* streaming brute-force scan: every point against every disk     */

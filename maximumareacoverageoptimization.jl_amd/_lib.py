@@ -28,6 +28,8 @@ MAC_OPT_ALGO = 1
 MAC_OPT_STORAGE = 2
 MAC_OPT_TILE_POINTS = 3
 MAC_OPT_PROFILE = 4
+MAC_OPT_SHARED = 5
+SHARED_MODES = {"auto": 0, "fp64": 1, "bits": 2}
 MAC_ALGO_AUTO = 0
 MAC_ALGO_SCAN = 1
 MAC_ALGO_TILED = 2
@@ -269,6 +271,11 @@ class Context:
     # -- options
     def set_option(self, option: int, value: int) -> None:
         _check(self._L.mac_set_option(self._h, int(option), int(value)))
+
+    def set_shared(self, mode: str) -> None:
+        """How the poll walk decides the entries two disks' regions share (MAC_OPT_SHARED):
+        "auto" (default), "fp64" (the poll kernel's jobs) or "bits" (the bit-word kernel)."""
+        self.set_option(MAC_OPT_SHARED, SHARED_MODES[mode])
 
     def set_algo(self, algo: str) -> None:
         if algo not in ALGOS:

@@ -154,7 +154,7 @@ __global__ __launch_bounds__(kBitsThreads) void shared_bits_kernel(
     const uint16_t* __restrict__ nbrT, const float4* __restrict__ lane4,
     const float* __restrict__ lanexp, const int* __restrict__ ncount,
     const int* __restrict__ qual, int* __restrict__ dcount, const int* __restrict__ mode, int N,
-    int K, double* __restrict__ spart)
+    int K, double* __restrict__ spart, int min_disks)
 {
     __shared__ int sd[kBitsD], sU[kBitsD];
     __shared__ int4 sbox[kBitsD];
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(kBitsThreads) void shared_bits_kernel(
     __shared__ int sg_m[kBitsGrp], sg_lo[kBitsGrp], sg_hi[kBitsGrp];
 
     if (mode && *mode != kModePoll) return;                     // uniform
-    if (dcount[kDcBits] + dcount[kDcOther] <= kBitsMinDisks) return;   // the poll kernel's jobs
+    if (dcount[kDcBits] + dcount[kDcOther] <= min_disks) return;   // the poll kernel's jobs
     const int tid = threadIdx.x, lane = tid & (kWave - 1);
     const int wid = __builtin_amdgcn_readfirstlane(tid / kWave);   // wave-uniform (scalar loads)
 #ifdef MAC_DIAG

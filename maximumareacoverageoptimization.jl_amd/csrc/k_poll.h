@@ -155,7 +155,7 @@ __device__ __forceinline__ void coverage_poll_body(
         // kBitsMinDisks disks with neighbours the bit-word kernel (k_bits.h, launched next) takes
         // every disk it qualifies for; the jobs of those disks return at once here.
         const int nA = dcount[kDcBits], nB = dcount[kDcOther];
-        const bool bits = bits_on && lane4 != nullptr && nA + nB > kBitsMinDisks;
+        const bool bits = bits_on && lane4 != nullptr && nA + nB > (bits_on == 2 ? 0 : kBitsMinDisks);
         const int nlist = bits ? nB : nA + nB;   // list position q: dlist[N-1-q], then dlist[q-nB]
         const int C = nlist * ((K + kShC - 1) / kShC) > 2 * (int)gridDim.x ? kShCWide : kShC;
         const int nsub = (K + C - 1) / C;

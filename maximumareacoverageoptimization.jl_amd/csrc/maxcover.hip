@@ -167,6 +167,7 @@ struct mac_ctx {
     hipStream_t dev_stream = nullptr;   // ordered stream for *_dev calls passed stream = NULL
 
     int algo = MAC_ALGO_AUTO;
+    int shared_mode = MAC_SHARED_AUTO;   // MAC_OPT_SHARED
     bool profile = false;
     // In-kernel launch timing (k_common.h ts_begin / ts_end): each profiled walk launch takes
     // nwg consecutive {start, end} slots of `stamps`. a: the scan / tiled launch, b: the poll
@@ -739,7 +740,10 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                 L->dc_hist[0] = dc_now;
                 for (int q = 0; q < 8; ++q) dc_max = std::max(dc_max, L->dc_hist[q]);
             }
-            const int bits_on = dc_max > kBitsMinDisks ? 1 : 0;
+            // 0: fp64 jobs; 1: bit-word kernel above kBitsMinDisks disks with neighbours; 2: always
+            const int bits_on = ctx->shared_mode == MAC_SHARED_BITS ? 2
+                              : ctx->shared_mode == MAC_SHARED_FP64 ? 0
+                              : dc_max > kBitsMinDisks ? 1 : 0;
             const int gy = 1;   // walk workgroups loop over their disk's position slices
             const int chains = (K + kChainC - 1) / kChainC;
             const int n_chain = d_obj ? chains : 0;
@@ -769,14 +773,14 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                                    ctx->grid, d_urec, d_map, L->ucount.as<int>(), L->region.as<int4>(),
                                    L->nbr.as<uint16_t>(), L->lane4.as<float4>(), L->lanexp.as<float>(),
                                    L->ncount.as<int>(), L->qual.as<int>(), L->mode.as<int>() + 1, d_mode,
-                                   N, K, L->spart.as<double>());
+                                   N, K, L->spart.as<double>(), bits_on == 2 ? 0 : kBitsMinDisks);
             else
                 hipLaunchKernelGGL(shared_bits_kernel<false>, dim3(nbits), dim3(kBitsThreads), 0, s,
                                    ctx->xys.as<double2>(), ctx->ws.as<double>(), ctx->off.as<int32_t>(),
                                    ctx->grid, d_urec, d_map, L->ucount.as<int>(), L->region.as<int4>(),
                                    L->nbr.as<uint16_t>(), L->lane4.as<float4>(), L->lanexp.as<float>(),
                                    L->ncount.as<int>(), L->qual.as<int>(), L->mode.as<int>() + 1, d_mode,
-                                   N, K, L->spart.as<double>());
+                                   N, K, L->spart.as<double>(), bits_on == 2 ? 0 : kBitsMinDisks);
             HCK(hipGetLastError());
             chain_done = true;
             d_spart = L->spart.as<double>();
@@ -1209,6 +1213,10 @@ int32_t mac_set_option(mac_ctx* ctx, int32_t option, int64_t value)
         return MAC_OK;
         ABI_END
     }
+    case MAC_OPT_SHARED:
+        if (value < MAC_SHARED_AUTO || value > MAC_SHARED_BITS) return fail(MAC_E_INVAL, "bad shared mode");
+        ctx->shared_mode = (int)value;
+        return MAC_OK;
     case MAC_OPT_TILE_POINTS:
         if (value < 1 || value > 4096) return fail(MAC_E_INVAL, "tile points out of range");
         ctx->tile_ppt = (int)value;

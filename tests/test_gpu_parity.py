@@ -527,6 +527,79 @@ def test_poll_walk_stress(ctx, pkg, orc, case):
     assert np.array_equal(r["poll"], r["tiled"]) or case == "mixed_weights"
 
 
+@pytest.mark.parametrize("case", ["crowded", "real_clustered", "mixed_weights", "pythagorean",
+                                  "lattice_mixed"])
+def test_shared_entry_passes(ctx, pkg, orc, case):
+    """Both shared-entry passes of the poll walk, forced (MAC_OPT_SHARED): the poll kernel's fp64
+    jobs and the bit-word kernel (k_bits.h: per-position coverage words, band entries in fp64,
+    weighted credit bit by bit), each against the C oracle. "crowded": 100 disks over one square
+    (neighbour lists past 64 go to the fp64 jobs even when the bit-words are forced);
+    "real_clustered": non-lattice coordinates (band decisions); "mixed_weights": real weights
+    (rtol 1e-12, the summation order differs from the list order); "pythagorean": entries exactly
+    at distance r (every one in the band, not covered); "lattice_mixed": integer weights (exact)."""
+    wl = pkg.workloads
+    rng = wl.SplitMix64(9090 + len(case))
+    if case == "pythagorean":
+        g = np.arange(160, dtype=np.float64)
+        x, y = np.repeat(g, 160), np.tile(g, 160)
+        w = np.full(x.size, 25.0)
+        N = 24
+        radii = np.array([5.0, 10.0, 13.0, 25.0, 15.0, 17.0])
+        x0 = np.concatenate([np.floor(rng.uniform(N) * 50) + 55, np.floor(rng.uniform(N) * 50) + 55,
+                             radii[np.floor(rng.uniform(N) * radii.size).astype(int)]])
+        ell = 1
+    else:
+        M = 40000
+        x = np.floor(rng.uniform(M) * 400.0) if case != "real_clustered" else rng.uniform(M) * 400.0
+        y = np.floor(rng.uniform(M) * 400.0) if case != "real_clustered" else rng.uniform(M) * 400.0
+        w = (np.full(M, 25.0) if case in ("crowded", "real_clustered") else
+             rng.uniform(M) * 3 + 1 if case == "mixed_weights" else np.floor(rng.uniform(M) * 7) + 1)
+        N = 100 if case == "crowded" else 40
+        span = 60 if case == "crowded" else 120
+        x0 = np.concatenate([np.floor(200 + rng.uniform(N) * span - span / 2),
+                             np.floor(200 + rng.uniform(N) * span - span / 2),
+                             np.floor(rng.uniform(N) * 20 + 15)])
+        ell = 2
+    ctx.set_points(x, y, w)
+    C = np.concatenate([x0[None, :], wl.poll_candidates(x0, rng, ell=ell)], axis=0)
+    if case == "pythagorean":
+        C[:, 2 * N:] = np.maximum(C[:, 2 * N:], 1.0)
+    if case in ("real_clustered", "mixed_weights"):
+        C[1:, :] += (rng.uniform(C[1:].size) * 0.02 - 0.01).reshape(C[1:].shape)
+    want = orc.PointerList(recs(x, y, w)).area_batch(C)
+    rmax = np.full(N, 30.0)
+    want_obj = -want + orc.violation_batch(C, rmax) * 1e5 if case != "mixed_weights" else None
+    ctx.set_algo("poll")
+    try:
+        for mode in ("fp64", "bits"):
+            ctx.set_shared(mode)
+            got = ctx.area_batch(C)
+            if case == "mixed_weights":
+                np.testing.assert_allclose(got, want, rtol=1e-12, atol=0, err_msg=mode)
+            else:
+                assert np.array_equal(got, want), (mode, np.flatnonzero(got != want)[:5])
+                bo, bi, objs = ctx.poll_best(C, rmax, want_all=True)
+                assert np.array_equal(objs, want_obj), mode
+                k = int(np.argmin(want_obj))
+                assert bi == k and bo == want_obj[k], mode
+    finally:
+        ctx.set_shared("auto")
+        ctx.set_algo("auto")
+
+
+@pytest.mark.parametrize("mode", ["fp64", "bits"])
+def test_config4_clustered_shared_passes(ctx, pkg, orc, mode):
+    """The clustered config-4 poll at full size through each forced shared-entry pass: every
+    candidate == the exact lattice count, objectives, cons3 and argmin bit-exact."""
+    x, y, w, C, rmax = pkg.workloads.make_config(4, disks="clustered")
+    ctx.set_points(x, y, w)
+    ctx.set_shared(mode)
+    try:
+        _full_poll_check(ctx, orc, C, rmax, 4096, ["poll"], "config4-clustered-" + mode)
+    finally:
+        ctx.set_shared("auto")
+
+
 # ---------------------------------------------------------------------------- native MADS driver
 
 @pytest.mark.parametrize("with_cons3", [False, True])
