@@ -78,6 +78,11 @@ for s in $STEPS; do
         run bench3 600 python bench.py --config 3 --no-cpu ; rc=$? ;;
     bench5)
         run bench5 600 python bench.py --config 5 --steps 3 --warmup 1 --no-cpu ; rc=$? ;;
+    shards)   # per-rank chain floor of the strong split: rank 0's shard alone on one GPU
+        for P in 2 4 8; do
+            run shard$P 300 python bench.py --no-cpu --shard-of $P ; rc=$?
+            fatal $rc && break
+        done ;;
     bench2)
         run bench2 600 python bench.py --config 2 --no-cpu ; rc=$? ;;
     prof)
