@@ -49,6 +49,7 @@ constexpr int kBitsK = kBitsPT * kBitsThreads;      // candidates per job (4096)
 constexpr int kBitsWP = 2;                          // 64-entry words per pass
 constexpr int kBitsGrp = 4;                         // disks per table group
 constexpr int kBitsD = kPollNbr + 1;
+constexpr int kBitsSplit = 2;                       // jobs per disk (equal weights)
 constexpr int kBitsPL = 2;                          // positions per lane in the tables
 constexpr int kBitsBlk = kBitsPL * kWave;           // positions per wave block
 constexpr int kBitsE = 1024;                        // shared entries staged in LDS at a time
@@ -182,14 +183,19 @@ __global__ __launch_bounds__(kBitsThreads) void shared_bits_kernel(
 #endif
     // jobs in descending disk order: higher-index disks have more lower-index neighbours, so the
     // heavy jobs go first; disks not listed for this kernel (qual[i] == 0) are skipped
+    // equal weights: each disk's passes are split over kBitsSplit jobs whose counts add up in
+    // spart with integer atomics (exact in any order; the poll kernel zeroed those rows);
+    // weights: one job per disk and candidate chunk, stored (a fixed fp64 summation order)
+    constexpr int kSplit = kCounts ? kBitsSplit : 1;
     const int nsub = (K + kBitsK - 1) / kBitsK;
-    const int njobs = N * nsub;
+    const int njobs = N * nsub * kSplit;
     constexpr int kPass = kWave * kBitsWP;
     typedef typename std::conditional<kCounts, uint32_t, double>::type Acc;
 
     for (int job = blockIdx.x;;) {
         if (job >= njobs) break;   // uniform
-        const int i = N - 1 - job / nsub, kb = (job % nsub) * kBitsK;
+        const int i = N - 1 - job / (nsub * kSplit);
+        const int kb = ((job / kSplit) % nsub) * kBitsK, split = job % kSplit;
         if (qual[i]) {
             const int nc = ncount[i], nd = 1 + nc;
             if (tid < nd) {
@@ -220,9 +226,12 @@ __global__ __launch_bounds__(kBitsThreads) void shared_bits_kernel(
             Acc acc[kBitsPT];
 #pragma unroll
             for (int c = 0; c < kBitsPT; ++c) acc[c] = 0;
-            for (int pb = 0; pb < total; pb += kPass) {
+            // this job's passes: a contiguous share of the disk's
+            const int npass = (total + kPass - 1) / kPass;
+            const int pbeg = (split * npass / kSplit) * kPass, pend = min(total, ((split + 1) * npass / kSplit) * kPass);
+            for (int pb = pbeg; pb < pend; pb += kPass) {
                 __syncthreads();   // the previous pass's entries, weights and tables are done
-                if (pb % kBitsE == 0) {
+                if ((pb - pbeg) % kBitsE == 0) {
                     // the next kBitsE shared entries: exact coordinates (NaN past the list),
                     // tiles, weights
                     for (int t = tid; t < kBitsE; t += kBitsThreads) {
@@ -241,9 +250,9 @@ __global__ __launch_bounds__(kBitsThreads) void shared_bits_kernel(
                         if (!kCounts) swa[t] = ww;
                     }
                 }
-                const double2* const s64 = s64a + pb % kBitsE;
-                const int2* const stile = stilea + pb % kBitsE;
-                const double* const sw = swa + pb % kBitsE;
+                const double2* const s64 = s64a + (pb - pbeg) % kBitsE;
+                const int2* const stile = stilea + (pb - pbeg) % kBitsE;
+                const double* const sw = swa + (pb - pbeg) % kBitsE;
                 uint64_t W0[kBitsPT], W1[kBitsPT];
 #pragma unroll
                 for (int c = 0; c < kBitsPT; ++c) W0[c] = W1[c] = 0;
@@ -297,7 +306,7 @@ __global__ __launch_bounds__(kBitsThreads) void shared_bits_kernel(
                         eu[2 + (e & 1)] = f ? fv : 0.0f;
                         reinterpret_cast<float*>(&entq[q][e >> 1])[e & 1] =
                             f ? __builtin_fmaf(fu, fu, fv * fv) : __builtin_inff();
-                        if (in) slive[q] = 1;
+                        if (in) atomicOr(&slive[q], 1 << (e >> 5));   // live 32-entry words
                     }
                     __syncthreads();
                     if (tid == 0) {   // kBitsPL * 64-position blocks of the live pieces, flattened
@@ -339,6 +348,7 @@ __global__ __launch_bounds__(kBitsThreads) void shared_bits_kernel(
                         }
                         const float4* const eq = ent[q];
                         const f32x2* const eqq = entq[q];
+                        const int wlive = slive[q];   // words holding an entry in the disk's box
                         float bmin[kBitsPL];
                         // per position the four words (32 entries each) side by side: independent
                         // chains (bit e % 32 of word e / 32 = entry e covered); every entry read
@@ -354,6 +364,8 @@ __global__ __launch_bounds__(kBitsThreads) void shared_bits_kernel(
                         for (int j = 0; j < 16; ++j) {
 #pragma unroll
                             for (int wv = 0; wv < 4; ++wv) {
+                                if (!((wlive >> wv) & 1)) continue;   // uniform: no entry of the
+                                                                      // word can be covered (0 bits)
                                 const float4 uv = eq[16 * wv + j];
                                 const f32x2 qq = eqq[16 * wv + j];
                                 const f32x2 U2 = {uv.x, uv.y}, V2 = {uv.z, uv.w};
@@ -462,8 +474,11 @@ __global__ __launch_bounds__(kBitsThreads) void shared_bits_kernel(
             for (int c = 0; c < kBitsPT; ++c) {
                 const int k = kb + tid + c * kBitsThreads;
                 if (k >= kend) continue;
-                if constexpr (kCounts) reinterpret_cast<unsigned*>(spart)[(int64_t)i * K + k] = acc[c];
-                else spart[(int64_t)i * K + k] = acc[c];
+                if constexpr (kCounts) {
+                    if (acc[c]) atomicAdd(reinterpret_cast<unsigned*>(spart) + (int64_t)i * K + k, acc[c]);
+                } else {
+                    spart[(int64_t)i * K + k] = acc[c];
+                }
             }
         }
         // the next job

@@ -131,7 +131,8 @@ __device__ __forceinline__ void coverage_poll_body(
     const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
     int* __restrict__ jobctr, int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
     double* __restrict__ spart, int n_chain, const double* __restrict__ pen, double penalty,
-    double* __restrict__ vp, int n_shared, int counts, int bits_on, int* __restrict__ dc_out)
+    double* __restrict__ vp, int n_shared, int counts, int bits_on, int* __restrict__ dc_out,
+    const int* __restrict__ qual)
 {
     static_assert(kPollSlots == 2 * kPollPairs, "the hot loop pairs candidate slots");
 #ifdef MAC_DIAG
@@ -244,6 +245,10 @@ __device__ __forceinline__ void coverage_poll_body(
         }
     };
     load_lanes(0);
+    // the bit-word kernel (launched next) adds its per-split counts into spart row i
+    if (counts && qual && qual[i] && bits_on &&
+        dcount[kDcBits] + dcount[kDcOther] > (bits_on == 2 ? 0 : kBitsMinDisks))
+        for (int k = tid; k < K; k += kPollThreads) reinterpret_cast<unsigned*>(spart)[row + k] = 0u;
     if (R.x > R.y) {  // disk i covers nothing in any candidate (uniform across the block)
         if (counts)
             for (int k = tid; k < K; k += kPollThreads) reinterpret_cast<unsigned*>(partial)[row + k] = 0u;
@@ -494,13 +499,14 @@ __global__ __launch_bounds__(kPollThreads) __attribute__((amdgpu_waves_per_eu(3)
     const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
     int* __restrict__ jobctr, int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
     double* __restrict__ spart, int n_chain, const double* __restrict__ pen, double penalty,
-    double* __restrict__ vp, int n_shared, int counts, int bits_on, int* __restrict__ dc_out)
+    double* __restrict__ vp, int n_shared, int counts, int bits_on, int* __restrict__ dc_out,
+    const int* __restrict__ qual)
 {
     ts_begin(ts);
     coverage_poll_body(xy, w, off, g, urec, umap, ucount, region, nbrT, nboxT, lane4, lanexp, rows,
                        ncount, dlist, dcount, jobctr, N, K, mode, partial, spart, n_chain, pen,
                        penalty, vp,
-                       n_shared, counts, bits_on, dc_out);
+                       n_shared, counts, bits_on, dc_out, qual);
     ts_end(ts);
 }
 

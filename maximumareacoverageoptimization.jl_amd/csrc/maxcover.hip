@@ -760,7 +760,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                                L->ncount.as<int>(), L->dlist.as<int>(), L->mode.as<int>() + 1,
                                L->mode.as<int>() + 2, N, K,
                                d_mode, L->partial.as<double>(), L->spart.as<double>(), n_chain, d_pen,
-                               penalty, d_vp, n_shared, counts, bits_on, L->d_dc);
+                               penalty, d_vp, n_shared, counts, bits_on, L->d_dc, L->qual.as<int>());
             HCK(hipGetLastError());
             // the shared entries of crowded polls: bit-words per distinct position (k_bits.h);
             // returns at once when few disks have neighbours (the poll kernel took them)
