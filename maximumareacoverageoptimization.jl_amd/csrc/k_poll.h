@@ -138,10 +138,26 @@ __device__ __forceinline__ void coverage_poll_body(
 #ifdef MAC_DIAG
     const uint64_t diag_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    const int bx = blockIdx.x;
-    // the launch hint for the next poll's bit-word kernel (mapped host memory, maxcover.hip)
-    if (bx == 0 && threadIdx.x == 0 && dc_out && (!mode || *mode == kModePoll))
-        *(volatile int*)dc_out = dcount[kDcBits] + dcount[kDcOther];
+    const int bx = blockIdx.x, by = blockIdx.y;
+    // launch hints for the next poll (mapped host memory, maxcover.hip): the disks with
+    // neighbours (the bit-word kernel) and the most distinct positions of a disk (walk rows)
+    if (bx == 0 && by == 0 && dc_out && (!mode || *mode == kModePoll)) {
+        int um = 0;
+        for (int d = threadIdx.x; d < N; d += kPollThreads) um = max(um, ucount[d]);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) um = max(um, __shfl_xor(um, o, kWave));
+        __shared__ int sum_[kPollWaves];
+        if ((threadIdx.x & (kWave - 1)) == 0) sum_[threadIdx.x / kWave] = um;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int q = 1; q < kPollWaves; ++q) um = max(um, sum_[q]);
+            *(volatile int*)dc_out = dcount[kDcBits] + dcount[kDcOther];
+            *((volatile int*)dc_out + 2) = sum_[0] > um ? sum_[0] : um;
+        }
+    }
+    // grid rows past the first: further walk workgroups of the same disks (position slices
+    // by, by + gridDim.y, ...); every other role runs in row 0 only
+    if (by > 0 && bx >= N) return;
 
     // The shared-entry jobs (disk with neighbours x kShC-candidate slice, k_poll_shared.h) are
     // taken from a counter (the index kernel cleared it) by the shared workgroups and by every
@@ -244,13 +260,17 @@ __device__ __forceinline__ void coverage_poll_body(
             }
         }
     };
-    load_lanes(0);
+    const int kb0 = by * kPollKPB;   // this workgroup's first position slice
+    if (kb0 >= U && by > 0) break;     // uniform: no slice of this disk for this row
+    load_lanes(kb0);
     // the bit-word kernel (launched next) adds its per-split counts into spart row i
-    if (counts && qual && qual[i] && bits_on &&
+    if (by == 0 && counts && qual && qual[i] && bits_on &&
         dcount[kDcBits] + dcount[kDcOther] > (bits_on == 2 ? 0 : kBitsMinDisks))
         for (int k = tid; k < K; k += kPollThreads) reinterpret_cast<unsigned*>(spart)[row + k] = 0u;
     if (R.x > R.y) {  // disk i covers nothing in any candidate (uniform across the block)
-        if (counts)
+        if (by > 0)
+            ;   // row 0 writes the zeros
+        else if (counts)
             for (int k = tid; k < K; k += kPollThreads) reinterpret_cast<unsigned*>(partial)[row + k] = 0u;
         else
             for (int p = tid; p < U; p += kPollThreads) partial[row + p] = 0.0;
@@ -271,10 +291,10 @@ __device__ __forceinline__ void coverage_poll_body(
     const double oy = g.gy0 + 0.5 * (double)(R.z + R.w + 1) * g.S;
 
     // slices of kPollKPB positions (one for any MADS poll: a few hundred distinct disks)
-    for (int kb = 0; kb < U; kb += kPollKPB) {
+    for (int kb = kb0; kb < U; kb += (int)gridDim.y * kPollKPB) {
         const int ke = min(U, kb + kPollKPB);
         MAC_WALK_STAMP(0);
-        if (kb > 0) load_lanes(kb);
+        if (kb > kb0) load_lanes(kb);
         uint32_t live = 0;
         double acc[kPollSlots];
 #pragma unroll

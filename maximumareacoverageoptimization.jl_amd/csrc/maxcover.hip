@@ -143,6 +143,7 @@ struct Lane {
     PinnedBuf h_dc;                            // disks with neighbours of the last poll (mapped)
     int* d_dc = nullptr;                       // ... its device address
     int dc_hist[8] = {};                       // ... as read at the last 8 poll enqueues
+    int um_hist[8] = {};                       // most distinct positions of a disk, last 8 polls
 };
 
 struct mac_ctx {
@@ -727,6 +728,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             if (!L->h_dc.p) {
                 L->h_dc.reserve(64, hipHostMallocMapped | hipHostMallocCoherent);
                 *(volatile int*)L->h_dc.p = 1 << 30;   // first poll: launch
+                ((volatile int*)L->h_dc.p)[2] = 0;     // most positions: not reported yet
                 void* dp = nullptr;
                 HCK(hipHostGetDevicePointer(&dp, L->h_dc.p, 0));
                 L->d_dc = (int*)dp;
@@ -744,7 +746,14 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             const int bits_on = ctx->shared_mode == MAC_SHARED_BITS ? 2
                               : ctx->shared_mode == MAC_SHARED_FP64 ? 0
                               : dc_max > kBitsMinDisks ? 1 : 0;
-            const int gy = 1;   // walk workgroups loop over their disk's position slices
+            // walk rows: the lane's last 8 polls' most distinct positions of a disk (poll kernel
+            // hint), one row per kPollKPB-position slice up to 4 (further slices loop)
+            const int um_now = ((volatile int*)L->h_dc.p)[2];
+            for (int q = 7; q > 0; --q) L->um_hist[q] = L->um_hist[q - 1];
+            L->um_hist[0] = um_now;
+            int um_max = 0;
+            for (int q = 0; q < 8; ++q) um_max = std::max(um_max, L->um_hist[q]);
+            const int gy = std::max(1, std::min(4, (um_max + kPollKPB - 1) / kPollKPB));
             const int chains = (K + kChainC - 1) / kChainC;
             const int n_chain = d_obj ? chains : 0;
             L->spart.reserve(sizeof(double) * (size_t)N * K);
