@@ -83,6 +83,12 @@ for s in $STEPS; do
             run shard$P 300 python bench.py --no-cpu --shard-of $P ; rc=$?
             fatal $rc && break
         done ;;
+    prof5)    # kernel stats of the config-5 MPC loop and of the clustered config-4 poll
+        rm -rf gpurun_out/prof5 gpurun_out/profc
+        run prof5 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof5 -o run \
+            -- python3 bench.py --config 5 --steps 2 --warmup 1 --no-cpu ; rc=$?
+        fatal $rc || run profc 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profc -o run \
+            -- python3 bench.py --disks clustered --steps 10 --warmup 2 --no-cpu --no-extras ; rc=$? ;;
     bench2)
         run bench2 600 python bench.py --config 2 --no-cpu ; rc=$? ;;
     prof)
