@@ -211,10 +211,38 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
         double cx[P], cy[P], cr[P];
         // ---- keys: every load in flight at once, then the fp32 offsets (exactness voted)
         get3(0, bx, by, br);
+        const int n = 3 * N;
+        if (!src.cands && 3 * n <= 2 * kIndexSlots && src.b <= 16384) {
+            // the generator: candidates k and k + n are x + d and x - d of the same LTMADS entry
+            // d = L[rp[v]][cp[k mod n]] (k_prep.h CandSrc), so disk i's 3 x n entries are drawn
+            // once into the table's LDS (integers |d| <= b, as int16) and both signs built from
+            // them: the same doubles as src.get, half the stream draws, spread over all threads
+            int16_t* const dtab = reinterpret_cast<int16_t*>(table);
+            const int r3[3] = {src.rp[i], src.rp[N + i], src.rp[2 * N + i]};
+            for (int t = tid; t < 3 * n; t += kIdxThreads) {
+                const int a = t / n, kk = t - a * n;
+                dtab[t] = (int16_t)ltmads_entry(src.state, n, src.b, r3[a], src.cp[kk]);
+            }
+            __syncthreads();
+            const double xi = src.xinc[i], yi = src.xinc[N + i], ri = src.xinc[2 * N + i];
 #pragma unroll
-        for (int j = 0; j < P; ++j) {
-            const int k = j < kIdxPer ? tid + j * kIdxThreads : (tid == 0 ? kIndexMaxK : K);
-            get3(min(k, K - 1), cx[j], cy[j], cr[j]);
+            for (int j = 0; j < P; ++j) {
+                const int kl = min(j < kIdxPer ? tid + j * kIdxThreads : (tid == 0 ? kIndexMaxK : K), K - 1);
+                const int kg = kl + src.k0;
+                const bool plus = kg < n;
+                const int kk = plus ? kg : kg - n;
+                const double dx = (double)dtab[kk], dy = (double)dtab[n + kk], dr = (double)dtab[2 * n + kk];
+                cx[j] = plus ? xi + dx : xi - dx;
+                cy[j] = plus ? yi + dy : yi - dy;
+                cr[j] = plus ? ri + dr : ri - dr;
+            }
+            __syncthreads();   // the table is cleared next
+        } else {
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                const int k = j < kIdxPer ? tid + j * kIdxThreads : (tid == 0 ? kIndexMaxK : K);
+                get3(min(k, K - 1), cx[j], cy[j], cr[j]);
+            }
         }
         for (int q = tid; q < kIndexSlots; q += kIdxThreads) table[q] = -1;
         if (tid == 0) ucnt = 0;

@@ -8,12 +8,25 @@ import __graft_entry__ as ge  # noqa: E402
 pkg = ge.load_package()
 L = pkg.load_library()
 L.mac_diag_index_read.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int64]
-x, y, w, C, rmax = pkg.workloads.make_config(4)
-ctx = pkg.Context(0, algo="poll")
-ctx.set_points(x, y, w)
-for _ in range(3):
-    ctx.poll_best(C, rmax)
-N = C.shape[1] // 3
+if "--config" in sys.argv and sys.argv[sys.argv.index("--config") + 1] == "5":
+    # the last index launch of two config-5 MPC steps (LTMADS polls generated on the device)
+    wl = pkg.workloads
+    rng = wl.SplitMix64(wl.SEED)
+    cfg = wl.CONFIGS[5]
+    fire_kw, x0 = wl.config5_setup(rng, cfg["G"], cfg["N"], cfg["ignition"])
+    ctx = pkg.Context(0, algo="poll")
+    D = pkg.DynamicArea.DynamicArea(**fire_kw, seed=wl.SEED, device=0)
+    sim = pkg.FullSimulation.Simulation(ctx, x0, fire=D, N_iter=100, seed=wl.SEED)
+    for _ in range(2):
+        sim.step()
+    N = x0.size // 3
+else:
+    x, y, w, C, rmax = pkg.workloads.make_config(4)
+    ctx = pkg.Context(0, algo="poll")
+    ctx.set_points(x, y, w)
+    for _ in range(3):
+        ctx.poll_best(C, rmax)
+    N = C.shape[1] // 3
 buf = (ctypes.c_uint64 * (8 * N))()
 assert L.mac_diag_index_read(buf, 8 * N) == 0
 a = np.frombuffer(buf, dtype=np.uint64).reshape(N, 8).astype(np.int64)[:, :6]
