@@ -536,7 +536,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                          int K, bool tiled, const double* d_rmax, double penalty,
                          const double* d_prev, const double* d_dlimT, const double* d_dlim_raw,
                          double tan_half_fov, double* d_area, double* d_obj, double* d_best,
-                         int64_t idx_base, double* d_mirror = nullptr, uint64_t mirror_seq = 0)
+                         int64_t idx_base, double* d_mirror = nullptr, uint64_t mirror_seq = 0,
+                         uint64_t* d_hblk = nullptr)
 {
     if (use_fused(ctx, N, K)) {
         enqueue_fused(ctx, L, s, src, N, K, d_rmax, penalty, d_prev, d_dlim_raw, tan_half_fov,
@@ -813,9 +814,12 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         L->finblk.reserve(2 * sizeof(unsigned long long) * nfin);
         if (L->finarrive.grow(sizeof(unsigned)))   // zero once; the last block of each launch resets it
             HCK(hipMemsetAsync(L->finarrive.p, 0, L->finarrive.cap, s));
+        // the per-block minima go to the caller's mapped words (d_hblk: the MADS stepper) or the
+        // context's (a mirrored device poll), when the grid fits them
+        uint64_t* const hblk = nfin > (unsigned)kFinMaxBlk ? nullptr
+                             : d_hblk ? d_hblk : d_mirror ? ctx->d_blk : nullptr;
         fb = FinBest{d_best, d_mirror, mirror_seq, idx_base, L->finblk.as<unsigned long long>(),
-                     L->finarrive.as<unsigned>(),
-                     d_mirror && nfin <= (unsigned)kFinMaxBlk ? ctx->d_blk : nullptr};
+                     L->finarrive.as<unsigned>(), hblk};
     }
     uint64_t* tsf = ts_c >= 0 ? take_ts(nfin, ts_f, ts_nf) : nullptr;
     hipLaunchKernelGGL(finalize_kernel, dim3(nfin), dim3(kFinThreads), 0, s,
@@ -1579,18 +1583,73 @@ struct mac_mads {
     double* hb = nullptr;
     double* hx = nullptr;
     int* hperm = nullptr;
+    // finalize's per-block minima of each poll in mapped host memory (k_final.h FinBest.hblk):
+    // the poll's best is reduced here without a copy or a stream synchronisation
+    PinnedBuf hblk;
+    uint64_t* d_hblk = nullptr;
+    uint64_t seq = 0;
+    int nblk = 0;
     int64_t polled_b = 0;        // 2^ell of the poll awaiting its update (0: none)
     double h_enq = 0, h_perm = 0, h_wait = 0, h_post = 0;
     std::chrono::steady_clock::time_point t0;
 };
 
-static void mads_best_of(mac_mads* m, const CandSrc& src, int Kc, int64_t idx_base)
+// blk: the poll's best through finalize's per-block minima (mads_wait_best), else a 16-B copy
+static void mads_best_of(mac_mads* m, const CandSrc& src, int Kc, int64_t idx_base, bool blk = false)
 {
+    const int nfin = 8 * ((Kc + 8 * kFinC - 1) / (8 * kFinC));   // finalize's grid (enqueue_eval)
+    blk = blk && nfin <= kFinMaxBlk && !use_fused(m->ctx, m->N, Kc);   // fused: no finalize blocks
+    if (blk && !m->d_hblk) {
+        m->hblk.reserve(sizeof(uint64_t) * 4 * kFinMaxBlk, hipHostMallocMapped | hipHostMallocCoherent);
+        std::memset(m->hblk.p, 0, sizeof(uint64_t) * 4 * kFinMaxBlk);
+        void* dp = nullptr;
+        HCK(hipHostGetDevicePointer(&dp, m->hblk.p, 0));
+        m->d_hblk = (uint64_t*)dp;
+    }
+    m->nblk = blk ? nfin : 0;
     enqueue_eval(m->ctx, m->L, m->s, src, m->N, Kc, use_tiled(m->ctx, m->N, nullptr, m->n),
                  m->L->rmax.as<double>(), m->penalty, m->d_prev, m->d_dlimT,
                  m->d_prev ? m->L->dlimraw.as<double>() : nullptr, m->tan_half_fov,
-                 m->L->area.as<double>(), m->L->obj.as<double>(), m->L->best.as<double>(), idx_base);
-    HCK(hipMemcpyAsync(m->hb, m->L->best.p, 16, hipMemcpyDeviceToHost, m->s));
+                 m->L->area.as<double>(), m->L->obj.as<double>(), m->L->best.as<double>(), idx_base,
+                 nullptr, blk ? ++m->seq : 0, blk ? m->d_hblk : nullptr);
+    if (!blk) HCK(hipMemcpyAsync(m->hb, m->L->best.p, 16, hipMemcpyDeviceToHost, m->s));
+}
+
+// The best {objective, global index} of the poll mads_best_of enqueued: the per-block minima once
+// every block's sequence has landed (lexicographic, as finalize's last block), or, after 50 ms
+// (a failed launch) or without them, the stream synchronised and the copy / device record.
+static void mads_wait_best(mac_mads* m, int64_t idx_base, double* obj, int64_t* idx)
+{
+    if (m->nblk > 0) {
+        const uint64_t* hk = (const uint64_t*)m->hblk.p;
+        const auto t0 = std::chrono::steady_clock::now();
+        int b = 0;
+        for (int spin = 0; b < m->nblk; ++spin) {
+            while (b < m->nblk && __atomic_load_n(hk + 4 * b + 2, __ATOMIC_ACQUIRE) == m->seq) ++b;
+            if (b < m->nblk && (spin & 1023) == 1023 &&
+                std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50))
+                break;
+        }
+        if (b == m->nblk) {
+            double bv = INFINITY;
+            int64_t bi = -1;
+            for (int q = 0; q < m->nblk; ++q) {
+                const double v = __builtin_bit_cast(double, hk[4 * q]);
+                const int64_t i = (int64_t)hk[4 * q + 1];
+                if (i >= 0 && (bi < 0 || v < bv || (v == bv && i < bi))) {
+                    bv = v;
+                    bi = i;
+                }
+            }
+            *obj = bi >= 0 ? bv : INFINITY;
+            *idx = bi >= 0 ? idx_base + bi : -1;
+            return;
+        }
+        HCK(hipMemcpyAsync(m->hb, m->L->best.p, 16, hipMemcpyDeviceToHost, m->s));
+    }
+    HCK(hipStreamSynchronize(m->s));
+    *obj = m->hb[0];
+    *idx = __builtin_bit_cast(int64_t, m->hb[1]);
 }
 
 static void mads_free(mac_mads* m)
@@ -1708,19 +1767,22 @@ int32_t mac_mads_poll(mac_mads* m, int32_t* done, double* best_obj, int64_t* bes
     const int Kc = (int)(m->hi - m->lo);
     if (Kc > 0) {
         // (the staging is free: the previous iteration's copies completed at its sync)
+        // one copy of the contiguous staging [incumbent 8n][permutations 4*2n] (n = 3N); the
+        // staging is free: the previous poll's copy preceded its finalize, whose results were read
         std::copy(m->rp.begin(), m->rp.end(), m->hperm);
         std::copy(m->cp.begin(), m->cp.end(), m->hperm + n);
         std::copy(m->x.begin(), m->x.end(), m->hx);
-        HCK(hipMemcpyAsync(m->L->perm.p, m->hperm, sizeof(int) * 2 * n, hipMemcpyHostToDevice, m->s));
-        HCK(hipMemcpyAsync(m->L->xinc.p, m->hx, sizeof(double) * n, hipMemcpyHostToDevice, m->s));
+        m->L->xinc.reserve(sizeof(double) * n + sizeof(int) * 2 * n);
+        HCK(hipMemcpyAsync(m->L->xinc.p, m->hx, sizeof(double) * n + sizeof(int) * 2 * n,
+                           hipMemcpyHostToDevice, m->s));
         CandSrc src{};
         src.xinc = m->L->xinc.as<double>();
-        src.rp = m->L->perm.as<int>();
-        src.cp = m->L->perm.as<int>() + n;
+        src.rp = reinterpret_cast<int*>(m->L->xinc.as<double>() + n);
+        src.cp = src.rp + n;
         src.state = m->state;
         src.b = b;
         src.k0 = (int)m->lo;
-        mads_best_of(m, src, Kc, m->lo);
+        mads_best_of(m, src, Kc, m->lo, true);
     }
     const auto tb = clk::now();
     if (m->it < m->prm.n_iter) {
@@ -1730,9 +1792,7 @@ int32_t mac_mads_poll(mac_mads* m, int32_t* done, double* best_obj, int64_t* bes
     }
     const auto tc = clk::now();
     if (Kc > 0) {
-        HCK(hipStreamSynchronize(m->s));
-        *best_obj = m->hb[0];
-        *best_idx = __builtin_bit_cast(int64_t, m->hb[1]);
+        mads_wait_best(m, m->lo, best_obj, best_idx);
     } else {
         *best_obj = INFINITY;
         *best_idx = -1;
@@ -1998,7 +2058,7 @@ static int32_t poll_best_dev(mac_ctx* ctx, const T* d_cands_in, int64_t three_n,
         ctx->mirror_for = d_best;
         // finalize's grid (enqueue_eval): its blocks mirror their minima when it fits h_blk
         const int nfin = 8 * (int)((K + 8 * kFinC - 1) / (8 * kFinC));
-        ctx->mirror_nblk = nfin <= kFinMaxBlk ? nfin : 0;
+        ctx->mirror_nblk = nfin <= kFinMaxBlk && !use_fused(ctx, N, K) ? nfin : 0;
         ctx->mirror_base = idx_base;
     }
     enqueue_eval(ctx, L, s, matrix_src(d_cands, N), N, (int)K, use_tiled(ctx, N, nullptr, three_n), d_rmax,
