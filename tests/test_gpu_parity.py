@@ -634,6 +634,45 @@ def test_native_mads_matches_python_driver(ctx, pkg, with_cons3):
     assert (st["status"] == 0) == (res.status.optimization_status == "MeshPrecisionLimit")
 
 
+@pytest.mark.parametrize("algo", ["auto", "poll"])
+def test_native_mads_matches_oracle_loop(ctx, pkg, orc, algo):
+    """mac_mads_run against the reference's own per-trial-point loop on the C oracle: the Python
+    driver TDM_STATIC_opt.mads with an objective that is a plain callable (no batch, no poll),
+    so every feasible candidate goes through orc.ref_objective (src/TDM_STATIC_opt.jl:82-100)
+    one at a time, cons1 and cons3 checked per candidate (src/TDM_Constraints.jl). N = 12 UAVs:
+    K = 72 candidates per poll, past the poll walk's threshold, disks overlapping (shared
+    entries). Same iterate, objective and iteration count; libmaxcover is not on the reference
+    side at all."""
+    wl = pkg.workloads
+    TS = pkg.TDM_STATIC_opt
+    TC = pkg.TDM_Constraints
+    x, y, w = wl.grid_points(160)
+    rec = np.stack([x, y, w, w, np.zeros_like(x)], axis=1)
+    rng = wl.SplitMix64(2024)
+    N = 12
+    x0 = np.concatenate([np.round(320 + rng.uniform(N) * 160), np.round(320 + rng.uniform(N) * 160),
+                         np.full(N, 36.0)])
+    r_max = np.full(N, 30.0 * TAN50)
+    c3 = TC.create_cons3(x0, 100 / 180 * math.pi, np.full(N, 10.0))
+
+    def oracle_objective(v):
+        return orc.ref_objective(v, rec, r_max, 1e5)
+
+    res = TS.mads(x0, oracle_objective, [TC.cons1, c3], N_iter=30, ell0=2, ell_max=5, seed=99)
+    ctx.set_points_records(rec)
+    ctx.set_algo(algo)
+    try:
+        xn, st = ctx.mads_run(x0, r_max, 1e5, prev=c3.prev, d_lim=c3.d_lim,
+                              tan_half_fov=c3.tan_half_fov, n_iter=30, ell0=2, ell_max=5, seed=99)
+    finally:
+        ctx.set_algo("auto")
+    want_x = res.x if res.x is not None else res.i
+    assert res.x_cost < oracle_objective(x0)   # the loop moved (~1,100 feasible evaluations)
+    assert np.array_equal(xn, want_x)
+    assert st["f"] == res.x_cost
+    assert st["iterations"] == res.status.iteration
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_native_mads_sharded_steppers(ctx, pkg, world):
     """The multi-GPU MADS loop's native side in one process: `world` steppers (mac_mads_begin with
