@@ -190,7 +190,7 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
     cfg = wl.CONFIGS[5]
     rng = wl.SplitMix64(args.seed)
     fire_kw, x0 = wl.config5_setup(rng, cfg["G"], cfg["N"], cfg["ignition"])
-    ctx = pkg.Context(dev_index)
+    ctx = pkg.Context(dev_index, algo=args.algo)
     t_set = time.perf_counter()
     D = pkg.DynamicArea.DynamicArea(**fire_kw, seed=args.seed, device=dev_index)
     shard = (rank, world) if world > 1 else None

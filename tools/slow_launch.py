@@ -11,11 +11,13 @@ d = [rows[i]["e"] - rows[i]["s"] for i in ws]
 med = statistics.median(d)
 print("walk_setup launches", len(ws), "median us", med / 1e3, "max us", max(d) / 1e3)
 keys = [k for k in rows[0] if k not in ("Kernel_Name", "s", "e")]
-for i, dur in zip(ws, d):
+t0 = rows[0]["s"]
+for n, (i, dur) in enumerate(zip(ws, d)):
     if dur < 20 * med:
         continue
     r = rows[i]
-    print("SLOW", dur / 1e3, "us", {k: r[k] for k in keys if "Size" in k or "Count" in k or "Queue" in k or "Stream" in k})
+    print("SLOW", dur / 1e3, "us", "poll #", n, "of", len(ws), "at ms", (r["s"] - t0) / 1e6,
+          "after the first kernel", {k: r[k] for k in keys if "Size" in k or "Count" in k or "Queue" in k or "Stream" in k})
     for j in range(max(0, i - 4), min(len(rows), i + 4)):
         q = rows[j]
         gap = (q["s"] - rows[j - 1]["e"]) / 1e3 if j else 0
