@@ -79,7 +79,7 @@ __device__ __forceinline__ void neighbors_block(int i, int N, const int4* __rest
 // x the per-candidate walk's (cost[i].y summed) — its visits are broadcast LDS reads, the other's
 // scattered global loads — or `forced`. The costs are integer-valued doubles, so the sums are
 // exact and every block that computes the choice gets the same one. Block-uniform result.
-__device__ __forceinline__ int walk_choice(int N, const double2* __restrict__ cost, double ratio,
+__device__ __forceinline__ int walk_choice(int N, int K, const double2* __restrict__ cost, double ratio,
                                            int forced)
 {
     __shared__ double red[kWavesPerBlock];
@@ -92,7 +92,10 @@ __device__ __forceinline__ int walk_choice(int N, const double2* __restrict__ co
     }
     const double A = block_sum_f64(a, red);
     __syncthreads();
-    const double B = block_sum_f64(b, red);
+    // + the per-candidate walk's neighbour-list build (k_walk.h): every (candidate, slice) unit
+    // tests all disk pairs, N(N-1)/2 box tests, which its visit count leaves out
+    // (a config-5 poll of clustered disks chose that walk on visits alone and took 3.96 ms)
+    const double B = block_sum_f64(b, red) + (double)K * N * (N - 1) / 2.0;
     if (threadIdx.x == 0) smode = A <= ratio * B ? kModePoll : kModeTiled;
     __syncthreads();
     return smode;

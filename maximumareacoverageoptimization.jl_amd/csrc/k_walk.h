@@ -252,7 +252,7 @@ __global__ __launch_bounds__(kBlock) void walk_setup_kernel(
     int* __restrict__ qual)
 {
     ts_begin(ts);
-    const int m = walk_choice(N, cost, ratio, forced);
+    const int m = walk_choice(N, K, cost, ratio, forced);
     if (blockIdx.x == 0 && threadIdx.x == 0) mode[0] = m;
     if (m == kModePoll) {
         if ((int)blockIdx.x < N)
