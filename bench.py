@@ -293,7 +293,7 @@ def main():
                     help="4 (default): one MADS poll per step; 5: one end-to-end MPC step "
                          "(CA fire stream + rmvCoveredPOI + a MADS run) per step")
     ap.add_argument("--mads-iters", type=int, default=100, help="config 5: N_iter per MPC step")
-    ap.add_argument("--algo", default="auto", choices=("auto", "tiled", "scan", "poll", "fused"))
+    ap.add_argument("--algo", default="auto", choices=("auto", "tiled", "scan", "poll"))
     ap.add_argument("--polls", type=int, default=4, help="distinct poll sets cycled over steps")
     ap.add_argument("--tile-points", type=int, default=None,
                     help="points per spatial tile of the index (library default when omitted)")
@@ -469,8 +469,7 @@ def main():
     value = total_evals / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
-    # roofline. The unit is one poll's device chain (the fused poll: launch 1 +
-    # launch 2; the legacy chain: its coverage kernel), timed live by in-kernel workgroup stamps
+    # roofline. The unit is one poll's device chain, timed live by in-kernel workgroup stamps
     # over the timed steps. Its algorithmic floor is what any exact culling evaluation must move:
     # the candidate matrix read once, every entry that lies in some disk's poll-wide footprint
     # box read once (xy, 16 B; w only when the weights differ), and the 16-B result.
@@ -547,9 +546,7 @@ def main():
                 "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "traffic": traffic,
-                "kernel": ("fused poll chain: fused_prep_kernel + fused_walk_kernel"
-                           if k_walk == "fused" else
-                           f"poll chain (cands_keys, disk_index, walk_setup, coverage_{k_walk}, "
+                "kernel": (f"poll chain (column_pass, disk_index, walk_setup, coverage_{k_walk}, "
                            f"finalize + argmin); dominant kernel coverage_{k_walk}_kernel"),
                 "chain_ms": chain_ms,
                 "avg_launch_ms": avg_launch_ms,

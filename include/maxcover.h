@@ -71,10 +71,7 @@ extern "C" {
 #define MAC_ALGO_TILED  2  /* per-candidate walk over the tile-binned point list (exact culling) */
 #define MAC_ALGO_POLL   3  /* per-disk walk over the whole poll: region entries staged in LDS,
                               one candidate per lane (the six-launch chain; weighted lists) */
-#define MAC_ALGO_FUSED  4  /* the two-launch poll for lists whose entries all weigh the same (every
-                              reference input): disk index + walk + ownership + objective + argmin
-                              (k_fused.h). Opt-in (slower than the chain AUTO picks, DESIGN.md
-                              section 4); weighted lists fall back to the AUTO choice */
+/* (4 was an opt-in two-launch poll, measured slower than the chain and removed: refused) */
 
 #define MAC_STORE_F64   0
 #define MAC_STORE_F32   1
@@ -201,6 +198,12 @@ int32_t mac_mads_poll(mac_mads* m, int32_t* done, double* best_obj, int64_t* bes
 int32_t mac_mads_update(mac_mads* m, double best_obj, int64_t best_idx);
 int32_t mac_mads_result(mac_mads* m, double* x_out, mac_mads_stats* stats);
 void mac_mads_destroy(mac_mads* m);
+/* Every later poll of the stepper also writes its 16-byte shard best {objective, index as
+ * int64 bits} to d_best16 (device memory of the context's device, 8-byte aligned; NULL: stop):
+ * once mac_mads_poll has returned, the buffer holds that poll's best for device work on any
+ * stream (mac_best_fetch's ordering), so a multi-GPU loop all-gathers straight from it with no
+ * host-to-device copy per iteration (dist.DeviceGather). */
+int32_t mac_mads_best_buffer(mac_mads* m, void* d_best16);
 
 /* fp32 candidates (config 3's "fp32" caller path; SURVEY 8(b) "*_f32: coords f32, accum f64"):
  * the candidate matrix (and prev) are uploaded as floats and widened exactly on the device;
@@ -231,8 +234,15 @@ int32_t mac_poll_best_dev_f32(mac_ctx* ctx, const float* d_cands, int64_t three_
                               const double* d_rmax, double penalty,
                               const float* d_prev, const double* d_dlim, double tan_half_fov,
                               int64_t idx_base, double* d_obj, void* d_best, void* stream);
-/* Waits for `stream` (NULL = the context's own stream) and returns the 16 bytes a device poll
- * wrote to d_best, through a pinned staging buffer: the host side of one MADS poll step. */
+/* The host side of one MADS poll step: returns the {objective, index} the latest
+ * mac_poll_best_dev_* on d_best wrote. Each d_best buffer gets a mapped host slot that the
+ * poll's last finalize block fills (after its d_best stores have reached the device's L2), so
+ * the call returns as soon as the result exists, without a copy: at that point d_best holds the
+ * result for device work, but the poll's launch may still be retiring on `stream` — order later
+ * work that reads d_best or reuses the poll's inputs on `stream`, or synchronise it first.
+ * Without a slot (a K = 0 poll, or the slot taken by 64 newer d_best buffers) or after 2 ms,
+ * it waits for `stream` (NULL = the context's own stream) and copies d_best. Polls on different
+ * d_best buffers may be issued and fetched concurrently from several host threads. */
 int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* best_obj,
                        int64_t* best_idx);
 
@@ -242,14 +252,14 @@ int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* b
  * packet or dependency is added to the stream. Reads (after a device sync) the summed coverage-
  * kernel time in ms (last end - first start per launch), the launch count and the candidates
  * evaluated by those launches, and the walk the LAST of them used (MAC_ALGO_SCAN / _TILED /
- * _POLL / _FUSED, 0 = none); reset != 0 clears the record. */
+ * _POLL, 0 = none); reset != 0 clears the record. */
 int32_t mac_profile_read(mac_ctx* ctx, double* kernel_ms, int64_t* launches,
                          int64_t* candidates, int32_t* last_algo, int32_t reset);
 
 /* Split of the poll chains recorded since the last reset (call before mac_profile_read with
  * reset), summed: launch chain: prep = first launch's first start .. the walk's first start,
- * walk = the walk launch, gap = the walk's last end .. finalize's (+ argmin) last end; fused
- * polls: launch 1, launch 2, the idle gap between them. polls = chains counted. */
+ * walk = the walk launch, gap = the walk's last end .. finalize's (+ argmin) last end.
+ * polls = chains counted. */
 int32_t mac_profile_split(mac_ctx* ctx, double* prep_ms, double* walk_ms, double* gap_ms,
                           int64_t* polls);
 

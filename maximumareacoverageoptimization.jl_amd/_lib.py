@@ -34,12 +34,11 @@ MAC_ALGO_AUTO = 0
 MAC_ALGO_SCAN = 1
 MAC_ALGO_TILED = 2
 MAC_ALGO_POLL = 3
-MAC_ALGO_FUSED = 4
 MAC_STORE_F64 = 0
 MAC_STORE_F32 = 1
 
 ALGOS = {"auto": MAC_ALGO_AUTO, "scan": MAC_ALGO_SCAN, "tiled": MAC_ALGO_TILED,
-         "poll": MAC_ALGO_POLL, "fused": MAC_ALGO_FUSED}
+         "poll": MAC_ALGO_POLL}
 
 # Every symbol include/maxcover.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -57,6 +56,7 @@ EXPORTS = (
     "mac_set_points_f32", "mac_set_points_dev_f32", "mac_area_f32", "mac_area_batch_f32",
     "mac_poll_best_f32", "mac_poll_best_dev_f32",
     "mac_mads_begin", "mac_mads_poll", "mac_mads_update", "mac_mads_result", "mac_mads_destroy",
+    "mac_mads_best_buffer",
 )
 
 
@@ -155,6 +155,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mac_mads_update": ([_vp, ctypes.c_double, _i64], _i32),
         "mac_mads_result": ([_vp, _dp, ctypes.POINTER(MadsStats)], _i32),
         "mac_mads_destroy": ([_vp], None),
+        "mac_mads_best_buffer": ([_vp, _vp], _i32),
         "mac_set_points_f32": ([_vp, _fp, _fp, _fp, _i64], _i32),
         "mac_set_points_dev_f32": ([_vp, _vp, _vp, _vp, _i64], _i32),
         "mac_area_f32": ([_vp, _fp, _i64, _dp], _i32),
@@ -294,12 +295,11 @@ class Context:
         a = _i32()
         _check(self._L.mac_profile_read(self._h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(k),
                                         ctypes.byref(a), 1 if reset else 0))
-        name = {MAC_ALGO_SCAN: "scan", MAC_ALGO_TILED: "tiled", MAC_ALGO_POLL: "poll",
-                MAC_ALGO_FUSED: "fused"}.get(a.value)
+        name = {MAC_ALGO_SCAN: "scan", MAC_ALGO_TILED: "tiled", MAC_ALGO_POLL: "poll"}.get(a.value)
         return ms.value, int(n.value), int(k.value), name
 
     def profile_split(self):
-        """Fused polls since the last reset: (launch-1 ms, launch-2 ms, gap ms, polls), summed.
+        """Poll chains since the last reset: (prep ms, walk ms, after-walk ms, polls), summed.
         Call before profile_read(reset=True)."""
         p1, p2, gap = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
         n = _i64()
@@ -541,9 +541,9 @@ class Context:
         return step
 
     def best_fetch(self, d_best, stream=None):
-        """Wait for ``stream`` and return the (objective, index) a device poll wrote to d_best."""
-        self._bo = getattr(self, "_bo", None) or (ctypes.c_double(), ctypes.c_int64())
-        bo, bi = self._bo
+        """The (objective, index) the latest device poll on d_best wrote (mac_best_fetch).
+        Thread-safe: the output words are per call."""
+        bo, bi = ctypes.c_double(), ctypes.c_int64()
         _check(self._L.mac_best_fetch(self._h, _devptr(d_best), _devptr(stream),
                                       ctypes.byref(bo), ctypes.byref(bi)))
         return bo.value, bi.value
@@ -581,6 +581,13 @@ class MadsStepper:
 
     def update(self, best_obj: float, best_idx: int) -> None:
         _check(self._L.mac_mads_update(self._h, float(best_obj), int(best_idx)))
+
+    def best_buffer(self, d_best16) -> None:
+        """Later polls also write their 16-B shard best into ``d_best16`` (a device tensor of
+        2 float64, or None to stop): mac_mads_best_buffer."""
+        self._best_buf = d_best16   # kept alive while the stepper writes it
+        _check(self._L.mac_mads_best_buffer(self._h, _devptr(d_best16) if d_best16 is not None
+                                            else None))
 
     def result(self):
         out = np.empty(self.n)

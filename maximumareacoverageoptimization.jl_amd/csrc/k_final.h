@@ -1,4 +1,5 @@
-// k_final.h — objective penalty + cons3 mask, partial-sum reduction and the poll argmin.
+// k_final.h — partial-sum reduction, objective (the column pass's penalty, k_prep.h) and the
+// poll argmin.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -14,68 +15,6 @@ namespace mac {
 constexpr int kFinC = 16;   // candidates per finalize block (x 64 slice groups)
 constexpr int kFinMaxBlk = 256;   // finalize blocks whose minima the last block loads at once
 constexpr int kFinThreads = 1024;
-
-// Sequential objective penalty (src/TDM_STATIC_opt.jl:88-92): violation_k = sum over i = 0..N-1
-// of pen[i*K + k] (the index's per-candidate term, k_index.h), accumulated IN ORDER from 0.0
-// (bit-exact with the reference's loop); vp_k = violation_k * penalty, or +inf when a term is
-// negative (cons3 fails, src/TDM_Constraints.jl:54-75: the extreme barrier never evaluates the
-// objective).
-//
-// One workgroup = kChainC candidates x kChainG disk groups. Thread (c, grp) loads its group's
-// kChainSeg consecutive disks of candidate k0 + c in one go (rows of 16 consecutive candidates:
-// one cache line per row; every load in flight at once), then the running sum is relayed through
-// LDS: group 0 adds its terms, then group 1, ... (one barrier per group), so the additions stay
-// in order while the loads cost one latency per kChainG * kChainSeg disks instead of one per
-// disk. Used by the poll kernel's chain workgroups (overlapping the walk) and by
-// penalty_chain_kernel on the other paths. Needs kChainG * kChainC == kBlock threads.
-constexpr int kChainC = 16;
-constexpr int kChainG = kBlock / kChainC;
-constexpr int kChainSeg = 32;
-__device__ __forceinline__ void penalty_chain_block(const double* __restrict__ pen, int K, int N,
-                                                    int k0, double penalty,
-                                                    double* __restrict__ vp)
-{
-    __shared__ double carry[kChainC];
-    __shared__ int bad[kChainC];
-    const int t = threadIdx.x, c = t % kChainC, grp = t / kChainC;
-    const int k = k0 + c;
-    if (t < kChainC) {
-        carry[t] = 0.0;
-        bad[t] = 0;
-    }
-    for (int base = 0; base < N; base += kChainG * kChainSeg) {
-        const int i0 = base + grp * kChainSeg;
-        double v[kChainSeg];
-#pragma unroll
-        for (int j = 0; j < kChainSeg; ++j) {
-            const int ii = i0 + j;
-            v[j] = (k < K && ii < N) ? pen[(int64_t)ii * K + k] : 0.0;   // pad: + 0.0, exact
-        }
-        __syncthreads();
-        for (int sgrp = 0; sgrp < kChainG; ++sgrp) {
-            if (grp == sgrp) {
-                double acc = carry[c];
-                bool neg = false;
-#pragma unroll
-                for (int j = 0; j < kChainSeg; ++j) {
-                    neg |= v[j] < 0.0;
-                    acc += v[j];
-                }
-                carry[c] = acc;
-                if (neg) bad[c] = 1;
-            }
-            __syncthreads();
-        }
-    }
-    if (t < kChainC && k < K) vp[k] = bad[t] ? __builtin_inf() : carry[t] * penalty;
-}
-
-__global__ __launch_bounds__(kBlock) void penalty_chain_kernel(const double* __restrict__ pen,
-                                                               int K, int N, double penalty,
-                                                               double* __restrict__ vp)
-{
-    penalty_chain_block(pen, K, N, blockIdx.x * kChainC, penalty, vp);
-}
 
 // Block = 16 candidates x 64 slice groups. area_k = sum over slices g of the slice's credit in a
 // fixed order (thread (c, sg) sums g = sg, sg+64, ... in batches of 8, then the 64 groups in
@@ -93,15 +32,24 @@ __global__ __launch_bounds__(kBlock) void penalty_chain_kernel(const double* __r
 // reduces the published minima (finalize_argmin below).
 struct FinBest {
     double* best;          // {objective, index bits} (null: no argmin)
-    double* mirror;        // mapped pinned host words {obj, idx, seq} (may be null)
+    uint64_t* mirror;      // mapped host slot {obj bits, index, seq, check} (may be null)
     uint64_t seq;
     int64_t idx_base;
     unsigned long long* blk;   // [gridDim.x][2] per-block minima {obj bits, index}
     unsigned* arrive;          // arrival counter, zero between launches (the last block resets it)
-    uint64_t* hblk;            // mapped host words, [block][4] = {obj bits, local index, seq, -}:
-                               // the host reduces them without waiting for the last block (may
-                               // be null)
 };
+
+// Check word of a mirrored result (host: mirror_check in maxcover.hip): the host accepts the slot
+// only when seq is the one it waits for AND the check word matches the three words it read, so a
+// slot read while its stores are still landing (no fence orders them: a system-scope release
+// would write back the XCD's L2) is read again, never accepted torn.
+__host__ __device__ __forceinline__ uint64_t mirror_check(uint64_t o, uint64_t i, uint64_t q)
+{
+    uint64_t z = o ^ (i * 0x9E3779B97F4A7C15ull) ^ (q * 0xC2B2AE3D27D4EB4Full) ^ 0x5851F42D4C957F2Dull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
 
 __device__ __forceinline__ void argmin_take(double& v1, int& i1, double v2, int i2)
 {
@@ -116,7 +64,7 @@ __device__ __forceinline__ void argmin_take(double& v1, int& i1, double v2, int 
 // row of the sc1 table): lane 0 alone stores its block's minimum with 8-B agent-scope (sc1) stores,
 // waits for them (vmcnt(0)), then adds to ONE counter; the block whose add returns the last count
 // loads every minimum with sc1 loads, in the same wave. The lexicographic (objective, index)
-// minimum is order-independent, so the result equals argmin_kernel's; NaN / +inf never selected.
+// minimum is order-independent (the sequential first-best order); NaN / +inf never selected.
 __device__ __forceinline__ void finalize_argmin(const FinBest& fb, double o, int k, bool have)
 {
     const int lane = threadIdx.x & (kWave - 1);
@@ -130,12 +78,6 @@ __device__ __forceinline__ void finalize_argmin(const FinBest& fb, double o, int
     for (int off = kFinC / 2; off >= 1; off >>= 1)
         argmin_take(bv, bi, __shfl_xor(bv, off, kWave), __shfl_xor(bi, off, kWave));
     unsigned old = 0;
-    if (lane == 0 && fb.hblk) {   // this block's minimum to the host, then (released) its sequence
-        uint64_t* const h = fb.hblk + 4 * blockIdx.x;
-        h[0] = __builtin_bit_cast(uint64_t, bv);
-        h[1] = (uint64_t)(int64_t)bi;
-        __hip_atomic_store(h + 2, fb.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
     if (lane == 0) {
         __hip_atomic_store(fb.blk + 2 * blockIdx.x, __builtin_bit_cast(unsigned long long, bv),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -173,15 +115,22 @@ __device__ __forceinline__ void finalize_argmin(const FinBest& fb, double o, int
     for (int off = 32; off >= 1; off >>= 1)
         argmin_take(bv, bi, __shfl_xor(bv, off, kWave), __shfl_xor(bi, off, kWave));
     if (lane == 0) {
-        fb.best[0] = bi >= 0 ? bv : __builtin_inf();
+        const double bo = bi >= 0 ? bv : __builtin_inf();
         const int64_t gidx = bi >= 0 ? fb.idx_base + bi : (int64_t)-1;
+        fb.best[0] = bo;
         fb.best[1] = __builtin_bit_cast(double, gidx);
         __hip_atomic_store(fb.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (fb.mirror) {  // pinned coherent host words: the result, then (released) its sequence
-            fb.mirror[0] = fb.best[0];
-            fb.mirror[1] = fb.best[1];
-            __hip_atomic_store(reinterpret_cast<uint64_t*>(fb.mirror + 2), fb.seq, __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
+        if (fb.mirror) {
+            // d_best's stores acknowledged by L2 first (a host that has read the mirror may hand
+            // d_best to device work on another stream), then the slot: plain stores to the
+            // mapped words, validated on the host by seq + check (no system-scope fence)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint64_t o = __builtin_bit_cast(uint64_t, bo);
+            const uint64_t ix = (uint64_t)gidx;
+            fb.mirror[0] = o;
+            fb.mirror[1] = ix;
+            fb.mirror[2] = fb.seq;
+            fb.mirror[3] = mirror_check(o, ix, fb.seq);
         }
     }
 }
@@ -285,71 +234,6 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
     }
     if (fb.best && t < kWave) finalize_argmin(fb, o, k, k < K);
     ts_end(ts);
-}
-
-// Single block: lexicographic minimum over (obj, index); NaN / +inf never selected.
-// best[0] = objective, best[1] = index (int64 bits), index = idx_base + k, -1 if none. With a
-// mirror (mapped pinned host memory), the two words are also written there followed by seq in
-// mirror[2], so the host reads the result without a copy (mac_best_fetch).
-// 16 waves; each thread keeps its first minimum over k = t, t + 1024, ... (4 loads in flight),
-// then wave butterflies and one pass over the 16 wave results.
-constexpr int kArgThreads = 1024;
-
-__global__ __launch_bounds__(kArgThreads) void argmin_kernel(const double* __restrict__ obj, int K,
-                                                             int64_t idx_base, double* __restrict__ best,
-                                                             double* __restrict__ mirror, uint64_t seq)
-{
-    __shared__ double sv[kArgThreads / kWave];
-    __shared__ int si[kArgThreads / kWave];
-    double bv = __builtin_inf();
-    int bi = -1;
-    constexpr int B = 4;
-    for (int k0 = threadIdx.x; k0 < K; k0 += B * kArgThreads) {
-        double v[B];
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-            const int k = k0 + b * kArgThreads;
-            v[b] = k < K ? obj[k] : __builtin_inf();
-        }
-#pragma unroll
-        for (int b = 0; b < B; ++b)
-            if (v[b] < bv) {  // ascending k per thread: first minimum kept
-                bv = v[b];
-                bi = k0 + b * kArgThreads;
-            }
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1)
-        argmin_take(bv, bi, __shfl_xor(bv, off, kWave), __shfl_xor(bi, off, kWave));
-    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-    if (lane == 0) {
-        sv[wid] = bv;
-        si[wid] = bi;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int q = 1; q < kArgThreads / kWave; ++q) argmin_take(sv[0], si[0], sv[q], si[q]);
-    }
-    if (threadIdx.x == 0) {
-        const int i = si[0];
-        best[0] = i >= 0 ? sv[0] : __builtin_inf();
-        const int64_t gidx = i >= 0 ? idx_base + i : (int64_t)-1;
-        best[1] = __builtin_bit_cast(double, gidx);
-        if (mirror) {  // pinned coherent host words: the result, then (released) its sequence number
-            mirror[0] = best[0];
-            mirror[1] = best[1];
-            __threadfence_system();
-            __hip_atomic_store(reinterpret_cast<uint64_t*>(mirror + 2), seq, __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
-}
-
-__global__ void dlim_threshold_kernel(const double* __restrict__ dlim, int N,
-                                      double* __restrict__ out)
-{
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < N) out[i] = dlim_threshold(dlim[i]);
 }
 
 }  // namespace mac

@@ -3,7 +3,6 @@
 // Everything the tiled / poll walks need about disk i of candidate k depends only on that disk's
 // own (cx, cy, r):
 //   * its record {cx, cy, T(r), r};
-//   * its objective-penalty term |r - r_max_i| and cons3 mark (pen_term);
 //   * its tile span;
 //   * in the poll walk, its credit over region i's non-shared entries (no other disk can cover
 //     those, k_poll.h "Ownership").
@@ -15,8 +14,7 @@
 // disk_index_kernel reads the K candidates' (x_i, y_i, r_i) once, straight from the candidate
 // source (the matrix's fp32 keys, or the LTMADS generator). It numbers the distinct disks in an
 // LDS hash table (exact keys, see "Keys" below) and writes per distinct disk u the record
-// urec[i*K + u], plus, for every candidate, the map umap[i*K + k] = u and the penalty term
-// pen[i*K + k], and the count ucount[i]. It also writes disk i's region (the union of its tile
+// urec[i*K + u], plus, for every candidate, the map umap[i*K + k] = u, and the count ucount[i]. It also writes disk i's region (the union of its tile
 // spans over the K candidates) and the two walk costs (K * |region|, sum of span areas).
 // Consumers read disk i of candidate k as urec[i*K + umap[i*K + k]]: the result is bit-identical
 // to per-candidate records (same inputs, same arithmetic), and every candidate is still
@@ -83,7 +81,6 @@ constexpr int kRowInfo = 32;   // region rows described per disk (larger regions
 
 struct IndexOut {
     DiskRec* urec;
-    double* pen;     // per candidate: pen[i*K + k] (null: no objective)
     int* umap;
     int* ucount;
     int4* region;
@@ -119,7 +116,7 @@ __device__ __forceinline__ float key_of(double v, double b, bool& ok)
 // (src.keysT, src.kbad; exact doubles from src.cands); else the generator (src.get), keyed here.
 template <bool kKeys, int kPer>
 __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPer <= 3 ? 8 : 4))) void disk_index_kernel(
-    uint64_t* ts, CandSrc src, int N, int K, Grid g, PenArgs pa, int dedup, IndexOut o)
+    uint64_t* ts, CandSrc src, int N, int K, Grid g, int dedup, IndexOut o)
 {
     constexpr int kIdxPer = kPer;
     constexpr int kIndexMaxK = IdxShape<kPer>::MaxK;
@@ -145,7 +142,6 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
     // candidates of this thread: k = tid + j * kIdxThreads (j < kIdxPer), and thread 0 also
     // takes k = kIndexMaxK (a full MADS poll is 2n + 1 = kIndexMaxK + 1 candidates at most here)
     const bool fits = dedup && K > 0 && K <= kIndexMaxK + 1;
-    const double T3 = o.pen ? pen_threshold(pa, i) : 0.0;   // cons3 threshold of UAV i
 
     int4 R = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
     double span_area = 0.0;
@@ -179,9 +175,9 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
     if (fits && kKeys) {
         // ---- keys: rows of the fp32 key matrix (coalesced) and the tiles' exactness flags
         get3(0, bx, by, br);
-        const float* fx = src.keysT + row;
-        const float* fy = fx + (int64_t)N * K;
-        const float* fr = fy + (int64_t)N * K;
+        const float* fx = src.keysT + (int64_t)i * src.ldk;
+        const float* fy = fx + (int64_t)N * src.ldk;
+        const float* fr = fy + (int64_t)N * src.ldk;
         float qx[P], qy[P], qr[P];
 #pragma unroll
         for (int j = 0; j < P; ++j) {
@@ -193,7 +189,7 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
         bool bad = false;
         for (int q = tid; q < 3 * src.nkt; q += kIdxThreads) {
             const int a = q / src.nkt;
-            bad |= src.kbad[(int64_t)(a * N + i) * src.nkt + (q - a * src.nkt)] != 0;
+            bad |= src.kbad[(int64_t)(q - a * src.nkt) * 3 * N + a * N + i] != 0;   // [block][3N]
         }
         for (int q = tid; q < kIndexSlots; q += kIdxThreads) table[q] = -1;
         if (tid == 0) ucnt = 0;
@@ -265,7 +261,6 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
             get3(k, x, y, r);
             add_span(x, y, r);
             o.urec[row + k] = make_disk(x, y, r);
-            if (o.pen) o.pen[row + k] = pen_term(x, y, r, i, N, pa, T3);
             o.umap[row + k] = k;
         }
         if (tid == 0) o.ucount[i] = K;
@@ -308,8 +303,8 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
         }
         __syncthreads();
         MAC_IDX_STAMP(3);
-        // ---- per candidate: the map, the penalty term and the span (exact doubles rebuilt from
-        // the keys: base + offset)
+        // ---- per candidate: the map and the span (exact doubles rebuilt from the keys:
+        // base + offset)
 #pragma unroll
         for (int j = 0; j < P; ++j) {
             const int k = j < kIdxPer ? tid + j * kIdxThreads : (tid == 0 ? kIndexMaxK : K);
@@ -317,7 +312,6 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
             const int u = table[slot[j]] & ((1 << kIdBits) - 1);
             const double x = bx + (double)kx[k], y = by + (double)ky[k], r = br + (double)kr[k];
             o.umap[row + k] = u;
-            if (o.pen) o.pen[row + k] = pen_term(x, y, r, i, N, pa, T3);
             add_span(x, y, r);
         }
         if (tid == 0) o.ucount[i] = ucnt;
@@ -402,11 +396,10 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
 
 // Small batches (K < 64 under AUTO: the per-candidate walk, which shares nothing between
 // candidates): the identity map built with one thread per (disk, candidate) instead of a
-// workgroup per disk, and no key pass. urec[i*K + k], umap[i*K + k] = k, pen[i*K + k].
+// workgroup per disk, and no key pass. urec[i*K + k], umap[i*K + k] = k.
 __global__ __launch_bounds__(256) void disk_index_identity_kernel(CandSrc src, int N, int K,
-                                                                  PenArgs pa, DiskRec* __restrict__ urec,
-                                                                  int* __restrict__ umap,
-                                                                  double* __restrict__ pen)
+                                                                  DiskRec* __restrict__ urec,
+                                                                  int* __restrict__ umap)
 {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (int64_t)N * K) return;
@@ -414,7 +407,6 @@ __global__ __launch_bounds__(256) void disk_index_identity_kernel(CandSrc src, i
     const double x = src.get(k, i, N), y = src.get(k, N + i, N), r = src.get(k, 2 * N + i, N);
     urec[t] = make_disk(x, y, r);
     umap[t] = k;
-    if (pen) pen[t] = pen_term(x, y, r, i, N, pa, pen_threshold(pa, i));
 }
 
 // disk i of candidate k through the index

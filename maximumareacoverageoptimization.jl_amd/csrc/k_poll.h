@@ -111,7 +111,7 @@ __device__ __forceinline__ void poll_hot(const float4* __restrict__ s32, int ng,
 #undef MAC_POLL_PAIR
 }
 
-// Grid (N + n_shared + n_chain); roles by x, in dispatch order: x < N, when
+// Grid (N + n_shared); roles by x, in dispatch order: x < N, when
 // *mode == kModePoll (or mode == null): one workgroup per disk i, over slices of kPollKPB
 // positions of disk i's distinct disks (urec / ucount, k_index.h): partial[i*K + p] = weight of
 // the non-shared entries credited to position p (finalize gathers it for every candidate through
@@ -119,8 +119,7 @@ __device__ __forceinline__ void poll_hot(const float4* __restrict__ s32, int ng,
 // staged entries: per entry group the LDS reads feed up to 4 candidate pairs, so the loop is
 // VALU-dense even when a disk has only a few hundred positions. Then n_shared workgroups
 // deciding the shared entries into spart, grid-striding over the jobs (disk with neighbours x
-// kShC-candidate slice, k_poll_shared.h); last, whatever the walk, the objective-penalty chains
-// of candidates [16c, 16c + 16), c = x - N - n_shared, into vp (k_final.h).
+// kShC-candidate slice, k_poll_shared.h).
 __device__ __forceinline__ void coverage_poll_body(
     const double2* __restrict__ xy, const double* __restrict__ w,
     const int32_t* __restrict__ off, Grid g, const DiskRec* __restrict__ urec,
@@ -130,8 +129,7 @@ __device__ __forceinline__ void coverage_poll_body(
     const float* __restrict__ lanexp, const int2* __restrict__ rows,
     const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
     int* __restrict__ jobctr, int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
-    double* __restrict__ spart, int n_chain, const double* __restrict__ pen, double penalty,
-    double* __restrict__ vp, int n_shared, int counts, int bits_on, int* __restrict__ dc_out,
+    double* __restrict__ spart, int n_shared, int counts, int bits_on, int* __restrict__ dc_out,
     const int* __restrict__ qual)
 {
     static_assert(kPollSlots == 2 * kPollPairs, "the hot loop pairs candidate slots");
@@ -193,13 +191,6 @@ __device__ __forceinline__ void coverage_poll_body(
             job = -1;
         }
     };
-    if (bx >= N + n_shared) {  // last: the objective-penalty chains (whatever the walk)
-        static_assert(kPollThreads == kBlock, "penalty_chain_block needs kBlock threads");
-        const int k0 = (bx - N - n_shared) * kChainC;
-        if (k0 < K) penalty_chain_block(pen, K, N, k0, penalty, vp);
-        MAC_DIAG_STAMP(diag_t0, 1, 0);
-        return;
-    }
     if (mode && *mode != kModePoll) return;
     if (bx >= N) {  // then: the shared entries
         shared_jobs(bx - N);
@@ -518,15 +509,13 @@ __global__ __launch_bounds__(kPollThreads) __attribute__((amdgpu_waves_per_eu(3)
     const float* __restrict__ lanexp, const int2* __restrict__ rows,
     const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
     int* __restrict__ jobctr, int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
-    double* __restrict__ spart, int n_chain, const double* __restrict__ pen, double penalty,
-    double* __restrict__ vp, int n_shared, int counts, int bits_on, int* __restrict__ dc_out,
+    double* __restrict__ spart, int n_shared, int counts, int bits_on, int* __restrict__ dc_out,
     const int* __restrict__ qual)
 {
     ts_begin(ts);
     coverage_poll_body(xy, w, off, g, urec, umap, ucount, region, nbrT, nboxT, lane4, lanexp, rows,
-                       ncount, dlist, dcount, jobctr, N, K, mode, partial, spart, n_chain, pen,
-                       penalty, vp,
-                       n_shared, counts, bits_on, dc_out, qual);
+                       ncount, dlist, dcount, jobctr, N, K, mode, partial, spart, n_shared, counts,
+                       bits_on, dc_out, qual);
     ts_end(ts);
 }
 

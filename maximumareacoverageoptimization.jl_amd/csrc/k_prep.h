@@ -86,8 +86,9 @@ struct CandSrc {
     const double* cands;   // matrix source when non-null
     int ldc;
     const float* keysT;    // matrix: fp32 keys, variable-major (cands_keys_kernel), when non-null
-    const int* kbad;       // matrix: per (variable, 32-candidate tile) "a key is inexact" flags
-    int nkt;               // tiles per variable
+    const int* kbad;       // matrix: per (column-pass block, variable) "a key is inexact" flags
+    int nkt;               // column-pass blocks (flags) per variable
+    int ldk;               // keysT row pitch (keys_ld(K))
     const double* xinc;    // generator: incumbent (3N), row / column permutations (n each)
     const int* rp;
     const int* cp;
@@ -106,75 +107,164 @@ struct CandSrc {
     }
 };
 
-// cands (3N x K column-major) -> keysT (3N x K variable-major: candidates contiguous) of fp32
-// keys, key = fl32(x - x0) with x0 = the variable's value in candidate 0, through 32 x 64 LDS
-// tiles so that both sides are coalesced. A key is exact when x0 + (double)key reproduces x bit
-// for bit (k_index.h "Keys"); kbad[v*nkt + tile] = 1 when some key of variable v in this tile is
-// not (every tile writes its flag, so nothing needs clearing). Half the bytes of a transposed
-// fp64 copy are written here and read by the index.
-constexpr int kKeysK = 128;  // candidates per cands_keys_kernel tile (x 32 variables)
+// ------------------------------------------------------------------ the column pass
+// The first launch of every evaluation: one 16-wave workgroup per kColC = 16 consecutive
+// candidates (columns of the 3N x K matrix as Julia hands it over, or of the LTMADS generator);
+// wave w owns candidate k0 + w. Per block of kColB UAVs, every lane issues all its loads at once
+// (x, y, r of UAVs l, l + 64, ...: contiguous 512-B segments of the column), while the workgroup
+// stages what every candidate shares in LDS: candidate 0's values (the key bases) and each
+// UAV's prev / r_max / cons3 threshold.
+//   objective (vp != null): term_i = |R_i - rmax_i|, or -1 when UAV i's move fails cons3
+//     (pen_term's arithmetic). The wave folds its candidate's terms IN ORDER i = 0, 1, ..., N-1
+//     from 0.0, as src/TDM_STATIC_opt.jl:88-92 does (bit-exact): term i sits in lane i % 64, so
+//     the fold reads it with v_readlane (no LDS round trip per term) into one sequential chain
+//     of fp64 adds, identical in every lane. vp[k] = violation * penalty, or +inf when a term is
+//     negative (the extreme barrier of src/TDM_Constraints.jl:54-75);
+//   keys (kKeys, matrix source, for the disk index): the fp32 key fl32(v - v0) of every value
+//     (v0 = candidate 0's value), transposed through LDS into keysT[v*ldk + k] (64-B row
+//     segments), and kbad[blockIdx.x * 3N + v] = 1 when some key of variable v in this block
+//     does not reproduce v bit for bit (k_index.h "Keys": the disk then takes the identity map).
+// The penalty chain thereby costs no buffer (one term per disk and candidate was 12.6 MB written
+// and re-read at config 4) and no workgroups of the later launches.
+constexpr int kColC = 16;                         // candidates (waves) per workgroup
+constexpr int kColThreads = kColC * kWave;
+constexpr int kColJ = 8;                          // UAVs per lane per block
+constexpr int kColB = kColJ * kWave;              // UAVs per block
 
-__global__ __launch_bounds__(kBlock) void cands_keys_kernel(uint64_t* ts, const double* __restrict__ cands,
-                                                            int n, int K, float* __restrict__ keysT,
-                                                            int* __restrict__ kbad, int nkt)
+__host__ __device__ inline int keys_ld(int K) { return (K + kColC - 1) / kColC * kColC; }
+
+__device__ __forceinline__ double readlane_f64(double v, int l)
+{
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+// kMat: the source is a matrix (src.cands; the generator path is compiled out), kKeys: write the
+// index's keys (matrix sources only).
+template <bool kMat, bool kKeys>
+__global__ __launch_bounds__(kColThreads) void column_pass_kernel(uint64_t* ts, CandSrc src, int N,
+                                                                  int K, PenArgs pa, double penalty,
+                                                                  double* __restrict__ vp,
+                                                                  float* __restrict__ keysT,
+                                                                  int* __restrict__ kbad)
 {
     ts_begin(ts);   // profiling only (the chain's first launch: k_common.h)
-    constexpr int NB = kKeysK / 32;   // 32-candidate flag tiles per workgroup tile
-    __shared__ float t[kKeysK][33];
-    __shared__ int sbad[NB][32];
-    const int v0 = blockIdx.x * 32, k0 = blockIdx.y * kKeysK;
-    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
-    if (threadIdx.x < 32 * NB) sbad[threadIdx.x >> 5][threadIdx.x & 31] = 0;
-    const int vr = v0 + tx;
-    const double base = vr < n ? cands[vr] : 0.0;
-    constexpr int J = kKeysK / 8;
-    double x[J];
+    __shared__ double sb[3][kColB];             // candidate 0's values (keys)
+    __shared__ double su[5][kColB];             // prev x, y, z / tan, r_max, cons3 threshold
+    __shared__ float kt[kColB][kColC + 1];      // one variable block's keys: [UAV][candidate]
+    __shared__ int kfl[3][kColB];
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+    const int k0 = blockIdx.x * kColC;
+    const int k = k0 + w;
+    const int kc = min(k, K - 1);
+    const int ldk = keys_ld(K);
+    const bool obj = vp != nullptr;
+    double acc = 0.0;
+    bool bad = false;
+    for (int ib = 0; ib < N; ib += kColB) {
+        const int nb = min(kColB, N - ib);
+        // this lane's values: UAV ib + lane + 64 j, variables x, y, r (all loads in flight)
+        double v[3][kColJ];
 #pragma unroll
-    for (int j = 0; j < J; ++j) {   // every load in flight at once
-        const int k = k0 + ty + 8 * j;
-        x[j] = (k < K && vr < n) ? cands[(int64_t)k * n + vr] : base;
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int j = 0; j < kColJ; ++j) {
+                const int i = ib + min(lane + kWave * j, nb - 1);
+                v[a][j] = kMat ? src.cands[(int64_t)kc * src.ldc + a * N + i] : src.get(kc, a * N + i, N);
+            }
+        // what every candidate shares, staged once per workgroup
+        for (int q = tid; q < nb; q += kColThreads) {
+            const int i = ib + q;
+            if (kKeys) {
+#pragma unroll
+                for (int a = 0; a < 3; ++a) sb[a][q] = src.cands[a * N + i];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) kfl[a][q] = 0;
+            }
+            if (obj) {
+                su[0][q] = pa.prev ? pa.prev[i] : 0.0;
+                su[1][q] = pa.prev ? pa.prev[N + i] : 0.0;
+                su[2][q] = pa.prev ? pa.prev[2 * N + i] / pa.tan_half_fov : 0.0;   // z1
+                su[3][q] = pa.rmax ? pa.rmax[i] : 0.0;
+                su[4][q] = pen_threshold(pa, i);
+            }
+        }
+        __syncthreads();
+        if (obj) {
+            // the terms of this lane's UAVs (pen_term's operations in the same order), then the
+            // chain over the block in UAV order: term of UAV ib + 64 j + l is lane l's t[j]
+            double t[kColJ];
+#pragma unroll
+            for (int j = 0; j < kColJ; ++j) {
+                const int q = min(lane + kWave * j, nb - 1);
+                const double R2 = v[2][j];
+                double tt = pa.rmax ? __builtin_fabs(R2 - su[3][q]) : 0.0;
+                if (pa.prev) {
+                    const double z2 = R2 / pa.tan_half_fov;
+                    const double ddx = su[0][q] - v[0][j], ddy = su[1][q] - v[1][j], ddz = su[2][q] - z2;
+                    const double sq = ddx * ddx + ddy * ddy + ddz * ddz;
+                    if (sq > su[4][q]) tt = -1.0;
+                }
+                t[j] = tt;
+                bad |= __ballot(lane + kWave * j < nb && tt < 0.0) != 0;
+            }
+#pragma unroll
+            for (int j = 0; j < kColJ; ++j) {
+                if (kWave * j >= nb) break;   // uniform
+                const int n = min(kWave, nb - kWave * j);
+                if (n == kWave) {
+#pragma unroll
+                    for (int l = 0; l < kWave; ++l) acc += readlane_f64(t[j], l);
+                } else {
+                    for (int l = 0; l < n; ++l) acc += readlane_f64(t[j], l);
+                }
+            }
+        }
+        if (kKeys) {
+            // per variable block: the keys through LDS, then 64-B row segments
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                bool ok = true;
+#pragma unroll
+                for (int j = 0; j < kColJ; ++j) {
+                    const int q = lane + kWave * j;
+                    if (q >= nb) break;
+                    const double b = sb[a][q];
+                    const float f = (float)(v[a][j] - b);
+                    const bool e = __builtin_bit_cast(uint64_t, b + (double)f) == __builtin_bit_cast(uint64_t, v[a][j]);
+                    if (!e && k < K) atomicOr(&kfl[a][q], 1);
+                    kt[q][w] = f;
+                }
+                __syncthreads();
+                for (int q4 = tid; q4 < nb * (kColC / 4); q4 += kColThreads) {
+                    const int q = q4 / (kColC / 4), part = q4 % (kColC / 4);
+                    const float* s4 = &kt[q][4 * part];
+                    *reinterpret_cast<float4*>(keysT + ((int64_t)a * N + ib + q) * ldk + k0 + 4 * part) =
+                        make_float4(s4[0], s4[1], s4[2], s4[3]);
+                }
+                __syncthreads();
+                (void)ok;
+            }
+            for (int q = tid; q < 3 * nb; q += kColThreads) {
+                const int a = q / nb, qq = q - a * nb;
+                kbad[(int64_t)blockIdx.x * 3 * N + a * N + ib + qq] = kfl[a][qq];
+            }
+        }
+        __syncthreads();   // LDS reuse by the next block
     }
-    bool ok[NB];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) ok[b] = true;
-#pragma unroll
-    for (int j = 0; j < J; ++j) {   // candidate ty + 8j lies in flag tile (8j) / 32 = j / 4
-        const float f = (float)(x[j] - base);
-        ok[j / 4] &= __builtin_bit_cast(uint64_t, base + (double)f) == __builtin_bit_cast(uint64_t, x[j]);
-        t[ty + 8 * j][tx] = f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-        if (!ok[b]) atomicOr(&sbad[b][tx], 1);
-    // rows of kKeysK keys per variable: 64 consecutive threads write one row (256 B)
-    const int kk = threadIdx.x & (kKeysK - 1), vq = threadIdx.x / kKeysK;
-#pragma unroll
-    for (int j = 0; j < 32 / (kBlock / kKeysK); ++j) {
-        const int vv = vq + (kBlock / kKeysK) * j;
-        const int v = v0 + vv, k = k0 + kk;
-        if (k < K && v < n) keysT[(int64_t)v * K + k] = t[kk][vv];
-    }
-    __syncthreads();
-    if (threadIdx.x < 32 * NB) {
-        const int h = threadIdx.x >> 5, vv = threadIdx.x & 31, v = v0 + vv;
-        const int tile = NB * blockIdx.y + h;
-        if (v < n && tile < nkt) kbad[(int64_t)v * nkt + tile] = sbad[h][vv];
-    }
+    if (obj && lane == 0 && k < K) vp[k] = bad ? __builtin_inf() : acc * penalty;
     ts_end(ts);
 }
 
-// cands: see CandSrc. Writes disks[k*N + i] (scan walk) and, when pen != null,
-// pen[i*K + k] = pen_term (disk-major, as penalty_chain reads it).
-__global__ void disk_prep_kernel(CandSrc src, int N, int K, DiskRec* __restrict__ disks,
-                                 PenArgs pa, double* __restrict__ pen)
+// cands: see CandSrc. Writes disks[k*N + i] (the streaming scan's records).
+__global__ void disk_prep_kernel(CandSrc src, int N, int K, DiskRec* __restrict__ disks)
 {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (int64_t)N * K) return;
     const int k = (int)(t / N), i = (int)(t % N);
-    const double x = src.get(k, i, N), y = src.get(k, N + i, N), r = src.get(k, 2 * N + i, N);
-    disks[t] = make_disk(x, y, r);
-    if (pen) pen[(int64_t)i * K + k] = pen_term(x, y, r, i, N, pa, pen_threshold(pa, i));
+    disks[t] = make_disk(src.get(k, i, N), src.get(k, N + i, N), src.get(k, 2 * N + i, N));
 }
 
 }  // namespace mac

@@ -19,7 +19,7 @@
 //                         (batches too small for the poll walk)
 //   coverage_scan_kernel  streaming brute force (every entry x every disk), the fallback
 //   finalize_kernel       fixed-order sum of per-slice partials -> area, objective
-//   argmin_kernel         lexicographic (objective, index) minimum
+//   closure_kernel        one candidate in one launch (the per-trial-point objective callback)
 // (Completion-counter "last block" fusions of decide/argmin were measured slower: the
 // device-scope fence each block needs writes back its XCD's L2 on gfx950.)
 // An entry is credited to the LOWEST-index disk covering it (exactly-once union count), so the
@@ -34,4 +34,4 @@
 #include "k_poll.h"
 #include "k_final.h"
 #include "k_setup.h"
-#include "k_fused.h"
+#include "k_closure.h"

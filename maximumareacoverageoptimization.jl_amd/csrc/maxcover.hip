@@ -130,19 +130,19 @@ struct Lane {
     hipStream_t stream = nullptr;
     hipStream_t last = nullptr;   // stream of the most recent use
     hipEvent_t done = nullptr;
-    DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode, pen, nbr,
+    DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode, nbr,
         ncount, dlist, spart, vp, xinc, perm, ucount, umap, keysT, kbad, lane4, lanexp, rows, nboxT,
         cnt, dlimraw, finblk, finarrive, c32, p32, qual;
-    // the fused equal-weight poll (k_fused.h): keys, regions (generation-tagged), chains, counts,
-    // neighbour lists, hand-off counters
-    DevBuf f_keys, f_kbad, f_part, f_dtctr, f_vp, f_cnt, f_region, f_nbr, f_nboxT, f_ncount,
-        f_dlist, f_ctl;
     std::vector<double> h_dlim;
     PinnedBuf h_stage;                         // native MADS driver: best, permutations, incumbent
     PinnedBuf h_io;                            // host-pointer calls: candidates in, results out
     PinnedBuf h_dc;                            // disks with neighbours of the last poll (mapped)
     int* d_dc = nullptr;                       // ... its device address
     int dc_hist[8] = {};                       // ... as read at the last 8 poll enqueues
+    PinnedBuf h_cl;                            // closure_kernel's result slot (mapped)
+    uint64_t* d_cl = nullptr;                  // ... its device address
+    uint64_t cl_seq = 0;
+    DevBuf cpart, carrive;                     // closure_kernel: per-disk credits, arrivals
     int um_hist[8] = {};                       // most distinct positions of a disk, last 8 polls
 };
 
@@ -153,18 +153,16 @@ struct mac_ctx {
     std::vector<Lane*> lanes_free;
     std::vector<Lane*> lanes_all;
     hipStream_t setup_stream = nullptr;
-    // device polls' result mirror (guarded by mu): mapped coherent host words {obj, idx, seq}
-    // written by the argmin kernel of the latest mac_poll_best_dev_f64 on mirror_for
-    PinnedBuf h_best;
-    double* d_mirror = nullptr;
-    uint64_t mirror_seq = 0;
-    const void* mirror_for = nullptr;
-    // ... and the per-block minima of the latest such poll's finalize (k_final.h FinBest.hblk):
-    // the host reduces them as soon as every block has written its own
-    PinnedBuf h_blk;
-    uint64_t* d_blk = nullptr;
-    int mirror_nblk = 0;
-    int64_t mirror_base = 0;
+    // device polls' result mirror (guarded by mu): one mapped coherent slot {obj bits, index,
+    // seq, check} per d_best buffer (k_final.h mirror_check), reassigned least recently used; the
+    // finalize of a device poll writes its result into its d_best's slot under a fresh seq
+    static constexpr int kMirrorSlots = 64;
+    PinnedBuf h_mirror;
+    uint64_t* d_mirror = nullptr;
+    const void* mirror_key[kMirrorSlots] = {};
+    uint64_t mirror_want[kMirrorSlots] = {};
+    uint64_t mirror_used[kMirrorSlots] = {};
+    uint64_t mirror_seq = 0, mirror_clock = 0;
     hipStream_t dev_stream = nullptr;   // ordered stream for *_dev calls passed stream = NULL
 
     int algo = MAC_ALGO_AUTO;
@@ -173,8 +171,6 @@ struct mac_ctx {
     // In-kernel launch timing (k_common.h ts_begin / ts_end): each profiled walk launch takes
     // nwg consecutive {start, end} slots of `stamps`. a: the scan / tiled launch, b: the poll
     // launch when the device picks the walk (mode != null): the launch that ran is read.
-    // fused polls: a = launch 1, b = launch 2, mode = null, algo = MAC_ALGO_FUSED (the span is
-    // taken over both launches)
     // c / f: the chain's first launch (cands_keys or the index) and its last (finalize), whose
     // stamps give the whole poll chain's device span (-1: not stamped)
     struct Prof { int64_t a, na, b, nb; int64_t K; const int* mode; int algo;
@@ -253,6 +249,33 @@ struct LaneGuard {
     LaneGuard(mac_ctx* c, hipStream_t s) : ctx(c), lane(acquire_lane(c, s)), used(s) {}
     ~LaneGuard() { release_lane(ctx, lane, used); }
 };
+
+// A mapped result slot {obj bits, index, seq, check} (k_final.h) read once: true when it holds
+// seq `want` and its check word matches (else its stores are still landing, or it is another
+// poll's).
+static bool mirror_read(const uint64_t* h, uint64_t want, double* obj, int64_t* idx)
+{
+    if (__atomic_load_n(h + 2, __ATOMIC_ACQUIRE) != want) return false;
+    const uint64_t o = __atomic_load_n(h + 0, __ATOMIC_ACQUIRE);
+    const uint64_t i = __atomic_load_n(h + 1, __ATOMIC_ACQUIRE);
+    const uint64_t c = __atomic_load_n(h + 3, __ATOMIC_ACQUIRE);
+    if (c != mirror_check(o, i, want) || __atomic_load_n(h + 2, __ATOMIC_ACQUIRE) != want) return false;
+    *obj = __builtin_bit_cast(double, o);
+    *idx = (int64_t)i;
+    return true;
+}
+
+// Spin on a slot for up to `ms` milliseconds.
+static bool mirror_wait(const uint64_t* h, uint64_t want, double ms, double* obj, int64_t* idx)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int spin = 0;; ++spin) {
+        if (mirror_read(h, want, obj, idx)) return true;
+        if ((spin & 1023) == 1023 &&
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > ms)
+            return false;
+    }
+}
 
 static inline unsigned grid1d(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
 
@@ -433,138 +456,19 @@ static bool use_tiled(mac_ctx* ctx, int N, const double* h_cands, int64_t three_
     return visits < 0.5 * (double)ctx->M * (double)N;
 }
 
-// The fused equal-weight poll (k_fused.h) runs only when asked for (MAC_ALGO_FUSED) and every
-// entry weighs the same. Measured on the MI355X (profiles/r02a_*), its two launches take 0.19 ms
-// per config-4 poll against the six-launch chain's 0.087 ms, so AUTO keeps the chain.
-static bool use_fused(const mac_ctx* ctx, int N, int64_t K)
-{
-    return ctx->algo == MAC_ALGO_FUSED && ctx->w_uniform && ctx->M > 0 && N > 0 && K > 0;
-}
-
-// Two launches (k_fused.h): fused_prep_kernel, fused_walk_kernel. d_dlim: raw d_lim per UAV.
-static void enqueue_fused(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& src, int N, int K,
-                          const double* d_rmax, double penalty, const double* d_prev,
-                          const double* d_dlim, double tan_half_fov, double* d_area, double* d_obj,
-                          double* d_best, int64_t idx_base, double* d_mirror, uint64_t mirror_seq)
-{
-    FusedArgs a{};
-    a.src = src;
-    a.N = N;
-    a.K = K;
-    a.ndt = (N + kFD - 1) / kFD;
-    a.nct = (K + kFC - 1) / kFC;
-    a.Kp = a.nct * kFC;
-    const bool objective = d_obj != nullptr || d_best != nullptr;
-    a.n_chain = objective ? (K + kFChainCands - 1) / kFChainCands : 0;
-    a.n_shared = kSharedWG;
-    a.g = ctx->grid;
-    a.rmax = objective ? d_rmax : nullptr;
-    a.prev = objective ? d_prev : nullptr;
-    a.dlim = d_dlim;
-    a.tan_half_fov = tan_half_fov;
-    a.penalty = penalty;
-    a.w0 = ctx->w0;
-    const size_t n = (size_t)N;
-    L->f_keys.reserve(sizeof(int16_t) * 3 * n * (size_t)a.Kp);
-    L->f_kbad.reserve(n * (size_t)a.nct);
-    L->f_part.reserve(sizeof(int4) * (size_t)a.ndt * a.nct * kFD);
-    const bool fresh_dt = L->f_dtctr.grow(sizeof(unsigned) * (size_t)a.ndt);
-    L->f_vp.reserve(sizeof(double) * (size_t)K);
-    L->f_cnt.reserve(sizeof(unsigned) * (size_t)K);
-    L->f_region.reserve(sizeof(int4) * n);
-    L->f_nbr.reserve(sizeof(uint16_t) * n * kPollNbr);
-    L->f_nboxT.reserve(sizeof(int4) * n * kPollNbr);
-    L->f_ncount.reserve(sizeof(int) * n);
-    L->f_dlist.reserve(sizeof(int) * n);
-    const bool fresh_ctl = L->f_ctl.grow(sizeof(int) * kCtlWords);
-    // the arrival counters reset themselves (atomicInc wraps at the last arrival): zero only
-    // when (re)allocated
-    if (fresh_dt) HCK(hipMemsetAsync(L->f_dtctr.p, 0, L->f_dtctr.cap, s));
-    if (fresh_ctl) HCK(hipMemsetAsync(L->f_ctl.p, 0, L->f_ctl.cap, s));
-    a.keys = L->f_keys.as<int16_t>();
-    a.kbad = L->f_kbad.as<uint8_t>();
-    a.part = L->f_part.as<int4>();
-    a.dtctr = L->f_dtctr.as<unsigned>();
-    a.vp = L->f_vp.as<double>();
-    a.cnt = L->f_cnt.as<unsigned>();
-    a.region = L->f_region.as<int4>();
-    a.nbr = L->f_nbr.as<uint16_t>();
-    a.nboxT = L->f_nboxT.as<int4>();
-    a.ncount = L->f_ncount.as<int>();
-    a.dlist = L->f_dlist.as<int>();
-    a.ctl = L->f_ctl.as<int>();
-    a.xy = ctx->xys.as<double2>();
-    a.off = ctx->off.as<int32_t>();
-    a.area_out = d_area;
-    a.obj_out = d_obj;
-    a.best = d_best;
-    a.mirror = d_mirror;
-    a.seq = mirror_seq;
-    a.idx_base = idx_base;
-
-    const unsigned n1 = (unsigned)(a.n_chain + a.ndt * a.nct);
-    const unsigned n2 = (unsigned)(N + a.n_shared);
-    int64_t ts_a = -1, ts_na = 0, ts_b = -1, ts_nb = 0;
-    uint64_t* ts1 = nullptr;
-    uint64_t* ts2 = nullptr;
-    if (ctx->profile) {
-        std::lock_guard<std::mutex> lk(ctx->mu);
-        if (ctx->stamp_used + n1 + n2 <= ctx->stamp_cap) {
-            ts_a = ctx->stamp_used;
-            ts_na = n1;
-            ts_b = ts_a + n1;
-            ts_nb = n2;
-            ctx->stamp_used += n1 + n2;
-            ts1 = ctx->stamps.as<uint64_t>() + 2 * ts_a;
-            ts2 = ctx->stamps.as<uint64_t>() + 2 * ts_b;
-        }
-    }
-    hipLaunchKernelGGL(fused_prep_kernel, dim3(n1), dim3(kBlock), 0, s, ts1, a);
-    HCK(hipGetLastError());
-    hipLaunchKernelGGL(fused_walk_kernel, dim3(n2), dim3(kPollThreads), 0, s, ts2, a);
-    HCK(hipGetLastError());
-    if (ts1) {
-        std::lock_guard<std::mutex> lk(ctx->mu);
-        ctx->prof.push_back({ts_a, ts_na, ts_b, ts_nb, (int64_t)K, nullptr, MAC_ALGO_FUSED});
-    }
-}
-
-// Enqueue disk prep + coverage + finalize (+ argmin) on stream s. All pointers device.
+// Enqueue the column pass + coverage + finalize (+ argmin) on stream s. All pointers device.
 // area_out/obj_out may be null; best may be null.
-// d_dlimT: cons3 thresholds per UAV (legacy chain); d_dlim_raw: the raw d_lim (fused poll).
+// d_dlimT: cons3 thresholds per UAV (host calls), else d_dlim_raw: the raw d_lim, thresholded
+// where it is read (device calls).
 static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& src, int N,
                          int K, bool tiled, const double* d_rmax, double penalty,
                          const double* d_prev, const double* d_dlimT, const double* d_dlim_raw,
                          double tan_half_fov, double* d_area, double* d_obj, double* d_best,
-                         int64_t idx_base, double* d_mirror = nullptr, uint64_t mirror_seq = 0,
-                         uint64_t* d_hblk = nullptr)
+                         int64_t idx_base, uint64_t* d_mirror = nullptr, uint64_t mirror_seq = 0)
 {
-    if (use_fused(ctx, N, K)) {
-        enqueue_fused(ctx, L, s, src, N, K, d_rmax, penalty, d_prev, d_dlim_raw, tan_half_fov,
-                      d_area, d_obj, d_best, idx_base, d_mirror, mirror_seq);
-        return;
-    }
     const int64_t M = ctx->M;
     int n_poll = N, n_other = 1;
     const int* d_mode = nullptr;
-    // objective penalty terms + cons3 marks are written by the prep kernels (one term per disk
-    // and candidate); the finalize kernel runs the sequential violation chain
-    const PenArgs pa{d_rmax, d_prev, d_dlimT, d_dlim_raw, tan_half_fov};
-    double* d_pen = nullptr;           // penalty terms, pen[i*K + k]
-    double* d_vp = nullptr;            // per-candidate penalty (or +inf: cons3)
-    bool chain_done = false;           // the poll kernel ran the chains
-    const double* d_spart = nullptr;   // poll walk: shared-entry rows
-    const int* d_umap = nullptr;       // poll walk: candidate -> distinct-disk position
-    const int* d_ncount = nullptr;
-    int counts = 0;                    // poll walk with equal weights: integer count rows
-    if (d_obj) {
-        L->vp.reserve(sizeof(double) * (size_t)std::max(K, 1));
-        d_vp = L->vp.as<double>();
-        if (N > 0) {
-            L->pen.reserve(sizeof(double) * (size_t)N * K);
-            d_pen = L->pen.as<double>();
-        }
-    }
     // Profiling: the measured walk launches stamp their own workgroups' start / end times
     // (k_common.h), so measuring adds no packet, event or dependency to the stream.
     int64_t ts_a = -1, ts_na = 0, ts_b = -1, ts_nb = 0, ts_c = -1, ts_nc = 0, ts_f = -1, ts_nf = 0;
@@ -577,6 +481,24 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         ctx->stamp_used += nwg;
         return ctx->stamps.as<uint64_t>() + 2 * base;
     };
+    // the objective's penalty and cons3 (the column pass: one sequential chain per candidate)
+    const PenArgs pa{d_rmax, d_prev, d_dlimT, d_dlim_raw, tan_half_fov};
+    double* d_vp = nullptr;            // per-candidate penalty (or +inf: cons3)
+    const double* d_spart = nullptr;   // poll walk: shared-entry rows
+    const int* d_umap = nullptr;       // poll walk: candidate -> distinct-disk position
+    const int* d_ncount = nullptr;
+    int counts = 0;                    // poll walk with equal weights: integer count rows
+    if (d_obj) {
+        L->vp.reserve(sizeof(double) * (size_t)std::max(K, 1));
+        d_vp = L->vp.as<double>();
+    }
+    const bool big = N > kTiledMaxN;
+    const bool poll_possible = tiled && N > 0 && M > 0 &&
+                               (ctx->algo == MAC_ALGO_POLL || big ||
+                                (ctx->algo == MAC_ALGO_AUTO && K >= kPollMinK));
+    // candidates per index thread: 3 (K <= 3073), 6 (K <= 6145); larger: identity map
+    const int iper = K <= kIndexMaxK + 1 ? kIdxPer : K <= kIndexMaxKWide + 1 ? kIdxPerWide : 0;
+    const bool want_keys = poll_possible && src.cands && iper;   // the index hashes fp32 keys
     auto prof_end = [&]() {
         if (!ctx->profile || (ts_a < 0 && ts_b < 0)) return;
         std::lock_guard<std::mutex> lk(ctx->mu);
@@ -584,19 +506,38 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                              tiled ? MAC_ALGO_TILED : MAC_ALGO_SCAN, ts_c, ts_nc, ts_f, ts_nf});
     };
 
+    CandSrc isrc = src;
+    if (d_obj || want_keys) {
+        // the column pass (k_prep.h): penalty chains + cons3 into vp, and the index's keys
+        const int ncb = (K + kColC - 1) / kColC;
+        uint64_t* tsk = poll_possible ? take_ts(ncb, ts_c, ts_nc) : nullptr;
+        if (want_keys) {
+            const int ldk = keys_ld(K);
+            L->keysT.reserve(sizeof(float) * (size_t)3 * N * ldk);
+            L->kbad.reserve(sizeof(int) * (size_t)3 * N * ncb);
+            hipLaunchKernelGGL((column_pass_kernel<true, true>), dim3(ncb), dim3(kColThreads), 0, s, tsk, src,
+                               N, K, pa, penalty, d_vp, L->keysT.as<float>(), L->kbad.as<int>());
+            isrc.keysT = L->keysT.as<float>();
+            isrc.kbad = L->kbad.as<int>();
+            isrc.nkt = ncb;
+            isrc.ldk = ldk;
+        } else if (src.cands) {
+            hipLaunchKernelGGL((column_pass_kernel<true, false>), dim3(ncb), dim3(kColThreads), 0, s, tsk,
+                               src, N, K, pa, penalty, d_vp, nullptr, nullptr);
+        } else {
+            hipLaunchKernelGGL((column_pass_kernel<false, false>), dim3(ncb), dim3(kColThreads), 0, s, tsk,
+                               src, N, K, pa, penalty, d_vp, nullptr, nullptr);
+        }
+        HCK(hipGetLastError());
+    }
+
     if (N == 0 || M == 0) {  // no UAV or no entry: every area is 0 (the loops never run)
         L->partial.reserve(sizeof(double) * (size_t)K);
         HCK(hipMemsetAsync(L->partial.p, 0, sizeof(double) * (size_t)K, s));
-        if (d_pen) {
-            L->disks.reserve(sizeof(DiskRec) * (size_t)N * K);
-            hipLaunchKernelGGL(disk_prep_kernel, dim3(grid1d((int64_t)N * K, 256)), dim3(256), 0, s,
-                               src, N, K, L->disks.as<DiskRec>(), pa, d_pen);
-            HCK(hipGetLastError());
-        }
     } else if (!tiled) {
         L->disks.reserve(sizeof(DiskRec) * (size_t)N * K);
         hipLaunchKernelGGL(disk_prep_kernel, dim3(grid1d((int64_t)N * K, 256)), dim3(256), 0, s,
-                           src, N, K, L->disks.as<DiskRec>(), pa, d_pen);
+                           src, N, K, L->disks.as<DiskRec>());
         HCK(hipGetLastError());
         constexpr int KB = 4, PPT = 4;
         const int64_t per_pass = (int64_t)kBlock * PPT;
@@ -615,9 +556,6 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                            L->disks.as<DiskRec>(), N, K, chunk, L->partial.as<double>());
         HCK(hipGetLastError());
     } else {
-        const bool big = N > kTiledMaxN;
-        const bool poll_possible = ctx->algo == MAC_ALGO_POLL || big ||
-                                   (ctx->algo == MAC_ALGO_AUTO && K >= kPollMinK);
         // the disk index: distinct disks per UAV, their records / penalty terms, the map, and
         // each disk's region and walk costs (k_index.h)
         L->disks.reserve(sizeof(DiskRec) * (size_t)N * K);
@@ -632,35 +570,18 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             L->rows.reserve(sizeof(int2) * (size_t)N * (kRowInfo + 1));
         }
         counts = poll_possible && ctx->w_uniform ? 1 : 0;   // equal weights: the walks count
-        const IndexOut io{L->disks.as<DiskRec>(), d_pen, L->umap.as<int>(), L->ucount.as<int>(),
+        const IndexOut io{L->disks.as<DiskRec>(), L->umap.as<int>(), L->ucount.as<int>(),
                           L->region.as<int4>(), L->cost.as<double2>(), L->mode.as<int>() + 1,
                           poll_possible ? L->lane4.as<float4>() : nullptr,
                           poll_possible ? L->lanexp.as<float>() : nullptr,
                           poll_possible ? L->rows.as<int2>() : nullptr, ctx->off.as<int32_t>()};
-        CandSrc isrc = src;
-        // candidates per index thread: 3 (K <= 3073), 6 (K <= 6145); larger: identity map
-        const int iper = K <= kIndexMaxK + 1 ? kIdxPer : K <= kIndexMaxKWide + 1 ? kIdxPerWide : 0;
         if (!poll_possible) {
             // the per-candidate walk alone (small batches, the single-candidate closure): the
             // identity map, one thread per (disk, candidate), no key pass
             const int64_t nk = (int64_t)N * K;
             hipLaunchKernelGGL(disk_index_identity_kernel, dim3(grid1d(nk, 256)), dim3(256), 0, s,
-                               src, N, K, pa, L->disks.as<DiskRec>(), L->umap.as<int>(), d_pen);
+                               src, N, K, L->disks.as<DiskRec>(), L->umap.as<int>());
             HCK(hipGetLastError());
-        }
-        if (poll_possible && src.cands && iper) {  // matrix: fp32 keys, variable-major, so each
-                                                 // disk's K keys are a row
-            const int nkt = (K + 31) / 32;
-            L->keysT.reserve(sizeof(float) * (size_t)3 * N * K);
-            L->kbad.reserve(sizeof(int) * (size_t)3 * N * nkt);
-            const dim3 kgrid((3 * N + 31) / 32, (K + kKeysK - 1) / kKeysK);
-            uint64_t* tsk = take_ts((int64_t)kgrid.x * kgrid.y, ts_c, ts_nc);
-            hipLaunchKernelGGL(cands_keys_kernel, kgrid, dim3(kBlock), 0, s, tsk,
-                               src.cands, 3 * N, K, L->keysT.as<float>(), L->kbad.as<int>(), nkt);
-            HCK(hipGetLastError());
-            isrc.keysT = L->keysT.as<float>();
-            isrc.kbad = L->kbad.as<int>();
-            isrc.nkt = nkt;
         }
         const unsigned nidx = 8 * ((N + 7) / 8);
         uint64_t* tsi = (poll_possible && ts_c < 0) ? take_ts(nidx, ts_c, ts_nc) : nullptr;
@@ -669,16 +590,16 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             ;   // indexed above
         else if (isrc.keysT && iper == kIdxPerWide)
             hipLaunchKernelGGL((disk_index_kernel<true, kIdxPerWide>), dim3(nidx), dim3(kIdxThreads), 0,
-                               s, tsi, isrc, N, K, ctx->grid, pa, dedup, io);
+                               s, tsi, isrc, N, K, ctx->grid, dedup, io);
         else if (isrc.keysT)
             hipLaunchKernelGGL((disk_index_kernel<true, kIdxPer>), dim3(nidx), dim3(kIdxThreads), 0, s,
-                               tsi, isrc, N, K, ctx->grid, pa, dedup, io);
+                               tsi, isrc, N, K, ctx->grid, dedup, io);
         else if (iper == kIdxPerWide)
             hipLaunchKernelGGL((disk_index_kernel<false, kIdxPerWide>), dim3(nidx), dim3(kIdxThreads), 0,
-                               s, tsi, isrc, N, K, ctx->grid, pa, dedup, io);
+                               s, tsi, isrc, N, K, ctx->grid, dedup, io);
         else
             hipLaunchKernelGGL((disk_index_kernel<false, kIdxPer>), dim3(nidx), dim3(kIdxThreads), 0, s,
-                               tsi, isrc, N, K, ctx->grid, pa, dedup, io);
+                               tsi, isrc, N, K, ctx->grid, dedup, io);
         HCK(hipGetLastError());
         const DiskRec* d_urec = L->disks.as<DiskRec>();
         const int* d_map = L->umap.as<int>();
@@ -755,11 +676,9 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             int um_max = 0;
             for (int q = 0; q < 8; ++q) um_max = std::max(um_max, L->um_hist[q]);
             const int gy = std::max(1, std::min(4, (um_max + kPollKPB - 1) / kPollKPB));
-            const int chains = (K + kChainC - 1) / kChainC;
-            const int n_chain = d_obj ? chains : 0;
             L->spart.reserve(sizeof(double) * (size_t)N * K);
             const int n_shared = kSharedWG;
-            const dim3 pgrid(N + n_shared + n_chain, gy);
+            const dim3 pgrid(N + n_shared, gy);
             uint64_t* ts = take_ts((int64_t)pgrid.x * pgrid.y, ts_b, ts_nb);
             hipLaunchKernelGGL(coverage_poll_kernel, pgrid, dim3(kPollThreads), 0, s, ts,
                                ctx->xys.as<double2>(), ctx->ws.as<double>(),
@@ -769,8 +688,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                                L->rows.as<int2>(),
                                L->ncount.as<int>(), L->dlist.as<int>(), L->mode.as<int>() + 1,
                                L->mode.as<int>() + 2, N, K,
-                               d_mode, L->partial.as<double>(), L->spart.as<double>(), n_chain, d_pen,
-                               penalty, d_vp, n_shared, counts, bits_on, L->d_dc, L->qual.as<int>());
+                               d_mode, L->partial.as<double>(), L->spart.as<double>(), n_shared, counts,
+                               bits_on, L->d_dc, L->qual.as<int>());
             HCK(hipGetLastError());
             // the shared entries of crowded polls: bit-words per distinct position (k_bits.h);
             // returns at once when few disks have neighbours (the poll kernel took them)
@@ -792,20 +711,9 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                                    L->ncount.as<int>(), L->qual.as<int>(), L->mode.as<int>() + 1, d_mode,
                                    N, K, L->spart.as<double>(), bits_on == 2 ? 0 : kBitsMinDisks);
             HCK(hipGetLastError());
-            chain_done = true;
             d_spart = L->spart.as<double>();
             d_ncount = L->ncount.as<int>();
-        } else if (d_obj) {
-            hipLaunchKernelGGL(penalty_chain_kernel, dim3((K + kChainC - 1) / kChainC), dim3(kBlock), 0,
-                               s, d_pen, K, N, penalty, d_vp);
-            HCK(hipGetLastError());
-            chain_done = true;
         }
-    }
-    if (d_obj && !chain_done) {
-        hipLaunchKernelGGL(penalty_chain_kernel, dim3((K + kChainC - 1) / kChainC), dim3(kBlock), 0, s,
-                           d_pen, K, N, penalty, d_vp);
-        HCK(hipGetLastError());
     }
     // finalize, with the poll argmin taken by its last-arriving block (k_final.h)
     const unsigned nfin = 8 * (unsigned)((K + 8 * kFinC - 1) / (8 * kFinC));   // k_final.h: XCD map
@@ -814,12 +722,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         L->finblk.reserve(2 * sizeof(unsigned long long) * nfin);
         if (L->finarrive.grow(sizeof(unsigned)))   // zero once; the last block of each launch resets it
             HCK(hipMemsetAsync(L->finarrive.p, 0, L->finarrive.cap, s));
-        // the per-block minima go to the caller's mapped words (d_hblk: the MADS stepper) or the
-        // context's (a mirrored device poll), when the grid fits them
-        uint64_t* const hblk = nfin > (unsigned)kFinMaxBlk ? nullptr
-                             : d_hblk ? d_hblk : d_mirror ? ctx->d_blk : nullptr;
         fb = FinBest{d_best, d_mirror, mirror_seq, idx_base, L->finblk.as<unsigned long long>(),
-                     L->finarrive.as<unsigned>(), hblk};
+                     L->finarrive.as<unsigned>()};
     }
     uint64_t* tsf = ts_c >= 0 ? take_ts(nfin, ts_f, ts_nf) : nullptr;
     hipLaunchKernelGGL(finalize_kernel, dim3(nfin), dim3(kFinThreads), 0, s,
@@ -1024,17 +928,6 @@ int32_t mac_profile_read(mac_ctx* ctx, double* kernel_ms, int64_t* launches,
     };
     for (auto& p : ctx->prof) {
         algo = p.algo;
-        if (p.algo == MAC_ALGO_FUSED) {   // the chain: first start of launch 1 .. last end of launch 2
-            uint64_t t0 = ~(uint64_t)0, t1 = 0;
-            for (int64_t q = p.a; q < p.b + p.nb; ++q) {
-                t0 = std::min(t0, st[(size_t)(2 * q)]);
-                t1 = std::max(t1, st[(size_t)(2 * q + 1)]);
-            }
-            ms += t1 > t0 ? (double)(t1 - t0) / kRealtimeHz * 1e3 : 0.0;
-            ++n;
-            kc += p.K;
-            continue;
-        }
         int64_t a = p.a, na = p.na;
         if (p.mode) {  // the device's choice (the lane's mode word holds its latest decision)
             int m = 0;
@@ -1077,45 +970,29 @@ int32_t mac_profile_split(mac_ctx* ctx, double* prep_ms, double* walk_ms, double
     double a1 = 0.0, a2 = 0.0, gap = 0.0;
     int64_t n = 0;
     for (auto& p : ctx->prof) {
-        if (p.algo != MAC_ALGO_FUSED) {
-            // the launch chain: prep = first launch's start .. the walk's start, walk = the walk
-            // launch, gap = the walk's end .. finalize's end (the argmin included)
-            if (p.c < 0 || p.f < 0) continue;
-            int64_t wa = p.a, wn = p.na;
-            if (p.mode) {
-                int m = 0;
-                HCK(hipMemcpy(&m, p.mode, sizeof(int), hipMemcpyDeviceToHost));
-                if (m == kModePoll) {
-                    wa = p.b;
-                    wn = p.nb;
-                }
+        // the launch chain: prep = first launch's start .. the walk's start, walk = the walk
+        // launch, gap = the walk's end .. finalize's end (the argmin included)
+        if (p.c < 0 || p.f < 0) continue;
+        int64_t wa = p.a, wn = p.na;
+        if (p.mode) {
+            int m = 0;
+            HCK(hipMemcpy(&m, p.mode, sizeof(int), hipMemcpyDeviceToHost));
+            if (m == kModePoll) {
+                wa = p.b;
+                wn = p.nb;
             }
-            uint64_t s0 = ~(uint64_t)0, sw = ~(uint64_t)0, ew = 0, ef = 0;
-            for (int64_t q = p.c; q < p.c + p.nc; ++q) s0 = std::min(s0, st[(size_t)(2 * q)]);
-            for (int64_t q = wa; wa >= 0 && q < wa + wn; ++q) {
-                sw = std::min(sw, st[(size_t)(2 * q)]);
-                ew = std::max(ew, st[(size_t)(2 * q + 1)]);
-            }
-            for (int64_t q = p.f; q < p.f + p.nf; ++q) ef = std::max(ef, st[(size_t)(2 * q + 1)]);
-            if (!(ef > s0) || !(ew > sw) || sw < s0) continue;
-            a1 += (double)(sw - s0) / kRealtimeHz * 1e3;
-            a2 += (double)(ew - sw) / kRealtimeHz * 1e3;
-            gap += (double)(ef - ew) / kRealtimeHz * 1e3;
-            ++n;
-            continue;
         }
-        uint64_t s1 = ~(uint64_t)0, e1 = 0, s2 = ~(uint64_t)0, e2 = 0;
-        for (int64_t q = p.a; q < p.a + p.na; ++q) {
-            s1 = std::min(s1, st[(size_t)(2 * q)]);
-            e1 = std::max(e1, st[(size_t)(2 * q + 1)]);
+        uint64_t s0 = ~(uint64_t)0, sw = ~(uint64_t)0, ew = 0, ef = 0;
+        for (int64_t q = p.c; q < p.c + p.nc; ++q) s0 = std::min(s0, st[(size_t)(2 * q)]);
+        for (int64_t q = wa; wa >= 0 && q < wa + wn; ++q) {
+            sw = std::min(sw, st[(size_t)(2 * q)]);
+            ew = std::max(ew, st[(size_t)(2 * q + 1)]);
         }
-        for (int64_t q = p.b; q < p.b + p.nb; ++q) {
-            s2 = std::min(s2, st[(size_t)(2 * q)]);
-            e2 = std::max(e2, st[(size_t)(2 * q + 1)]);
-        }
-        if (e1 > s1) a1 += (double)(e1 - s1) / kRealtimeHz * 1e3;
-        if (e2 > s2) a2 += (double)(e2 - s2) / kRealtimeHz * 1e3;
-        if (s2 > e1 && e1 > 0) gap += (double)(s2 - e1) / kRealtimeHz * 1e3;
+        for (int64_t q = p.f; q < p.f + p.nf; ++q) ef = std::max(ef, st[(size_t)(2 * q + 1)]);
+        if (!(ef > s0) || !(ew > sw) || sw < s0) continue;
+        a1 += (double)(sw - s0) / kRealtimeHz * 1e3;
+        a2 += (double)(ew - sw) / kRealtimeHz * 1e3;
+        gap += (double)(ef - ew) / kRealtimeHz * 1e3;
         ++n;
     }
     if (prep_ms) *prep_ms = a1;
@@ -1165,18 +1042,18 @@ void mac_ctx_destroy(mac_ctx* ctx)
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
-    ctx->h_best.release();
+    ctx->h_mirror.release();
     for (Lane* l : ctx->lanes_all) {
         l->h_stage.release();
         l->h_io.release();
         l->h_dc.release();
+        l->h_cl.release();
         for (DevBuf* b : {&l->cands, &l->disks, &l->partial, &l->area, &l->obj, &l->best,
-                          &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->pen, &l->nbr,
+                          &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->nbr,
                           &l->ncount, &l->dlist, &l->qual, &l->spart, &l->vp, &l->xinc,
                           &l->perm, &l->ucount, &l->umap, &l->keysT, &l->kbad, &l->lane4,
-                          &l->lanexp, &l->rows, &l->nboxT, &l->cnt, &l->dlimraw, &l->finblk, &l->finarrive, &l->c32, &l->p32, &l->f_keys,
-                          &l->f_kbad, &l->f_part, &l->f_dtctr, &l->f_vp, &l->f_cnt,
-                          &l->f_region, &l->f_nbr, &l->f_nboxT, &l->f_ncount, &l->f_dlist, &l->f_ctl})
+                          &l->lanexp, &l->rows, &l->nboxT, &l->cnt, &l->dlimraw, &l->finblk, &l->finarrive, &l->c32, &l->p32,
+                          &l->cpart, &l->carrive})
             b->release();
         if (l->done) (void)hipEventDestroy(l->done);
         if (l->stream) (void)hipStreamDestroy(l->stream);
@@ -1198,7 +1075,7 @@ int32_t mac_set_option(mac_ctx* ctx, int32_t option, int64_t value)
     if (!ctx) return fail(MAC_E_INVAL, "null context");
     switch (option) {
     case MAC_OPT_ALGO:
-        if (value < MAC_ALGO_AUTO || value > MAC_ALGO_FUSED) return fail(MAC_E_INVAL, "bad algo");
+        if (value < MAC_ALGO_AUTO || value > MAC_ALGO_POLL) return fail(MAC_E_INVAL, "bad algo");
         ctx->algo = (int)value;
         return MAC_OK;
     case MAC_OPT_STORAGE:
@@ -1431,8 +1308,7 @@ static void compute_flags(mac_ctx* ctx, hipStream_t s, const double* circles, in
     if (N > 0) {
         HCK(hipMemcpyAsync(ctx->circ.p, circles, sizeof(double) * 3 * N, hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(disk_prep_kernel, dim3(grid1d(N, 256)), dim3(256), 0, s,
-                           matrix_src(ctx->circ.as<double>(), N), N, 1, ctx->cdisk.as<DiskRec>(),
-                           PenArgs{nullptr, nullptr, nullptr, nullptr, 1.0}, nullptr);
+                           matrix_src(ctx->circ.as<double>(), N), N, 1, ctx->cdisk.as<DiskRec>());
         HCK(hipGetLastError());
         const unsigned nb = (unsigned)std::max(1, std::min((N + kWavesPerBlock - 1) / kWavesPerBlock,
                                                            8 * ctx->cus));
@@ -1583,69 +1459,48 @@ struct mac_mads {
     double* hb = nullptr;
     double* hx = nullptr;
     int* hperm = nullptr;
-    // finalize's per-block minima of each poll in mapped host memory (k_final.h FinBest.hblk):
-    // the poll's best is reduced here without a copy or a stream synchronisation
-    PinnedBuf hblk;
-    uint64_t* d_hblk = nullptr;
+    // the poll's best, written by finalize's last block into a mapped slot {obj bits, index,
+    // seq, check} (k_final.h): read here without a copy or a stream synchronisation
+    PinnedBuf hslot;
+    uint64_t* d_slot = nullptr;
     uint64_t seq = 0;
-    int nblk = 0;
+    bool slotted = false;
+    double* ext_best = nullptr;   // mac_mads_best_buffer: the polls' best goes here
     int64_t polled_b = 0;        // 2^ell of the poll awaiting its update (0: none)
     double h_enq = 0, h_perm = 0, h_wait = 0, h_post = 0;
     std::chrono::steady_clock::time_point t0;
 };
 
-// blk: the poll's best through finalize's per-block minima (mads_wait_best), else a 16-B copy
-static void mads_best_of(mac_mads* m, const CandSrc& src, int Kc, int64_t idx_base, bool blk = false)
+static double* mads_best_ptr(mac_mads* m) { return m->ext_best ? m->ext_best : m->L->best.as<double>(); }
+
+// slot: the poll's best through the mapped slot finalize's last block writes (mads_wait_best),
+// else a 16-B copy
+static void mads_best_of(mac_mads* m, const CandSrc& src, int Kc, int64_t idx_base, bool slot = false)
 {
-    const int nfin = 8 * ((Kc + 8 * kFinC - 1) / (8 * kFinC));   // finalize's grid (enqueue_eval)
-    blk = blk && nfin <= kFinMaxBlk && !use_fused(m->ctx, m->N, Kc);   // fused: no finalize blocks
-    if (blk && !m->d_hblk) {
-        m->hblk.reserve(sizeof(uint64_t) * 4 * kFinMaxBlk, hipHostMallocMapped | hipHostMallocCoherent);
-        std::memset(m->hblk.p, 0, sizeof(uint64_t) * 4 * kFinMaxBlk);
+    if (slot && !m->d_slot) {
+        m->hslot.reserve(64, hipHostMallocMapped | hipHostMallocCoherent);
+        std::memset(m->hslot.p, 0, 64);
         void* dp = nullptr;
-        HCK(hipHostGetDevicePointer(&dp, m->hblk.p, 0));
-        m->d_hblk = (uint64_t*)dp;
+        HCK(hipHostGetDevicePointer(&dp, m->hslot.p, 0));
+        m->d_slot = (uint64_t*)dp;
     }
-    m->nblk = blk ? nfin : 0;
+    m->slotted = slot;
     enqueue_eval(m->ctx, m->L, m->s, src, m->N, Kc, use_tiled(m->ctx, m->N, nullptr, m->n),
                  m->L->rmax.as<double>(), m->penalty, m->d_prev, m->d_dlimT,
                  m->d_prev ? m->L->dlimraw.as<double>() : nullptr, m->tan_half_fov,
-                 m->L->area.as<double>(), m->L->obj.as<double>(), m->L->best.as<double>(), idx_base,
-                 nullptr, blk ? ++m->seq : 0, blk ? m->d_hblk : nullptr);
-    if (!blk) HCK(hipMemcpyAsync(m->hb, m->L->best.p, 16, hipMemcpyDeviceToHost, m->s));
+                 m->L->area.as<double>(), m->L->obj.as<double>(), mads_best_ptr(m), idx_base,
+                 slot ? m->d_slot : nullptr, slot ? ++m->seq : 0);
+    if (!slot) HCK(hipMemcpyAsync(m->hb, mads_best_ptr(m), 16, hipMemcpyDeviceToHost, m->s));
 }
 
-// The best {objective, global index} of the poll mads_best_of enqueued: the per-block minima once
-// every block's sequence has landed (lexicographic, as finalize's last block), or, after 50 ms
-// (a failed launch) or without them, the stream synchronised and the copy / device record.
-static void mads_wait_best(mac_mads* m, int64_t idx_base, double* obj, int64_t* idx)
+// The best {objective, global index} of the poll mads_best_of enqueued: from the mapped slot once
+// it holds this poll's seq and a matching check word, or, after 50 ms (a failed launch) or
+// without a slot, the stream synchronised and the copy.
+static void mads_wait_best(mac_mads* m, double* obj, int64_t* idx)
 {
-    if (m->nblk > 0) {
-        const uint64_t* hk = (const uint64_t*)m->hblk.p;
-        const auto t0 = std::chrono::steady_clock::now();
-        int b = 0;
-        for (int spin = 0; b < m->nblk; ++spin) {
-            while (b < m->nblk && __atomic_load_n(hk + 4 * b + 2, __ATOMIC_ACQUIRE) == m->seq) ++b;
-            if (b < m->nblk && (spin & 1023) == 1023 &&
-                std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50))
-                break;
-        }
-        if (b == m->nblk) {
-            double bv = INFINITY;
-            int64_t bi = -1;
-            for (int q = 0; q < m->nblk; ++q) {
-                const double v = __builtin_bit_cast(double, hk[4 * q]);
-                const int64_t i = (int64_t)hk[4 * q + 1];
-                if (i >= 0 && (bi < 0 || v < bv || (v == bv && i < bi))) {
-                    bv = v;
-                    bi = i;
-                }
-            }
-            *obj = bi >= 0 ? bv : INFINITY;
-            *idx = bi >= 0 ? idx_base + bi : -1;
-            return;
-        }
-        HCK(hipMemcpyAsync(m->hb, m->L->best.p, 16, hipMemcpyDeviceToHost, m->s));
+    if (m->slotted) {
+        if (mirror_wait((const uint64_t*)m->hslot.p, m->seq, 50.0, obj, idx)) return;
+        HCK(hipMemcpyAsync(m->hb, mads_best_ptr(m), 16, hipMemcpyDeviceToHost, m->s));
     }
     HCK(hipStreamSynchronize(m->s));
     *obj = m->hb[0];
@@ -1792,7 +1647,7 @@ int32_t mac_mads_poll(mac_mads* m, int32_t* done, double* best_obj, int64_t* bes
     }
     const auto tc = clk::now();
     if (Kc > 0) {
-        mads_wait_best(m, m->lo, best_obj, best_idx);
+        mads_wait_best(m, best_obj, best_idx);
     } else {
         *best_obj = INFINITY;
         *best_idx = -1;
@@ -1855,6 +1710,21 @@ int32_t mac_mads_result(mac_mads* m, double* x_out, mac_mads_stats* st)
     ABI_END
 }
 
+int32_t mac_mads_best_buffer(mac_mads* m, void* d_best16)
+{
+    if (!m) return fail(MAC_E_INVAL, "null stepper");
+    ABI_BEGIN
+    if (((uintptr_t)d_best16 & 7) != 0) return fail(MAC_E_INVAL, "d_best16 not 8-byte aligned");
+    m->ext_best = (double*)d_best16;
+    if (d_best16 && m->hi == m->lo) {   // an empty shard never polls: it offers {+inf, -1}
+        set_device(m->ctx);
+        const double none[2] = {INFINITY, __builtin_bit_cast(double, (int64_t)-1)};
+        HCK(hipMemcpy(d_best16, none, 16, hipMemcpyHostToDevice));
+    }
+    return MAC_OK;
+    ABI_END
+}
+
 void mac_mads_destroy(mac_mads* m)
 {
     if (!m) return;
@@ -1888,10 +1758,84 @@ int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const doub
     ABI_END
 }
 
+// The single-candidate closure (k_closure.h): the candidate through the lane's pinned staging, one
+// kernel, the area from the lane's mapped slot (no copy back, no stream synchronisation). AUTO /
+// TILED walks, N <= kClosureMaxN; otherwise (or if the slot has not landed within 2 ms: a failed
+// launch) the batch chain / a stream synchronisation report it.
+static int32_t closure_eval(mac_ctx* ctx, const double* circles, int64_t three_n, double* area_out,
+                            bool* handled)
+{
+    *handled = false;
+    int32_t rc = check_common(ctx, three_n, 1);
+    if (rc) return rc;
+    if (!circles) return fail(MAC_E_INVAL, "null circles");
+    const int N = (int)(three_n / 3);
+    if (ctx->algo != MAC_ALGO_AUTO && ctx->algo != MAC_ALGO_TILED) return MAC_OK;
+    if (N > kClosureMaxN) return MAC_OK;
+    *handled = true;
+    if (N == 0 || ctx->M == 0) {
+        *area_out = 0.0;
+        return MAC_OK;
+    }
+    set_device(ctx);
+    LaneGuard lg(ctx);
+    Lane* L = lg.lane;
+    hipStream_t s = L->stream;
+    const size_t in_bytes = sizeof(double) * (size_t)three_n;
+    L->h_io.reserve(std::max<size_t>(in_bytes, 64));
+    std::memcpy(L->h_io.p, circles, in_bytes);
+    L->cands.reserve(in_bytes);
+    L->area.reserve(sizeof(double));
+    L->cpart.reserve(sizeof(unsigned long long) * (size_t)N);
+    if (L->carrive.grow(sizeof(unsigned)))   // zero once; the last block of each launch resets it
+        HCK(hipMemsetAsync(L->carrive.p, 0, L->carrive.cap, s));
+    if (!L->h_cl.p) {
+        L->h_cl.reserve(64, hipHostMallocMapped | hipHostMallocCoherent);
+        std::memset(L->h_cl.p, 0, 64);
+        void* dp = nullptr;
+        HCK(hipHostGetDevicePointer(&dp, L->h_cl.p, 0));
+        L->d_cl = (uint64_t*)dp;
+    }
+    const uint64_t seq = ++L->cl_seq;
+    HCK(hipMemcpyAsync(L->cands.p, L->h_io.p, in_bytes, hipMemcpyHostToDevice, s));
+    int64_t ts_a = -1;
+    uint64_t* ts = nullptr;
+    if (ctx->profile) {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        if (ctx->stamp_used + N <= ctx->stamp_cap) {
+            ts_a = ctx->stamp_used;
+            ctx->stamp_used += N;
+            ts = ctx->stamps.as<uint64_t>() + 2 * ts_a;
+        }
+    }
+    const ClosureOut co{L->cpart.as<unsigned long long>(), L->carrive.as<unsigned>(),
+                        L->area.as<double>(), L->d_cl, seq};
+    hipLaunchKernelGGL(closure_kernel, dim3((unsigned)N), dim3(kBlock), (uint32_t)closure_lds_bytes(N), s,
+                       ts, L->cands.as<double>(), N, ctx->grid, ctx->xys.as<double2>(),
+                       ctx->ws.as<double>(), ctx->off.as<int32_t>(), ctx->w_uniform ? 1 : 0, ctx->w0, co);
+    HCK(hipGetLastError());
+    if (ts) {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        ctx->prof.push_back({ts_a, N, -1, 0, 1, nullptr, MAC_ALGO_TILED});
+    }
+    double a = 0.0;
+    int64_t unused = 0;
+    if (!mirror_wait((const uint64_t*)L->h_cl.p, seq, 2.0, &a, &unused)) {
+        HCK(hipStreamSynchronize(s));
+        if (!mirror_read((const uint64_t*)L->h_cl.p, seq, &a, &unused))
+            HCK(hipMemcpy(&a, L->area.p, sizeof(double), hipMemcpyDeviceToHost));
+    }
+    *area_out = a;
+    return MAC_OK;
+}
+
 int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, double* area_out)
 {
     ABI_BEGIN
     if (!area_out) return fail(MAC_E_INVAL, "null area_out");
+    bool handled = false;
+    const int32_t rc = closure_eval(ctx, circles, three_n, area_out, &handled);
+    if (rc || handled) return rc;
     return host_eval<double>(ctx, circles, three_n, 1, nullptr, 0.0, nullptr, nullptr, 1.0, area_out,
                      nullptr, nullptr, nullptr);
     ABI_END
@@ -2018,7 +1962,8 @@ static int32_t poll_best_dev(mac_ctx* ctx, const T* d_cands_in, int64_t three_n,
     if (K == 0) {
         {
             std::lock_guard<std::mutex> lk(ctx->mu);
-            ctx->mirror_for = nullptr;
+            for (int q = 0; q < mac_ctx::kMirrorSlots; ++q)
+                if (ctx->mirror_key[q] == d_best) ctx->mirror_key[q] = nullptr;   // fetch: copy
         }
         double hb[2] = {INFINITY, __builtin_bit_cast(double, (int64_t)-1)};
         L->best.reserve(16);
@@ -2035,31 +1980,32 @@ static int32_t poll_best_dev(mac_ctx* ctx, const T* d_cands_in, int64_t three_n,
         L->obj.reserve(sizeof(double) * K);
         d_o = L->obj.as<double>();
     }
-    double* d_mirror = nullptr;
+    uint64_t* d_mirror = nullptr;
     uint64_t seq = 0;
     {
+        // d_best's result slot: its own, else the least recently used one (a fetch still waiting
+        // on a reassigned slot sees another seq and falls back to the stream + copy)
         std::lock_guard<std::mutex> lk(ctx->mu);
         if (!ctx->d_mirror) {
-            ctx->h_best.reserve(64, hipHostMallocMapped | hipHostMallocCoherent);
-            std::memset(ctx->h_best.p, 0, 64);
+            const size_t b = sizeof(uint64_t) * 4 * mac_ctx::kMirrorSlots;
+            ctx->h_mirror.reserve(b, hipHostMallocMapped | hipHostMallocCoherent);
+            std::memset(ctx->h_mirror.p, 0, b);
             void* dp = nullptr;
-            HCK(hipHostGetDevicePointer(&dp, ctx->h_best.p, 0));
-            ctx->d_mirror = (double*)dp;
+            HCK(hipHostGetDevicePointer(&dp, ctx->h_mirror.p, 0));
+            ctx->d_mirror = (uint64_t*)dp;
         }
-        if (!ctx->d_blk) {
-            ctx->h_blk.reserve(sizeof(uint64_t) * 4 * kFinMaxBlk, hipHostMallocMapped | hipHostMallocCoherent);
-            std::memset(ctx->h_blk.p, 0, sizeof(uint64_t) * 4 * kFinMaxBlk);
-            void* dp = nullptr;
-            HCK(hipHostGetDevicePointer(&dp, ctx->h_blk.p, 0));
-            ctx->d_blk = (uint64_t*)dp;
+        int q = 0;
+        for (int j = 0; j < mac_ctx::kMirrorSlots; ++j) {
+            if (ctx->mirror_key[j] == d_best) {
+                q = j;
+                break;
+            }
+            if (ctx->mirror_used[j] < ctx->mirror_used[q]) q = j;
         }
-        d_mirror = ctx->d_mirror;
-        seq = ++ctx->mirror_seq;
-        ctx->mirror_for = d_best;
-        // finalize's grid (enqueue_eval): its blocks mirror their minima when it fits h_blk
-        const int nfin = 8 * (int)((K + 8 * kFinC - 1) / (8 * kFinC));
-        ctx->mirror_nblk = nfin <= kFinMaxBlk && !use_fused(ctx, N, K) ? nfin : 0;
-        ctx->mirror_base = idx_base;
+        ctx->mirror_key[q] = d_best;
+        ctx->mirror_used[q] = ++ctx->mirror_clock;
+        seq = ctx->mirror_want[q] = ++ctx->mirror_seq;
+        d_mirror = ctx->d_mirror + 4 * q;
     }
     enqueue_eval(ctx, L, s, matrix_src(d_cands, N), N, (int)K, use_tiled(ctx, N, nullptr, three_n), d_rmax,
                  penalty, d_prev, d_dlimT, d_dlim, tan_half_fov, nullptr, d_o, (double*)d_best, idx_base,
@@ -2099,56 +2045,31 @@ int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* b
     if (!d_best) return fail(MAC_E_INVAL, "null d_best");
     set_device(ctx);
     hipStream_t s = stream ? (hipStream_t)stream : ctx->dev_stream;
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    const double* hb = (const double*)ctx->h_best.p;
-    if (ctx->mirror_for == d_best && hb) {
-        // the latest device poll on d_best mirrors its result: spin on its sequence number (the
-        // poll takes ~0.1 ms), and after 2 ms wait for the stream instead (which also reports a
-        // failed launch)
-        const uint64_t want = ctx->mirror_seq;
-        if (ctx->mirror_nblk > 0) {
-            // every finalize block's minimum, reduced here (lexicographic (obj, index), as the
-            // device's last block does) as soon as the last one lands
-            const uint64_t* hk = (const uint64_t*)ctx->h_blk.p;
-            const auto t0 = std::chrono::steady_clock::now();
-            int b = 0;
-            for (int spin = 0; b < ctx->mirror_nblk; ++spin) {
-                while (b < ctx->mirror_nblk && __atomic_load_n(hk + 4 * b + 2, __ATOMIC_ACQUIRE) == want) ++b;
-                if (b < ctx->mirror_nblk && (spin & 1023) == 1023 &&
-                    std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2))
-                    break;   // slow or failed: the single-word mirror / the stream below
-            }
-            if (b == ctx->mirror_nblk) {
-                double bv = INFINITY;
-                int64_t bi = -1;
-                for (int q = 0; q < ctx->mirror_nblk; ++q) {
-                    const double v = __builtin_bit_cast(double, hk[4 * q]);
-                    const int64_t i = (int64_t)hk[4 * q + 1];
-                    if (i >= 0 && (bi < 0 || v < bv || (v == bv && i < bi))) {
-                        bv = v;
-                        bi = i;
-                    }
-                }
-                if (best_obj) *best_obj = bi >= 0 ? bv : INFINITY;
-                if (best_idx) *best_idx = bi >= 0 ? ctx->mirror_base + bi : -1;
-                return MAC_OK;
-            }
-        }
-        const uint64_t* flag = (const uint64_t*)(hb + 2);
-        const auto t0 = std::chrono::steady_clock::now();
-        bool ready = false;
-        for (int spin = 0; !ready; ++spin) {
-            ready = __atomic_load_n(flag, __ATOMIC_ACQUIRE) == want;
-            if (!ready && (spin & 1023) == 1023 &&
-                std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
-                HCK(hipStreamSynchronize(s));
-                ready = __atomic_load_n(flag, __ATOMIC_ACQUIRE) == want;
+    const uint64_t* slot = nullptr;
+    uint64_t want = 0;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);   // (released before any wait)
+        for (int q = 0; q < mac_ctx::kMirrorSlots; ++q)
+            if (ctx->mirror_key[q] == d_best && ctx->h_mirror.p) {
+                slot = (const uint64_t*)ctx->h_mirror.p + 4 * q;
+                want = ctx->mirror_want[q];
                 break;
             }
+    }
+    if (slot) {
+        // the latest device poll on d_best writes its result into this slot (the poll takes
+        // ~0.1 ms); after 2 ms wait for the stream (which also reports a failed launch), then
+        // read the slot once more, else copy d_best
+        double o = 0.0;
+        int64_t i = -1;
+        bool ok = mirror_wait(slot, want, 2.0, &o, &i);
+        if (!ok) {
+            HCK(hipStreamSynchronize(s));
+            ok = mirror_read(slot, want, &o, &i);
         }
-        if (ready) {
-            if (best_obj) *best_obj = hb[0];
-            if (best_idx) *best_idx = __builtin_bit_cast(int64_t, hb[1]);
+        if (ok) {
+            if (best_obj) *best_obj = o;
+            if (best_idx) *best_idx = i;
             return MAC_OK;
         }
     }

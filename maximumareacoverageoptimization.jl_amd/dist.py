@@ -64,6 +64,52 @@ def gather_best(best16, group=None):
     return reduce_best(objs, idxs)
 
 
+class DeviceGather:
+    """The per-iteration exchange of the sharded MADS loop without per-iteration allocations:
+    on a GPU backend (RCCL) the stepper's polls write their 16-B shard best straight into a
+    persistent device buffer (mac_mads_best_buffer, bound by ``mads_loop``) that the all-gather
+    reads, and one pinned host read of the world x 16 B result follows; on gloo (CPU rehearsal)
+    the host (obj, idx) goes into a persistent CPU record. ``seconds`` / ``calls``: time spent
+    here (the loop's host overhead beside the stepper's own, mac_mads_stats)."""
+
+    def __init__(self, device="cpu", group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.device = torch.device(device)
+        self.on_device = self.device.type == "cuda"
+        self.best = torch.zeros(2, dtype=torch.float64, device=self.device)
+        self.out = torch.empty((self.world, 2), dtype=torch.float64, device=self.device)
+        self.host = (torch.empty((self.world, 2), dtype=torch.float64, pin_memory=True)
+                     if self.on_device else self.out)
+        self.seconds = 0.0
+        self.calls = 0
+
+    def bind(self, stepper) -> None:
+        if self.on_device:
+            stepper.best_buffer(self.best)
+
+    def __call__(self, obj, idx):
+        import time
+        import torch
+        import torch.distributed as dist
+
+        t0 = time.perf_counter()
+        if not self.on_device:
+            self.best[0] = float(obj)
+            self.best.view(torch.int64)[1] = int(idx)
+        dist.all_gather_into_tensor(self.out, self.best.reshape(1, 2), group=self.group)
+        if self.on_device:
+            self.host.copy_(self.out)   # (synchronous: the one host read per iteration)
+        h = self.host
+        r = reduce_best(h[:, 0].numpy(), h.view(torch.int64)[:, 1].numpy())
+        self.seconds += time.perf_counter() - t0
+        self.calls += 1
+        return r
+
+
 def pack_best(obj: float, idx: int, device="cpu"):
     """Host-side constructor of the 16-byte record (for tests and CPU ranks)."""
     import torch
@@ -76,22 +122,21 @@ def pack_best(obj: float, idx: int, device="cpu"):
 
 def make_gather(device="cpu", group=None):
     """(obj, idx) -> the lexicographic minimum over all ranks' (obj, idx): one 16-byte all_gather
-    per call (RCCL for a device tensor, gloo for a CPU one). Identity for a single process."""
+    per call into persistent buffers (DeviceGather: straight from the stepper's device buffer
+    for a GPU device, a CPU record for gloo). Identity for a single process."""
     import torch.distributed as dist
 
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return lambda obj, idx: (obj, idx)
-
-    def gather(obj, idx):
-        return gather_best(pack_best(obj, idx, device), group)
-
-    return gather
+    return DeviceGather(device, group)
 
 
 def mads_loop(stepper, gather=None):
     """The sharded MADS loop's host side (mac_mads_poll / mac_mads_update, include/maxcover.h):
     per iteration the stepper polls its shard, ``gather`` combines the ranks' local bests and
     every rank applies the same global best. Returns stepper.result()."""
+    if gather is not None and hasattr(gather, "bind"):
+        gather.bind(stepper)
     while True:
         done, obj, idx = stepper.poll()
         if done:

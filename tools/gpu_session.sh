@@ -33,6 +33,8 @@ for s in $STEPS; do
         run pytest_gpu 600 python -u -m pytest tests -m gpu -x -v -rfE -p no:cacheprovider --timeout 120 --timeout-method thread ; rc=$? ;;
     smoke)
         run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ; rc=$? ;;
+    benchq)
+        run benchq 300 python bench.py --no-cpu ; rc=$? ;;
     bench)
         run bench 400 python bench.py ; rc=$?
         grep '^{' gpurun_out/bench.log > gpurun_out/bench_${TAG}.json ;;
@@ -45,12 +47,6 @@ for s in $STEPS; do
         make -s -C maximumareacoverageoptimization.jl_amd/csrc diag
         MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
             run diag 600 python tools/diag_poll.py ; rc=$? ;;
-    dfused)
-        make -s -C maximumareacoverageoptimization.jl_amd/csrc diag
-        MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
-            run dfused 300 python tools/diag_fused.py ; rc=$?
-        fatal $rc || MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
-            run dfusedc 300 python tools/diag_fused.py --disks clustered ; rc=$? ;;
     diag5)
         make -s -C maximumareacoverageoptimization.jl_amd/csrc diag
         MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
@@ -89,6 +85,10 @@ for s in $STEPS; do
             -- python3 bench.py --config 5 --steps 2 --warmup 1 --no-cpu ; rc=$?
         fatal $rc || run profc 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profc -o run \
             -- python3 bench.py --disks clustered --steps 10 --warmup 2 --no-cpu --no-extras ; rc=$? ;;
+    cprof)   # the single-candidate closure path: latency + kernel stats
+        rm -rf gpurun_out/cprof
+        run cprof 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/cprof -o run \
+            -- python3 tools/closure_prof.py ; rc=$? ;;
     bench2)
         run bench2 600 python bench.py --config 2 --no-cpu ; rc=$? ;;
     prof)
@@ -105,7 +105,7 @@ for s in $STEPS; do
                 -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-extras ; rc=$?
         fi
         fatal $rc || python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write --config 4 \
-            --chain 'mac::cands_keys_kernel;mac::disk_index_kernel<true, 3>;mac::walk_setup_kernel;mac::coverage_poll_kernel;mac::finalize_kernel' \
+            --chain 'mac::column_pass_kernel<true>;mac::disk_index_kernel<true, 3>;mac::walk_setup_kernel;mac::coverage_poll_kernel;mac::finalize_kernel' \
             --out gpurun_out/pmc_traffic_config4.json ;;
     *) echo "unknown step $s"; rc=0 ;;
     esac
