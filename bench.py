@@ -546,7 +546,7 @@ def main():
                 "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "traffic": traffic,
-                "kernel": (f"poll chain (column_pass, disk_index, walk_setup, coverage_{k_walk}, "
+                "kernel": (f"poll chain (prep, disk_index, walk_setup, coverage_{k_walk}, "
                            f"finalize + argmin); dominant kernel coverage_{k_walk}_kernel"),
                 "chain_ms": chain_ms,
                 "avg_launch_ms": avg_launch_ms,

@@ -101,6 +101,28 @@ __device__ __forceinline__ bool disk_span(const DiskRec& d, const Grid& g, int4&
 }
 
 
+__device__ __forceinline__ bool box_overlap(const int4& a, const int4& b)
+{
+    return a.x <= a.y && a.x <= b.y && b.x <= a.y && a.z <= b.w && b.z <= a.w;
+}
+
+__device__ __forceinline__ bool box_has(const int4& b, int tx, int ty)
+{
+    return b.x <= tx && tx <= b.y && b.z <= ty && ty <= b.w;
+}
+
+// tile span of disk (x, y, r): the same decision as disk_span(make_disk(x, y, r)) without the
+// threshold (T(r) >= 0 exactly when r > 0)
+__device__ __forceinline__ bool span_of(double x, double y, double r, const Grid& g, int4& sp)
+{
+    int x0, x1, y0, y1;
+    if (!(r > 0.0)) return false;
+    if (!tile_span(x, r, g.gx0, g.invS, g.nTx, x0, x1)) return false;
+    if (!tile_span(y, r, g.gy0, g.invS, g.nTy, y0, y1)) return false;
+    sp = make_int4(x0, x1, y0, y1);
+    return true;
+}
+
 // ------------------------------------------------------------------ in-kernel launch timing
 // Profiling only (ts == null otherwise): workgroup b writes ts[2b] = its start and ts[2b+1] = the
 // end of its last wave, in s_memrealtime ticks (the constant 100 MHz clock, 10 ns). The host takes

@@ -160,20 +160,31 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
     const int G = poll ? n_poll : n_other;
     // the candidate's penalty, loaded with the first batch of rows (one round trip fewer)
     const double vpk = (vp && sg == 0 && k < K) ? vp[k] : 0.0;
-    if (counts && poll && spart) {  // equal weights: integer rows, exact in any order
+    if (counts && poll && spart && map) {  // equal weights: integer rows, exact in any order
         const unsigned* const crow = reinterpret_cast<const unsigned*>(partial);
         const unsigned* const srow = reinterpret_cast<const unsigned*>(spart);
         __shared__ uint64_t ired[kFinThreads / kFinC][kFinC];
         uint64_t a = 0;
         if (k < K) {
+            // per row: the count at candidate k's position (the poll walk writes one per
+            // position, the map gives candidate k's), plus its shared-entry count when the disk
+            // has neighbours; the two dependent load pairs run side by side
             constexpr int B = 8;
             for (int g = sg; g < G; g += B * SG) {
                 unsigned v[B], sv[B];
+                int pos[B];
+                bool sh[B];
 #pragma unroll
                 for (int b = 0; b < B; ++b) {
                     const int gb = g + b * SG;
-                    v[b] = gb < G ? crow[(int64_t)gb * K + k] : 0u;
-                    sv[b] = gb < G && ncount[gb] > 0 ? srow[(int64_t)gb * K + k] : 0u;
+                    pos[b] = gb < G ? map[(int64_t)gb * K + k] : -1;
+                    sh[b] = gb < G && ncount[gb] > 0;
+                }
+#pragma unroll
+                for (int b = 0; b < B; ++b) {
+                    const int64_t rb = (int64_t)(g + b * SG) * K;
+                    v[b] = pos[b] >= 0 ? crow[rb + pos[b]] : 0u;
+                    sv[b] = sh[b] ? srow[rb + k] : 0u;
                 }
 #pragma unroll
                 for (int b = 0; b < B; ++b) a += (uint64_t)v[b] + sv[b];

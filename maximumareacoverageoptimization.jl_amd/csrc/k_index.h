@@ -14,8 +14,10 @@
 // disk_index_kernel reads the K candidates' (x_i, y_i, r_i) once, straight from the candidate
 // source (the matrix's fp32 keys, or the LTMADS generator). It numbers the distinct disks in an
 // LDS hash table (exact keys, see "Keys" below) and writes per distinct disk u the record
-// urec[i*K + u], plus, for every candidate, the map umap[i*K + k] = u, and the count ucount[i]. It also writes disk i's region (the union of its tile
-// spans over the K candidates) and the two walk costs (K * |region|, sum of span areas).
+// urec[i*K + u], plus, for every candidate, the map umap[i*K + k] = u, and the count ucount[i].
+// Disk i's region (the union of its tile spans over the K candidates) and its walk costs
+// (K * |region|, the summed span areas) are reduced here from the prep launch's per-workgroup
+// partials (k_prep.h), while the keys load; its row descriptors are in flight during the hashing.
 // Consumers read disk i of candidate k as urec[i*K + umap[i*K + k]]: the result is bit-identical
 // to per-candidate records (same inputs, same arithmetic), and every candidate is still
 // evaluated. Polls larger than kIndexMaxK + 1 use the identity map (one position per candidate).
@@ -65,27 +67,17 @@ __device__ __forceinline__ uint32_t key_hash(uint32_t a, uint32_t b, uint32_t c)
     return (uint32_t)(z ^ (z >> 32));
 }
 
-// tile span of disk (x, y, r): the same decision as disk_span(make_disk(x, y, r)) without the
-// threshold (T(r) >= 0 exactly when r > 0)
-__device__ __forceinline__ bool span_of(double x, double y, double r, const Grid& g, int4& sp)
-{
-    int x0, x1, y0, y1;
-    if (!(r > 0.0)) return false;
-    if (!tile_span(x, r, g.gx0, g.invS, g.nTx, x0, x1)) return false;
-    if (!tile_span(y, r, g.gy0, g.invS, g.nTy, y0, y1)) return false;
-    sp = make_int4(x0, x1, y0, y1);
-    return true;
-}
-
 constexpr int kRowInfo = 32;   // region rows described per disk (larger regions: walks read off)
 
 struct IndexOut {
     DiskRec* urec;
     int* umap;
     int* ucount;
-    int4* region;
-    double2* cost;
-    int* dcount;     // the poll walk's counters (k_common.h kDc*), cleared here
+    int4* region;           // disk i's region (written)
+    double2* cost;          // disk i's walk costs {K * |region|, summed span areas} (written)
+    int* dcount;            // the poll walk's counters (k_common.h kDc*), cleared here
+    const int4* prec;       // the prep launch's records [nchain][N] (k_prep.h)
+    int nchain;
     // poll walk inputs (null: not needed): per position the scaled-filter constants (k_lane.h)
     // {S*2cu, S*2cv, S*(T - C), -S} and X' (-1: inert), relative to the region centre; per disk
     // kRowInfo + 1 row descriptors of its region {first entry of the row's run, entries before
@@ -112,8 +104,9 @@ __device__ __forceinline__ float key_of(double v, double b, bool& ok)
 // only slower walks). Each thread holds its kIdxPer candidates' doubles in registers through
 // every phase, and the LDS holds only the fp32 keys, the table and the owners (~60 KB), so two
 // workgroups fit a CU and the whole index runs in one round at N = 512.
-// kKeys: a candidate matrix, whose fp32 keys and exactness flags cands_keys_kernel wrote
-// (src.keysT, src.kbad; exact doubles from src.cands); else the generator (src.get), keyed here.
+// kKeys: a candidate matrix, whose fp32 keys and exactness flags the prep launch wrote
+// (src.keysT, the records' flags; exact doubles from src.cands); else the generator (src.get),
+// keyed here.
 template <bool kKeys, int kPer>
 __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPer <= 3 ? 8 : 4))) void disk_index_kernel(
     uint64_t* ts, CandSrc src, int N, int K, Grid g, int dedup, IndexOut o)
@@ -128,11 +121,14 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
     __shared__ uint16_t owner_of[kIndexMaxK + 1];
     __shared__ int ucnt;
     __shared__ int sred[4][kIdxWaves];
-    __shared__ double dred[kIdxWaves];
+    __shared__ float fred[kIdxWaves];
 
     const int per_xcd = (N + 7) / 8;
     const int i = (int)(blockIdx.x % 8) * per_xcd + (int)(blockIdx.x / 8);
-    if (i >= N) return;                                   // uniform
+    if (i >= N) {   // uniform
+        ts_end(ts);
+        return;
+    }
     MAC_IDX_STAMP(0);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         for (int q = 0; q < 4; ++q) o.dcount[q] = 0;   // the poll walk's counters (k_common.h)
@@ -143,16 +139,41 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
     // takes k = kIndexMaxK (a full MADS poll is 2n + 1 = kIndexMaxK + 1 candidates at most here)
     const bool fits = dedup && K > 0 && K <= kIndexMaxK + 1;
 
-    int4 R = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
-    double span_area = 0.0;
-    auto add_span = [&](double x, double y, double r) {
-        int4 sp;
-        if (span_of(x, y, r, g, sp)) {
-            R.x = min(R.x, sp.x);
-            R.y = max(R.y, sp.y);
-            R.z = min(R.z, sp.z);
-            R.w = max(R.w, sp.w);
-            span_area += (double)(sp.y - sp.x + 1) * (double)(sp.w - sp.z + 1);
+    // disk i's region, costs and key flag from the prep launch's records (k_prep.h): loaded
+    // with the keys, reduced per wave into sred / fred (published by the keys phase's barrier),
+    // then by every thread
+    uint32_t ax = 0xFFFF, bx_ = 0, ay = 0xFFFF, by_ = 0;
+    float ps = 0.0f;
+    bool pbad = false;
+    auto load_partials = [&]() {
+        for (int q = tid; q < o.nchain; q += kIdxThreads) {
+            const int4 r = o.prec[(int64_t)q * N + i];
+            ax = min(ax, (uint32_t)r.x & 0xFFFFu);
+            bx_ = max(bx_, (uint32_t)r.x >> 16);
+            ay = min(ay, (uint32_t)r.y & 0xFFFFu);
+            by_ = max(by_, (uint32_t)r.y >> 16);
+            ps += __builtin_bit_cast(float, r.z);
+            pbad |= r.w != 0;
+        }
+    };
+    auto publish_partials = [&]() {
+        int4 PR;
+        range_unpack(ax, bx_, range_shift(g.nTx), g.nTx, PR.x, PR.y);
+        range_unpack(ay, by_, range_shift(g.nTy), g.nTy, PR.z, PR.w);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            PR.x = min(PR.x, __shfl_xor(PR.x, off, kWave));
+            PR.y = max(PR.y, __shfl_xor(PR.y, off, kWave));
+            PR.z = min(PR.z, __shfl_xor(PR.z, off, kWave));
+            PR.w = max(PR.w, __shfl_xor(PR.w, off, kWave));
+            ps += __shfl_xor(ps, off, kWave);   // (the same butterfly in every lane: fixed order)
+        }
+        if (lane == 0) {
+            sred[0][wid] = PR.x;
+            sred[1][wid] = PR.y;
+            sred[2][wid] = PR.z;
+            sred[3][wid] = PR.w;
+            fred[wid] = ps;
         }
     };
     auto get3 = [&](int k, double& x, double& y, double& r) {
@@ -186,11 +207,8 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
             qy[j] = fy[k];
             qr[j] = fr[k];
         }
-        bool bad = false;
-        for (int q = tid; q < 3 * src.nkt; q += kIdxThreads) {
-            const int a = q / src.nkt;
-            bad |= src.kbad[(int64_t)(q - a * src.nkt) * 3 * N + a * N + i] != 0;   // [block][3N]
-        }
+        load_partials();
+        const bool bad = pbad;   // a key of disk i is inexact (the records' flags)
         for (int q = tid; q < kIndexSlots; q += kIdxThreads) table[q] = -1;
         if (tid == 0) ucnt = 0;
 #pragma unroll
@@ -202,11 +220,13 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
                 kr[k] = qr[j];
             }
         }
+        publish_partials();
         hashed = !__syncthreads_or(bad);                  // (the barrier also publishes the keys)
     } else if (fits) {
         double cx[P], cy[P], cr[P];
         // ---- keys: every load in flight at once, then the fp32 offsets (exactness voted)
         get3(0, bx, by, br);
+        load_partials();
         const int n = 3 * N;
         if (!src.cands && 3 * n <= 2 * kIndexSlots && src.b <= 16384) {
             // the generator: candidates k and k + n are x + d and x - d of the same LTMADS entry
@@ -252,14 +272,45 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
                 kr[k] = key_of(cr[j], br, ok);
             }
         }
+        publish_partials();
         hashed = !__syncthreads_or(!ok);                  // (the barrier also publishes the keys)
+    } else {
+        load_partials();
+        publish_partials();
+        __syncthreads();
     }
     MAC_IDX_STAMP(1);
+    // ---- region and costs (every thread reduces the waves' partials: no further barrier); the
+    // region's row descriptors load now and are written after the map
+    int4 Rg = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
+    float psum = 0.0f;
+#pragma unroll
+    for (int q = 0; q < kIdxWaves; ++q) {
+        Rg.x = min(Rg.x, sred[0][q]);
+        Rg.y = max(Rg.y, sred[1][q]);
+        Rg.z = min(Rg.z, sred[2][q]);
+        Rg.w = max(Rg.w, sred[3][q]);
+        psum += fred[q];
+    }
+    if (Rg.x > Rg.y || Rg.z > Rg.w) Rg = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
+    const bool any = Rg.x <= Rg.y;
+    if (tid == 0) {
+        o.region[i] = Rg;
+        const double rc = any ? (double)(Rg.y - Rg.x + 1) * (double)(Rg.w - Rg.z + 1) : 0.0;
+        o.cost[i] = make_double2(rc * (double)K, (double)psum);
+    }
+    const bool want_rows = o.rows && any && Rg.w - Rg.z + 1 <= kRowInfo && tid < kWave;
+    const int nr = Rg.w - Rg.z + 1;
+    int rs0 = 0, rs1 = 0;
+    if (want_rows && tid < nr) {
+        const int64_t rb = (int64_t)(Rg.z + tid) * g.nTx;
+        rs0 = o.off[rb + Rg.x];
+        rs1 = o.off[rb + Rg.y + 1];
+    }
     if (!hashed) {  // identity: one position per candidate
         for (int k = tid; k < K; k += kIdxThreads) {
             double x, y, r;
             get3(k, x, y, r);
-            add_span(x, y, r);
             o.urec[row + k] = make_disk(x, y, r);
             o.umap[row + k] = k;
         }
@@ -303,64 +354,20 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
         }
         __syncthreads();
         MAC_IDX_STAMP(3);
-        // ---- per candidate: the map and the span (exact doubles rebuilt from the keys:
-        // base + offset)
+        // ---- per candidate: the map
 #pragma unroll
         for (int j = 0; j < P; ++j) {
             const int k = j < kIdxPer ? tid + j * kIdxThreads : (tid == 0 ? kIndexMaxK : K);
             if (k >= K) continue;
-            const int u = table[slot[j]] & ((1 << kIdBits) - 1);
-            const double x = bx + (double)kx[k], y = by + (double)ky[k], r = br + (double)kr[k];
-            o.umap[row + k] = u;
-            add_span(x, y, r);
+            o.umap[row + k] = table[slot[j]] & ((1 << kIdBits) - 1);
         }
         if (tid == 0) o.ucount[i] = ucnt;
     }
     MAC_IDX_STAMP(4);
-    // ---- region (block min / max) and costs (block sum: exact, integer-valued)
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        R.x = min(R.x, __shfl_xor(R.x, off, kWave));
-        R.y = max(R.y, __shfl_xor(R.y, off, kWave));
-        R.z = min(R.z, __shfl_xor(R.z, off, kWave));
-        R.w = max(R.w, __shfl_xor(R.w, off, kWave));
-    }
-    if (lane == 0) {
-        sred[0][wid] = R.x;
-        sred[1][wid] = R.y;
-        sred[2][wid] = R.z;
-        sred[3][wid] = R.w;
-    }
-    const double csum = block_sum_f64<kIdxWaves>(span_area, dred);   // (contains a barrier)
-    __shared__ int4 sRg;
-    if (tid == 0) {
-        int4 Rg = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
-        for (int q = 0; q < kIdxWaves; ++q) {
-            Rg.x = min(Rg.x, sred[0][q]);
-            Rg.y = max(Rg.y, sred[1][q]);
-            Rg.z = min(Rg.z, sred[2][q]);
-            Rg.w = max(Rg.w, sred[3][q]);
-        }
-        if (Rg.x > Rg.y || Rg.z > Rg.w) Rg = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
-        o.region[i] = Rg;
-        const double rc = Rg.x <= Rg.y ? (double)(Rg.y - Rg.x + 1) * (double)(Rg.w - Rg.z + 1) : 0.0;
-        o.cost[i] = make_double2(rc * (double)K, csum);
-        sRg = Rg;
-    }
-    __syncthreads();
-    const int4 Rg = sRg;
-    const bool any = Rg.x <= Rg.y;
-    // ---- the region's row descriptors (one wave)
-    if (o.rows && any && Rg.w - Rg.z + 1 <= kRowInfo && tid < kWave) {
-        const int nr = Rg.w - Rg.z + 1;
-        int s0 = 0, len = 0;
-        if (tid < nr) {
-            const int64_t rb = (int64_t)(Rg.z + tid) * g.nTx;
-            s0 = o.off[rb + Rg.x];
-            len = o.off[rb + Rg.y + 1] - s0;
-        }
+    if (want_rows) {   // (wave-uniform)
+        const int len = rs1 - rs0;
         const int incl = wave_incl_scan_i32(len, tid);
-        if (tid <= nr) o.rows[(int64_t)i * (kRowInfo + 1) + tid] = make_int2(s0, incl - len);
+        if (tid <= nr) o.rows[(int64_t)i * (kRowInfo + 1) + tid] = make_int2(rs0, incl - len);
     }
     // ---- per position: the record (hashed: from the owner's exact key, base + offset; identity:
     // written above) and the poll walk's lane constants relative to the region centre (the same

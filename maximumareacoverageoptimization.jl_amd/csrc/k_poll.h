@@ -153,9 +153,12 @@ __device__ __forceinline__ void coverage_poll_body(
             *((volatile int*)dc_out + 2) = sum_[0] > um ? sum_[0] : um;
         }
     }
-    // grid rows past the first: further walk workgroups of the same disks (position slices
-    // by, by + gridDim.y, ...); every other role runs in row 0 only
-    if (by > 0 && bx >= N) return;
+    // walk workgroups first: 8 * ceil(N/8) of them, workgroup b on disk (b % 8) * ceil(N/8) + b / 8
+    // (the disk index's map, k_index.h: a disk's index outputs are in its XCD's L2); then the
+    // shared-entry workgroups. Grid rows past the first: further walk workgroups of the same
+    // disks (position slices by, by + gridDim.y, ...); every other role runs in row 0 only
+    const int per_xcd = (N + 7) / 8, nwalk = 8 * per_xcd;
+    if (by > 0 && bx >= nwalk) return;
 
     // The shared-entry jobs (disk with neighbours x kShC-candidate slice, k_poll_shared.h) are
     // taken from a counter (the index kernel cleared it) by the shared workgroups and by every
@@ -192,8 +195,8 @@ __device__ __forceinline__ void coverage_poll_body(
         }
     };
     if (mode && *mode != kModePoll) return;
-    if (bx >= N) {  // then: the shared entries
-        shared_jobs(bx - N);
+    if (bx >= nwalk) {  // then: the shared entries
+        shared_jobs(bx - nwalk);
         MAC_DIAG_STAMP(diag_t0, 2, (uint64_t)(dcount[kDcBits] + dcount[kDcOther]));
         return;
     }
@@ -215,7 +218,8 @@ __device__ __forceinline__ void coverage_poll_body(
     __shared__ int rs[kPollRB], rpre[kPollRB + 1];
     __shared__ int4 nbox[kPollNbr];
 
-    const int i = bx;
+    const int i = (bx % 8) * per_xcd + bx / 8;
+    if (i >= N) break;   // uniform: a padding workgroup (takes shared jobs below)
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
     const int64_t row = (int64_t)i * K;
     // One memory round trip for everything indexed by disk i, loaded speculatively (bounds are
@@ -262,7 +266,7 @@ __device__ __forceinline__ void coverage_poll_body(
         if (by > 0)
             ;   // row 0 writes the zeros
         else if (counts)
-            for (int k = tid; k < K; k += kPollThreads) reinterpret_cast<unsigned*>(partial)[row + k] = 0u;
+            for (int p = tid; p < U; p += kPollThreads) reinterpret_cast<unsigned*>(partial)[row + p] = 0u;
         else
             for (int p = tid; p < U; p += kPollThreads) partial[row + p] = 0.0;
         break;
@@ -475,23 +479,16 @@ __device__ __forceinline__ void coverage_poll_body(
 #pragma unroll
         for (int u = 0; u < kPollSlots; ++u) red[wid][u * kWave + lane] = acc[u];
         __syncthreads();
+        // per position: its credit (equal weights: the covered-entry count, a uint32; finalize
+        // reads candidate k's through the map)
         for (int p = tid; p < ke - kb; p += kPollThreads) {
             double a = 0.0;
 #pragma unroll
             for (int q = 0; q < kPollWaves; ++q) a += red[q][p];
-            if (counts) red[0][p] = a;   // column p: this thread's alone
+            if (counts) reinterpret_cast<unsigned*>(partial)[row + kb + p] = (unsigned)a;
             else partial[row + kb + p] = a;
         }
         __syncthreads();
-        if (counts) {  // per candidate whose disk i sits at one of this slice's positions: its
-                       // covered-entry count, a uint32 row of partial (finalize adds the rows)
-            unsigned* const crow = reinterpret_cast<unsigned*>(partial) + row;
-            for (int k = tid; k < K; k += kPollThreads) {
-                const int u = umap[row + k] - kb;
-                if (u >= 0 && u < ke - kb) crow[k] = (unsigned)red[0][u];
-            }
-            __syncthreads();
-        }
         MAC_WALK_STAMP(5);
     }
     MAC_DIAG_STAMP(diag_t0, 3, ((uint64_t)nc << 40) | ((uint64_t)U << 20) | (uint64_t)diag_entries);

@@ -19,20 +19,10 @@
 
 namespace mac {
 
-__device__ __forceinline__ bool box_overlap(const int4& a, const int4& b)
-{
-    return a.x <= a.y && a.x <= b.y && b.x <= a.y && a.z <= b.w && b.z <= a.w;
-}
-
-__device__ __forceinline__ bool box_has(const int4& b, int tx, int ty)
-{
-    return b.x <= tx && tx <= b.y && b.z <= ty && ty <= b.w;
-}
-
 // Disk i's lower-index neighbours: the disks j < i whose region boxes overlap region i's (at
 // most kPollNbr kept in nbr[i*kPollNbr ...]; ncount[i] is the true count, > kPollNbr meaning
 // "overflowed"), their region boxes in nboxT. Disks with neighbours are appended to dlist (order irrelevant: each is processed
-// independently); *dcount must be zero on entry (the index kernel clears it).
+// independently); *dcount must be zero on entry (the disk index clears it).
 // A disk with neighbours goes to the bit-word kernel's list (front of dlist, k_bits.h) when its
 // list did not overflow and its region is at most 64 x 64 tiles; otherwise to the back of dlist
 // (the poll kernel's fp64 jobs).

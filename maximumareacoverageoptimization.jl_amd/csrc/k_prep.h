@@ -85,9 +85,7 @@ __host__ __device__ __forceinline__ double ltmads_entry(uint64_t state, int64_t 
 struct CandSrc {
     const double* cands;   // matrix source when non-null
     int ldc;
-    const float* keysT;    // matrix: fp32 keys, variable-major (cands_keys_kernel), when non-null
-    const int* kbad;       // matrix: per (column-pass block, variable) "a key is inexact" flags
-    int nkt;               // column-pass blocks (flags) per variable
+    const float* keysT;    // matrix: fp32 keys, variable-major (the prep launch), when non-null
     int ldk;               // keysT row pitch (keys_ld(K))
     const double* xinc;    // generator: incumbent (3N), row / column permutations (n each)
     const int* rp;
@@ -107,154 +105,234 @@ struct CandSrc {
     }
 };
 
-// ------------------------------------------------------------------ the column pass
-// The first launch of every evaluation: one 16-wave workgroup per kColC = 16 consecutive
-// candidates (columns of the 3N x K matrix as Julia hands it over, or of the LTMADS generator);
-// wave w owns candidate k0 + w. Per block of kColB UAVs, every lane issues all its loads at once
-// (x, y, r of UAVs l, l + 64, ...: contiguous 512-B segments of the column), while the workgroup
-// stages what every candidate shares in LDS: candidate 0's values (the key bases) and each
-// UAV's prev / r_max / cons3 threshold.
+// ------------------------------------------------------------------ the prep launch
+// The first launch of every evaluation: workgroup cw takes candidates [8cw, 8cw + 8), thread u
+// UAV u of each block of kPrepU UAVs, and reads that UAV's (x, y, r) of its 8 candidates — 24
+// coalesced loads, all in flight at once — from the 3N x K matrix as Julia hands it over (or the
+// LTMADS generator). The matrix is read once per evaluation, here; from those values:
 //   objective (vp != null): term_i = |R_i - rmax_i|, or -1 when UAV i's move fails cons3
-//     (pen_term's arithmetic). The wave folds its candidate's terms IN ORDER i = 0, 1, ..., N-1
-//     from 0.0, as src/TDM_STATIC_opt.jl:88-92 does (bit-exact): term i sits in lane i % 64, so
-//     the fold reads it with v_readlane (no LDS round trip per term) into one sequential chain
-//     of fp64 adds, identical in every lane. vp[k] = violation * penalty, or +inf when a term is
-//     negative (the extreme barrier of src/TDM_Constraints.jl:54-75);
-//   keys (kKeys, matrix source, for the disk index): the fp32 key fl32(v - v0) of every value
-//     (v0 = candidate 0's value), transposed through LDS into keysT[v*ldk + k] (64-B row
-//     segments), and kbad[blockIdx.x * 3N + v] = 1 when some key of variable v in this block
-//     does not reproduce v bit for bit (k_index.h "Keys": the disk then takes the identity map).
-// The penalty chain thereby costs no buffer (one term per disk and candidate was 12.6 MB written
-// and re-read at config 4) and no workgroups of the later launches.
-constexpr int kColC = 16;                         // candidates (waves) per workgroup
-constexpr int kColThreads = kColC * kWave;
-constexpr int kColJ = 8;                          // UAVs per lane per block
-constexpr int kColB = kColJ * kWave;              // UAVs per block
+//     (pen_term's arithmetic), into LDS; lane c of wave 0 folds candidate 8cw + c's terms IN
+//     ORDER i = 0, 1, ..., N-1 from 0.0, as src/TDM_STATIC_opt.jl:88-92 does (bit-exact): one
+//     lane per chain. vp[k] = violation * penalty, or +inf when a term is negative (the extreme
+//     barrier of src/TDM_Constraints.jl:54-75);
+//   poll walk (prec != null): one 16-B record per (workgroup, UAV), prec[cw*N + i] (a
+//     coalesced store): {x range, y range, span-area estimate, key flag}. The range is a tile box
+//     containing the tile span (predicate.h tile_span) of every one of the 8 disks,
+//     from min(c - r), max(c + r) and max(|c| + r) per axis: tile_span's rounding steps are
+//     monotone in those, so the box bounds each span from outside (a superset region only
+//     makes the walk stage or share more entries, never changes a result), packed as two
+//     16-bit tile numbers (range_pack); the estimate is the disks' span areas as (2r/S + 1)^2
+//     (the walk choice's cost). The disk index reduces disk i's records (k_index.h);
+//   keys (keysT != null, matrix sources): the fp32 key fl32(v - v0) of each value, v0 =
+//     candidate 0's, into keysT[v*ldk + k] (8 consecutive keys: two 16-B stores); the record's
+//     key flag is 1 when one of UAV i's 24 keys does not reproduce its double bit for bit
+//     (k_index.h "Keys": the disk then takes the identity map).
+constexpr int kPrepC = 8;        // candidates per workgroup
+constexpr int kPrepU = 512;      // UAVs per block = threads per workgroup
 
-__host__ __device__ inline int keys_ld(int K) { return (K + kColC - 1) / kColC * kColC; }
+// keysT row pitch: rows start on 128-B boundaries (and hold every workgroup's 8 keys)
+__host__ __device__ inline int keys_ld(int K) { return (K + 31) & ~31; }
 
-__device__ __forceinline__ double readlane_f64(double v, int l)
+struct PrepArgs {
+    CandSrc src;
+    int N, K;
+    PenArgs pa;
+    double penalty;
+    double* vp;                // per-candidate penalty (null: no objective)
+    int nchain;                // workgroups
+    int4* prec;                // [nchain][N] records (null: no poll walk)
+    Grid g;
+    float* keysT;              // keys (null: none), rows of pitch ldk
+    int ldk;
+};
+
+// the tile range [lo, hi] on one axis covering every span of disks with min(c - r) = a,
+// max(c + r) = b, max(|c| + r) = m (tile_span's steps, each monotone); false: empty
+__device__ __forceinline__ bool partial_range(double a, double b, double m, double g0, double invS,
+                                              int n, int& lo, int& hi)
 {
-    const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, l);
-    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), l);
-    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+    const double ulo = (a - g0) * invS;
+    const double uhi = (b - g0) * invS;
+    const double err = (m + __builtin_fabs(g0)) * invS * 1e-14 + 1e-9;
+    const double flo = __builtin_floor(ulo - err);
+    const double fhi = __builtin_floor(uhi + err);
+    if (!(flo == flo) || !(fhi == fhi)) { lo = 0; hi = n - 1; return true; }
+    if (fhi < 0.0 || flo > (double)(n - 1)) return false;
+    lo = flo < 0.0 ? 0 : (int)flo;
+    hi = fhi > (double)(n - 1) ? n - 1 : (int)fhi;
+    return true;
 }
 
-// kMat: the source is a matrix (src.cands; the generator path is compiled out), kKeys: write the
-// index's keys (matrix sources only).
-template <bool kMat, bool kKeys>
-__global__ __launch_bounds__(kColThreads) void column_pass_kernel(uint64_t* ts, CandSrc src, int N,
-                                                                  int K, PenArgs pa, double penalty,
-                                                                  double* __restrict__ vp,
-                                                                  float* __restrict__ keysT,
-                                                                  int* __restrict__ kbad)
+// A tile range [lo, hi] of an axis of n tiles as two 16-bit numbers lo >> s, hi >> s, with s the
+// least shift that fits n - 1 below 0xFFFF (0 for every grid of up to 65535 tiles a side);
+// unpacking rounds outwards (a superset); the empty range packs as {0xFFFF, 0}, the identity of
+// the (min, max) reduction.
+__host__ __device__ inline int range_shift(int n)
 {
-    ts_begin(ts);   // profiling only (the chain's first launch: k_common.h)
-    __shared__ double sb[3][kColB];             // candidate 0's values (keys)
-    __shared__ double su[5][kColB];             // prev x, y, z / tan, r_max, cons3 threshold
-    __shared__ float kt[kColB][kColC + 1];      // one variable block's keys: [UAV][candidate]
-    __shared__ int kfl[3][kColB];
-    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
-    const int k0 = blockIdx.x * kColC;
-    const int k = k0 + w;
-    const int kc = min(k, K - 1);
-    const int ldk = keys_ld(K);
-    const bool obj = vp != nullptr;
-    double acc = 0.0;
-    bool bad = false;
-    for (int ib = 0; ib < N; ib += kColB) {
-        const int nb = min(kColB, N - ib);
-        // this lane's values: UAV ib + lane + 64 j, variables x, y, r (all loads in flight)
-        double v[3][kColJ];
+    int s = 0;
+    while (((n - 1) >> s) > 0xFFFE) ++s;
+    return s;
+}
+__device__ __forceinline__ uint32_t range_pack(bool any, int lo, int hi, int s)
+{
+    return any ? (uint32_t)(lo >> s) | ((uint32_t)(hi >> s) << 16) : 0xFFFFu;
+}
+__device__ __forceinline__ void range_unpack(uint32_t lo16, uint32_t hi16, int s, int n, int& lo, int& hi)
+{
+    lo = (int)(lo16 << s);
+    hi = min((int)(((hi16 + 1) << s) - 1), n - 1);
+}
+
+#ifdef MAC_DIAG
+__device__ uint64_t g_diag_prep[64 * 16];   // diagnostic build only: workgroup phase stamps
+#define MAC_PREP_STAMP(q) if (threadIdx.x == 0 && cw < 64 && (q) < 16) g_diag_prep[16 * cw + (q)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define MAC_PREP_STAMP(q)
+#endif
+
+// A workgroup barrier for LDS only: global stores still in flight are not waited for
+// (__syncthreads would drain them first)
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <bool kMat>
+__device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
+{
+    __shared__ double term[kPrepC][kPrepU + 1];   // [candidate][UAV] (+1: lanes on distinct banks)
+    const int N = a.N, K = a.K;
+    const int u = threadIdx.x;
+    const int k0 = cw * kPrepC;
+    const bool obj = a.vp != nullptr;
+    const PenArgs& pa = a.pa;
+    MAC_PREP_STAMP(0);
+    double acc = 0.0, mn = 0.0;   // the chain, and its least term (< 0: a cons3 violation)
+    for (int ib = 0; ib < N; ib += kPrepU) {
+        const int nb = min(kPrepU, N - ib);
+        const int i = ib + u;
+        const bool iv = u < nb;
+        const int ii = min(i, N - 1);
+        double v[kPrepC][3];
 #pragma unroll
-        for (int a = 0; a < 3; ++a)
+        for (int c = 0; c < kPrepC; ++c) {
+            const int k = min(k0 + c, K - 1);
 #pragma unroll
-            for (int j = 0; j < kColJ; ++j) {
-                const int i = ib + min(lane + kWave * j, nb - 1);
-                v[a][j] = kMat ? src.cands[(int64_t)kc * src.ldc + a * N + i] : src.get(kc, a * N + i, N);
-            }
-        // what every candidate shares, staged once per workgroup
-        for (int q = tid; q < nb; q += kColThreads) {
-            const int i = ib + q;
-            if (kKeys) {
-#pragma unroll
-                for (int a = 0; a < 3; ++a) sb[a][q] = src.cands[a * N + i];
-#pragma unroll
-                for (int a = 0; a < 3; ++a) kfl[a][q] = 0;
-            }
-            if (obj) {
-                su[0][q] = pa.prev ? pa.prev[i] : 0.0;
-                su[1][q] = pa.prev ? pa.prev[N + i] : 0.0;
-                su[2][q] = pa.prev ? pa.prev[2 * N + i] / pa.tan_half_fov : 0.0;   // z1
-                su[3][q] = pa.rmax ? pa.rmax[i] : 0.0;
-                su[4][q] = pen_threshold(pa, i);
+            for (int q = 0; q < 3; ++q) {
+                if constexpr (kMat) v[c][q] = a.src.cands[(int64_t)k * a.src.ldc + q * N + ii];
+                else v[c][q] = a.src.get(k, q * N + ii, N);
             }
         }
-        __syncthreads();
-        if (obj) {
-            // the terms of this lane's UAVs (pen_term's operations in the same order), then the
-            // chain over the block in UAV order: term of UAV ib + 64 j + l is lane l's t[j]
-            double t[kColJ];
+        double base[3] = {0.0, 0.0, 0.0};
+        if (kMat && a.keysT) {
 #pragma unroll
-            for (int j = 0; j < kColJ; ++j) {
-                const int q = min(lane + kWave * j, nb - 1);
-                const double R2 = v[2][j];
-                double tt = pa.rmax ? __builtin_fabs(R2 - su[3][q]) : 0.0;
+            for (int q = 0; q < 3; ++q) base[q] = a.src.cands[q * N + ii];
+        }
+        if (obj) {
+            // pen_term (above), the same operations in the same order; the chains first, so
+            // that no store is in flight at the barrier
+            const double x1 = pa.prev ? pa.prev[ii] : 0.0, y1 = pa.prev ? pa.prev[N + ii] : 0.0;
+            const double z1 = pa.prev ? pa.prev[2 * N + ii] / pa.tan_half_fov : 0.0;
+            const double rm = pa.rmax ? pa.rmax[ii] : 0.0;
+            const double T3 = pen_threshold(pa, ii);
+#pragma unroll
+            for (int c = 0; c < kPrepC; ++c) {
+                const double R2 = v[c][2];
+                double t = pa.rmax ? __builtin_fabs(R2 - rm) : 0.0;
                 if (pa.prev) {
                     const double z2 = R2 / pa.tan_half_fov;
-                    const double ddx = su[0][q] - v[0][j], ddy = su[1][q] - v[1][j], ddz = su[2][q] - z2;
+                    const double ddx = x1 - v[c][0], ddy = y1 - v[c][1], ddz = z1 - z2;
                     const double sq = ddx * ddx + ddy * ddy + ddz * ddz;
-                    if (sq > su[4][q]) tt = -1.0;
+                    if (sq > T3) t = -1.0;
                 }
-                t[j] = tt;
-                bad |= __ballot(lane + kWave * j < nb && tt < 0.0) != 0;
+                term[c][u] = t;
             }
+            MAC_PREP_STAMP(1 + 3 * (ib / kPrepU));
+            lds_barrier();
+            if (u < kPrepC) {   // the chains, sequential in UAV order (register batches)
+                int q = 0;
+                for (; q + 16 <= nb; q += 16) {
+                    double t[16];
 #pragma unroll
-            for (int j = 0; j < kColJ; ++j) {
-                if (kWave * j >= nb) break;   // uniform
-                const int n = min(kWave, nb - kWave * j);
-                if (n == kWave) {
+                    for (int j = 0; j < 16; ++j) t[j] = term[u][q + j];
 #pragma unroll
-                    for (int l = 0; l < kWave; ++l) acc += readlane_f64(t[j], l);
-                } else {
-                    for (int l = 0; l < n; ++l) acc += readlane_f64(t[j], l);
+                    for (int j = 0; j < 16; ++j) {
+                        acc += t[j];
+                        mn = fmin(mn, t[j]);   // (a second, independent chain)
+                    }
                 }
-            }
-        }
-        if (kKeys) {
-            // per variable block: the keys through LDS, then 64-B row segments
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                bool ok = true;
-#pragma unroll
-                for (int j = 0; j < kColJ; ++j) {
-                    const int q = lane + kWave * j;
-                    if (q >= nb) break;
-                    const double b = sb[a][q];
-                    const float f = (float)(v[a][j] - b);
-                    const bool e = __builtin_bit_cast(uint64_t, b + (double)f) == __builtin_bit_cast(uint64_t, v[a][j]);
-                    if (!e && k < K) atomicOr(&kfl[a][q], 1);
-                    kt[q][w] = f;
+                for (; q < nb; ++q) {
+                    const double t = term[u][q];
+                    acc += t;
+                    mn = fmin(mn, t);
                 }
-                __syncthreads();
-                for (int q4 = tid; q4 < nb * (kColC / 4); q4 += kColThreads) {
-                    const int q = q4 / (kColC / 4), part = q4 % (kColC / 4);
-                    const float* s4 = &kt[q][4 * part];
-                    *reinterpret_cast<float4*>(keysT + ((int64_t)a * N + ib + q) * ldk + k0 + 4 * part) =
-                        make_float4(s4[0], s4[1], s4[2], s4[3]);
-                }
-                __syncthreads();
-                (void)ok;
-            }
-            for (int q = tid; q < 3 * nb; q += kColThreads) {
-                const int a = q / nb, qq = q - a * nb;
-                kbad[(int64_t)blockIdx.x * 3 * N + a * N + ib + qq] = kfl[a][qq];
             }
         }
-        __syncthreads();   // LDS reuse by the next block
+        MAC_PREP_STAMP(2 + 3 * (ib / kPrepU));
+        if (a.prec && iv) {
+            double xa = __builtin_inf(), xb = -__builtin_inf(), ya = __builtin_inf(), yb = -__builtin_inf();
+            double xm = 0.0, ym = 0.0, est = 0.0;
+            bool any = false;
+#pragma unroll
+            for (int c = 0; c < kPrepC; ++c) {
+                const double x = v[c][0], y = v[c][1], r = v[c][2];
+                // span_of's cases: r <= 0 or NaN, or a non-finite centre, covers nothing
+                if (k0 + c < K && r > 0.0 && __builtin_isfinite(x) && __builtin_isfinite(y)) {
+                    any = true;
+                    xa = fmin(xa, x - r);
+                    xb = fmax(xb, x + r);
+                    ya = fmin(ya, y - r);
+                    yb = fmax(yb, y + r);
+                    xm = fmax(xm, __builtin_fabs(x) + r);
+                    ym = fmax(ym, __builtin_fabs(y) + r);
+                    const double e = 2.0 * r * a.g.invS + 1.0;
+                    est += e * e;
+                }
+            }
+            int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
+            any = any && partial_range(xa, xb, xm, a.g.gx0, a.g.invS, a.g.nTx, x0, x1) &&
+                  partial_range(ya, yb, ym, a.g.gy0, a.g.invS, a.g.nTy, y0, y1);
+            bool kb = false;
+            if (kMat && a.keysT) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+#pragma unroll
+                    for (int c = 0; c < kPrepC; ++c) {
+                        const float f = (float)(v[c][q] - base[q]);
+                        kb |= __builtin_bit_cast(uint64_t, base[q] + (double)f) != __builtin_bit_cast(uint64_t, v[c][q]);
+                    }
+            }
+            a.prec[(int64_t)cw * N + i] =
+                make_int4((int)range_pack(any, x0, x1, range_shift(a.g.nTx)),
+                          (int)range_pack(any, y0, y1, range_shift(a.g.nTy)),
+                          __builtin_bit_cast(int, (float)est), kb ? 1 : 0);
+        }
+        if (kMat && a.keysT && iv) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                float f[kPrepC];
+#pragma unroll
+                for (int c = 0; c < kPrepC; ++c) f[c] = (float)(v[c][q] - base[q]);
+                float4* dst = reinterpret_cast<float4*>(a.keysT + (int64_t)(q * N + i) * a.ldk + k0);
+                dst[0] = make_float4(f[0], f[1], f[2], f[3]);
+                dst[1] = make_float4(f[4], f[5], f[6], f[7]);
+            }
+        }
+        MAC_PREP_STAMP(3 + 3 * (ib / kPrepU));
+        if (obj && ib + kPrepU < N) lds_barrier();   // the fold has read the terms
     }
-    if (obj && lane == 0 && k < K) vp[k] = bad ? __builtin_inf() : acc * penalty;
+    if (obj && u < kPrepC && k0 + u < K) a.vp[k0 + u] = mn < 0.0 ? __builtin_inf() : acc * a.penalty;
+}
+
+__global__ __launch_bounds__(kPrepU) void prep_kernel(uint64_t* ts, PrepArgs a)
+{
+    ts_begin(ts);   // profiling only (the chain's first launch: k_common.h)
+    // XCD-aware: workgroups b and b + 8 share an XCD (round-robin dispatch), so consecutive
+    // candidate groups — which fill the same lines of keysT and of the records — go to one XCD
+    const int per = (int)((gridDim.x + 7) / 8), b = (int)blockIdx.x;
+    const int cw = (int)(gridDim.x % 8) == 0 ? (b % 8) * per + b / 8 : b;
+    if (a.src.cands) prep_block<true>(a, cw);
+    else prep_block<false>(a, cw);
     ts_end(ts);
 }
 

@@ -263,4 +263,5 @@ __global__ __launch_bounds__(kBlock) void walk_setup_kernel(
     ts_end(ts);
 }
 
+
 }  // namespace mac

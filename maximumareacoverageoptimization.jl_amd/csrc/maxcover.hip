@@ -130,8 +130,8 @@ struct Lane {
     hipStream_t stream = nullptr;
     hipStream_t last = nullptr;   // stream of the most recent use
     hipEvent_t done = nullptr;
-    DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, cost, mode, nbr,
-        ncount, dlist, spart, vp, xinc, perm, ucount, umap, keysT, kbad, lane4, lanexp, rows, nboxT,
+    DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, mode, nbr,
+        ncount, dlist, spart, vp, xinc, perm, ucount, umap, keysT, lane4, lanexp, rows, nboxT,
         cnt, dlimraw, finblk, finarrive, c32, p32, qual;
     std::vector<double> h_dlim;
     PinnedBuf h_stage;                         // native MADS driver: best, permutations, incumbent
@@ -143,6 +143,7 @@ struct Lane {
     uint64_t* d_cl = nullptr;                  // ... its device address
     uint64_t cl_seq = 0;
     DevBuf cpart, carrive;                     // closure_kernel: per-disk credits, arrivals
+    DevBuf prec, cost;                         // prep launch: per-disk records; walk costs
     int um_hist[8] = {};                       // most distinct positions of a disk, last 8 polls
 };
 
@@ -507,27 +508,37 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
     };
 
     CandSrc isrc = src;
-    if (d_obj || want_keys) {
-        // the column pass (k_prep.h): penalty chains + cons3 into vp, and the index's keys
-        const int ncb = (K + kColC - 1) / kColC;
-        uint64_t* tsk = poll_possible ? take_ts(ncb, ts_c, ts_nc) : nullptr;
+    const int target = 8 * ctx->cus;
+    const int G = (int)std::max<int64_t>(
+        1, std::min<int64_t>((target + K - 1) / K, std::max(1, N / kWavesPerBlock)));
+    const int64_t units = (int64_t)K * G;
+    const int nchain = (K + kPrepC - 1) / kPrepC;
+    if ((d_obj || poll_possible) && K > 0) {
+        // the prep launch (k_prep.h): penalty chains + cons3 into vp, the poll walk's partial
+        // regions, and the index's fp32 keys
+        PrepArgs pr{};
+        pr.src = src;
+        pr.N = N;
+        pr.K = K;
+        pr.pa = pa;
+        pr.penalty = penalty;
+        pr.vp = d_vp;
+        pr.nchain = nchain;
+        pr.g = ctx->grid;
+        if (poll_possible) {
+            L->prec.reserve(sizeof(int4) * (size_t)nchain * N);
+            pr.prec = L->prec.as<int4>();
+        }
         if (want_keys) {
             const int ldk = keys_ld(K);
             L->keysT.reserve(sizeof(float) * (size_t)3 * N * ldk);
-            L->kbad.reserve(sizeof(int) * (size_t)3 * N * ncb);
-            hipLaunchKernelGGL((column_pass_kernel<true, true>), dim3(ncb), dim3(kColThreads), 0, s, tsk, src,
-                               N, K, pa, penalty, d_vp, L->keysT.as<float>(), L->kbad.as<int>());
-            isrc.keysT = L->keysT.as<float>();
-            isrc.kbad = L->kbad.as<int>();
-            isrc.nkt = ncb;
+            pr.keysT = L->keysT.as<float>();
+            pr.ldk = ldk;
+            isrc.keysT = pr.keysT;
             isrc.ldk = ldk;
-        } else if (src.cands) {
-            hipLaunchKernelGGL((column_pass_kernel<true, false>), dim3(ncb), dim3(kColThreads), 0, s, tsk,
-                               src, N, K, pa, penalty, d_vp, nullptr, nullptr);
-        } else {
-            hipLaunchKernelGGL((column_pass_kernel<false, false>), dim3(ncb), dim3(kColThreads), 0, s, tsk,
-                               src, N, K, pa, penalty, d_vp, nullptr, nullptr);
         }
+        uint64_t* tsk = poll_possible ? take_ts(nchain, ts_c, ts_nc) : nullptr;
+        hipLaunchKernelGGL(prep_kernel, dim3((unsigned)nchain), dim3(kPrepU), 0, s, tsk, pr);
         HCK(hipGetLastError());
     }
 
@@ -556,25 +567,20 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                            L->disks.as<DiskRec>(), N, K, chunk, L->partial.as<double>());
         HCK(hipGetLastError());
     } else {
-        // the disk index: distinct disks per UAV, their records / penalty terms, the map, and
-        // each disk's region and walk costs (k_index.h)
+        // the disk index: distinct disks per UAV, their records, the map and the poll walk's lane
+        // constants (k_index.h)
         L->disks.reserve(sizeof(DiskRec) * (size_t)N * K);
         L->umap.reserve(sizeof(int) * (size_t)N * K);
         L->ucount.reserve(sizeof(int) * (size_t)N);
-        L->region.reserve(sizeof(int4) * N);
-        L->cost.reserve(sizeof(double2) * N);
-        L->mode.reserve(8 * sizeof(int));  // [0] walk, [1..4] the poll walk's counters (k_common.h)
         if (poll_possible) {  // the poll walk's lane constants and row descriptors
             L->lane4.reserve(sizeof(float4) * (size_t)N * K);
             L->lanexp.reserve(sizeof(float) * (size_t)N * K);
             L->rows.reserve(sizeof(int2) * (size_t)N * (kRowInfo + 1));
         }
         counts = poll_possible && ctx->w_uniform ? 1 : 0;   // equal weights: the walks count
-        const IndexOut io{L->disks.as<DiskRec>(), L->umap.as<int>(), L->ucount.as<int>(),
-                          L->region.as<int4>(), L->cost.as<double2>(), L->mode.as<int>() + 1,
-                          poll_possible ? L->lane4.as<float4>() : nullptr,
-                          poll_possible ? L->lanexp.as<float>() : nullptr,
-                          poll_possible ? L->rows.as<int2>() : nullptr, ctx->off.as<int32_t>()};
+        n_other = G;
+        const DiskRec* d_urec = L->disks.as<DiskRec>();
+        const int* d_map = L->umap.as<int>();
         if (!poll_possible) {
             // the per-candidate walk alone (small batches, the single-candidate closure): the
             // identity map, one thread per (disk, candidate), no key pass
@@ -582,45 +588,48 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             hipLaunchKernelGGL(disk_index_identity_kernel, dim3(grid1d(nk, 256)), dim3(256), 0, s,
                                src, N, K, L->disks.as<DiskRec>(), L->umap.as<int>());
             HCK(hipGetLastError());
-        }
-        const unsigned nidx = 8 * ((N + 7) / 8);
-        uint64_t* tsi = (poll_possible && ts_c < 0) ? take_ts(nidx, ts_c, ts_nc) : nullptr;
-        const int dedup = iper ? 1 : 0;
-        if (!poll_possible)
-            ;   // indexed above
-        else if (isrc.keysT && iper == kIdxPerWide)
-            hipLaunchKernelGGL((disk_index_kernel<true, kIdxPerWide>), dim3(nidx), dim3(kIdxThreads), 0,
-                               s, tsi, isrc, N, K, ctx->grid, dedup, io);
-        else if (isrc.keysT)
-            hipLaunchKernelGGL((disk_index_kernel<true, kIdxPer>), dim3(nidx), dim3(kIdxThreads), 0, s,
-                               tsi, isrc, N, K, ctx->grid, dedup, io);
-        else if (iper == kIdxPerWide)
-            hipLaunchKernelGGL((disk_index_kernel<false, kIdxPerWide>), dim3(nidx), dim3(kIdxThreads), 0,
-                               s, tsi, isrc, N, K, ctx->grid, dedup, io);
-        else
-            hipLaunchKernelGGL((disk_index_kernel<false, kIdxPer>), dim3(nidx), dim3(kIdxThreads), 0, s,
-                               tsi, isrc, N, K, ctx->grid, dedup, io);
-        HCK(hipGetLastError());
-        const DiskRec* d_urec = L->disks.as<DiskRec>();
-        const int* d_map = L->umap.as<int>();
-        // per-candidate walk: enough workgroups to fill the chip, >= 1 disk per wave
-        const int target = 8 * ctx->cus;
-        const int G = (int)std::max<int64_t>(
-            1, std::min<int64_t>((target + K - 1) / K, std::max(1, N / kWavesPerBlock)));
-        n_other = G;
-        L->partial.reserve(sizeof(double) * (size_t)K * std::max(G, poll_possible ? N : 1));
-        const bool run_tiled = ctx->algo != MAC_ALGO_POLL && !big;
-        const int64_t units = (int64_t)K * G;
-        if (poll_possible) {
-            // walk choice + neighbour lists (poll) or the per-candidate walk itself, one launch;
-            // when the poll walk is chosen the extra blocks just exit, so the per-candidate walk
-            // gets one workgroup per CU (grid-striding over its units)
-            const int forced = (ctx->algo == MAC_ALGO_POLL || big) ? kModePoll : 0;
+            L->partial.reserve(sizeof(double) * (size_t)K * G);
+            uint64_t* ts = take_ts(units, ts_a, ts_na);
+            hipLaunchKernelGGL(coverage_tiled_kernel, dim3((unsigned)units), dim3(kBlock),
+                               (uint32_t)tiled_lds_bytes(N), s, ts, ctx->xys.as<double2>(),
+                               ctx->ws.as<double>(), ctx->off.as<int32_t>(), ctx->grid, d_urec, d_map,
+                               N, K, G, nullptr, L->partial.as<double>());
+            HCK(hipGetLastError());
+        } else {
+            L->region.reserve(sizeof(int4) * N);
+            L->cost.reserve(sizeof(double2) * N);
+            L->mode.reserve(8 * sizeof(int));  // [0] walk, [1..4] the poll walk's counters (k_common.h)
+            const IndexOut io{L->disks.as<DiskRec>(), L->umap.as<int>(), L->ucount.as<int>(),
+                              L->region.as<int4>(), L->cost.as<double2>(), L->mode.as<int>() + 1,
+                              L->prec.as<int4>(), nchain,
+                              L->lane4.as<float4>(), L->lanexp.as<float>(), L->rows.as<int2>(),
+                              ctx->off.as<int32_t>()};
+            const unsigned nidx = 8 * ((N + 7) / 8);
+            const int dedup = iper ? 1 : 0;
+            if (isrc.keysT && iper == kIdxPerWide)
+                hipLaunchKernelGGL((disk_index_kernel<true, kIdxPerWide>), dim3(nidx), dim3(kIdxThreads),
+                                   0, s, nullptr, isrc, N, K, ctx->grid, dedup, io);
+            else if (isrc.keysT)
+                hipLaunchKernelGGL((disk_index_kernel<true, kIdxPer>), dim3(nidx), dim3(kIdxThreads), 0, s,
+                                   nullptr, isrc, N, K, ctx->grid, dedup, io);
+            else if (iper == kIdxPerWide)
+                hipLaunchKernelGGL((disk_index_kernel<false, kIdxPerWide>), dim3(nidx), dim3(kIdxThreads),
+                                   0, s, nullptr, isrc, N, K, ctx->grid, dedup, io);
+            else
+                hipLaunchKernelGGL((disk_index_kernel<false, kIdxPer>), dim3(nidx), dim3(kIdxThreads), 0,
+                                   s, nullptr, isrc, N, K, ctx->grid, dedup, io);
+            HCK(hipGetLastError());
+            // walk choice + neighbour lists (poll) or the per-candidate walk itself, one launch
+            // (k_walk.h); when the poll walk is chosen the extra blocks just exit, so the
+            // per-candidate walk gets one workgroup per CU (grid-striding over its units)
+            const bool run_tiled = ctx->algo != MAC_ALGO_POLL && !big;
+            const int forced = run_tiled ? 0 : kModePoll;
             L->nbr.reserve(sizeof(uint16_t) * (size_t)N * kPollNbr);
             L->ncount.reserve(sizeof(int) * (size_t)N);
             L->dlist.reserve(sizeof(int) * (size_t)N);
             L->qual.reserve(sizeof(int) * (size_t)N);
             L->nboxT.reserve(sizeof(int4) * (size_t)N * kPollNbr);
+            L->partial.reserve(sizeof(double) * (size_t)K * std::max(G, N));
             const size_t lds = run_tiled ? tiled_lds_bytes(N) : 0;
             const unsigned nwg = (unsigned)std::max<int64_t>(
                 N, run_tiled ? std::min<int64_t>(units, ctx->cus) : 0);
@@ -635,13 +644,6 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             HCK(hipGetLastError());
             d_mode = L->mode.as<int>();
             d_umap = d_map;
-        } else {
-            uint64_t* ts = take_ts(units, ts_a, ts_na);
-            hipLaunchKernelGGL(coverage_tiled_kernel, dim3((unsigned)units), dim3(kBlock),
-                               (uint32_t)tiled_lds_bytes(N), s, ts, ctx->xys.as<double2>(),
-                               ctx->ws.as<double>(), ctx->off.as<int32_t>(), ctx->grid, d_urec, d_map,
-                               N, K, G, nullptr, L->partial.as<double>());
-            HCK(hipGetLastError());
         }
         if (poll_possible) {
             // the bit-word kernel runs when the previous poll on this lane had more than
@@ -678,7 +680,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             const int gy = std::max(1, std::min(4, (um_max + kPollKPB - 1) / kPollKPB));
             L->spart.reserve(sizeof(double) * (size_t)N * K);
             const int n_shared = kSharedWG;
-            const dim3 pgrid(N + n_shared, gy);
+            const dim3 pgrid(8 * ((N + 7) / 8) + n_shared, gy);   // walk workgroups, then shared
             uint64_t* ts = take_ts((int64_t)pgrid.x * pgrid.y, ts_b, ts_nb);
             hipLaunchKernelGGL(coverage_poll_kernel, pgrid, dim3(kPollThreads), 0, s, ts,
                                ctx->xys.as<double2>(), ctx->ws.as<double>(),
@@ -859,6 +861,16 @@ int32_t mac_diag_walk_read(uint64_t* out, int64_t n)
 {
     if (n > (int64_t)(8 * 65536)) n = 8 * 65536;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_walk), sizeof(uint64_t) * n, 0,
+                            hipMemcpyDeviceToHost) != hipSuccess)
+        return MAC_E_HIP;
+    return MAC_OK;
+}
+
+// diagnostic build only: phase stamps of the prep launch's first 64 chain workgroups (k_prep.h)
+int32_t mac_diag_prep_read(uint64_t* out, int64_t n)
+{
+    if (n > 64 * 16) n = 64 * 16;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_prep), sizeof(uint64_t) * n, 0,
                             hipMemcpyDeviceToHost) != hipSuccess)
         return MAC_E_HIP;
     return MAC_OK;
@@ -1049,11 +1061,11 @@ void mac_ctx_destroy(mac_ctx* ctx)
         l->h_dc.release();
         l->h_cl.release();
         for (DevBuf* b : {&l->cands, &l->disks, &l->partial, &l->area, &l->obj, &l->best,
-                          &l->rmax, &l->prev, &l->dlim, &l->region, &l->cost, &l->mode, &l->nbr,
+                          &l->rmax, &l->prev, &l->dlim, &l->region, &l->mode, &l->nbr,
                           &l->ncount, &l->dlist, &l->qual, &l->spart, &l->vp, &l->xinc,
-                          &l->perm, &l->ucount, &l->umap, &l->keysT, &l->kbad, &l->lane4,
+                          &l->perm, &l->ucount, &l->umap, &l->keysT, &l->lane4,
                           &l->lanexp, &l->rows, &l->nboxT, &l->cnt, &l->dlimraw, &l->finblk, &l->finarrive, &l->c32, &l->p32,
-                          &l->cpart, &l->carrive})
+                          &l->cpart, &l->carrive, &l->prec, &l->cost})
             b->release();
         if (l->done) (void)hipEventDestroy(l->done);
         if (l->stream) (void)hipStreamDestroy(l->stream);

@@ -105,7 +105,7 @@ for s in $STEPS; do
                 -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-extras ; rc=$?
         fi
         fatal $rc || python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write --config 4 \
-            --chain 'mac::column_pass_kernel<true>;mac::disk_index_kernel<true, 3>;mac::walk_setup_kernel;mac::coverage_poll_kernel;mac::finalize_kernel' \
+            --chain 'mac::prep_kernel;mac::disk_index_kernel<true, 3>;mac::walk_setup_kernel;mac::coverage_poll_kernel;mac::finalize_kernel' \
             --out gpurun_out/pmc_traffic_config4.json ;;
     *) echo "unknown step $s"; rc=0 ;;
     esac

@@ -45,7 +45,7 @@ def main():
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("--config", type=int, default=4)
-    ap.add_argument("--chain", default="mac::column_pass_kernel<true>;mac::disk_index_kernel<true, 3>;"
+    ap.add_argument("--chain", default="mac::prep_kernel;mac::disk_index_kernel<true, 3>;"
                     "mac::walk_setup_kernel;mac::coverage_poll_kernel;mac::finalize_kernel",
                     help="semicolon-separated kernels of one poll")
     ap.add_argument("--out", required=True)
