@@ -26,35 +26,39 @@ namespace mac {
 // A disk with neighbours goes to the bit-word kernel's list (front of dlist, k_bits.h) when its
 // list did not overflow and its region is at most 64 x 64 tiles; otherwise to the back of dlist
 // (the poll kernel's fp64 jobs).
-__device__ __forceinline__ void neighbors_block(int i, int N, const int4* __restrict__ region,
+// R: region i; Q[q]: region j = threadIdx.x + q * kBlock (j < i), loaded by the caller beside the
+// walk choice's costs (one round trip); further j are loaded here.
+constexpr int kNbrPre = 4;   // regions per thread loaded up front (i <= 1024)
+__device__ __forceinline__ void neighbors_block(int i, int N, const int4& R, const int4 (&Q)[kNbrPre],
+                                                const int4* __restrict__ region,
                                                 uint16_t* __restrict__ nbr, int4* __restrict__ nboxT,
                                                 int* __restrict__ ncount,
                                                 int* __restrict__ dlist, int* __restrict__ dcount,
-                                                const int* __restrict__ ucount, int* __restrict__ qual)
+                                                int* __restrict__ qual)
 {
     __shared__ int cnt;
     if (threadIdx.x == 0) cnt = 0;
     __syncthreads();
-    const int4 R = region[i];
     if (R.x <= R.y) {
-        for (int j = threadIdx.x; j < i; j += kBlock) {
-            const int4 Q = region[j];
-            if (box_overlap(Q, R)) {
+        auto test = [&](int j, const int4& B) {
+            if (box_overlap(B, R)) {
                 const int p = atomicAdd(&cnt, 1);  // list order is irrelevant (a boolean OR)
                 if (p < kPollNbr) {
                     nbr[i * kPollNbr + p] = (uint16_t)j;
-                    nboxT[i * kPollNbr + p] = Q;   // the neighbour's region box
+                    nboxT[i * kPollNbr + p] = B;   // the neighbour's region box
                 }
             }
+        };
+#pragma unroll
+        for (int q = 0; q < kNbrPre; ++q) {
+            const int j = threadIdx.x + q * kBlock;
+            if (j < i) test(j, Q[q]);
         }
+        for (int j = threadIdx.x + kNbrPre * kBlock; j < i; j += kBlock) test(j, region[j]);
     }
     __syncthreads();
-    const int nc = cnt;
-    bool bad = false;
-    if (nc > 0) {
-        bad = nc > kPollNbr || R.y - R.x + 1 > 64 || R.w - R.z + 1 > 64;
-    }
-    bad = __syncthreads_or(bad);
+    const int nc = cnt;   // (uniform, as R is)
+    const bool bad = nc > 0 && (nc > kPollNbr || R.y - R.x + 1 > 64 || R.w - R.z + 1 > 64);
     if (threadIdx.x == 0) {
         ncount[i] = nc;
         qual[i] = nc > 0 && !bad ? 1 : 0;
@@ -65,10 +69,14 @@ __device__ __forceinline__ void neighbors_block(int i, int N, const int4* __rest
     }
 }
 
-// The device-side walk choice: poll when its point-visits (cost[i].x summed) stay within `ratio`
-// x the per-candidate walk's (cost[i].y summed) — its visits are broadcast LDS reads, the other's
-// scattered global loads — or `forced`. The costs are integer-valued doubles, so the sums are
-// exact and every block that computes the choice gets the same one. Block-uniform result.
+// The device-side walk choice, both costs in poll-walk test units: the poll walk tests every
+// entry of region i against every candidate's disk i (A = sum of cost[i].x = K * |region i|
+// entry visits, broadcast LDS reads); the per-candidate walk visits each candidate's span
+// entries (cost[i].y summed) with scattered global loads and builds each candidate's
+// neighbour lists from N(N-1)/2 fp64 disk-pair tests — each of those ~`ratio` poll-walk tests
+// (4: measured) — so its cost is ratio * (sum of spans + K N(N-1)/2). Poll when A is the lower
+// cost, or `forced`. Every block sums in the same fixed order, so every block gets the same
+// choice. Block-uniform result.
 __device__ __forceinline__ int walk_choice(int N, int K, const double2* __restrict__ cost, double ratio,
                                            int forced)
 {
@@ -82,8 +90,7 @@ __device__ __forceinline__ int walk_choice(int N, int K, const double2* __restri
     }
     const double A = block_sum_f64(a, red);
     __syncthreads();
-    // + the per-candidate walk's neighbour-list build (k_walk.h): every (candidate, slice) unit
-    // tests all disk pairs, N(N-1)/2 box tests, which its visit count leaves out
+    // the per-candidate walk: span visits + every (candidate, slice) unit's N(N-1)/2 pair tests
     // (a config-5 poll of clustered disks chose that walk on visits alone and took 3.96 ms)
     const double B = block_sum_f64(b, red) + (double)K * N * (N - 1) / 2.0;
     if (threadIdx.x == 0) smode = A <= ratio * B ? kModePoll : kModeTiled;

@@ -201,13 +201,15 @@ template <bool kMat>
 __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
 {
     __shared__ double term[kPrepC][kPrepU + 1];   // [candidate][UAV] (+1: lanes on distinct banks)
+    __shared__ int wbad[kPrepU / kWave][kPrepC];  // per wave: a term of the candidate is negative
     const int N = a.N, K = a.K;
-    const int u = threadIdx.x;
+    const int u = threadIdx.x, lane = u & (kWave - 1), wid = u / kWave;
     const int k0 = cw * kPrepC;
     const bool obj = a.vp != nullptr;
     const PenArgs& pa = a.pa;
     MAC_PREP_STAMP(0);
-    double acc = 0.0, mn = 0.0;   // the chain, and its least term (< 0: a cons3 violation)
+    double acc = 0.0;   // the chain (lane c of wave 0: candidate k0 + c)
+    bool bad = false;   // ... and whether a term of it is negative (cons3)
     for (int ib = 0; ib < N; ib += kPrepU) {
         const int nb = min(kPrepU, N - ib);
         const int i = ib + u;
@@ -229,8 +231,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
             for (int q = 0; q < 3; ++q) base[q] = a.src.cands[q * N + ii];
         }
         if (obj) {
-            // pen_term (above), the same operations in the same order; the chains first, so
-            // that no store is in flight at the barrier
+            // pen_term (above), the same operations in the same order
             const double x1 = pa.prev ? pa.prev[ii] : 0.0, y1 = pa.prev ? pa.prev[N + ii] : 0.0;
             const double z1 = pa.prev ? pa.prev[2 * N + ii] / pa.tan_half_fov : 0.0;
             const double rm = pa.rmax ? pa.rmax[ii] : 0.0;
@@ -246,29 +247,11 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
                     if (sq > T3) t = -1.0;
                 }
                 term[c][u] = t;
+                const uint64_t neg = __ballot(iv && t < 0.0);
+                if (lane == 0) wbad[wid][c] = neg != 0;
             }
             MAC_PREP_STAMP(1 + 3 * (ib / kPrepU));
-            lds_barrier();
-            if (u < kPrepC) {   // the chains, sequential in UAV order (register batches)
-                int q = 0;
-                for (; q + 16 <= nb; q += 16) {
-                    double t[16];
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) t[j] = term[u][q + j];
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) {
-                        acc += t[j];
-                        mn = fmin(mn, t[j]);   // (a second, independent chain)
-                    }
-                }
-                for (; q < nb; ++q) {
-                    const double t = term[u][q];
-                    acc += t;
-                    mn = fmin(mn, t);
-                }
-            }
         }
-        MAC_PREP_STAMP(2 + 3 * (ib / kPrepU));
         if (a.prec && iv) {
             double xa = __builtin_inf(), xb = -__builtin_inf(), ya = __builtin_inf(), yb = -__builtin_inf();
             double xm = 0.0, ym = 0.0, est = 0.0;
@@ -318,13 +301,32 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
                 dst[1] = make_float4(f[4], f[5], f[6], f[7]);
             }
         }
+        MAC_PREP_STAMP(2 + 3 * (ib / kPrepU));
+        if (obj) {
+            // the chains, after every wave's other work (the adds are the critical path: the
+            // folding wave then has its SIMD to itself), sequential in UAV order
+            lds_barrier();
+            if (u < kPrepC) {
+#pragma unroll
+                for (int w = 0; w < kPrepU / kWave; ++w) bad |= wbad[w][u] != 0;
+                int q = 0;
+                for (; q + 16 <= nb; q += 16) {
+                    double t[16];
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) t[j] = term[u][q + j];
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) acc += t[j];
+                }
+                for (; q < nb; ++q) acc += term[u][q];
+            }
+        }
         MAC_PREP_STAMP(3 + 3 * (ib / kPrepU));
         if (obj && ib + kPrepU < N) lds_barrier();   // the fold has read the terms
     }
-    if (obj && u < kPrepC && k0 + u < K) a.vp[k0 + u] = mn < 0.0 ? __builtin_inf() : acc * a.penalty;
+    if (obj && u < kPrepC && k0 + u < K) a.vp[k0 + u] = bad ? __builtin_inf() : acc * a.penalty;
 }
 
-__global__ __launch_bounds__(kPrepU) void prep_kernel(uint64_t* ts, PrepArgs a)
+__global__ __launch_bounds__(kPrepU) __attribute__((amdgpu_waves_per_eu(4))) void prep_kernel(uint64_t* ts, PrepArgs a)
 {
     ts_begin(ts);   // profiling only (the chain's first launch: k_common.h)
     // XCD-aware: workgroups b and b + 8 share an XCD (round-robin dispatch), so consecutive

@@ -252,11 +252,20 @@ __global__ __launch_bounds__(kBlock) void walk_setup_kernel(
     int* __restrict__ qual)
 {
     ts_begin(ts);
+    // the neighbour lists' regions, loaded beside the walk choice's costs (one round trip)
+    const int i = blockIdx.x;
+    const int4 none = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
+    const int4 R = i < N ? region[i] : none;
+    int4 Q[kNbrPre];
+#pragma unroll
+    for (int q = 0; q < kNbrPre; ++q) {
+        const int j = threadIdx.x + q * kBlock;
+        Q[q] = j < i && i < N ? region[j] : none;
+    }
     const int m = walk_choice(N, K, cost, ratio, forced);
     if (blockIdx.x == 0 && threadIdx.x == 0) mode[0] = m;
     if (m == kModePoll) {
-        if ((int)blockIdx.x < N)
-            neighbors_block(blockIdx.x, N, region, nbr, nboxT, ncount, dlist, dcount, ucount, qual);
+        if (i < N) neighbors_block(i, N, R, Q, region, nbr, nboxT, ncount, dlist, dcount, qual);
     } else {
         coverage_tiled_body(xy, w, off, g, urec, umap, N, K, G, nullptr, partial);
     }

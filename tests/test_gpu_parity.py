@@ -497,6 +497,59 @@ def test_config4_clustered_full_poll(ctx, pkg, orc, algo):
     _full_poll_check(ctx, orc, C, rmax, 4096, [algo], "config4-clustered")
 
 
+def _walk_of(ctx, C):
+    """(areas, the walk the device chose for the batch)."""
+    ctx.profile(True)
+    ctx.profile_read(reset=True)
+    area = ctx.area_batch(C)
+    walk = ctx.profile_read(reset=True)[3]
+    ctx.profile(False)
+    return area, walk
+
+
+@pytest.mark.parametrize("disks", ["clustered", "uniform"])
+def test_walk_choice_poll_batches(ctx, pkg, orc, disks):
+    """The device's walk choice (k_poll_shared.h walk_choice, costs in poll-walk test units) on
+    MADS polls of K >= 64: crowded (every disk overlapping lower-index ones: the per-candidate
+    walk would rebuild N(N-1)/2 neighbour pairs per candidate — the config-5 cliff) and
+    scattered disks both take the poll walk under AUTO; the forced per-candidate walk gives the
+    same areas (slower, never different). Areas == the exact lattice counts."""
+    wl = pkg.workloads
+    rng = wl.SplitMix64(4242 if disks == "clustered" else 4243)
+    G, N = 512, 96
+    x, y, w = wl.grid_points(G)
+    ctx.set_points(x, y, w)
+    x0 = (wl.clustered_disks if disks == "clustered" else wl.uniform_disks)(N, G, rng)
+    C = wl.poll_candidates(x0, rng)
+    assert C.shape[0] == 6 * N + 1 >= 64
+    want = 25.0 * orc.lattice_count_batch(C, G).astype(np.float64)
+    ctx.set_algo("auto")
+    area, walk = _walk_of(ctx, C)
+    assert walk == "poll", walk
+    assert np.array_equal(area, want)
+    ctx.set_algo("tiled")
+    area_t, walk_t = _walk_of(ctx, C[:64])
+    ctx.set_algo("auto")
+    assert walk_t == "tiled", walk_t
+    assert np.array_equal(area_t, want[:64])
+
+
+def test_walk_choice_scattered_batch(ctx, pkg, orc):
+    """A batch that is not a poll (64 unrelated random layouts of 8 disks: no shared footprint
+    across candidates) takes the per-candidate walk under AUTO; areas == exact lattice counts."""
+    wl = pkg.workloads
+    rng = wl.SplitMix64(4244)
+    G, N, K = 512, 8, 64
+    x, y, w = wl.grid_points(G)
+    ctx.set_points(x, y, w)
+    C = np.stack([wl.uniform_disks(N, G, rng) for _ in range(K)])
+    want = 25.0 * orc.lattice_count_batch(C, G).astype(np.float64)
+    ctx.set_algo("auto")
+    area, walk = _walk_of(ctx, C)
+    assert walk == "tiled", walk
+    assert np.array_equal(area, want)
+
+
 @pytest.mark.parametrize("case", ["real_clustered", "big_radius", "mixed_weights", "pythagorean",
                                   "crowded", "lattice_mixed", "key_mix"])
 def test_poll_walk_stress(ctx, pkg, orc, case):
