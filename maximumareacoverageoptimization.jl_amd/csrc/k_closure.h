@@ -3,20 +3,16 @@
 // DirectSearch calls the objective closure once per trial point (SetObjective,
 // src/TDM_STATIC_opt.jl:125; AreaMaxObjective :82-100 -> calculateArea
 // src/AreaCoverageCalculation.jl:63-78). For that path a batch chain (index, walk, finalize) is
-// all latency, so mac_area_f64 runs one kernel, and no copy: workgroup i = disk i of the candidate.
-//   0. workgroup 0 copies the candidate's 3N doubles from the caller's mapped host staging into a
-//      device buffer (one PCIe round trip) and publishes them under the call's sequence number;
-//      the other workgroups wait for that number (workgroup 0 is always resident first, so the
-//      wait cannot block it);
-//   1. disk i's lower-index neighbours: the disks j < i that may share a covered entry with it
-//      (disks_may_overlap, conservative), tested from registers, their exact thresholds T(r_j)
-//      listed in LDS;
-//   2. the entries of disk i's tile span (CSR rows of the tile-sorted list) that disk i covers and
+// all latency, so mac_area_f64 runs one kernel instead: workgroup i = disk i of the candidate.
+//   1. every workgroup stages the candidate's N disks (x, y, r) in LDS (one coalesced read);
+//   2. disk i's lower-index neighbours: the disks j < i that may share a covered entry with it
+//      (disks_may_overlap, conservative), their exact thresholds T(r_j) in LDS;
+//   3. the entries of disk i's tile span (CSR rows of the tile-sorted list) that disk i covers and
 //      no listed neighbour covers — each covered entry is credited to the LOWEST-index disk
 //      covering it, so the sum over disks is the reference's first-hit `break` sum over the same
 //      multiset of entries — counted (every weight equal: integer, exact in any order) or summed
 //      in fp64 in a fixed order;
-//   3. counts: one 64-bit atomic add per workgroup of (1 << 40 | count) — the workgroup whose add
+//   4. counts: one 64-bit atomic add per workgroup of (1 << 40 | count) — the workgroup whose add
 //      sees N - 1 earlier arrivals holds the total; weights: the credit goes to part[i]
 //      (agent-scope store, then one counter add) and the workgroup whose add arrives last sums
 //      part[0 .. N) in disk order. It writes the area to the device word and to the caller's
@@ -35,8 +31,10 @@
 
 namespace mac {
 
-constexpr int kClosureMaxN = 2048;   // disks per candidate (one workgroup each)
+constexpr int kClosureMaxN = 2048;   // disks staged in LDS: 24 B each (dynamic LDS)
 constexpr int kClosureNbr = 64;      // neighbours kept per disk (more: every lower-index disk)
+
+__host__ __device__ inline size_t closure_lds_bytes(int N) { return (size_t)24 * (size_t)N; }
 
 struct ClosureOut {
     unsigned long long* part;   // [N] per-disk credit (double bits), weighted entries
@@ -45,69 +43,50 @@ struct ClosureOut {
     double* area;               // the area on the device
     uint64_t* slot;             // mapped host slot {area bits, 0, seq, check}
     uint64_t seq;
-    const double* hcand;        // the candidate in mapped host memory (3N doubles)
-    double* dcand;              // ... its device copy
-    uint64_t* ready;            // the device copy's sequence number
 };
 
-__device__ __forceinline__ double ld_agent(const double* p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__global__ __launch_bounds__(kBlock) void closure_kernel(uint64_t* ts, int N, Grid g,
-                                                         const double2* __restrict__ xy,
+__global__ __launch_bounds__(kBlock) void closure_kernel(uint64_t* ts, const double* __restrict__ cand,
+                                                         int N, Grid g, const double2* __restrict__ xy,
                                                          const double* __restrict__ w,
                                                          const int32_t* __restrict__ off, int counts,
                                                          double w0, ClosureOut o)
 {
     ts_begin(ts);
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    double* sx = (double*)lds_raw;
+    double* sy = sx + N;
+    double* sr = sy + N;
     __shared__ int nb[kClosureNbr];
-    __shared__ double nx[kClosureNbr], ny[kClosureNbr], nT[kClosureNbr];
+    __shared__ double nT[kClosureNbr];
     __shared__ int ncnt;
     __shared__ double dred[kWavesPerBlock];
     __shared__ unsigned long long ired[kWavesPerBlock];
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
     const int i = blockIdx.x;
-    // 0. the candidate on the device (agent-scope stores and loads: any XCD reads it fresh)
-    if (i == 0) {
-        for (int j = tid; j < 3 * N; j += kBlock)
-            __hip_atomic_store(o.dcand + j, o.hcand[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) __hip_atomic_store(o.ready, o.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        if (tid == 0)
-            while (__hip_atomic_load(o.ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != o.seq)
-                __builtin_amdgcn_s_sleep(1);
-        __syncthreads();
+    for (int j = tid; j < N; j += kBlock) {
+        sx[j] = cand[j];
+        sy[j] = cand[N + j];
+        sr[j] = cand[2 * N + j];
     }
     if (tid == 0) ncnt = 0;
-    const double* c = o.dcand;
-    const double cx = ld_agent(c + i), cy = ld_agent(c + N + i), r = ld_agent(c + 2 * N + i);
+    __syncthreads();
+    const double cx = sx[i], cy = sy[i], r = sr[i];
     const double T = cover_threshold(r);
     int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
     const bool any = T >= 0.0 && tile_span(cx, r, g.gx0, g.invS, g.nTx, x0, x1) &&
                      tile_span(cy, r, g.gy0, g.invS, g.nTy, y0, y1);
-    __syncthreads();
-    // 1. the lower-index neighbours (list order is irrelevant: a boolean OR)
     if (any) {
         for (int j = tid; j < i; j += kBlock) {
-            const double xj = ld_agent(c + j), yj = ld_agent(c + N + j), rj = ld_agent(c + 2 * N + j);
-            if (rj > 0.0 && disks_may_overlap(cx, cy, r, xj, yj, rj)) {
-                const int q = atomicAdd(&ncnt, 1);
-                if (q < kClosureNbr) {
-                    nb[q] = j;
-                    nx[q] = xj;
-                    ny[q] = yj;
-                    nT[q] = cover_threshold(rj);
-                }
+            if (sr[j] > 0.0 && disks_may_overlap(cx, cy, r, sx[j], sy[j], sr[j])) {
+                const int q = atomicAdd(&ncnt, 1);   // list order is irrelevant (a boolean OR)
+                if (q < kClosureNbr) nb[q] = j;
             }
         }
     }
     __syncthreads();
     const int nc = ncnt;
-    // 2. the span's entries disk i owns
+    if (tid < min(nc, kClosureNbr)) nT[tid] = cover_threshold(sr[nb[tid]]);
+    __syncthreads();
     uint64_t cnt = 0;
     double acc = 0.0;
     if (any) {
@@ -119,11 +98,13 @@ __global__ __launch_bounds__(kBlock) void closure_kernel(uint64_t* ts, int N, Gr
                 if (!(sqdist(p.x, p.y, cx, cy) <= T)) continue;
                 bool owned = true;
                 if (nc <= kClosureNbr) {
-                    for (int q = 0; q < nc && owned; ++q) owned = !(sqdist(p.x, p.y, nx[q], ny[q]) <= nT[q]);
+                    for (int q = 0; q < nc && owned; ++q) {
+                        const int c2 = nb[q];
+                        owned = !(sqdist(p.x, p.y, sx[c2], sy[c2]) <= nT[q]);
+                    }
                 } else {   // overflowed list: every lower-index disk
                     for (int c2 = 0; c2 < i && owned; ++c2)
-                        owned = !(sqdist(p.x, p.y, ld_agent(c + c2), ld_agent(c + N + c2)) <=
-                                  cover_threshold(ld_agent(c + 2 * N + c2)));
+                        owned = !(sqdist(p.x, p.y, sx[c2], sy[c2]) <= cover_threshold(sr[c2]));
                 }
                 if (owned) {
                     ++cnt;
@@ -132,7 +113,7 @@ __global__ __launch_bounds__(kBlock) void closure_kernel(uint64_t* ts, int N, Gr
             }
         }
     }
-    // 3. the area
+    // the area
     if (counts) {
 #pragma unroll
         for (int off2 = 32; off2 >= 1; off2 >>= 1) cnt += __shfl_xor(cnt, off2, kWave);

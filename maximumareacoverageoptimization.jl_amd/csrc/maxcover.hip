@@ -142,13 +142,8 @@ struct Lane {
     PinnedBuf h_cl;                            // closure_kernel's result slot (mapped)
     uint64_t* d_cl = nullptr;                  // ... its device address
     uint64_t cl_seq = 0;
-    DevBuf cpart, carrive, ctot, cready;       // closure_kernel: credits, arrivals, count, copy seq
-    PinnedBuf h_cin;                           // closure_kernel: the candidate (mapped, coherent)
-    void* h_cin_key = nullptr;                 // ... the allocation d_cin belongs to
-    double* d_cin = nullptr;
+    DevBuf cpart, carrive, ctot;               // closure_kernel: credits, arrivals, packed count
     DevBuf prec, cost;                         // prep launch: per-disk records; walk costs
-    hipStream_t side = nullptr;                // the penalty chains' stream (forked per poll)
-    hipEvent_t fork = nullptr, join = nullptr;
     int um_hist[8] = {};                       // most distinct positions of a disk, last 8 polls
 };
 
@@ -518,7 +513,6 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         1, std::min<int64_t>((target + K - 1) / K, std::max(1, N / kWavesPerBlock)));
     const int64_t units = (int64_t)K * G;
     const int nchain = (K + kPrepC - 1) / kPrepC;
-    bool join_chain = false;   // the penalty chains ran on the side stream (joined before finalize)
     if ((d_obj || poll_possible) && K > 0) {
         // the prep launch (k_prep.h): penalty chains + cons3 into vp, the poll walk's partial
         // regions, and the index's fp32 keys
@@ -542,32 +536,6 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             pr.ldk = ldk;
             isrc.keysT = pr.keysT;
             isrc.ldk = ldk;
-        }
-        // With the poll walk the penalty chains (N dependent fp64 adds per candidate, ~6.5 us
-        // at N = 512) run on the lane's side stream, forked here and joined before finalize:
-        // they overlap the keys, the index and the walks instead of lengthening the prep launch.
-        if (d_obj && poll_possible && N > 0) {
-            if (!L->side) {
-                HCK(hipStreamCreateWithFlags(&L->side, hipStreamNonBlocking));
-                HCK(hipEventCreateWithFlags(&L->fork, hipEventDisableTiming));
-                HCK(hipEventCreateWithFlags(&L->join, hipEventDisableTiming));
-            }
-            PrepArgs pc{};
-            pc.src = src;
-            pc.N = N;
-            pc.K = K;
-            pc.pa = pa;
-            pc.penalty = penalty;
-            pc.vp = d_vp;
-            pc.nchain = nchain;
-            pc.g = ctx->grid;
-            HCK(hipEventRecord(L->fork, s));
-            HCK(hipStreamWaitEvent(L->side, L->fork, 0));
-            hipLaunchKernelGGL(prep_kernel, dim3((unsigned)nchain), dim3(kPrepU), 0, L->side, nullptr, pc);
-            HCK(hipGetLastError());
-            HCK(hipEventRecord(L->join, L->side));
-            join_chain = true;
-            pr.vp = nullptr;
         }
         uint64_t* tsk = poll_possible ? take_ts(nchain, ts_c, ts_nc) : nullptr;
         hipLaunchKernelGGL(prep_kernel, dim3((unsigned)nchain), dim3(kPrepU), 0, s, tsk, pr);
@@ -759,7 +727,6 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         fb = FinBest{d_best, d_mirror, mirror_seq, idx_base, L->finblk.as<unsigned long long>(),
                      L->finarrive.as<unsigned>()};
     }
-    if (join_chain) HCK(hipStreamWaitEvent(s, L->join, 0));
     uint64_t* tsf = ts_c >= 0 ? take_ts(nfin, ts_f, ts_nf) : nullptr;
     hipLaunchKernelGGL(finalize_kernel, dim3(nfin), dim3(kFinThreads), 0, s,
                        L->partial.as<double>(), d_mode, n_poll, n_other, K, N, d_umap, d_spart, d_ncount,
@@ -1093,18 +1060,15 @@ void mac_ctx_destroy(mac_ctx* ctx)
         l->h_io.release();
         l->h_dc.release();
         l->h_cl.release();
-        l->h_cin.release();
         for (DevBuf* b : {&l->cands, &l->disks, &l->partial, &l->area, &l->obj, &l->best,
                           &l->rmax, &l->prev, &l->dlim, &l->region, &l->mode, &l->nbr,
                           &l->ncount, &l->dlist, &l->qual, &l->spart, &l->vp, &l->xinc,
                           &l->perm, &l->ucount, &l->umap, &l->keysT, &l->lane4,
                           &l->lanexp, &l->rows, &l->nboxT, &l->cnt, &l->dlimraw, &l->finblk, &l->finarrive, &l->c32, &l->p32,
-                          &l->cpart, &l->carrive, &l->ctot, &l->cready, &l->prec, &l->cost})
+                          &l->cpart, &l->carrive, &l->ctot, &l->prec, &l->cost})
             b->release();
         if (l->done) (void)hipEventDestroy(l->done);
-        if (l->fork) (void)hipEventDestroy(l->fork);
-        if (l->join) (void)hipEventDestroy(l->join);
-        if (l->side) (void)hipStreamDestroy(l->side);
+
         if (l->stream) (void)hipStreamDestroy(l->stream);
         delete l;
     }
@@ -1831,23 +1795,14 @@ static int32_t closure_eval(mac_ctx* ctx, const double* circles, int64_t three_n
     Lane* L = lg.lane;
     hipStream_t s = L->stream;
     const size_t in_bytes = sizeof(double) * (size_t)three_n;
-    // the candidate goes to mapped coherent host memory; the kernel's workgroup 0 copies it to
-    // the device (k_closure.h): no copy launch
-    L->h_cin.reserve(std::max<size_t>(in_bytes, 64), hipHostMallocMapped | hipHostMallocCoherent);
-    if (L->h_cin_key != L->h_cin.p) {
-        void* dp = nullptr;
-        HCK(hipHostGetDevicePointer(&dp, L->h_cin.p, 0));
-        L->d_cin = (double*)dp;
-        L->h_cin_key = L->h_cin.p;
-    }
-    std::memcpy(L->h_cin.p, circles, in_bytes);
+    L->h_io.reserve(std::max<size_t>(in_bytes, 64));
+    std::memcpy(L->h_io.p, circles, in_bytes);
     L->cands.reserve(in_bytes);
     L->area.reserve(sizeof(double));
     L->cpart.reserve(sizeof(unsigned long long) * (size_t)N);
-    // zero once; the last block of each launch resets them (the copy's seq only grows)
+    // zero once; the last block of each launch resets them
     if (L->carrive.grow(sizeof(unsigned))) HCK(hipMemsetAsync(L->carrive.p, 0, L->carrive.cap, s));
     if (L->ctot.grow(sizeof(uint64_t))) HCK(hipMemsetAsync(L->ctot.p, 0, L->ctot.cap, s));
-    if (L->cready.grow(sizeof(uint64_t))) HCK(hipMemsetAsync(L->cready.p, 0, L->cready.cap, s));
     if (!L->h_cl.p) {
         L->h_cl.reserve(64, hipHostMallocMapped | hipHostMallocCoherent);
         std::memset(L->h_cl.p, 0, 64);
@@ -1856,6 +1811,7 @@ static int32_t closure_eval(mac_ctx* ctx, const double* circles, int64_t three_n
         L->d_cl = (uint64_t*)dp;
     }
     const uint64_t seq = ++L->cl_seq;
+    HCK(hipMemcpyAsync(L->cands.p, L->h_io.p, in_bytes, hipMemcpyHostToDevice, s));
     int64_t ts_a = -1;
     uint64_t* ts = nullptr;
     if (ctx->profile) {
@@ -1867,11 +1823,10 @@ static int32_t closure_eval(mac_ctx* ctx, const double* circles, int64_t three_n
         }
     }
     const ClosureOut co{L->cpart.as<unsigned long long>(), L->ctot.as<unsigned long long>(),
-                        L->carrive.as<unsigned>(), L->area.as<double>(), L->d_cl, seq, L->d_cin,
-                        L->cands.as<double>(), L->cready.as<uint64_t>()};
-    hipLaunchKernelGGL(closure_kernel, dim3((unsigned)N), dim3(kBlock), 0, s, ts, N, ctx->grid,
-                       ctx->xys.as<double2>(), ctx->ws.as<double>(), ctx->off.as<int32_t>(),
-                       ctx->w_uniform ? 1 : 0, ctx->w0, co);
+                        L->carrive.as<unsigned>(), L->area.as<double>(), L->d_cl, seq};
+    hipLaunchKernelGGL(closure_kernel, dim3((unsigned)N), dim3(kBlock), (uint32_t)closure_lds_bytes(N), s,
+                       ts, L->cands.as<double>(), N, ctx->grid, ctx->xys.as<double2>(),
+                       ctx->ws.as<double>(), ctx->off.as<int32_t>(), ctx->w_uniform ? 1 : 0, ctx->w0, co);
     HCK(hipGetLastError());
     if (ts) {
         std::lock_guard<std::mutex> lk(ctx->mu);
