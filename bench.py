@@ -179,10 +179,10 @@ def cpu_baseline(x, y, w, cands, seconds_target: float, threads: int):
     del rec
     # calibrate on one candidate over a slice of the list, then size the sample
     t0 = time.perf_counter()
-    sub = orc.PointerList(np.stack([x[:200000], y[:200000], w[:200000], w[:200000],
-                                    np.zeros(200000)], axis=1))
+    m = max(1, min(200000, x.size))
+    sub = orc.PointerList(np.stack([x[:m], y[:m], w[:m], w[:m], np.zeros(m)], axis=1))
     sub.area_batch(cands[:1], 1)
-    per_eval = (time.perf_counter() - t0) * (x.size / 200000.0)
+    per_eval = (time.perf_counter() - t0) * (x.size / float(m))
     sub.close()
     n = max(1, min(cands.shape[0], int(round(seconds_target / max(per_eval, 1e-9))) * threads))
     n = max(threads if n >= threads else n, 1)

@@ -72,9 +72,10 @@ __device__ __forceinline__ void neighbors_block(int i, int N, const int4& R, con
 // The device-side walk choice, both costs in poll-walk test units: the poll walk tests every
 // entry of region i against every candidate's disk i (A = sum of cost[i].x = K * |region i|
 // entry visits, broadcast LDS reads); the per-candidate walk visits each candidate's span
-// entries (cost[i].y summed) with scattered global loads and builds each candidate's
-// neighbour lists from N(N-1)/2 fp64 disk-pair tests — each of those ~`ratio` poll-walk tests
-// (4: measured) — so its cost is ratio * (sum of spans + K N(N-1)/2). Poll when A is the lower
+// entries (cost[i].y summed) with scattered global loads, and each candidate's G slice units
+// together test its N(N-1)/2 disk pairs in fp64 (k_walk.h: a unit tests its own slice's disks
+// against every lower-index disk) — each visit and each pair test ~`ratio` poll-walk tests (4:
+// measured) — so its cost is ratio * (sum of spans + K N(N-1)/2). Poll when A is the lower
 // cost, or `forced`. Every block sums in the same fixed order, so every block gets the same
 // choice. Block-uniform result.
 __device__ __forceinline__ int walk_choice(int N, int K, const double2* __restrict__ cost, double ratio,
@@ -90,8 +91,9 @@ __device__ __forceinline__ int walk_choice(int N, int K, const double2* __restri
     }
     const double A = block_sum_f64(a, red);
     __syncthreads();
-    // the per-candidate walk: span visits + every (candidate, slice) unit's N(N-1)/2 pair tests
-    // (a config-5 poll of clustered disks chose that walk on visits alone and took 3.96 ms)
+    // the per-candidate walk: span visits + N(N-1)/2 pair tests per candidate (over its slice
+    // units); a config-5 poll of clustered disks chose that walk on visits alone and took 3.96 ms
+    // (tests/test_gpu_parity.py test_walk_choice_poll_batches pins the choice)
     const double B = block_sum_f64(b, red) + (double)K * N * (N - 1) / 2.0;
     if (threadIdx.x == 0) smode = A <= ratio * B ? kModePoll : kModeTiled;
     __syncthreads();
