@@ -178,9 +178,9 @@ def cpu_baseline(x, y, w, cands, seconds_target: float, threads: int):
     pl = orc.PointerList(rec)
     del rec
     # calibrate on one candidate over a slice of the list, then size the sample
-    t0 = time.perf_counter()
     m = max(1, min(200000, x.size))
     sub = orc.PointerList(np.stack([x[:m], y[:m], w[:m], w[:m], np.zeros(m)], axis=1))
+    t0 = time.perf_counter()
     sub.area_batch(cands[:1], 1)
     per_eval = (time.perf_counter() - t0) * (x.size / float(m))
     sub.close()
