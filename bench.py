@@ -350,6 +350,10 @@ def main():
     ap.add_argument("--shard-of", type=int, default=1,
                     help="time rank 0's shard of a P-way strong split alone on one GPU (no "
                          "collective; value = shard candidates / time)")
+    ap.add_argument("--disk-shard-of", type=int, default=1,
+                    help="time rank 0's share of a P-way DISK split alone on one GPU: every "
+                         "candidate's first ceil(N/P) UAVs (a lower bound of a disk-sharded rank: "
+                         "no lower-index halo, no all-reduce of the K partial counts)")
     ap.add_argument("--disks", default="uniform", choices=("uniform", "clustered"),
                     help="UAV disks: uniform over the domain (default) or SURVEY 8(d)'s "
                          "clustered variant (sqrt(N)*40 m around the centre, overlapping)")
@@ -403,6 +407,12 @@ def main():
             wl.SplitMix64(args.seed ^ (0x9E3779B97F4A7C15 * rank & 0xFFFFFFFFFFFFFFFF))
         polls = [wl.poll_candidates(x0, prng) for _ in range(args.polls)]
     K = polls[0].shape[0]
+    if args.disk_shard_of > 1 and not distributed:
+        # rank 0's disks of a P-way disk split: UAVs [0, n) of every candidate
+        n = -(-N // args.disk_shard_of)
+        cols = np.concatenate([np.arange(n), N + np.arange(n), 2 * N + np.arange(n)])
+        polls = [np.ascontiguousarray(p[:, cols]) for p in polls]
+        N = n
     r_max = np.full(N, 30.0 * np.tan(100 / 180 * np.pi / 2))
     M = x.size
     if args.scaling == "weak":
@@ -571,7 +581,10 @@ def main():
                 "disks": ("integer centres uniform over the domain, R=36" if args.disks == "uniform"
                           else "clustered: integer centres within sqrt(N)*40 m of the centre, R=36"),
                 "cons3": "prev = incumbent, d_lim = 10 m, FOV 100 deg (every candidate checked)",
-                "parallelism": (f"rank 0 of a {args.shard_of}-way candidate split, timed alone on "
+                "parallelism": (f"rank 0 of a {args.disk_shard_of}-way disk split (UAVs 0..{N - 1} "
+                                f"of every candidate), timed alone on 1 GPU (no halo, no collective)"
+                                if args.disk_shard_of > 1 and not distributed else
+                                f"rank 0 of a {args.shard_of}-way candidate split, timed alone on "
                                 f"1 GPU (no collective)" if args.shard_of > 1 and not distributed else
                                 f"{world} GPU(s), one full poll set each, 16-B argmin all-gather"
                                 if args.scaling == "weak" else

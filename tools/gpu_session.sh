@@ -79,6 +79,11 @@ for s in $STEPS; do
             run shard$P 300 python bench.py --no-cpu --shard-of $P ; rc=$?
             fatal $rc && break
         done ;;
+    dshards)   # per-rank floor of a disk split: rank 0's disks alone on one GPU
+        for P in 2 4 8; do
+            run dshard$P 300 python bench.py --no-cpu --no-extras --disk-shard-of $P ; rc=$?
+            fatal $rc && break
+        done ;;
     prof5)    # kernel stats of the config-5 MPC loop and of the clustered config-4 poll
         rm -rf gpurun_out/prof5 gpurun_out/profc
         run prof5 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof5 -o run \
