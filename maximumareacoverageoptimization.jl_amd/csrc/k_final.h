@@ -1,4 +1,4 @@
-// k_final.h — partial-sum reduction, objective (the column pass's penalty, k_prep.h) and the
+// k_final.h — partial-sum reduction, objective (the prep launch's penalty, k_prep.h) and the
 // poll argmin.
 #pragma once
 

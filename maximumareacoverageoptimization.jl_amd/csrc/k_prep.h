@@ -1,4 +1,4 @@
-// k_prep.h — per-poll disk preparation, per-disk regions and the device-side walk choice.
+// k_prep.h — the prep launch (penalty chains, fp32 keys, per-disk range records) and the scan's disk records.
 #pragma once
 
 #include <hip/hip_runtime.h>

@@ -172,7 +172,7 @@ struct mac_ctx {
     // In-kernel launch timing (k_common.h ts_begin / ts_end): each profiled walk launch takes
     // nwg consecutive {start, end} slots of `stamps`. a: the scan / tiled launch, b: the poll
     // launch when the device picks the walk (mode != null): the launch that ran is read.
-    // c / f: the chain's first launch (cands_keys or the index) and its last (finalize), whose
+    // c / f: the chain's first launch (the prep) and its last (finalize), whose
     // stamps give the whole poll chain's device span (-1: not stamped)
     struct Prof { int64_t a, na, b, nb; int64_t K; const int* mode; int algo;
                   int64_t c = -1, nc = 0, f = -1, nf = 0; };
@@ -457,7 +457,7 @@ static bool use_tiled(mac_ctx* ctx, int N, const double* h_cands, int64_t three_
     return visits < 0.5 * (double)ctx->M * (double)N;
 }
 
-// Enqueue the column pass + coverage + finalize (+ argmin) on stream s. All pointers device.
+// Enqueue the prep launch + index + walks + finalize (+ argmin) on stream s. All pointers device.
 // area_out/obj_out may be null; best may be null.
 // d_dlimT: cons3 thresholds per UAV (host calls), else d_dlim_raw: the raw d_lim, thresholded
 // where it is read (device calls).
@@ -482,7 +482,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         ctx->stamp_used += nwg;
         return ctx->stamps.as<uint64_t>() + 2 * base;
     };
-    // the objective's penalty and cons3 (the column pass: one sequential chain per candidate)
+    // the objective's penalty and cons3 (the prep launch: one sequential chain per candidate)
     const PenArgs pa{d_rmax, d_prev, d_dlimT, d_dlim_raw, tan_half_fov};
     double* d_vp = nullptr;            // per-candidate penalty (or +inf: cons3)
     const double* d_spart = nullptr;   // poll walk: shared-entry rows
