@@ -104,9 +104,9 @@ __device__ __forceinline__ float key_of(double v, double b, bool& ok)
 // only slower walks). Each thread holds its kIdxPer candidates' doubles in registers through
 // every phase, and the LDS holds only the fp32 keys, the table and the owners (~60 KB), so two
 // workgroups fit a CU and the whole index runs in one round at N = 512.
-// kKeys: a candidate matrix, whose fp32 keys and exactness flags the prep launch wrote
-// (src.keysT, the records' flags; exact doubles from src.cands); else the generator (src.get),
-// keyed here.
+// kKeys: fp32 keys and exactness flags written by the prep launch (src.keysT, the records'
+// flags; exact doubles from src.cands or the generator); else keyed here from src.get (the
+// generator's distinct directions drawn once per disk).
 template <bool kKeys, int kPer>
 __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPer <= 3 ? 8 : 4))) void disk_index_kernel(
     uint64_t* ts, CandSrc src, int N, int K, Grid g, int dedup, IndexOut o)
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
         }
     };
     auto get3 = [&](int k, double& x, double& y, double& r) {
-        if constexpr (kKeys) {  // the column-major matrix (strided: identity path and bases only)
+        if (kKeys && src.cands) {  // the column-major matrix (strided: identity path and bases only)
             const double* c = src.cands + (int64_t)k * src.ldc;
             x = c[i];
             y = c[N + i];

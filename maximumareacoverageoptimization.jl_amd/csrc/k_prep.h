@@ -123,7 +123,7 @@ struct CandSrc {
 //     makes the walk stage or share more entries, never changes a result), packed as two
 //     16-bit tile numbers (range_pack); the estimate is the disks' span areas as (2r/S + 1)^2
 //     (the walk choice's cost). The disk index reduces disk i's records (k_index.h);
-//   keys (keysT != null, matrix sources): the fp32 key fl32(v - v0) of each value, v0 =
+//   keys (keysT != null; matrix or generator): the fp32 key fl32(v - v0) of each value, v0 =
 //     candidate 0's, into keysT[v*ldk + k] (8 consecutive keys: two 16-B stores); the record's
 //     key flag is 1 when one of UAV i's 24 keys does not reproduce its double bit for bit
 //     (k_index.h "Keys": the disk then takes the identity map).
@@ -225,10 +225,13 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
                 else v[c][q] = a.src.get(k, q * N + ii, N);
             }
         }
-        double base[3] = {0.0, 0.0, 0.0};
-        if (kMat && a.keysT) {
+        double base[3] = {0.0, 0.0, 0.0};   // candidate 0's values: the keys' base
+        if (a.keysT) {
 #pragma unroll
-            for (int q = 0; q < 3; ++q) base[q] = a.src.cands[q * N + ii];
+            for (int q = 0; q < 3; ++q) {
+                if constexpr (kMat) base[q] = a.src.cands[q * N + ii];
+                else base[q] = a.src.get(0, q * N + ii, N);
+            }
         }
         if (obj) {
             // pen_term (above), the same operations in the same order
@@ -272,11 +275,8 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
                     est += e * e;
                 }
             }
-            int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
-            any = any && partial_range(xa, xb, xm, a.g.gx0, a.g.invS, a.g.nTx, x0, x1) &&
-                  partial_range(ya, yb, ym, a.g.gy0, a.g.invS, a.g.nTy, y0, y1);
-            bool kb = false;
-            if (kMat && a.keysT) {
+            bool kb = false;   // a key of this disk is inexact (k_index.h "Keys")
+            if (a.keysT) {
 #pragma unroll
                 for (int q = 0; q < 3; ++q)
 #pragma unroll
@@ -285,12 +285,15 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
                         kb |= __builtin_bit_cast(uint64_t, base[q] + (double)f) != __builtin_bit_cast(uint64_t, v[c][q]);
                     }
             }
+            int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
+            any = any && partial_range(xa, xb, xm, a.g.gx0, a.g.invS, a.g.nTx, x0, x1) &&
+                  partial_range(ya, yb, ym, a.g.gy0, a.g.invS, a.g.nTy, y0, y1);
             a.prec[(int64_t)cw * N + i] =
                 make_int4((int)range_pack(any, x0, x1, range_shift(a.g.nTx)),
                           (int)range_pack(any, y0, y1, range_shift(a.g.nTy)),
                           __builtin_bit_cast(int, (float)est), kb ? 1 : 0);
         }
-        if (kMat && a.keysT && iv) {
+        if (a.keysT && iv) {   // the keys: two 16-B stores per variable
 #pragma unroll
             for (int q = 0; q < 3; ++q) {
                 float f[kPrepC];

@@ -499,7 +499,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                                 (ctx->algo == MAC_ALGO_AUTO && K >= kPollMinK));
     // candidates per index thread: 3 (K <= 3073), 6 (K <= 6145); larger: identity map
     const int iper = K <= kIndexMaxK + 1 ? kIdxPer : K <= kIndexMaxKWide + 1 ? kIdxPerWide : 0;
-    const bool want_keys = poll_possible && src.cands && iper;   // the index hashes fp32 keys
+    const bool want_keys = poll_possible && iper;   // the index hashes the prep's fp32 keys
     auto prof_end = [&]() {
         if (!ctx->profile || (ts_a < 0 && ts_b < 0)) return;
         std::lock_guard<std::mutex> lk(ctx->mu);

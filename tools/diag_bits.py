@@ -7,15 +7,28 @@ import __graft_entry__ as ge  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--disks", default="clustered")
+ap.add_argument("--config", type=int, default=4)
 args = ap.parse_args()
 pkg = ge.load_package()
 L = pkg.load_library()
 L.mac_diag_bits_read.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int64]
-x, y, w, C, rmax = pkg.workloads.make_config(4, disks=args.disks)
-ctx = pkg.Context(0, algo="auto")
-ctx.set_points(x, y, w)
-for _ in range(3):
-    ctx.poll_best(C, rmax)
+if args.config == 5:
+    # the last bit-word launch of two config-5 MPC steps (LTMADS polls generated on the device)
+    wl = pkg.workloads
+    rng = wl.SplitMix64(wl.SEED)
+    cfg = wl.CONFIGS[5]
+    fire_kw, x0 = wl.config5_setup(rng, cfg["G"], cfg["N"], cfg["ignition"])
+    ctx = pkg.Context(0, algo="auto")
+    D = pkg.DynamicArea.DynamicArea(**fire_kw, seed=wl.SEED, device=0)
+    sim = pkg.FullSimulation.Simulation(ctx, x0, fire=D, N_iter=100, seed=wl.SEED)
+    for _ in range(2):
+        sim.step()
+else:
+    x, y, w, C, rmax = pkg.workloads.make_config(4, disks=args.disks)
+    ctx = pkg.Context(0, algo="auto")
+    ctx.set_points(x, y, w)
+    for _ in range(3):
+        ctx.poll_best(C, rmax)
 buf = (ctypes.c_uint64 * (256 * 16))()
 assert L.mac_diag_bits_read(buf, 256 * 16) == 0
 a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 16).astype(np.int64)
