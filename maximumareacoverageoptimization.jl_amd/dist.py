@@ -10,8 +10,10 @@ lowest index wins ties, the order in which a sequential poll keeps its first bes
 
 The same exchange drives the multi-GPU MADS loop (config 5, `mads_loop`): every rank steps the
 same LTMADS sequence over its shard of each poll and applies the same global best, so all ranks
-hold the single-GPU loop's iterates. The point list needs no transfer either: the fire stream is
-a deterministic counter-based CA, so every rank regenerates it on its own GPU (DynamicArea).
+hold the single-GPU loop's iterates. The config-5 point list needs no transfer: the fire stream
+is a deterministic counter-based CA, so every rank regenerates it on its own GPU (DynamicArea).
+A list no rank can regenerate (the FirePoints table, an external feed) goes out from one rank by
+one broadcast of the packed list (`broadcast_points`) instead of a host upload per rank.
 """
 from __future__ import annotations
 
@@ -108,6 +110,34 @@ class DeviceGather:
         self.seconds += time.perf_counter() - t0
         self.calls += 1
         return r
+
+
+def broadcast_points(x=None, y=None, w=None, src: int = 0, device="cpu", group=None):
+    """The point list (or a batch of appended points, src/CellFunctions.jl:59-79) from rank
+    `src`'s host arrays to every rank's `device`: rank `src` uploads once, then ONE broadcast of
+    the packed 3 x M float64 tensor (RCCL over xGMI for GPU tensors, gloo for CPU) instead of a
+    host upload per rank — for lists a rank cannot regenerate (the FirePoints table, an external
+    feed; config 5's CA fire is regenerated per rank instead). Returns (x, y, w) tensors on
+    `device` on every rank; feed them to Context.set_points_device / append_points_device."""
+    import torch
+    import torch.distributed as dist
+
+    dev = torch.device(device)
+    rank = dist.get_rank(group)
+    n = torch.zeros(1, dtype=torch.int64, device=dev)
+    if rank == src:
+        n[0] = int(np.asarray(x).size)
+    dist.broadcast(n, src, group=group)
+    M = int(n.item())
+    if rank == src:
+        buf = torch.from_numpy(np.stack([np.asarray(x, dtype=np.float64).ravel(),
+                                         np.asarray(y, dtype=np.float64).ravel(),
+                                         np.asarray(w, dtype=np.float64).ravel()])).to(dev)
+    else:
+        buf = torch.empty((3, M), dtype=torch.float64, device=dev)
+    if M:
+        dist.broadcast(buf, src, group=group)
+    return buf[0].contiguous(), buf[1].contiguous(), buf[2].contiguous()
 
 
 def pack_best(obj: float, idx: int, device="cpu"):

@@ -142,3 +142,40 @@ def test_gloo_world2_sharded_mads_loop():
     for rank, xs, f, it, want_x, want_f, want_it in res:
         assert xs == want_x and f == want_f and it == want_it, rank
     assert res[0][1] == res[1][1]
+
+
+def _bcast_worker(rank, world, port, q):
+    import sys
+    import torch.distributed as dist
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    from importlib import import_module
+    d = import_module(pkg.__name__ + ".dist")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    x, y, w = pkg.workloads.grid_points(30)
+    args = (x, y, w) if rank == 0 else (None, None, None)
+    bx, by, bw = d.broadcast_points(*args)
+    e0 = d.broadcast_points(*(([], [], []) if rank == 0 else (None, None, None)))
+    q.put((rank, np.array_equal(bx.numpy(), x) and np.array_equal(by.numpy(), y)
+           and np.array_equal(bw.numpy(), w), int(e0[0].numel())))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_broadcast_points():
+    """The point list of rank 0 arrives bit-identical on every rank in one broadcast; an empty
+    batch broadcasts as empty."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bcast_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, same, n_empty in res:
+        assert same and n_empty == 0, rank
