@@ -184,9 +184,10 @@ def cpu_baseline(x, y, w, cands, seconds_target: float, threads: int):
     sub.area_batch(cands[:1], 1)
     per_eval = (time.perf_counter() - t0) * (x.size / float(m))
     sub.close()
-    n = max(1, min(cands.shape[0], int(round(seconds_target / max(per_eval, 1e-9))) * threads))
-    n = max(threads if n >= threads else n, 1)
-    n = (n // threads) * threads if n >= threads else n
+    K = cands.shape[0]
+    n = max(1, min(K, int(round(seconds_target / max(per_eval, 1e-9))) * threads))
+    n = max(n, min(threads, K))                          # at least one candidate per thread
+    n = (n // threads) * threads if n >= threads else n  # whole rounds of the threads
     t0 = time.perf_counter()
     pl.area_batch(cands[:n], threads)
     dt = time.perf_counter() - t0
