@@ -25,8 +25,9 @@ constexpr int kFinThreads = 1024;
 // disks are never written and never read). Per batch the map and ncount loads go first, then the
 // gathers and shared rows they select: two memory round trips per batch.
 // obj_k = -area_k + vp_k when obj_out != null. With `counts` (every entry weighs w0) and the poll
-// walk chosen, the rows hold uint32 covered-entry counts per candidate (partial[i][k], and
-// spart[i][k] of the disks with neighbours): area_k = (their integer sum) * w0.
+// walk chosen, the rows hold uint32 covered-entry counts (partial[i][u] per position, gathered
+// through the map, and spart[i][k] per candidate of the disks with neighbours): area_k = (their
+// integer sum) * w0.
 // The poll argmin (fb.best != null) is taken here too, with no launch of its own: every block
 // publishes the lexicographic minimum of its kFinC candidates and the block that arrives last
 // reduces the published minima (finalize_argmin below).
@@ -156,55 +157,76 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
                                                  : (int)blockIdx.x;
     const int k0 = cb * kFinC;
     const int k = k0 + c;
-    const bool poll = mode && *mode == kModePoll;
-    const int G = poll ? n_poll : n_other;
+    // the walk the device chose, loaded first and checked once the first loads are out (the
+    // poll walk's map and neighbour counts are read speculatively: both are valid memory for
+    // either walk), so it costs no round trip of its own
+    const int mv = mode ? *mode : 0;
     // the candidate's penalty, loaded with the first batch of rows (one round trip fewer)
     const double vpk = (vp && sg == 0 && k < K) ? vp[k] : 0.0;
-    if (counts && poll && spart && map) {  // equal weights: integer rows, exact in any order
-        const unsigned* const crow = reinterpret_cast<const unsigned*>(partial);
-        const unsigned* const srow = reinterpret_cast<const unsigned*>(spart);
-        __shared__ uint64_t ired[kFinThreads / kFinC][kFinC];
-        uint64_t a = 0;
-        if (k < K) {
-            // per row: the count at candidate k's position (the poll walk writes one per
-            // position, the map gives candidate k's), plus its shared-entry count when the disk
-            // has neighbours; the two dependent load pairs run side by side
-            constexpr int B = 8;
-            for (int g = sg; g < G; g += B * SG) {
-                unsigned v[B], sv[B];
-                int pos[B];
-                bool sh[B];
+    if (counts && spart && map) {  // equal weights: integer rows, exact in any order
+        constexpr int B = 8;
+        int pos0[B];
+        bool sh0[B];
 #pragma unroll
-                for (int b = 0; b < B; ++b) {
-                    const int gb = g + b * SG;
-                    pos[b] = gb < G ? map[(int64_t)gb * K + k] : -1;
-                    sh[b] = gb < G && ncount[gb] > 0;
+        for (int b = 0; b < B; ++b) {
+            const int gb = sg + b * SG;
+            const bool in = k < K && gb < n_poll;
+            pos0[b] = in ? map[(int64_t)gb * K + k] : -1;
+            sh0[b] = in && ncount[gb] > 0;
+        }
+        if (mv == kModePoll) {
+            const unsigned* const crow = reinterpret_cast<const unsigned*>(partial);
+            const unsigned* const srow = reinterpret_cast<const unsigned*>(spart);
+            __shared__ uint64_t ired[kFinThreads / kFinC][kFinC];
+            const int G = n_poll;
+            uint64_t a = 0;
+            if (k < K) {
+                // per row: the count at candidate k's position (the poll walk writes one per
+                // position, the map gives candidate k's), plus its shared-entry count when the
+                // disk has neighbours
+                for (int g = sg; g < G; g += B * SG) {
+                    unsigned v[B], sv[B];
+                    int pos[B];
+                    bool sh[B];
+#pragma unroll
+                    for (int b = 0; b < B; ++b) {
+                        const int gb = g + b * SG;
+                        if (g == sg) {
+                            pos[b] = pos0[b];
+                            sh[b] = sh0[b];
+                        } else {
+                            pos[b] = gb < G ? map[(int64_t)gb * K + k] : -1;
+                            sh[b] = gb < G && ncount[gb] > 0;
+                        }
+                    }
+#pragma unroll
+                    for (int b = 0; b < B; ++b) {
+                        const int64_t rb = (int64_t)(g + b * SG) * K;
+                        v[b] = pos[b] >= 0 ? crow[rb + pos[b]] : 0u;
+                        sv[b] = sh[b] ? srow[rb + k] : 0u;
+                    }
+#pragma unroll
+                    for (int b = 0; b < B; ++b) a += (uint64_t)v[b] + sv[b];
                 }
-#pragma unroll
-                for (int b = 0; b < B; ++b) {
-                    const int64_t rb = (int64_t)(g + b * SG) * K;
-                    v[b] = pos[b] >= 0 ? crow[rb + pos[b]] : 0u;
-                    sv[b] = sh[b] ? srow[rb + k] : 0u;
-                }
-#pragma unroll
-                for (int b = 0; b < B; ++b) a += (uint64_t)v[b] + sv[b];
             }
-        }
-        ired[sg][c] = a;
-        __syncthreads();
-        if (sg == 0 && k < K) {
-            uint64_t n = 0;
+            ired[sg][c] = a;
+            __syncthreads();
+            if (sg == 0 && k < K) {
+                uint64_t n = 0;
 #pragma unroll
-            for (int q = 0; q < SG; ++q) n += ired[q][c];
-            const double area = (double)n * w0;
-            if (area_out) area_out[k] = area;
-            if (vp) o = -area + vpk;
-            if (obj_out) obj_out[k] = o;
+                for (int q = 0; q < SG; ++q) n += ired[q][c];
+                const double area = (double)n * w0;
+                if (area_out) area_out[k] = area;
+                if (vp) o = -area + vpk;
+                if (obj_out) obj_out[k] = o;
+            }
+            if (fb.best && t < kWave) finalize_argmin(fb, o, k, k < K);
+            ts_end(ts);
+            return;
         }
-        if (fb.best && t < kWave) finalize_argmin(fb, o, k, k < K);
-        ts_end(ts);
-        return;
     }
+    const bool poll = mv == kModePoll;
+    const int G = poll ? n_poll : n_other;
     const bool rows = spart && poll;
     const int* mp = (map && poll) ? map : nullptr;
     constexpr int kFinB = 8;

@@ -137,9 +137,11 @@ __device__ __forceinline__ void coverage_poll_body(
     const uint64_t diag_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
     const int bx = blockIdx.x, by = blockIdx.y;
+    // the walk the device chose: loaded first, checked once each role's first loads are out
+    const int mv = mode ? *mode : kModePoll;
     // launch hints for the next poll (mapped host memory, maxcover.hip): the disks with
     // neighbours (the bit-word kernel) and the most distinct positions of a disk (walk rows)
-    if (bx == 0 && by == 0 && dc_out && (!mode || *mode == kModePoll)) {
+    if (bx == 0 && by == 0 && dc_out && mv == kModePoll) {
         int um = 0;
         for (int d = threadIdx.x; d < N; d += kPollThreads) um = max(um, ucount[d]);
 #pragma unroll
@@ -194,8 +196,8 @@ __device__ __forceinline__ void coverage_poll_body(
             job = -1;
         }
     };
-    if (mode && *mode != kModePoll) return;
     if (bx >= nwalk) {  // then: the shared entries
+        if (mv != kModePoll) return;
         shared_jobs(bx - nwalk);
         MAC_DIAG_STAMP(diag_t0, 2, (uint64_t)(dcount[kDcBits] + dcount[kDcOther]));
         return;
@@ -256,8 +258,9 @@ __device__ __forceinline__ void coverage_poll_body(
         }
     };
     const int kb0 = by * kPollKPB;   // this workgroup's first position slice
-    if (kb0 >= U && by > 0) break;     // uniform: no slice of this disk for this row
+    if (by > 0 && kb0 >= U) break;     // uniform: no slice of this disk for this row
     load_lanes(kb0);
+    if (mv != kModePoll) return;       // (after the first loads: the check costs no round trip)
     // the bit-word kernel (launched next) adds its per-split counts into spart row i
     if (by == 0 && counts && qual && qual[i] && bits_on &&
         dcount[kDcBits] + dcount[kDcOther] > (bits_on == 2 ? 0 : kBitsMinDisks))
@@ -493,7 +496,7 @@ __device__ __forceinline__ void coverage_poll_body(
     }
     MAC_DIAG_STAMP(diag_t0, 3, ((uint64_t)nc << 40) | ((uint64_t)U << 20) | (uint64_t)diag_entries);
     } while (0);
-    shared_jobs(-1);
+    if (mv == kModePoll) shared_jobs(-1);
 }
 
 // timed entry point (ts: in-kernel launch timing, k_common.h)
