@@ -12,8 +12,14 @@
 
 namespace mac {
 
-constexpr int kFinC = 16;   // candidates per finalize block (x 64 slice groups)
-constexpr int kFinMaxBlk = 256;   // finalize blocks whose minima the last block loads at once
+#ifndef MAC_FIN_C
+#define MAC_FIN_C 16
+#endif
+constexpr int kFinC = MAC_FIN_C;   // candidates per finalize block (x 1024 / kFinC slice groups)
+#ifndef MAC_FIN_MAXBLK
+#define MAC_FIN_MAXBLK 256
+#endif
+constexpr int kFinMaxBlk = MAC_FIN_MAXBLK;   // finalize blocks whose minima the last block loads at once
 constexpr int kFinThreads = 1024;
 
 // Block = 16 candidates x 64 slice groups. area_k = sum over slices g of the slice's credit in a

@@ -127,10 +127,13 @@ struct CandSrc {
 //     candidate 0's, into keysT[v*ldk + k] (8 consecutive keys: two 16-B stores); the record's
 //     key flag is 1 when one of UAV i's 24 keys does not reproduce its double bit for bit
 //     (k_index.h "Keys": the disk then takes the identity map).
-constexpr int kPrepC = 8;        // candidates per workgroup
+#ifndef MAC_PREP_C
+#define MAC_PREP_C 8
+#endif
+constexpr int kPrepC = MAC_PREP_C;   // candidates per workgroup (a multiple of 4)
 constexpr int kPrepU = 512;      // UAVs per block = threads per workgroup
 
-// keysT row pitch: rows start on 128-B boundaries (and hold every workgroup's 8 keys)
+// keysT row pitch: rows start on 128-B boundaries (and hold every workgroup's kPrepC keys)
 __host__ __device__ inline int keys_ld(int K) { return (K + 31) & ~31; }
 
 struct PrepArgs {
@@ -300,8 +303,9 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
 #pragma unroll
                 for (int c = 0; c < kPrepC; ++c) f[c] = (float)(v[c][q] - base[q]);
                 float4* dst = reinterpret_cast<float4*>(a.keysT + (int64_t)(q * N + i) * a.ldk + k0);
-                dst[0] = make_float4(f[0], f[1], f[2], f[3]);
-                dst[1] = make_float4(f[4], f[5], f[6], f[7]);
+#pragma unroll
+                for (int h = 0; h < kPrepC / 4; ++h)
+                    dst[h] = make_float4(f[4 * h], f[4 * h + 1], f[4 * h + 2], f[4 * h + 3]);
             }
         }
         MAC_PREP_STAMP(2 + 3 * (ib / kPrepU));
