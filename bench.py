@@ -328,8 +328,12 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # config 4's default timed region: 200 polls (~18 ms of device work, a steady state the
+    # 20-poll region's 1.8 ms did not always reach), after 20 warmup polls
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: 200 for configs 2-4, 3 for config 5)")
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="warmup steps (default: 20 for configs 2-4, 1 for config 5)")
     ap.add_argument("--config", type=int, default=4, choices=(2, 3, 4, 5),
                     help="4 (default): one MADS poll per step; 5: one end-to-end MPC step "
                          "(CA fire stream + rmvCoveredPOI + a MADS run) per step")
@@ -362,6 +366,10 @@ def main():
                     help="nccl (= RCCL on ROCm) for the real multi-GPU run; gloo only to rehearse "
                          "N>1 with several ranks sharing one GPU (MAXCOVER_BENCH_DEVICE)")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 3 if args.config == 5 else 200
+    if args.warmup is None:
+        args.warmup = 1 if args.config == 5 else 20
 
     import torch
     import torch.distributed as dist
