@@ -296,6 +296,8 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
             "evaluations": evals,
             "time_split_s": {k: float(np.sum([r[k] for r in recs]))
                              for k in ("fire_s", "remove_s", "mads_s")},
+            "mads_host_split_s": {k: float(np.sum([r.get("mads_host_s", {}).get(k, 0.0) for r in recs]))
+                                  for k in ("host_enqueue_s", "host_perm_s", "wait_s", "host_post_s")},
             "parallelism": ("1 GPU" if world == 1 else
                             f"{world} GPUs: every poll's 2n candidates sharded, 16-B all-gather "
                             f"per MADS iteration; fire stream regenerated per GPU"),

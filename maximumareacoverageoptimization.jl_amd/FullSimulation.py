@@ -132,6 +132,8 @@ class Simulation:
         rec = dict(t=t, points=int(ctx.num_points), added=int(added), kept=int(kept.size),
                    f=st["f"], iterations=st["iterations"], evaluations=st["evaluations"],
                    fire_s=t1 - t0, remove_s=t2 - t1, mads_s=t3 - t2, step_s=t3 - t0,
+                   mads_host_s={k: float(st.get(k, 0.0)) for k in
+                                ("host_enqueue_s", "host_perm_s", "wait_s", "host_post_s")},
                    input=single_input)
         self.records.append(rec)
         self.x_prev = x_out                                              # perfect tracking

@@ -49,7 +49,10 @@ constexpr int kBitsK = kBitsPT * kBitsThreads;      // candidates per job (4096)
 constexpr int kBitsWP = 2;                          // 64-entry words per pass
 constexpr int kBitsGrp = 4;                         // disks per table group
 constexpr int kBitsD = kPollNbr + 1;
-constexpr int kBitsSplit = 2;                       // jobs per disk (equal weights)
+#ifndef MAC_BITS_SPLIT
+#define MAC_BITS_SPLIT 2
+#endif
+constexpr int kBitsSplit = MAC_BITS_SPLIT;          // jobs per disk (equal weights)
 constexpr int kBitsPL = 2;                          // positions per lane in the tables
 constexpr int kBitsBlk = kBitsPL * kWave;           // positions per wave block
 constexpr int kBitsE = 1024;                        // shared entries staged in LDS at a time
