@@ -7,6 +7,7 @@
 
 #include "predicate.h"
 #include "k_common.h"
+#include "k_prep.h"
 
 #pragma clang fp contract(off)
 
@@ -44,6 +45,16 @@ struct FinBest {
     int64_t idx_base;
     unsigned long long* blk;   // [gridDim.x][2] per-block minima {obj bits, index}
     unsigned* arrive;          // arrival counter, zero between launches (the last block resets it)
+    // the pipelined native MADS loop (k_prep.h MadsState): the last block also applies the poll's
+    // update (mads_step); st == null: none
+    MadsState* st;
+    const double* x;           // the poll's incumbent (its generator's xinc), 3N
+    double* x_next;            // the incumbent after the poll
+    const int* rp;             // the poll's row / column permutations
+    const int* cp;
+    uint64_t state;            // the poll's stream state
+    int n, ell_max;
+    uint64_t done_seq;         // mirror seq word once the loop has stopped (the host's wait ends)
 };
 
 // Check word of a mirrored result (host: mirror_check in maxcover.hip): the host accepts the slot
@@ -56,6 +67,37 @@ __host__ __device__ __forceinline__ uint64_t mirror_check(uint64_t o, uint64_t i
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
+}
+
+// The pipelined MADS loop's update, by the wave that took the poll's argmin (every lane holds
+// bo, gidx): mac_mads_update's arithmetic (maxcover.hip; src/TDM_STATIC_opt.jl's NOMAD poll
+// acceptance: a strictly better objective moves the incumbent and coarsens the mesh, else the mesh
+// is refined), with the same ltmads_entry values and per-variable adds, so the pipelined loop visits
+// the stepper's incumbents bit for bit. ell, f: the state before the poll.
+__device__ __forceinline__ void mads_step(const FinBest& fb, double bo, int64_t gidx, int ell, double f)
+{
+    const int lane = threadIdx.x & (kWave - 1);
+    const int n = fb.n;
+    const double* __restrict__ x = fb.x;
+    double* __restrict__ xn = fb.x_next;
+    const bool better = gidx >= 0 && bo < f;
+    if (better) {
+        const int64_t b = (int64_t)1 << ell;
+        const bool plus = gidx < n;
+        const int c = fb.cp[plus ? (int)gidx : (int)gidx - n];
+        for (int v = lane; v < n; v += kWave) {
+            const double d = ltmads_entry(fb.state, n, b, fb.rp[v], c);
+            xn[v] = plus ? x[v] + d : x[v] - d;
+        }
+    } else {
+        for (int v = lane; v < n; v += kWave) xn[v] = x[v];
+    }
+    if (lane == 0) {
+        const int e = better ? (ell + 1 < fb.ell_max ? ell + 1 : fb.ell_max) : ell - 1;
+        fb.st->f = better ? bo : f;
+        fb.st->ell = e;
+        fb.st->it += 1;
+    }
 }
 
 __device__ __forceinline__ void argmin_take(double& v1, int& i1, double v2, int i2)
@@ -95,6 +137,9 @@ __device__ __forceinline__ void finalize_argmin(const FinBest& fb, double o, int
     }
     old = __shfl(old, 0, kWave);
     if (old != gridDim.x - 1) return;   // wave-uniform: not the last block
+    // the pipelined MADS loop's state, loaded beside the minima (a stopped loop: no result)
+    const int ell = fb.st ? fb.st->ell : 0;
+    const double fcur = fb.st ? fb.st->f : 0.0;
     bv = __builtin_inf();
     bi = -1;
     // every block's minimum in flight at once (kFinMaxBlk / 64 per lane), then the reduction
@@ -121,9 +166,14 @@ __device__ __forceinline__ void finalize_argmin(const FinBest& fb, double o, int
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1)
         argmin_take(bv, bi, __shfl_xor(bv, off, kWave), __shfl_xor(bi, off, kWave));
+    const double bo = bi >= 0 ? bv : __builtin_inf();
+    const int64_t gidx = bi >= 0 ? fb.idx_base + bi : (int64_t)-1;
+    if (fb.st && ell < 0) {   // the loop stopped before this poll
+        if (lane == 0) __hip_atomic_store(fb.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    if (fb.st) mads_step(fb, bo, gidx, ell, fcur);
     if (lane == 0) {
-        const double bo = bi >= 0 ? bv : __builtin_inf();
-        const int64_t gidx = bi >= 0 ? fb.idx_base + bi : (int64_t)-1;
         fb.best[0] = bo;
         fb.best[1] = __builtin_bit_cast(double, gidx);
         __hip_atomic_store(fb.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -138,6 +188,9 @@ __device__ __forceinline__ void finalize_argmin(const FinBest& fb, double o, int
             fb.mirror[1] = ix;
             fb.mirror[2] = fb.seq;
             fb.mirror[3] = mirror_check(o, ix, fb.seq);
+            // a pipelined loop that has just stopped: polls after this one write no slot, so the
+            // seq word jumps past every seq the host may wait for
+            if (fb.st && !(gidx >= 0 && bo < fcur) && ell == 0) fb.mirror[2] = fb.done_seq;
         }
     }
 }

@@ -109,8 +109,9 @@ __device__ __forceinline__ float key_of(double v, double b, bool& ok)
 // generator's distinct directions drawn once per disk).
 template <bool kKeys, int kPer>
 __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPer <= 3 ? 8 : 4))) void disk_index_kernel(
-    uint64_t* ts, CandSrc src, int N, int K, Grid g, int dedup, IndexOut o)
+    uint64_t* ts, CandSrc src0, int N, int K, Grid g, int dedup, IndexOut o)
 {
+    CandSrc src = src0;
     constexpr int kIdxPer = kPer;
     constexpr int kIndexMaxK = IdxShape<kPer>::MaxK;
     constexpr int kIndexSlots = IdxShape<kPer>::Slots;
@@ -125,7 +126,7 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
 
     const int per_xcd = (N + 7) / 8;
     const int i = (int)(blockIdx.x % 8) * per_xcd + (int)(blockIdx.x / 8);
-    if (i >= N) {   // uniform
+    if (i >= N || !src.resolve()) {   // uniform
         ts_end(ts);
         return;
     }

@@ -78,6 +78,17 @@ __host__ __device__ __forceinline__ double ltmads_entry(uint64_t state, int64_t 
     return (double)(lo + (int64_t)__builtin_floor(u * (double)span));
 }
 
+// The native MADS loop's state on the device when its polls are pipelined (maxcover.hip
+// mads_run_pipelined): the finalize of poll t applies poll t's update (k_final.h mads_step) and
+// poll t + 1's launches read the mesh index from here, so the host enqueues polls ahead of their
+// outcomes. ell < 0 (the mesh precision limit) stops the loop: every later launch returns at once.
+struct MadsState {
+    double f;      // objective at the incumbent
+    int64_t it;    // polls applied
+    int ell;       // mesh index of the next poll (step 2^ell)
+    int pad;
+};
+
 // Where candidate coordinates come from: a 3N x K column-major matrix (the batch APIs), or a
 // complete LTMADS poll around an incumbent generated on the fly (the native MADS driver):
 // candidate k < n is x + B[:, k], k >= n is x - B[:, k - n], B = L[rp][:, cp] (variable v of a
@@ -94,6 +105,17 @@ struct CandSrc {
     int64_t b;             // 2^ell
     int k0;                // generator: candidate k of this source is candidate k0 + k of the poll
                            // (a rank's shard of it)
+    const MadsState* mst;  // generator, pipelined MADS loop: b from the device state (else null)
+    // Called at the top of every launch that reads the source: b = 2^ell from the device state;
+    // false once the loop has stopped (the launch returns at once). Uniform per workgroup.
+    __device__ __forceinline__ bool resolve()
+    {
+        if (!mst) return true;
+        const int e = mst->ell;
+        if (e < 0) return false;
+        b = (int64_t)1 << e;
+        return true;
+    }
     __device__ __forceinline__ double get(int kl, int v, int N) const
     {
         if (cands) return cands[(int64_t)kl * ldc + v];
@@ -336,6 +358,10 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
 __global__ __launch_bounds__(kPrepU) __attribute__((amdgpu_waves_per_eu(4))) void prep_kernel(uint64_t* ts, PrepArgs a)
 {
     ts_begin(ts);   // profiling only (the chain's first launch: k_common.h)
+    if (!a.src.resolve()) {
+        ts_end(ts);
+        return;
+    }
     // XCD-aware: workgroups b and b + 8 share an XCD (round-robin dispatch), so consecutive
     // candidate groups — which fill the same lines of keysT and of the records — go to one XCD
     const int per = (int)((gridDim.x + 7) / 8), b = (int)blockIdx.x;

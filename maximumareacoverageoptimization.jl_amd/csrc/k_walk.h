@@ -249,7 +249,7 @@ __global__ __launch_bounds__(kBlock) void walk_setup_kernel(
     int* __restrict__ ncount, int* __restrict__ dlist, int* __restrict__ dcount,
     const double2* __restrict__ cost,
     double ratio, int forced, int* __restrict__ mode, const int* __restrict__ ucount,
-    int* __restrict__ qual)
+    int* __restrict__ qual, const MadsState* __restrict__ halt)
 {
     ts_begin(ts);
     // the neighbour lists' regions, loaded beside the walk choice's costs (one round trip)
@@ -261,6 +261,14 @@ __global__ __launch_bounds__(kBlock) void walk_setup_kernel(
     for (int q = 0; q < kNbrPre; ++q) {
         const int j = threadIdx.x + q * kBlock;
         Q[q] = j < i && i < N ? region[j] : none;
+    }
+    // a stopped pipelined MADS loop (k_prep.h MadsState; checked once the regions are in
+    // flight): no walk; the poll kernel, the bit-word kernel and the finalize's argmin see
+    // mode 0 / the state and return
+    if (halt && halt->ell < 0) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) mode[0] = 0;
+        ts_end(ts);
+        return;
     }
     const int m = walk_choice(N, K, cost, ratio, forced);
     if (blockIdx.x == 0 && threadIdx.x == 0) mode[0] = m;

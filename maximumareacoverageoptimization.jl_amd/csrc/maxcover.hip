@@ -457,6 +457,14 @@ static bool use_tiled(mac_ctx* ctx, int N, const double* h_cands, int64_t three_
     return visits < 0.5 * (double)ctx->M * (double)N;
 }
 
+// The poll walk's chain (prep keys and records, disk index, walk choice, poll kernel) runs for this
+// evaluation: the tiled family, candidates and entries present, and the poll walk allowed.
+static bool poll_walk_possible(const mac_ctx* ctx, int N, int K, bool tiled)
+{
+    return tiled && N > 0 && ctx->M > 0 &&
+           (ctx->algo == MAC_ALGO_POLL || N > kTiledMaxN || (ctx->algo == MAC_ALGO_AUTO && K >= kPollMinK));
+}
+
 // Enqueue the prep launch + index + walks + finalize (+ argmin) on stream s. All pointers device.
 // area_out/obj_out may be null; best may be null.
 // d_dlimT: cons3 thresholds per UAV (host calls), else d_dlim_raw: the raw d_lim, thresholded
@@ -465,7 +473,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                          int K, bool tiled, const double* d_rmax, double penalty,
                          const double* d_prev, const double* d_dlimT, const double* d_dlim_raw,
                          double tan_half_fov, double* d_area, double* d_obj, double* d_best,
-                         int64_t idx_base, uint64_t* d_mirror = nullptr, uint64_t mirror_seq = 0)
+                         int64_t idx_base, uint64_t* d_mirror = nullptr, uint64_t mirror_seq = 0,
+                         const FinBest* fb_mads = nullptr)
 {
     const int64_t M = ctx->M;
     int n_poll = N, n_other = 1;
@@ -494,9 +503,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         d_vp = L->vp.as<double>();
     }
     const bool big = N > kTiledMaxN;
-    const bool poll_possible = tiled && N > 0 && M > 0 &&
-                               (ctx->algo == MAC_ALGO_POLL || big ||
-                                (ctx->algo == MAC_ALGO_AUTO && K >= kPollMinK));
+    const bool poll_possible = poll_walk_possible(ctx, N, K, tiled);
     // candidates per index thread: 3 (K <= 3073), 6 (K <= 6145); larger: identity map
     const int iper = K <= kIndexMaxK + 1 ? kIdxPer : K <= kIndexMaxKWide + 1 ? kIdxPerWide : 0;
     const bool want_keys = poll_possible && iper;   // the index hashes the prep's fp32 keys
@@ -640,7 +647,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                                L->region.as<int4>(), L->nbr.as<uint16_t>(), L->nboxT.as<int4>(),
                                L->ncount.as<int>(), L->dlist.as<int>(), L->mode.as<int>() + 1,
                                L->cost.as<double2>(), kPollCostRatio, forced, L->mode.as<int>(),
-                               L->ucount.as<int>(), L->qual.as<int>());
+                               L->ucount.as<int>(), L->qual.as<int>(), src.mst);
             HCK(hipGetLastError());
             d_mode = L->mode.as<int>();
             d_umap = d_map;
@@ -724,8 +731,13 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         L->finblk.reserve(2 * sizeof(unsigned long long) * nfin);
         if (L->finarrive.grow(sizeof(unsigned)))   // zero once; the last block of each launch resets it
             HCK(hipMemsetAsync(L->finarrive.p, 0, L->finarrive.cap, s));
-        fb = FinBest{d_best, d_mirror, mirror_seq, idx_base, L->finblk.as<unsigned long long>(),
-                     L->finarrive.as<unsigned>()};
+        if (fb_mads) fb = *fb_mads;   // the pipelined MADS loop's update fields
+        fb.best = d_best;
+        fb.mirror = d_mirror;
+        fb.seq = mirror_seq;
+        fb.idx_base = idx_base;
+        fb.blk = L->finblk.as<unsigned long long>();
+        fb.arrive = L->finarrive.as<unsigned>();
     }
     uint64_t* tsf = ts_c >= 0 ? take_ts(nfin, ts_f, ts_nf) : nullptr;
     hipLaunchKernelGGL(finalize_kernel, dim3(nfin), dim3(kFinThreads), 0, s,
@@ -1482,21 +1494,36 @@ struct mac_mads {
     int64_t polled_b = 0;        // 2^ell of the poll awaiting its update (0: none)
     double h_enq = 0, h_perm = 0, h_wait = 0, h_post = 0;
     std::chrono::steady_clock::time_point t0;
+    // the pipelined loop (mads_run_pipelined): incumbent double buffer, device state, permutation
+    // rings
+    DevBuf d_x, d_st, d_ring;
+    PinnedBuf h_ring;
+    ~mac_mads()
+    {
+        d_x.release();
+        d_st.release();
+        d_ring.release();
+        h_ring.release();
+    }
 };
 
 static double* mads_best_ptr(mac_mads* m) { return m->ext_best ? m->ext_best : m->L->best.as<double>(); }
 
 // slot: the poll's best through the mapped slot finalize's last block writes (mads_wait_best),
 // else a 16-B copy
+static void mads_make_slot(mac_mads* m)
+{
+    if (m->d_slot) return;
+    m->hslot.reserve(64, hipHostMallocMapped | hipHostMallocCoherent);
+    std::memset(m->hslot.p, 0, 64);
+    void* dp = nullptr;
+    HCK(hipHostGetDevicePointer(&dp, m->hslot.p, 0));
+    m->d_slot = (uint64_t*)dp;
+}
+
 static void mads_best_of(mac_mads* m, const CandSrc& src, int Kc, int64_t idx_base, bool slot = false)
 {
-    if (slot && !m->d_slot) {
-        m->hslot.reserve(64, hipHostMallocMapped | hipHostMallocCoherent);
-        std::memset(m->hslot.p, 0, 64);
-        void* dp = nullptr;
-        HCK(hipHostGetDevicePointer(&dp, m->hslot.p, 0));
-        m->d_slot = (uint64_t*)dp;
-    }
+    if (slot) mads_make_slot(m);
     m->slotted = slot;
     enqueue_eval(m->ctx, m->L, m->s, src, m->N, Kc, use_tiled(m->ctx, m->N, nullptr, m->n),
                  m->L->rmax.as<double>(), m->penalty, m->d_prev, m->d_dlimT,
@@ -1746,6 +1773,136 @@ void mac_mads_destroy(mac_mads* m)
     mads_free(m);
 }
 
+// ------------------------------------------------------------------ pipelined MADS loop
+// mac_mads_run on one GPU when the poll walk runs: every poll's finalize applies the poll's update on
+// the device (k_final.h mads_step) and the next poll's launches read the mesh index from the device
+// state (k_prep.h MadsState), so the host enqueues poll t + kMadsWindow - 1 while poll t runs and
+// waits only to bound that window (on the mapped slot's seq word). The permutations do not depend
+// on the outcomes: computed kMadsAhead iterations ahead into a pinned ring and uploaded kMadsChunk
+// iterations per copy. Same incumbents, objective and counts as the stepper loop, bit for bit (the
+// same arithmetic, only where it runs differs): tests/test_gpu_parity.py
+// test_native_mads_pipelined_matches_stepper.
+static constexpr int kMadsWindow = 3;   // polls in flight
+static constexpr int kMadsAhead = 16;   // permutations computed ahead of the enqueued poll
+static constexpr int kMadsChunk = 8;    // iterations per permutation upload
+static constexpr int kMadsRing = 32;    // permutation slots (device and pinned)
+static constexpr uint64_t kMadsDoneSeq = 1ull << 62;   // seq word of a stopped loop
+
+static bool mads_pipelinable(const mac_mads* m)
+{
+    return m->lo == 0 && m->hi == m->K && !m->ext_best && m->prm.n_iter > 0 &&
+           poll_walk_possible(m->ctx, m->N, m->K, use_tiled(m->ctx, m->N, nullptr, m->n));
+}
+
+static void mads_run_pipelined(mac_mads* m)
+{
+    using clk = std::chrono::steady_clock;
+    const int n = m->n;
+    const int64_t n_iter = m->prm.n_iter;
+    const size_t slot_ints = 2 * (size_t)n;
+    hipStream_t s = m->s;
+    mads_make_slot(m);
+    m->d_x.reserve(sizeof(double) * 2 * n);
+    m->d_st.reserve(sizeof(MadsState));
+    m->d_ring.reserve(sizeof(int) * slot_ints * kMadsRing);
+    m->h_ring.reserve(sizeof(int) * slot_ints * kMadsRing);
+    double* dx = m->d_x.as<double>();
+    MadsState* dst = m->d_st.as<MadsState>();
+    int* dring = m->d_ring.as<int>();
+    int* hring = (int*)m->h_ring.p;
+    const uint64_t step = m->per_iter * 0x9E3779B97F4A7C15ull;
+    const uint64_t seed_state = m->state;   // iteration t's stream state: seed + (t - 1) * step
+    auto state_of = [&](int64_t t) { return seed_state + (uint64_t)(t - 1) * step; };
+    auto perms_of = [&](int64_t t) {   // into the pinned ring
+        int* h = hring + (size_t)((t - 1) % kMadsRing) * slot_ints;
+        stream_permutation(state_of(t), (uint64_t)n + m->T + 1, n, m->rp_next);
+        stream_permutation(state_of(t), (uint64_t)n + m->T + n + 1, n, m->cp_next);
+        std::memcpy(h, m->rp_next.data(), sizeof(int) * n);
+        std::memcpy(h + n, m->cp_next.data(), sizeof(int) * n);
+    };
+    int64_t uploaded = 0;   // iterations [1, uploaded] on the device
+    auto upload_to = [&](int64_t t1) {   // [uploaded + 1, t1]: contiguous slots (chunk aligned)
+        const int64_t t0 = uploaded + 1;
+        if (t1 < t0) return;
+        const size_t q0 = (size_t)((t0 - 1) % kMadsRing);
+        HCK(hipMemcpyAsync(dring + q0 * slot_ints, hring + q0 * slot_ints,
+                           sizeof(int) * slot_ints * (size_t)(t1 - t0 + 1), hipMemcpyHostToDevice, s));
+        uploaded = t1;
+    };
+    // the incumbent and the state: x0 (begin's pinned staging holds it), f(x0), ell0
+    const auto ta = clk::now();
+    HCK(hipMemcpyAsync(dx, m->hx, sizeof(double) * n, hipMemcpyHostToDevice, s));
+    const MadsState st0{m->f, 0, m->ell, 0};
+    HCK(hipMemcpy(dst, &st0, sizeof(st0), hipMemcpyHostToDevice));
+    int64_t computed = std::min<int64_t>(n_iter, kMadsAhead);
+    for (int64_t t = 1; t <= computed; ++t) perms_of(t);
+    for (int64_t t = kMadsChunk; t <= computed; t += kMadsChunk) upload_to(t);
+    upload_to(computed);
+    m->h_perm += std::chrono::duration<double>(clk::now() - ta).count();
+
+    const volatile uint64_t* seqw = (const volatile uint64_t*)m->hslot.p + 2;
+    bool stopped = false;
+    for (int64_t t = 1; t <= n_iter && !stopped; ++t) {
+        const auto t1 = clk::now();
+        if (t > kMadsWindow) {   // poll t - kMadsWindow finished (or the loop stopped)
+            const uint64_t want = (uint64_t)(t - kMadsWindow);
+            for (int spin = 0; *seqw < want; ++spin) {
+                if ((spin & 1023) == 1023 &&
+                    std::chrono::duration<double, std::milli>(clk::now() - t1).count() > 50.0) {
+                    HCK(hipStreamSynchronize(s));   // a failed launch surfaces here
+                    if (*seqw < want) throw HipError{hipErrorUnknown, "pipelined MADS poll lost", __LINE__};
+                }
+            }
+            stopped = *seqw >= kMadsDoneSeq;
+            if (stopped) break;
+        }
+        const auto t2 = clk::now();
+        const int* rp = dring + (size_t)((t - 1) % kMadsRing) * slot_ints;
+        CandSrc src{};
+        src.xinc = dx + (size_t)((t - 1) & 1) * n;
+        src.rp = rp;
+        src.cp = rp + n;
+        src.state = state_of(t);
+        src.b = 0;   // from the device state
+        src.k0 = 0;
+        src.mst = dst;
+        FinBest fbm{};
+        fbm.st = dst;
+        fbm.x = src.xinc;
+        fbm.x_next = dx + (size_t)(t & 1) * n;
+        fbm.rp = src.rp;
+        fbm.cp = src.cp;
+        fbm.state = src.state;
+        fbm.n = n;
+        fbm.ell_max = (int)m->prm.ell_max;
+        fbm.done_seq = kMadsDoneSeq;
+        enqueue_eval(m->ctx, m->L, s, src, m->N, m->K, true, m->L->rmax.as<double>(), m->penalty,
+                     m->d_prev, m->d_dlimT, m->d_prev ? m->L->dlimraw.as<double>() : nullptr,
+                     m->tan_half_fov, m->L->area.as<double>(), m->L->obj.as<double>(),
+                     m->L->best.as<double>(), 0, m->d_slot, (uint64_t)t, &fbm);
+        const auto t3 = clk::now();
+        if (computed < n_iter) {   // one iteration's permutations per poll, uploaded per chunk
+            perms_of(++computed);
+            if (computed % kMadsChunk == 0 || computed == n_iter) upload_to(computed);
+        }
+        const auto t4 = clk::now();
+        m->h_wait += std::chrono::duration<double>(t2 - t1).count();
+        m->h_enq += std::chrono::duration<double>(t3 - t2).count();
+        m->h_perm += std::chrono::duration<double>(t4 - t3).count();
+    }
+    const auto t5 = clk::now();
+    HCK(hipStreamSynchronize(s));
+    MadsState st{};
+    HCK(hipMemcpy(&st, dst, sizeof(st), hipMemcpyDeviceToHost));
+    HCK(hipMemcpy(m->x.data(), dx + (size_t)(st.it & 1) * n, sizeof(double) * n, hipMemcpyDeviceToHost));
+    m->f = st.f;
+    m->it = st.it;
+    m->ell = st.ell;
+    m->evals = 1 + st.it * (int64_t)m->K;
+    m->state = state_of(st.it + 1);
+    m->h_wait += std::chrono::duration<double>(clk::now() - t5).count();
+}
+
 int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const double* r_max,
                      double penalty, const double* prev, const double* d_lim, double tan_half_fov,
                      const mac_mads_params* prm, double* x_out, mac_mads_stats* st)
@@ -1756,14 +1913,24 @@ int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const doub
     int32_t rc = mac_mads_begin(ctx, x0, three_n, r_max, penalty, prev, d_lim, tan_half_fov, prm,
                                 0, 2 * three_n, &m);
     if (rc) return rc;
-    for (;;) {
-        int32_t done = 0;
-        double bo = 0.0;
-        int64_t bi = -1;
-        rc = mac_mads_poll(m, &done, &bo, &bi);
-        if (rc || done) break;
-        rc = mac_mads_update(m, bo, bi);
-        if (rc) break;
+    if (mads_pipelinable(m)) {
+        try {
+            set_device(ctx);
+            mads_run_pipelined(m);
+        } catch (...) {
+            mac_mads_destroy(m);
+            throw;
+        }
+    } else {
+        for (;;) {
+            int32_t done = 0;
+            double bo = 0.0;
+            int64_t bi = -1;
+            rc = mac_mads_poll(m, &done, &bo, &bi);
+            if (rc || done) break;
+            rc = mac_mads_update(m, bo, bi);
+            if (rc) break;
+        }
     }
     if (!rc) rc = mac_mads_result(m, x_out, st);
     mac_mads_destroy(m);

@@ -841,3 +841,51 @@ def test_native_mads_sharded_steppers(ctx, pkg, world):
         assert np.array_equal(xs, want_x)
         assert st["f"] == want["f"] and st["iterations"] == want["iterations"]
         assert st["evaluations"] == want["evaluations"]
+
+
+@pytest.mark.parametrize("N,n_iter,ell0,ell_max,cons3,stall", [
+    (40, 60, 2, 5, True, False),     # iteration limit, cons3
+    (40, 200, 2, 4, False, True),    # mesh precision limit after 3 polls: later polls already enqueued
+    (40, 1, 2, 5, True, False),      # fewer polls than the window
+    (40, 2, 2, 5, False, False),
+    (300, 25, 3, 6, True, False),    # K = 1800
+])
+def test_native_mads_pipelined_matches_stepper(ctx, pkg, N, n_iter, ell0, ell_max, cons3, stall):
+    """mac_mads_run's pipelined loop (each poll's update applied on the device by its finalize,
+    polls enqueued ahead of their outcomes: maxcover.hip mads_run_pipelined) == the stepper driven
+    one poll at a time from Python (mac_mads_begin / _poll / _update, host update): same iterate
+    bit for bit, objective, iteration and evaluation counts and status. `stall`: two entries
+    under UAV 0 with every radius at r_max, so no poll can improve (a move keeps the union, a
+    radius change adds penalty) and the loop stops at the mesh precision limit after ell0 + 1
+    polls while later polls are already enqueued."""
+    wl = pkg.workloads
+    rng = wl.SplitMix64(9000 + N + n_iter)
+    r_max = np.full(N, 30.0 * TAN50)
+    x0 = np.concatenate([np.round(200 + rng.uniform(N) * 500), np.round(200 + rng.uniform(N) * 500),
+                         np.full(N, 30.0)])
+    if stall:
+        x0[2 * N:] = r_max
+        ctx.set_points(np.array([x0[0], x0[0] + 1.0]), np.array([x0[N], x0[N]]), np.ones(2))
+    else:
+        x, y, w = wl.grid_points(220)
+        ctx.set_points(x, y, w)
+    kw = dict(n_iter=n_iter, ell0=ell0, ell_max=ell_max, seed=31337 + N)
+    if cons3:
+        kw.update(prev=x0, d_lim=np.full(N, 12.0), tan_half_fov=TAN50)
+    want_x, want = ctx.mads_run(x0, r_max, 1e5, **kw)
+    st_ = ctx.mads_stepper(x0, r_max, 1e5, **kw)
+    try:
+        while True:
+            done, bo, bi = st_.poll()
+            if done:
+                break
+            st_.update(bo, bi)
+        xs, got = st_.result()
+    finally:
+        st_.close()
+    assert np.array_equal(want_x, xs)
+    for key in ("f", "iterations", "evaluations", "status", "feasible"):
+        assert want[key] == got[key], key
+    if stall:
+        assert want["status"] == 0 and want["iterations"] == ell0 + 1
+        assert np.array_equal(want_x, x0)
