@@ -104,9 +104,11 @@ __device__ __forceinline__ float key_of(double v, double b, bool& ok)
 // only slower walks). Each thread holds its kIdxPer candidates' doubles in registers through
 // every phase, and the LDS holds only the fp32 keys, the table and the owners (~60 KB), so two
 // workgroups fit a CU and the whole index runs in one round at N = 512.
-// kKeys: fp32 keys and exactness flags written by the prep launch (src.keysT, the records'
-// flags; exact doubles from src.cands or the generator); else keyed here from src.get (the
-// generator's distinct directions drawn once per disk).
+// kKeys: keys and exactness flags written by the prep launch (packed words src.keysP, fp32
+// offsets of escaped values src.keysT, the records' flags; exact doubles from src.cands or the
+// generator): a packed word (dx, dy, dr) is the fp32 key triple (dx, dy, dr), exact by
+// construction; else keyed here from src.get (the generator's distinct directions drawn once per
+// disk).
 template <bool kKeys, int kPer>
 __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPer <= 3 ? 8 : 4))) void disk_index_kernel(
     uint64_t* ts, CandSrc src0, int N, int K, Grid g, int dedup, IndexOut o)
@@ -197,18 +199,27 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
     if (fits && kKeys) {
         // ---- keys: rows of the fp32 key matrix (coalesced) and the tiles' exactness flags
         get3(0, bx, by, br);
-        const float* fx = src.keysT + (int64_t)i * src.ldk;
-        const float* fy = fx + (int64_t)N * src.ldk;
-        const float* fr = fy + (int64_t)N * src.ldk;
-        float qx[P], qy[P], qr[P];
+        const uint32_t* fp = src.keysP + (int64_t)i * src.ldk;
+        uint32_t pq[P];
 #pragma unroll
         for (int j = 0; j < P; ++j) {
             const int k = min(j < kIdxPer ? tid + j * kIdxThreads : (tid == 0 ? kIndexMaxK : K), K - 1);
-            qx[j] = fx[k];
-            qy[j] = fy[k];
-            qr[j] = fr[k];
+            pq[j] = fp[k];
         }
         load_partials();
+        // packed words to fp32 offsets; an escaped value's offsets from the fp32 rows (k_prep.h)
+        float qx[P], qy[P], qr[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            key_unpack(pq[j], qx[j], qy[j], qr[j]);
+            if (pq[j] == kKeyEsc) {
+                const int k = min(j < kIdxPer ? tid + j * kIdxThreads : (tid == 0 ? kIndexMaxK : K), K - 1);
+                const float* fx = src.keysT + (int64_t)i * src.ldk;
+                qx[j] = fx[k];
+                qy[j] = fx[(int64_t)N * src.ldk + k];
+                qr[j] = fx[(int64_t)2 * N * src.ldk + k];
+            }
+        }
         const bool bad = pbad;   // a key of disk i is inexact (the records' flags)
         for (int q = tid; q < kIndexSlots; q += kIdxThreads) table[q] = -1;
         if (tid == 0) ucnt = 0;

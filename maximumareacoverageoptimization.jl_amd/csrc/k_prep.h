@@ -96,8 +96,9 @@ struct MadsState {
 struct CandSrc {
     const double* cands;   // matrix source when non-null
     int ldc;
-    const float* keysT;    // matrix: fp32 keys, variable-major (the prep launch), when non-null
-    int ldk;               // keysT row pitch (keys_ld(K))
+    const uint32_t* keysP; // packed integer keys, one row per disk (the prep launch), when non-null
+    const float* keysT;    // ... and the fp32 keys of the escaped values, variable-major rows
+    int ldk;               // row pitch of both (keys_ld(K))
     const double* xinc;    // generator: incumbent (3N), row / column permutations (n each)
     const int* rp;
     const int* cp;
@@ -145,17 +146,18 @@ struct CandSrc {
 //     makes the walk stage or share more entries, never changes a result), packed as two
 //     16-bit tile numbers (range_pack); the estimate is the disks' span areas as (2r/S + 1)^2
 //     (the walk choice's cost). The disk index reduces disk i's records (k_index.h);
-//   keys (keysT != null; matrix or generator): the fp32 key fl32(v - v0) of each value, v0 =
-//     candidate 0's, into keysT[v*ldk + k] (8 consecutive keys: two 16-B stores); the record's
-//     key flag is 1 when one of UAV i's 24 keys does not reproduce its double bit for bit
-//     (k_index.h "Keys": the disk then takes the identity map).
+//   keys (keysP != null; matrix or generator): the packed key of each disk (below), relative to
+//     candidate 0's, into keysP[i*ldk + k] (8 consecutive words: two 16-B stores); an escaped
+//     disk's three fp32 offsets fl32(v - v0) into keysT[v*ldk + k]; the record's key flag is 1
+//     when one of those does not reproduce its double bit for bit (k_index.h "Keys": the disk
+//     then takes the identity map).
 #ifndef MAC_PREP_C
 #define MAC_PREP_C 8
 #endif
 constexpr int kPrepC = MAC_PREP_C;   // candidates per workgroup (a multiple of 4)
 constexpr int kPrepU = 512;      // UAVs per block = threads per workgroup
 
-// keysT row pitch: rows start on 128-B boundaries (and hold every workgroup's kPrepC keys)
+// keysP / keysT row pitch: rows start on 128-B boundaries (and hold every workgroup's kPrepC keys)
 __host__ __device__ inline int keys_ld(int K) { return (K + 31) & ~31; }
 
 struct PrepArgs {
@@ -167,9 +169,36 @@ struct PrepArgs {
     int nchain;                // workgroups
     int4* prec;                // [nchain][N] records (null: no poll walk)
     Grid g;
-    float* keysT;              // keys (null: none), rows of pitch ldk
+    uint32_t* keysP;           // packed keys (null: none), one row per disk, pitch ldk
+    float* keysT;              // fp32 keys of escaped values, 3N rows of pitch ldk
     int ldk;
 };
+
+// Packed keys. Disk i of candidate k is keyed by its offsets (dx, dy, dr) from candidate 0's
+// disk. When all three are integers that reproduce the doubles exactly (v0 + (double)d == v bit
+// for bit) with |dx|, |dy| <= 1023 and |dr| <= 511 — every MADS poll on the granular mesh up to
+// step 2^9 — the key is one 32-bit word (11 + 11 + 10 bits, two's complement); else the word is
+// the escape kKeyEsc (r field -512) and the value's three fp32 offsets go to the keysT rows
+// (k_index.h "Keys"). Either encoding satisfies v == v0 + (double)key, so equal keys still mean
+// equal disks; the index reads one word per candidate instead of three.
+constexpr uint32_t kKeyEsc = 0x200u << 22;
+__device__ __forceinline__ bool key_int(double v, double b, double lim, int& d)
+{
+    const double f = v - b;
+    if (!(f >= -lim && f <= lim)) return false;   // (NaN: false)
+    d = (int)f;
+    return (double)d == f && __builtin_bit_cast(uint64_t, b + (double)d) == __builtin_bit_cast(uint64_t, v);
+}
+__device__ __forceinline__ uint32_t key_pack(int dx, int dy, int dr)
+{
+    return ((uint32_t)dx & 0x7FFu) | (((uint32_t)dy & 0x7FFu) << 11) | (((uint32_t)dr & 0x3FFu) << 22);
+}
+__device__ __forceinline__ void key_unpack(uint32_t p, float& x, float& y, float& r)
+{
+    x = (float)((int)(p << 21) >> 21);
+    y = (float)((int)(p << 10) >> 21);
+    r = (float)((int)p >> 22);
+}
 
 // the tile range [lo, hi] on one axis covering every span of disks with min(c - r) = a,
 // max(c + r) = b, max(|c| + r) = m (tile_span's steps, each monotone); false: empty
@@ -251,7 +280,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
             }
         }
         double base[3] = {0.0, 0.0, 0.0};   // candidate 0's values: the keys' base
-        if (a.keysT) {
+        if (a.keysP) {
 #pragma unroll
             for (int q = 0; q < 3; ++q) {
                 if constexpr (kMat) base[q] = a.src.cands[q * N + ii];
@@ -301,14 +330,28 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
                 }
             }
             bool kb = false;   // a key of this disk is inexact (k_index.h "Keys")
-            if (a.keysT) {
+            if (a.keysP) {     // the keys: packed words (two 16-B stores), escapes in fp32
+                uint32_t pk[kPrepC];
 #pragma unroll
-                for (int q = 0; q < 3; ++q)
+                for (int c = 0; c < kPrepC; ++c) {
+                    int dx = 0, dy = 0, dr = 0;
+                    const bool packs = key_int(v[c][0], base[0], 1023.0, dx) &&
+                                       key_int(v[c][1], base[1], 1023.0, dy) &&
+                                       key_int(v[c][2], base[2], 511.0, dr);
+                    pk[c] = packs ? key_pack(dx, dy, dr) : kKeyEsc;
+                    if (!packs) {
 #pragma unroll
-                    for (int c = 0; c < kPrepC; ++c) {
-                        const float f = (float)(v[c][q] - base[q]);
-                        kb |= __builtin_bit_cast(uint64_t, base[q] + (double)f) != __builtin_bit_cast(uint64_t, v[c][q]);
+                        for (int q = 0; q < 3; ++q) {
+                            const float f = (float)(v[c][q] - base[q]);
+                            kb |= __builtin_bit_cast(uint64_t, base[q] + (double)f) != __builtin_bit_cast(uint64_t, v[c][q]);
+                            a.keysT[(int64_t)(q * N + i) * a.ldk + k0 + c] = f;
+                        }
                     }
+                }
+                uint4* dst = reinterpret_cast<uint4*>(a.keysP + (int64_t)i * a.ldk + k0);
+#pragma unroll
+                for (int h = 0; h < kPrepC / 4; ++h)
+                    dst[h] = make_uint4(pk[4 * h], pk[4 * h + 1], pk[4 * h + 2], pk[4 * h + 3]);
             }
             int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
             any = any && partial_range(xa, xb, xm, a.g.gx0, a.g.invS, a.g.nTx, x0, x1) &&
@@ -317,18 +360,6 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
                 make_int4((int)range_pack(any, x0, x1, range_shift(a.g.nTx)),
                           (int)range_pack(any, y0, y1, range_shift(a.g.nTy)),
                           __builtin_bit_cast(int, (float)est), kb ? 1 : 0);
-        }
-        if (a.keysT && iv) {   // the keys: two 16-B stores per variable
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                float f[kPrepC];
-#pragma unroll
-                for (int c = 0; c < kPrepC; ++c) f[c] = (float)(v[c][q] - base[q]);
-                float4* dst = reinterpret_cast<float4*>(a.keysT + (int64_t)(q * N + i) * a.ldk + k0);
-#pragma unroll
-                for (int h = 0; h < kPrepC / 4; ++h)
-                    dst[h] = make_float4(f[4 * h], f[4 * h + 1], f[4 * h + 2], f[4 * h + 3]);
-            }
         }
         MAC_PREP_STAMP(2 + 3 * (ib / kPrepU));
         if (obj) {
@@ -363,7 +394,7 @@ __global__ __launch_bounds__(kPrepU) __attribute__((amdgpu_waves_per_eu(4))) voi
         return;
     }
     // XCD-aware: workgroups b and b + 8 share an XCD (round-robin dispatch), so consecutive
-    // candidate groups — which fill the same lines of keysT and of the records — go to one XCD
+    // candidate groups — which fill the same lines of keysP and of the records — go to one XCD
     const int per = (int)((gridDim.x + 7) / 8), b = (int)blockIdx.x;
     const int cw = (int)(gridDim.x % 8) == 0 ? (b % 8) * per + b / 8 : b;
     if (a.src.cands) prep_block<true>(a, cw);

@@ -538,9 +538,12 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         }
         if (want_keys) {
             const int ldk = keys_ld(K);
-            L->keysT.reserve(sizeof(float) * (size_t)3 * N * ldk);
-            pr.keysT = L->keysT.as<float>();
+            // packed keys (one row per disk), then the fp32 rows of escaped values (k_prep.h)
+            L->keysT.reserve(sizeof(float) * (size_t)4 * N * ldk);
+            pr.keysP = L->keysT.as<uint32_t>();
+            pr.keysT = L->keysT.as<float>() + (size_t)N * ldk;
             pr.ldk = ldk;
+            isrc.keysP = pr.keysP;
             isrc.keysT = pr.keysT;
             isrc.ldk = ldk;
         }

@@ -551,7 +551,7 @@ def test_walk_choice_scattered_batch(ctx, pkg, orc):
 
 
 @pytest.mark.parametrize("case", ["real_clustered", "big_radius", "mixed_weights", "pythagorean",
-                                  "crowded", "lattice_mixed", "key_mix"])
+                                  "crowded", "lattice_mixed", "key_mix", "key_escape"])
 def test_poll_walk_stress(ctx, pkg, orc, case):
     """The poll walk's rare paths: fp64 band decisions on real-valued coordinates, ownership
     between overlapping disks, regions larger than one LDS chunk and more than 64 tile rows.
@@ -563,7 +563,10 @@ def test_poll_walk_stress(ctx, pkg, orc, case):
     word path; "lattice_mixed": lattice polls (few distinct positions) with unequal weights
     (the word path's bit-by-bit credit); "key_mix": a lattice poll whose odd UAVs carry offsets
     no fp32 key reproduces (and one UAV with -0.0 against candidate 0's +0.0), so those disks take
-    the index's identity map while the others are deduplicated (k_index.h "Keys")."""
+    the index's identity map while the others are deduplicated (k_index.h "Keys"); "key_escape":
+    a lattice poll where some candidates of some UAVs move by half-integers or by more than the
+    packed key holds (|dx| > 1023, |dr| > 511): those values take the fp32 escape rows while the
+    rest of the same disk packs (k_prep.h "Packed keys"), and the disk is still deduplicated."""
     wl = pkg.workloads
     rng = wl.SplitMix64(4242 + len(case))
     if case == "pythagorean":
@@ -603,6 +606,33 @@ def test_poll_walk_stress(ctx, pkg, orc, case):
         zero = np.flatnonzero(C[:, 0] == 0.0)
         C[zero[1::2], 0] = -0.0
         assert zero.size > 2 and K >= 64
+        want = orc.PointerList(recs(x, y, w)).area_batch(C)
+        r = both(ctx, lambda: ctx.area_batch(C))
+        for a, got in r.items():
+            assert np.array_equal(got, want), (a, np.flatnonzero(got != want)[:5])
+        rmax = np.full(N, 30.0)
+        bo, bi, objs = ctx.poll_best(C, rmax, want_all=True)
+        want_obj = np.array([orc.ref_objective(c, recs(x, y, w), rmax) for c in C])
+        assert np.array_equal(objs, want_obj)
+        return
+    if case == "key_escape":
+        M = 40000
+        x = np.floor(rng.uniform(M) * 400.0)
+        y = np.floor(rng.uniform(M) * 400.0)
+        w = np.full(M, 25.0)
+        N = 24
+        x0 = np.concatenate([np.floor(200 + rng.uniform(N) * 160 - 80),
+                             np.floor(200 + rng.uniform(N) * 160 - 80),
+                             np.floor(rng.uniform(N) * 20 + 15)])
+        ctx.set_points(x, y, w)
+        C = np.concatenate([x0[None, :], wl.poll_candidates(x0, rng, ell=2)], axis=0)
+        K = C.shape[0]
+        for v, d in [(1, 0.5), (2, 1500.0), (N + 4, -0.25), (N + 5, -2048.0), (2 * N + 6, 600.0),
+                     (2 * N + 7, 0.5)]:
+            pick = np.flatnonzero(rng.uniform(K) < 0.2)
+            pick = pick[pick > 0]
+            C[pick, v] += d
+        assert K >= 64
         want = orc.PointerList(recs(x, y, w)).area_batch(C)
         r = both(ctx, lambda: ctx.area_batch(C))
         for a, got in r.items():
