@@ -130,7 +130,7 @@ __device__ __forceinline__ void coverage_poll_body(
     const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
     int* __restrict__ jobctr, int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
     double* __restrict__ spart, int n_shared, int counts, int bits_on, int* __restrict__ dc_out,
-    const int* __restrict__ qual)
+    const int* __restrict__ qual, const double2* __restrict__ cost, double ratio)
 {
     static_assert(kPollSlots == 2 * kPollPairs, "the hot loop pairs candidate slots");
 #ifdef MAC_DIAG
@@ -198,6 +198,13 @@ __device__ __forceinline__ void coverage_poll_body(
     };
     if (bx >= nwalk) {  // then: the shared entries
         if (mv != kModePoll) return;
+        if (bx == nwalk && cost && dc_out) {
+            // launch hint for the next poll: the walk AUTO would choose now that the neighbour
+            // lists exist (k_poll_shared.h walk_choice); the host launches the per-candidate walk's
+            // kernel after a poll that would have chosen it (maxcover.hip enqueue_eval)
+            const int m = walk_choice(N, K, cost, ncount, ratio, 0);
+            if (threadIdx.x == 0) *((volatile int*)dc_out + 4) = m;
+        }
         shared_jobs(bx - nwalk);
         MAC_DIAG_STAMP(diag_t0, 2, (uint64_t)(dcount[kDcBits] + dcount[kDcOther]));
         return;
@@ -510,12 +517,12 @@ __global__ __launch_bounds__(kPollThreads) __attribute__((amdgpu_waves_per_eu(3)
     const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
     int* __restrict__ jobctr, int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
     double* __restrict__ spart, int n_shared, int counts, int bits_on, int* __restrict__ dc_out,
-    const int* __restrict__ qual)
+    const int* __restrict__ qual, const double2* __restrict__ cost, double ratio)
 {
     ts_begin(ts);
     coverage_poll_body(xy, w, off, g, urec, umap, ucount, region, nbrT, nboxT, lane4, lanexp, rows,
                        ncount, dlist, dcount, jobctr, N, K, mode, partial, spart, n_shared, counts,
-                       bits_on, dc_out, qual);
+                       bits_on, dc_out, qual, cost, ratio);
     ts_end(ts);
 }
 

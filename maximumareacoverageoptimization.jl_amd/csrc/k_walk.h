@@ -103,11 +103,17 @@ __host__ __device__ inline size_t tiled_lds_bytes(int N)
 // list built in LDS). Disk c of candidate k through the disk index (k_index.h);
 // partial[gi*K + k]. Runs only when *mode == kModeTiled
 // (or mode == null). Workgroups loop over units (grid-stride).
+// Poll chain (nbrP != null): the lower-index candidates of disk c are the poll-level neighbour
+// list walk_setup built once per poll (k_poll_shared.h neighbors_block: disks whose regions — the
+// unions of their spans over the poll — overlap c's; a superset of any candidate's overlaps), so a
+// unit tests sum over its disks of |list| pairs instead of every lower-index disk; an overflowed
+// poll-level list (more than kPollNbr) falls back to every lower-index disk.
 __device__ __forceinline__ void coverage_tiled_body(
     const double2* __restrict__ xy, const double* __restrict__ w,
     const int32_t* __restrict__ off, Grid g,
     const DiskRec* __restrict__ urec, const int* __restrict__ umap, int N, int K, int G,
-    const int* __restrict__ mode, double* __restrict__ partial)
+    const int* __restrict__ mode, double* __restrict__ partial,
+    const uint16_t* __restrict__ nbrP = nullptr, const int* __restrict__ ncountP = nullptr)
 {
     if (mode && *mode != kModeTiled) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -150,12 +156,18 @@ __device__ __forceinline__ void coverage_tiled_body(
     for (int c = gi; c < N; c += G) {
         if (span[c].x > span[c].y) continue;   // uniform
         const double cx = sx[c], cy = sy[c], r = sR[c];
-        for (int c2 = threadIdx.x; c2 < c; c2 += kBlock) {
-            if (span[c2].x > span[c2].y) continue;  // covers nothing
+        auto test = [&](int c2) {
+            if (span[c2].x > span[c2].y) return;  // covers nothing
             if (disks_may_overlap(cx, cy, r, sx[c2], sy[c2], sR[c2])) {
                 const int q = atomicAdd(&ncnt[c], 1);
                 if (q < kNbrCap) nbr[c * kNbrCap + q] = (uint16_t)c2;
             }
+        };
+        const int pc = nbrP ? ncountP[c] : kPollNbr + 1;   // (uniform)
+        if (pc <= kPollNbr) {
+            for (int q = threadIdx.x; q < pc; q += kBlock) test(nbrP[c * kPollNbr + q]);
+        } else {
+            for (int c2 = threadIdx.x; c2 < c; c2 += kBlock) test(c2);
         }
     }
     __syncthreads();
@@ -167,7 +179,8 @@ __device__ __forceinline__ void coverage_tiled_body(
         const int4 sp = span[c];
         if (sp.x > sp.y) continue;
         const double cx = sx[c], cy = sy[c], T = sT[c];
-        const int nc = ncnt[c] > kNbrCap ? 0xffff : ncnt[c];   // overflow: every lower disk
+        const int nc = ncnt[c] > kNbrCap ? 0xffff : ncnt[c];   // overflow: below
+        const int pcl = nbrP ? ncountP[c] : kPollNbr + 1;
         for (int rb = sp.z; rb <= sp.w; rb += kWave) {
             const int nr = (sp.w - rb + 1) < kWave ? (sp.w - rb + 1) : kWave;
             int s = 0, len = 0;
@@ -196,6 +209,11 @@ __device__ __forceinline__ void coverage_tiled_body(
                     if (nc != 0xffff) {
                         for (int q = 0; q < nc; ++q) {
                             const int c2 = nbr[c * kNbrCap + q];
+                            if (sqdist(p.x, p.y, sx[c2], sy[c2]) <= sT[c2]) { owned = false; break; }
+                        }
+                    } else if (pcl <= kPollNbr) {   // overflowed: the poll-level list
+                        for (int q = 0; q < pcl; ++q) {
+                            const int c2 = nbrP[c * kPollNbr + q];
                             if (sqdist(p.x, p.y, sx[c2], sy[c2]) <= sT[c2]) { owned = false; break; }
                         }
                     } else {
@@ -236,23 +254,47 @@ __global__ __launch_bounds__(kBlock) void coverage_tiled_kernel(
     ts_end(ts);
 }
 
-// The walk choice, then its launch-time work, in one launch (k_poll_shared.h walk_choice; every
-// block computes the same choice, block 0 stores it in mode[0] for the kernels that follow):
-// poll: block i < N builds disk i's neighbour list for the poll kernel; per-candidate walk: the
-// blocks grid-stride over its (candidate, slice) units. Dynamic LDS: tiled_lds_bytes(N) whenever
-// the per-candidate walk may be chosen.
-__global__ __launch_bounds__(kBlock) void walk_setup_kernel(
+// The poll chain's per-candidate walk (launched after walk_setup when the lane's recent polls
+// chose it, or it is forced; maxcover.hip enqueue_eval): every block makes the walk choice with
+// the poll-level neighbour counts known (k_poll_shared.h walk_choice), block 0 stores it in
+// mode[0] (the poll kernel, the bit-word kernel and finalize read it) and in the lane's mapped
+// hint word; when the per-candidate walk wins, the blocks grid-stride over its (candidate,
+// slice) units with the poll-level lists. A stopped pipelined MADS loop (mode[0] == 0 from
+// walk_setup) returns at once.
+__global__ __launch_bounds__(kBlock) void coverage_tiled_poll_kernel(
     uint64_t* ts, const double2* __restrict__ xy, const double* __restrict__ w,
     const int32_t* __restrict__ off, Grid g, const DiskRec* __restrict__ urec,
-    const int* __restrict__ umap, int N, int K, int G, double* __restrict__ partial,
-    const int4* __restrict__ region, uint16_t* __restrict__ nbr, int4* __restrict__ nboxT,
-    int* __restrict__ ncount, int* __restrict__ dlist, int* __restrict__ dcount,
-    const double2* __restrict__ cost,
-    double ratio, int forced, int* __restrict__ mode, const int* __restrict__ ucount,
-    int* __restrict__ qual, const MadsState* __restrict__ halt)
+    const int* __restrict__ umap, int N, int K, int G, int* __restrict__ mode,
+    double* __restrict__ partial, const uint16_t* __restrict__ nbr, const int* __restrict__ ncount,
+    const double2* __restrict__ cost, double ratio, int forced, int* __restrict__ hint)
 {
     ts_begin(ts);
-    // the neighbour lists' regions, loaded beside the walk choice's costs (one round trip)
+    const int m0 = *mode;
+    if (m0 == 0) {   // (uniform) the pipelined MADS loop has stopped
+        ts_end(ts);
+        return;
+    }
+    const int m = walk_choice(N, K, cost, ncount, ratio, forced);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        mode[0] = m;
+        if (hint) *(volatile int*)hint = m;
+    }
+    if (m == kModeTiled) coverage_tiled_body(xy, w, off, g, urec, umap, N, K, G, nullptr, partial, nbr, ncount);
+    ts_end(ts);
+}
+
+// The poll chain's set-up after the index: block i < N builds disk i's neighbour list (k_poll_shared.h
+// neighbors_block) for the poll kernel, the bit-word kernel, finalize and the per-candidate walk;
+// block 0 sets mode[0] to the poll walk (coverage_tiled_poll_kernel, when launched, makes the choice
+// after it), or to 0 when the pipelined MADS loop has stopped.
+__global__ __launch_bounds__(kBlock) void walk_setup_kernel(
+    uint64_t* ts, int N, const int4* __restrict__ region, uint16_t* __restrict__ nbr,
+    int4* __restrict__ nboxT, int* __restrict__ ncount, int* __restrict__ dlist,
+    int* __restrict__ dcount, int* __restrict__ mode, int* __restrict__ qual,
+    const MadsState* __restrict__ halt)
+{
+    ts_begin(ts);
+    // the neighbour lists' regions, loaded beside the halt word (one round trip)
     const int i = blockIdx.x;
     const int4 none = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
     const int4 R = i < N ? region[i] : none;
@@ -262,21 +304,15 @@ __global__ __launch_bounds__(kBlock) void walk_setup_kernel(
         const int j = threadIdx.x + q * kBlock;
         Q[q] = j < i && i < N ? region[j] : none;
     }
-    // a stopped pipelined MADS loop (k_prep.h MadsState; checked once the regions are in
-    // flight): no walk; the poll kernel, the bit-word kernel and the finalize's argmin see
-    // mode 0 / the state and return
+    // a stopped pipelined MADS loop (k_prep.h MadsState): no walk; the poll kernel, the
+    // bit-word kernel and the finalize's argmin see mode 0 / the state and return
     if (halt && halt->ell < 0) {
         if (blockIdx.x == 0 && threadIdx.x == 0) mode[0] = 0;
         ts_end(ts);
         return;
     }
-    const int m = walk_choice(N, K, cost, ratio, forced);
-    if (blockIdx.x == 0 && threadIdx.x == 0) mode[0] = m;
-    if (m == kModePoll) {
-        if (i < N) neighbors_block(i, N, R, Q, region, nbr, nboxT, ncount, dlist, dcount, qual);
-    } else {
-        coverage_tiled_body(xy, w, off, g, urec, umap, N, K, G, nullptr, partial);
-    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) mode[0] = kModePoll;
+    if (i < N) neighbors_block(i, N, R, Q, region, nbr, nboxT, ncount, dlist, dcount, qual);
     ts_end(ts);
 }
 

@@ -5,14 +5,17 @@
 //   disk_prep_kernel      (streaming scan) per (candidate, disk): {cx, cy, T(r), r}, T the exact
 //                         threshold
 //   prep_kernel           one pass over the 3N x K candidate matrix (or the LTMADS generator):
-//                         the penalty chains + cons3 (vp per candidate), the fp32 keys,
-//                         variable-major, and a packed tile-range record per (workgroup, disk)
+//                         the penalty chains + cons3 (vp per candidate), the packed integer
+//                         keys (one row per disk), and a packed tile-range record per
+//                         (workgroup, disk)
 //   disk_index_kernel     (tiled / poll walks) per disk over all K candidates: the distinct disks
 //                         (records), the candidate -> distinct map, the region and the two walk
 //                         costs reduced from the prep's records, row descriptors, lane constants
-//   walk_setup_kernel     the walk choice (every block; block 0 stores it), then per disk i the
-//                         lower-index disks whose regions overlap region i (poll walk), or the
-//                         per-candidate walk itself (grid-stride over candidate x slice units)
+//   walk_setup_kernel     per disk i the lower-index disks whose regions overlap region i (the
+//                         poll-level neighbour lists every walk uses)
+//   coverage_tiled_poll_kernel  (when forced, or AUTO chose it on the lane's recent polls) the
+//                         walk choice with the lists known, then the per-candidate walk over
+//                         (candidate x slice) units, pairs from the poll-level lists
 //   coverage_poll_kernel  workgroup = disk i: the entries of disk i's region staged in LDS once,
 //                         every wave holding all of the disk's distinct disks (8 per lane) over a
 //                         quarter of the entries, exact fp32 filter; further workgroups run the

@@ -145,6 +145,7 @@ struct Lane {
     DevBuf cpart, carrive, ctot;               // closure_kernel: credits, arrivals, packed count
     DevBuf prec, cost;                         // prep launch: per-disk records; walk costs
     int um_hist[8] = {};                       // most distinct positions of a disk, last 8 polls
+    int walk_hist[8] = {};                     // the walk AUTO would have chosen, last 8 polls
 };
 
 struct mac_ctx {
@@ -462,7 +463,8 @@ static bool use_tiled(mac_ctx* ctx, int N, const double* h_cands, int64_t three_
 static bool poll_walk_possible(const mac_ctx* ctx, int N, int K, bool tiled)
 {
     return tiled && N > 0 && ctx->M > 0 &&
-           (ctx->algo == MAC_ALGO_POLL || N > kTiledMaxN || (ctx->algo == MAC_ALGO_AUTO && K >= kPollMinK));
+           (ctx->algo == MAC_ALGO_POLL || N > kTiledMaxN ||
+            ((ctx->algo == MAC_ALGO_AUTO || ctx->algo == MAC_ALGO_TILED) && K >= kPollMinK));
 }
 
 // Enqueue the prep launch + index + walks + finalize (+ argmin) on stream s. All pointers device.
@@ -503,6 +505,10 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         d_vp = L->vp.as<double>();
     }
     const bool big = N > kTiledMaxN;
+    // the poll chain's walk: forced by the algorithm option (or N past the per-candidate walk's
+    // LDS limit), else 0 = the device's choice (k_poll_shared.h walk_choice)
+    const int walk_forced = (ctx->algo == MAC_ALGO_POLL || big) ? kModePoll
+                          : ctx->algo == MAC_ALGO_TILED ? kModeTiled : 0;
     const bool poll_possible = poll_walk_possible(ctx, N, K, tiled);
     // candidates per index thread: 3 (K <= 3073), 6 (K <= 6145); larger: identity map
     const int iper = K <= kIndexMaxK + 1 ? kIdxPer : K <= kIndexMaxKWide + 1 ? kIdxPerWide : 0;
@@ -629,29 +635,51 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                 hipLaunchKernelGGL((disk_index_kernel<false, kIdxPer>), dim3(nidx), dim3(kIdxThreads), 0,
                                    s, nullptr, isrc, N, K, ctx->grid, dedup, io);
             HCK(hipGetLastError());
-            // walk choice + neighbour lists (poll) or the per-candidate walk itself, one launch
-            // (k_walk.h); when the poll walk is chosen the extra blocks just exit, so the
-            // per-candidate walk gets one workgroup per CU (grid-striding over its units)
-            const bool run_tiled = ctx->algo != MAC_ALGO_POLL && !big;
-            const int forced = run_tiled ? 0 : kModePoll;
+            // launch hints from the lane's previous polls (mapped host memory the poll kernel
+            // writes): disks with neighbours, most positions of a disk, the walk AUTO would choose
+            if (!L->h_dc.p) {
+                L->h_dc.reserve(64, hipHostMallocMapped | hipHostMallocCoherent);
+                *(volatile int*)L->h_dc.p = 1 << 30;   // first poll: launch
+                ((volatile int*)L->h_dc.p)[2] = 0;     // most positions: not reported yet
+                ((volatile int*)L->h_dc.p)[4] = kModeTiled;   // walk: launch the choice kernel
+                void* dp = nullptr;
+                HCK(hipHostGetDevicePointer(&dp, L->h_dc.p, 0));
+                L->d_dc = (int*)dp;
+            }
+            // neighbour lists (k_walk.h walk_setup_kernel), then — when the per-candidate walk is
+            // forced, or AUTO chose it on one of the lane's last 8 polls — the walk choice and that
+            // walk (coverage_tiled_poll_kernel). Otherwise the poll walk runs; its kernel records
+            // the choice AUTO would have made, so a batch that favours the per-candidate walk gets
+            // it from the lane's next poll on (the choice only changes speed, never results).
+            const int walk_now = ((volatile int*)L->h_dc.p)[4];
+            for (int q = 7; q > 0; --q) L->walk_hist[q] = L->walk_hist[q - 1];
+            L->walk_hist[0] = walk_now;
+            bool hinted = false;
+            for (int q = 0; q < 8; ++q) hinted |= L->walk_hist[q] == kModeTiled;
+            const bool run_tiled = walk_forced == kModeTiled || (walk_forced == 0 && hinted);
             L->nbr.reserve(sizeof(uint16_t) * (size_t)N * kPollNbr);
             L->ncount.reserve(sizeof(int) * (size_t)N);
             L->dlist.reserve(sizeof(int) * (size_t)N);
             L->qual.reserve(sizeof(int) * (size_t)N);
             L->nboxT.reserve(sizeof(int4) * (size_t)N * kPollNbr);
             L->partial.reserve(sizeof(double) * (size_t)K * std::max(G, N));
-            const size_t lds = run_tiled ? tiled_lds_bytes(N) : 0;
-            const unsigned nwg = (unsigned)std::max<int64_t>(
-                N, run_tiled ? std::min<int64_t>(units, ctx->cus) : 0);
-            uint64_t* ts = run_tiled ? take_ts(nwg, ts_a, ts_na) : nullptr;
-            hipLaunchKernelGGL(walk_setup_kernel, dim3(nwg), dim3(kBlock), (uint32_t)lds, s, ts,
-                               ctx->xys.as<double2>(), ctx->ws.as<double>(), ctx->off.as<int32_t>(),
-                               ctx->grid, d_urec, d_map, N, K, G, L->partial.as<double>(),
+            hipLaunchKernelGGL(walk_setup_kernel, dim3((unsigned)N), dim3(kBlock), 0, s, nullptr, N,
                                L->region.as<int4>(), L->nbr.as<uint16_t>(), L->nboxT.as<int4>(),
                                L->ncount.as<int>(), L->dlist.as<int>(), L->mode.as<int>() + 1,
-                               L->cost.as<double2>(), kPollCostRatio, forced, L->mode.as<int>(),
-                               L->ucount.as<int>(), L->qual.as<int>(), src.mst);
+                               L->mode.as<int>(), L->qual.as<int>(), src.mst);
             HCK(hipGetLastError());
+            if (run_tiled) {
+                // one workgroup per CU at most, grid-striding over the (candidate, slice) units
+                const unsigned nwg = (unsigned)std::max<int64_t>(1, std::min<int64_t>(units, ctx->cus));
+                uint64_t* ts = take_ts(nwg, ts_a, ts_na);
+                hipLaunchKernelGGL(coverage_tiled_poll_kernel, dim3(nwg), dim3(kBlock),
+                                   (uint32_t)tiled_lds_bytes(N), s, ts, ctx->xys.as<double2>(),
+                                   ctx->ws.as<double>(), ctx->off.as<int32_t>(), ctx->grid, d_urec, d_map,
+                                   N, K, G, L->mode.as<int>(), L->partial.as<double>(),
+                                   L->nbr.as<uint16_t>(), L->ncount.as<int>(), L->cost.as<double2>(),
+                                   kPollCostRatio, walk_forced, L->d_dc + 4);
+                HCK(hipGetLastError());
+            }
             d_mode = L->mode.as<int>();
             d_umap = d_map;
         }
@@ -659,14 +687,6 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             // the bit-word kernel runs when the previous poll on this lane had more than
             // kBitsMinDisks disks with neighbours (the poll kernel writes the count to mapped host
             // memory): a hint only, the poll kernel takes every disk when it is not launched
-            if (!L->h_dc.p) {
-                L->h_dc.reserve(64, hipHostMallocMapped | hipHostMallocCoherent);
-                *(volatile int*)L->h_dc.p = 1 << 30;   // first poll: launch
-                ((volatile int*)L->h_dc.p)[2] = 0;     // most positions: not reported yet
-                void* dp = nullptr;
-                HCK(hipHostGetDevicePointer(&dp, L->h_dc.p, 0));
-                L->d_dc = (int*)dp;
-            }
             // (the maximum over the last 8 polls: MADS alternates crowded and quiet polls, and a
             // crowded poll without the bit-word kernel costs several times its launch)
             const int dc_now = *(volatile int*)L->h_dc.p;   // 1 << 30 until a poll wrote it
@@ -701,7 +721,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                                L->ncount.as<int>(), L->dlist.as<int>(), L->mode.as<int>() + 1,
                                L->mode.as<int>() + 2, N, K,
                                d_mode, L->partial.as<double>(), L->spart.as<double>(), n_shared, counts,
-                               bits_on, L->d_dc, L->qual.as<int>());
+                               bits_on, L->d_dc, L->qual.as<int>(),
+                               walk_forced == 0 ? L->cost.as<double2>() : nullptr, kPollCostRatio);
             HCK(hipGetLastError());
             // the shared entries of crowded polls: bit-words per distinct position (k_bits.h);
             // returns at once when few disks have neighbours (the poll kernel took them)

@@ -510,10 +510,10 @@ def _walk_of(ctx, C):
 @pytest.mark.parametrize("disks", ["clustered", "uniform"])
 def test_walk_choice_poll_batches(ctx, pkg, orc, disks):
     """The device's walk choice (k_poll_shared.h walk_choice, costs in poll-walk test units) on
-    MADS polls of K >= 64: crowded (every disk overlapping lower-index ones: the per-candidate
-    walk would rebuild N(N-1)/2 neighbour pairs per candidate — the config-5 cliff) and
-    scattered disks both take the poll walk under AUTO; the forced per-candidate walk gives the
-    same areas (slower, never different). Areas == the exact lattice counts."""
+    MADS polls of K >= 64: crowded (every disk overlapping lower-index ones: the config-5 poll
+    that once took 3.96 ms in the per-candidate walk) and scattered disks both take the poll walk
+    under AUTO; the forced per-candidate walk, with its pairs from the poll-level neighbour
+    lists, gives the same areas (slower, never different). Areas == the exact lattice counts."""
     wl = pkg.workloads
     rng = wl.SplitMix64(4242 if disks == "clustered" else 4243)
     G, N = 512, 96
@@ -529,14 +529,22 @@ def test_walk_choice_poll_batches(ctx, pkg, orc, disks):
     assert np.array_equal(area, want)
     ctx.set_algo("tiled")
     area_t, walk_t = _walk_of(ctx, C[:64])
+    # the whole crowded poll through the forced per-candidate walk: its pairs come from the
+    # poll-level neighbour lists (k_walk.h), no unit rebuilds all N(N-1)/2 of them
+    area_f, walk_f = _walk_of(ctx, C)
     ctx.set_algo("auto")
-    assert walk_t == "tiled", walk_t
+    assert walk_t == walk_f == "tiled", (walk_t, walk_f)
     assert np.array_equal(area_t, want[:64])
+    assert np.array_equal(area_f, want)
 
 
 def test_walk_choice_scattered_batch(ctx, pkg, orc):
     """A batch that is not a poll (64 unrelated random layouts of 8 disks: no shared footprint
-    across candidates) takes the per-candidate walk under AUTO; areas == exact lattice counts."""
+    across candidates) takes the per-candidate walk under AUTO; areas == exact lattice counts.
+    The choice is made on the device once the neighbour lists exist; the host launches that
+    walk's kernel when the lane's recent polls chose it (maxcover.hip enqueue_eval), so a lane
+    that ran poll-walk polls runs this batch once through the poll walk (same areas), records
+    the choice, and takes the per-candidate walk from the next call on."""
     wl = pkg.workloads
     rng = wl.SplitMix64(4244)
     G, N, K = 512, 8, 64
@@ -545,8 +553,10 @@ def test_walk_choice_scattered_batch(ctx, pkg, orc):
     C = np.stack([wl.uniform_disks(N, G, rng) for _ in range(K)])
     want = 25.0 * orc.lattice_count_batch(C, G).astype(np.float64)
     ctx.set_algo("auto")
+    area0, _ = _walk_of(ctx, C)
     area, walk = _walk_of(ctx, C)
     assert walk == "tiled", walk
+    assert np.array_equal(area0, want)
     assert np.array_equal(area, want)
 
 
