@@ -641,7 +641,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                 L->h_dc.reserve(64, hipHostMallocMapped | hipHostMallocCoherent);
                 *(volatile int*)L->h_dc.p = 1 << 30;   // first poll: launch
                 ((volatile int*)L->h_dc.p)[2] = 0;     // most positions: not reported yet
-                ((volatile int*)L->h_dc.p)[4] = kModeTiled;   // walk: launch the choice kernel
+                ((volatile int*)L->h_dc.p)[4] = 0;     // walk: not reported yet (launch)
                 void* dp = nullptr;
                 HCK(hipHostGetDevicePointer(&dp, L->h_dc.p, 0));
                 L->d_dc = (int*)dp;
@@ -651,10 +651,14 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             // walk (coverage_tiled_poll_kernel). Otherwise the poll walk runs; its kernel records
             // the choice AUTO would have made, so a batch that favours the per-candidate walk gets
             // it from the lane's next poll on (the choice only changes speed, never results).
+            // (a lane's first poll has no report yet: it launches the kernel once, and the
+            // sentinel stays out of the history)
             const int walk_now = ((volatile int*)L->h_dc.p)[4];
-            for (int q = 7; q > 0; --q) L->walk_hist[q] = L->walk_hist[q - 1];
-            L->walk_hist[0] = walk_now;
-            bool hinted = false;
+            bool hinted = walk_now == 0;
+            if (!hinted) {
+                for (int q = 7; q > 0; --q) L->walk_hist[q] = L->walk_hist[q - 1];
+                L->walk_hist[0] = walk_now;
+            }
             for (int q = 0; q < 8; ++q) hinted |= L->walk_hist[q] == kModeTiled;
             const bool run_tiled = walk_forced == kModeTiled || (walk_forced == 0 && hinted);
             L->nbr.reserve(sizeof(uint16_t) * (size_t)N * kPollNbr);
