@@ -7,7 +7,8 @@
 //   1. every workgroup stages the candidate's N disks (x, y, r) in LDS (one coalesced read);
 //   2. disk i's lower-index neighbours: the disks j < i that may share a covered entry with it
 //      (disks_may_overlap, conservative), their exact thresholds T(r_j) in LDS;
-//   3. the entries of disk i's tile span (CSR rows of the tile-sorted list) that disk i covers and
+//   3. the entries of disk i's tile span (CSR rows of the tile-sorted list, their offsets loaded
+//      in one round trip beside step 2) that disk i covers and
 //      no listed neighbour covers — each covered entry is credited to the LOWEST-index disk
 //      covering it, so the sum over disks is the reference's first-hit `break` sum over the same
 //      multiset of entries — counted (every weight equal: integer, exact in any order) or summed
@@ -75,6 +76,19 @@ __global__ __launch_bounds__(kBlock) void closure_kernel(uint64_t* ts, const dou
     int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
     const bool any = T >= 0.0 && tile_span(cx, r, g.gx0, g.invS, g.nTx, x0, x1) &&
                      tile_span(cy, r, g.gy0, g.invS, g.nTy, y0, y1);
+    // the span's row runs (a row of tiles is a contiguous run of the sorted list): every row's
+    // offsets loaded at once by wave 0, in flight during the neighbour tests, then flattened with
+    // a prefix (one memory round trip for the offsets and one for the entries, instead of two per
+    // row); spans of more than 64 rows walk row by row below
+    __shared__ int rs[kWave], rpre[kWave + 1];
+    const int nrows = any ? y1 - y0 + 1 : 0;
+    const bool flat = nrows <= kWave;
+    int rs0 = 0, rlen = 0;
+    if (any && flat && tid < nrows) {
+        const int64_t rb = (int64_t)(y0 + tid) * g.nTx;
+        rs0 = off[rb + x0];
+        rlen = off[rb + x1 + 1] - rs0;
+    }
     if (any) {
         for (int j = tid; j < i; j += kBlock) {
             if (sr[j] > 0.0 && disks_may_overlap(cx, cy, r, sx[j], sy[j], sr[j])) {
@@ -83,34 +97,52 @@ __global__ __launch_bounds__(kBlock) void closure_kernel(uint64_t* ts, const dou
             }
         }
     }
+    if (any && flat && tid < kWave) {   // wave 0: the rows' prefix
+        const int incl = wave_incl_scan_i32(rlen, tid);
+        if (tid < nrows) rs[tid] = rs0;
+        rpre[tid + 1] = incl;
+        if (tid == 0) rpre[0] = 0;
+    }
     __syncthreads();
     const int nc = ncnt;
     if (tid < min(nc, kClosureNbr)) nT[tid] = cover_threshold(sr[nb[tid]]);
     __syncthreads();
     uint64_t cnt = 0;
     double acc = 0.0;
-    if (any) {
+    // entry j: covered by disk i and by none of its listed lower-index neighbours
+    auto credit = [&](int j) {
+        const double2 p = xy[j];
+        if (!(sqdist(p.x, p.y, cx, cy) <= T)) return;
+        bool owned = true;
+        if (nc <= kClosureNbr) {
+            for (int q = 0; q < nc && owned; ++q) {
+                const int c2 = nb[q];
+                owned = !(sqdist(p.x, p.y, sx[c2], sy[c2]) <= nT[q]);
+            }
+        } else {   // overflowed list: every lower-index disk
+            for (int c2 = 0; c2 < i && owned; ++c2)
+                owned = !(sqdist(p.x, p.y, sx[c2], sy[c2]) <= cover_threshold(sr[c2]));
+        }
+        if (owned) {
+            ++cnt;
+            if (!counts) acc += w[j];
+        }
+    };
+    if (any && flat) {
+        const int total = rpre[nrows];
+        for (int f = tid; f < total; f += kBlock) {
+            int lo = 0, hi = nrows - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (rpre[mid] <= f) lo = mid; else hi = mid - 1;
+            }
+            credit(rs[lo] + (f - rpre[lo]));
+        }
+    } else if (any) {
         for (int ty = y0; ty <= y1; ++ty) {
             const int64_t rowbase = (int64_t)ty * g.nTx;
             const int s = off[rowbase + x0], e = off[rowbase + x1 + 1];
-            for (int j = s + tid; j < e; j += kBlock) {
-                const double2 p = xy[j];
-                if (!(sqdist(p.x, p.y, cx, cy) <= T)) continue;
-                bool owned = true;
-                if (nc <= kClosureNbr) {
-                    for (int q = 0; q < nc && owned; ++q) {
-                        const int c2 = nb[q];
-                        owned = !(sqdist(p.x, p.y, sx[c2], sy[c2]) <= nT[q]);
-                    }
-                } else {   // overflowed list: every lower-index disk
-                    for (int c2 = 0; c2 < i && owned; ++c2)
-                        owned = !(sqdist(p.x, p.y, sx[c2], sy[c2]) <= cover_threshold(sr[c2]));
-                }
-                if (owned) {
-                    ++cnt;
-                    if (!counts) acc += w[j];
-                }
-            }
+            for (int j = s + tid; j < e; j += kBlock) credit(j);
         }
     }
     // the area
