@@ -1,4 +1,5 @@
 """Shared fixtures. `-m "not gpu"` runs here (no GPU); `-m gpu` runs on an MI355X box."""
+import math
 import os
 import sys
 
@@ -45,3 +46,26 @@ def ctx(pkg):
     c = pkg.Context(0)
     yield c
     c.close()
+
+
+def _quadrotor_run():
+    path = os.path.join(ROOT, "tests", "golden", "quadrotor_run.csv")
+    return np.loadtxt(path, delimiter=",", comments="#")
+
+
+@pytest.fixture(scope="session")
+def quadrotor_steps(pkg):
+    """(prev, target) per MPC step of the reference's static N = 5 run for UAV 1, as [x; y; R]
+    (N = 1): prev = where the step's MADS started (the initial ring for step 1,
+    src/FullSimulation.jl:803; else the previous step's end state, R = z tan(FOV/2), :238-251);
+    target = the MADS output the reference recorded (z back to R = z tan(FOV/2))."""
+    D = _quadrotor_run()
+    tan = math.tan(100 / 180 * math.pi / 2)
+    x0 = pkg.Base_Functions.allocate_even_circles(15.0, 5, 10 * tan, 250.0, 250.0)
+    out = []
+    for t in range(D.shape[0]):
+        prev = (np.array([x0[0], x0[5], x0[10]]) if t == 0
+                else np.array([D[t - 1, 3], D[t - 1, 4], D[t - 1, 5] * tan]))
+        out.append((prev, np.array([D[t, 0], D[t, 1], D[t, 2] * tan])))
+    return out, tan
+

@@ -51,6 +51,28 @@ def test_golden_static_grid(ctx, pkg, golden, orc):
         assert bi == k and bo == want[k], a
 
 
+def test_reference_mads_outputs_device_cons3(ctx, pkg, orc, quadrotor_steps):
+    """The reference's recorded MADS outputs (UAV 1 of its static N = 5 run, tests/golden/
+    quadrotor_run.csv) through the device poll: per step, a batch of the target, the start and a
+    point 10.5 m from the start, with prev = the step's start and d_lim = 10 m. The device's
+    cons3 keeps the target and the start and rejects the far point (+inf), and the feasible
+    objectives equal the oracle's on the reference static grid (createPOI(5, 5, 100, 100))."""
+    steps, tan = quadrotor_steps
+    poi = pkg.AreaCoverageCalculation.createPOI(5.0, 5.0, 100.0, 100.0)
+    ctx.set_points_records(poi)
+    rmax = np.array([30 * tan])
+    for prev, tgt in steps:
+        cand = np.array([tgt[0], tgt[1], float(round(tgt[2]))])
+        far = np.array([prev[0] + 10.5, prev[1], prev[2]])
+        C = np.stack([cand, prev, far])
+        bo, bi, objs = ctx.poll_best(C, rmax, 1e5, prev=prev, d_lim=np.array([10.0]),
+                                     tan_half_fov=tan, want_all=True)
+        assert np.isinf(objs[2]) and objs[2] > 0
+        for k in (0, 1):
+            assert objs[k] == orc.ref_objective(C[k], poi, rmax), (k, objs[k])
+        assert bi == int(np.argmin(objs[:2])) and bo == objs[bi]
+
+
 def test_golden_firepoints(ctx, golden, firepoints):
     fp10 = np.concatenate(firepoints[:10])
     fpall = np.concatenate(firepoints)

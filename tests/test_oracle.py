@@ -1,5 +1,6 @@
 """CPU: the oracle itself, pinned against the reference's data and integer known answers."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -107,3 +108,26 @@ def test_cons3_oracle_matches_host_mirror(orc, pkg, golden):
     cons3 = TC.create_cons3(prev, 100 / 180 * math.pi, golden["A_dlim"])
     for c, f in zip(golden["A_cands"], golden["A_cons3"]):
         assert cons3(c) == bool(f) == orc.ref_cons3(prev, c, golden["A_dlim"], golden["A_tan"][0])
+
+
+def test_reference_mads_outputs_on_mesh_and_cons3_feasible(orc, pkg, quadrotor_steps):
+    """The reference's only recorded outputs on this path (UAV 1's MADS targets of its static
+    N = 5 run, Quadrotor_Targets.xlsx, with the UAV states of Quadrotor_States*.xlsx; converted
+    by tests/golden/make_quadrotor_fixture.py): every target lies on the granular mesh the
+    build's LTMADS driver uses (integer x, y and R = z tan(FOV/2); granularity 1.0,
+    src/TDM_STATIC_opt.jl:131-137), and passes cons3 (src/TDM_Constraints.jl:54-75, d_lim = 10 m,
+    src/FullSimulation.jl:740) against where its step started, through the C oracle and the host
+    mirror alike — the restated extreme barrier rejects none of the reference's own accepted
+    points; a point 10.5 m from the start fails it (the check has teeth). The other UAVs'
+    targets were never written (src/FullSimulation.jl:370-374), so objectives cannot be replayed."""
+    steps, tan = quadrotor_steps
+    assert len(steps) == 40
+    fov = 100 / 180 * math.pi
+    for prev, tgt in steps:
+        assert tgt[0] == round(tgt[0]) and tgt[1] == round(tgt[1])
+        assert abs(tgt[2] - round(tgt[2])) < 1e-9
+        cand = np.array([tgt[0], tgt[1], float(round(tgt[2]))])
+        assert orc.ref_cons3(prev, cand, np.array([10.0]), tan)
+        assert pkg.TDM_Constraints.create_cons3(prev, fov, np.array([10.0]))(cand)
+        far = np.array([prev[0] + 10.5, prev[1], prev[2]])   # 10.5 m from the start
+        assert not orc.ref_cons3(prev, far, np.array([10.0]), tan)
