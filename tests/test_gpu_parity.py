@@ -659,8 +659,11 @@ def test_poll_walk_stress(ctx, pkg, orc, case):
         ctx.set_points(x, y, w)
         C = np.concatenate([x0[None, :], wl.poll_candidates(x0, rng, ell=2)], axis=0)
         K = C.shape[0]
+        # escapes (half-integers, |d| past the packed range) and the packed range's edges
+        # (|dx|, |dy| = 1023 and |dr| = 511 pack; 1024 and 512 escape): sign extension checked
         for v, d in [(1, 0.5), (2, 1500.0), (N + 4, -0.25), (N + 5, -2048.0), (2 * N + 6, 600.0),
-                     (2 * N + 7, 0.5)]:
+                     (2 * N + 7, 0.5), (3, 1023.0), (4, -1023.0), (5, 1024.0), (N + 6, -1024.0),
+                     (2 * N + 8, 511.0), (2 * N + 9, 512.0), (2 * N + 10, -511.0)]:
             pick = np.flatnonzero(rng.uniform(K) < 0.2)
             pick = pick[pick > 0]
             C[pick, v] += d
