@@ -130,19 +130,40 @@ def src_hash():
 
 
 def pmc_traffic(config, disks, world, algo):
-    """(HBM bytes per poll chain, source note) from profiles/pmc_traffic_config{config}.json
-    when it was measured on these sources, this workload and the default walk; else (None, why)."""
+    """(HBM bytes per poll chain, source note, {kernel: bytes per launch}) from
+    profiles/pmc_traffic_config{config}.json when it was measured on these sources, this workload
+    and the default walk; else (None, why, {})."""
     path = os.path.join(ROOT, "profiles", f"pmc_traffic_config{config}.json")
     if world != 1 or algo != "auto" or disks != "uniform":
-        return None, "not profiled for this workload"
+        return None, "not profiled for this workload", {}
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None, "no PMC file"
+        return None, "no PMC file", {}
     if d.get("src_sha") != src_hash():
-        return None, f"PMC file is from another build (src_sha {d.get('src_sha')})"
-    return d.get("hbm_bytes_per_poll"), os.path.relpath(path, ROOT) + f" (src_sha {d['src_sha']})"
+        return None, f"PMC file is from another build (src_sha {d.get('src_sha')})", {}
+    per = {}
+    for name, v in d.get("kernels", {}).items():
+        base = name.split("<")[0]
+        if base.startswith("mac::"):
+            per[base[5:]] = v.get("hbm_bytes_per_launch")
+    return (d.get("hbm_bytes_per_poll"), os.path.relpath(path, ROOT) + f" (src_sha {d['src_sha']})",
+            per)
+
+
+def kernel_table(kern, pmc_per=None):
+    """{kernel: {"avg_us", "launches"[, "hbm_bytes"]}} of the poll chain's launches that ran
+    (Context.profile_kernels: in-kernel stamps over the timed steps) and the dominant one (the
+    longest average launch)."""
+    out = {}
+    for name, (ms, n) in kern.items():
+        if n:
+            out[name] = {"avg_us": ms / n * 1e3, "launches": n}
+            if pmc_per and pmc_per.get(name) is not None:
+                out[name]["hbm_bytes"] = pmc_per[name]
+    dom = max(out, key=lambda k: out[k]["avg_us"]) if out else None
+    return out, dom
 
 
 def usable_cpus():
@@ -198,6 +219,53 @@ def cpu_baseline(x, y, w, cands, seconds_target: float, threads: int):
     return n / dt, desc
 
 
+def rank_launch_command(n: int, argv, port: int):
+    """The command `bench.py --gpus N` runs when no launcher started it: torch.distributed.run
+    with N local ranks (one process per GPU, RANK / LOCAL_RANK / WORLD_SIZE in their env) over
+    127.0.0.1, each rank running this script with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__), *argv]
+
+
+def world_plan(gpus: int, env=None) -> str:
+    """'run' (this process is a rank, or the only one) or 'launch' (start --gpus ranks first).
+    Raises SystemExit (status 2) when a launcher's WORLD_SIZE disagrees with --gpus: a line for
+    N GPUs must come from N ranks, never from a silently smaller run."""
+    env = os.environ if env is None else env
+    if gpus < 1:
+        log("bench.py: --gpus must be >= 1")
+        raise SystemExit(2)
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "launch" if gpus > 1 else "run"
+    if int(ws) != gpus:
+        log(f"bench.py: WORLD_SIZE={ws} from the launcher but --gpus {gpus}: "
+            f"refusing to report a {ws}-rank run as {gpus} GPUs")
+        raise SystemExit(2)
+    return "run"
+
+
+def launch_ranks(gpus: int, argv) -> int:
+    """Start `gpus` ranks of this script (before this process touches any GPU) and return the
+    launcher's exit status. Each rank uses its LOCAL_RANK's GPU, so the node must show that
+    many devices, unless MAXCOVER_BENCH_DEVICE pins every rank to one device (rehearsals)."""
+    import socket
+    import subprocess
+    import torch   # device_count does not initialise the GPU on this image
+
+    if "MAXCOVER_BENCH_DEVICE" not in os.environ and torch.cuda.device_count() < gpus:
+        log(f"bench.py: --gpus {gpus} but {torch.cuda.device_count()} GPU(s) visible")
+        return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = rank_launch_command(gpus, argv, port)
+    log("bench.py: launching", " ".join(cmd))
+    return subprocess.run(cmd).returncode
+
+
 def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
     """Config 5: src/FullSimulation.jl's optimisation loop with the CA fire (src/DynamicArea.jl)
     streamed into the device list. One step = one MPC timestep: fire step + append/re-index,
@@ -239,6 +307,7 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     split = ctx.profile_split()
+    kern = ctx.profile_kernels()
     k_ms, k_launches, k_cands, k_walk = ctx.profile_read(reset=True)
     ctx.profile(False)
     if world > 1:
@@ -266,6 +335,7 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
     # representative one, the LTMADS poll (l = 2) around the final incumbent on the final point
     # list; the generated poll reads only the incumbent and the permutations (no matrix) — over
     # the mean device chain per poll (in-kernel stamps)
+    kernels, dominant = kernel_table(kern)
     x, y, w = ctx.get_points()
     polls = wl.poll_candidates(sim.x_prev, wl.SplitMix64(args.seed + 1))
     n = polls.shape[1]
@@ -307,11 +377,15 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
             "kernel": (f"poll chain (prep, disk_index, walk_setup, coverage_{k_walk}, "
-                       f"shared bit-words when crowded, finalize + argmin)"),
+                       f"shared bit-words when crowded, finalize + argmin); dominant kernel "
+                       f"{dominant}"),
             "chain_ms": chain_ms, "polls": split[3],
             "split_ms_per_poll": ({"prep": split[0] / split[3], "walk": split[1] / split[3],
                                    "after_walk": split[2] / split[3]} if split[3] else None),
-            "floor": floor, "evals_per_launch": cands_per_launch, "avg_launch_ms": avg_launch_ms,
+            "floor": floor, "evals_per_launch": cands_per_launch,
+            "dominant_kernel": dominant,
+            "avg_launch_ms": kernels[dominant]["avg_us"] * 1e-3 if dominant else avg_launch_ms,
+            "kernels": kernels,
             "brute_force_equiv": {"bytes_per_eval": b_eval,
                                   "note": "SURVEY 8(d)'s full-scan bytes per evaluation at the mean "
                                           "list length: not a roofline of this algorithm"},
@@ -322,6 +396,8 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
         "cpu_baseline": cpu,
         "setup_s": t_set,
     }
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: {world} rank(s) but --gpus {args.gpus}")
     print(json.dumps(out), flush=True)
     D.close()
     ctx.close()
@@ -372,6 +448,8 @@ def main():
         args.steps = 3 if args.config == 5 else 200
     if args.warmup is None:
         args.warmup = 1 if args.config == 5 else 20
+    if world_plan(args.gpus) == "launch":
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     import torch
     import torch.distributed as dist
@@ -441,8 +519,18 @@ def main():
     Kl = hi - lo
 
     ctx = pkg.Context(dev_index, algo=args.algo, tile_points=args.tile_points)
+    # once per MPC step (src/FullSimulation.jl:50-61), outside the per-poll step: the host upload
+    # of the list, then the device tile index over it (mac_set_points_dev_f64: sort, offsets)
     t_set = time.perf_counter()
-    ctx.set_points(x, y, w)   # once per MPC step: upload + tile index (not part of an eval)
+    t_up = time.perf_counter()
+    dx_, dy_, dw_ = (torch.from_numpy(a).to(dev) for a in (x, y, w))
+    torch.cuda.synchronize(dev)
+    t_up = time.perf_counter() - t_up
+    t_idx = time.perf_counter()
+    ctx.set_points_device(dx_, dy_, dw_)
+    torch.cuda.synchronize(dev)
+    t_idx = time.perf_counter() - t_idx
+    del dx_, dy_, dw_
     t_set = time.perf_counter() - t_set
     d_polls = [torch.from_numpy(np.ascontiguousarray(p[lo:hi])).to(dev) for p in polls]
     d_rmax = torch.from_numpy(r_max).to(dev)
@@ -462,6 +550,10 @@ def main():
                            tan_half_fov=tan_half, idx_base=idx_base, stream=s_handle)
              for d, pv in zip(d_polls, d_prevs)]
 
+    # N > 1: the 16-B all-gather straight from d_best, ordered after the poll on its stream,
+    # and one pinned host read of the world x 16-B result (dist.PollGather)
+    gat = pdist.PollGather(coll_dev) if distributed else None
+
     def step(i):
         """One MADS poll. It ends with the best (objective, index) on the host, because the
         next poll's candidates depend on it: polls never overlap."""
@@ -471,7 +563,7 @@ def main():
                               d_dlim=d_dlim, tan_half_fov=tan_half, idx_base=idx_base,
                               stream=s_handle)
             with torch.cuda.stream(stream):
-                return pdist.gather_best(d_best if coll_dev.type == "cuda" else d_best.cpu())
+                return gat(d_best)
         return steps[i % len(steps)]()   # poll + the 16-B result from pinned host memory
 
     for i in range(args.warmup):
@@ -504,6 +596,8 @@ def main():
 
     ctx.profile(True)
     ctx.profile_read(reset=True)
+    if gat is not None:
+        gat.seconds, gat.calls = 0.0, 0
     if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -516,6 +610,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     split = ctx.profile_split()
+    kern = ctx.profile_kernels()
     k_ms, k_launches, k_cands, k_walk = ctx.profile_read(reset=True)
     ctx.profile(False)
     if distributed:
@@ -543,7 +638,8 @@ def main():
     unit_ms = chain_ms if chain_ms else avg_launch_ms
     achieved = floor["bytes"] / (unit_ms * 1e-3) / 1e9 if (k_launches and unit_ms) else None
     b_eval = 3 * M * 8 + 3 * N * 8 + 8     # a brute-force scan per candidate
-    traffic, traffic_src = pmc_traffic(args.config, args.disks, world, args.algo)
+    traffic, traffic_src, pmc_per = pmc_traffic(args.config, args.disks, world, args.algo)
+    kernels, dominant = kernel_table(kern, pmc_per)
 
     # the single-candidate closure path (src/TDM_STATIC_opt.jl:125: DirectSearch calls the
     # objective once per trial point): host-pointer mac_area_f64 latency on the timed workload
@@ -611,9 +707,12 @@ def main():
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "traffic": traffic,
                 "kernel": (f"poll chain (prep, disk_index, walk_setup, coverage_{k_walk}, "
-                           f"finalize + argmin); dominant kernel coverage_{k_walk}_kernel"),
+                           f"finalize + argmin); dominant kernel {dominant}"),
                 "chain_ms": chain_ms,
-                "avg_launch_ms": avg_launch_ms,
+                "dominant_kernel": dominant,
+                "avg_launch_ms": (kernels[dominant]["avg_us"] * 1e-3 if dominant else avg_launch_ms),
+                "kernels": kernels,
+                "walk_avg_launch_ms": avg_launch_ms,
                 "evals_per_launch": cands_per_launch,
                 "split_ms_per_poll": ({"prep": split[0] / split[3], "walk": split[1] / split[3],
                                        "after_walk": split[2] / split[3]} if split[3] else None),
@@ -630,16 +729,31 @@ def main():
                 "timing": "in-kernel workgroup stamps (s_memrealtime) over the timed steps",
                 "note": "achieved = floor.bytes / chain_ms (first workgroup start of the chain's "
                         "first launch to the last workgroup end of its last); avg_launch_ms = the "
-                        "dominant kernel alone (compare with profiles/*rocprof*); traffic = "
-                        "PMC-measured HBM bytes of the whole chain per poll, attached only when "
-                        "the kernel sources hash to the profiled build",
+                        "dominant (longest) kernel alone, kernels = every launch of the chain "
+                        "(in-kernel stamps over the timed steps; compare with profiles/*rocprof*); "
+                        "traffic = PMC-measured HBM bytes of the whole chain per poll (per kernel "
+                        "in kernels.*.hbm_bytes), attached only when the kernel sources hash to "
+                        "the profiled build",
             },
             "cpu_baseline": cpu,
             "closure": closure,
             "best": {"objective": result[0], "index": result[1]},
             "check_timed_poll_vs_scan": check,
             "setup_s": t_set,
+            "setup": {
+                "host_upload_s": t_up, "index_rebuild_s": t_idx,
+                "note": "once per MPC step (the point list changes between MADS runs, "
+                        "src/FullSimulation.jl:50-61), outside ms_per_step: host upload of the "
+                        "x/y/w list, then the device tile index over it (mac_set_points_dev_f64: "
+                        "bbox, tile keys, radix sort, gather, offsets). Amortised over a run's "
+                        "polls: index_rebuild_s / polls per MPC step (100 in the reference)"},
         }
+        if distributed:
+            out["config"]["gather_host_us_per_poll"] = (gat.seconds / max(gat.calls, 1) * 1e6
+                                                        if gat else None)
+        ranks = dist.get_world_size() if distributed else 1
+        if out["n_gpus"] != ranks or ranks != args.gpus:
+            raise SystemExit(f"bench.py: n_gpus {out['n_gpus']}, {ranks} rank(s), --gpus {args.gpus}")
         print(json.dumps(out), flush=True)
     if distributed:
         dist.barrier()

@@ -263,6 +263,14 @@ int32_t mac_profile_read(mac_ctx* ctx, double* kernel_ms, int64_t* launches,
 int32_t mac_profile_split(mac_ctx* ctx, double* prep_ms, double* walk_ms, double* gap_ms,
                           int64_t* polls);
 
+/* Per-kernel split of the same poll chains (call before mac_profile_read with reset): for each
+ * launch role r < n_roles, the summed launch spans (last workgroup end - first workgroup start,
+ * in-kernel stamps) in ms_out[r] and the launches counted in launches_out[r]. Roles:
+ *   0 prep_kernel, 1 disk_index_kernel, 2 walk_setup_kernel, 3 coverage_tiled_poll_kernel,
+ *   4 coverage_poll_kernel, 5 shared_bits_kernel, 6 finalize_kernel (MAC_PROF_ROLES = 7). */
+#define MAC_PROF_ROLES 7
+int32_t mac_profile_kernels(mac_ctx* ctx, double* ms_out, int64_t* launches_out, int32_t n_roles);
+
 /* ---- fire generator (src/DynamicArea.jl, config 5) ------------------------------ */
 /* Cellular-automaton forest fire on an nx x ny grid of dx x dy cells, cell (i, j) 1-based with
  * i the row (x index) and j the column (y index), as the reference indexes grid[i, j].

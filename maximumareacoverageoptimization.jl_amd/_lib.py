@@ -37,6 +37,10 @@ MAC_ALGO_POLL = 3
 MAC_STORE_F64 = 0
 MAC_STORE_F32 = 1
 
+# mac_profile_kernels launch roles (include/maxcover.h MAC_PROF_ROLES)
+PROF_ROLES = ("prep_kernel", "disk_index_kernel", "walk_setup_kernel", "coverage_tiled_poll_kernel",
+              "coverage_poll_kernel", "shared_bits_kernel", "finalize_kernel")
+
 ALGOS = {"auto": MAC_ALGO_AUTO, "scan": MAC_ALGO_SCAN, "tiled": MAC_ALGO_TILED,
          "poll": MAC_ALGO_POLL}
 
@@ -48,7 +52,7 @@ EXPORTS = (
     "mac_remove_covered_f64", "mac_covered_flags_f64", "mac_area_f64", "mac_area_batch_f64",
     "mac_objective_batch_f64", "mac_poll_best_f64", "mac_area_batch_dev_f64",
     "mac_poll_best_dev_f64", "mac_best_fetch", "mac_cover_threshold", "mac_profile_read",
-    "mac_profile_split",
+    "mac_profile_split", "mac_profile_kernels",
     "mac_append_points_f64", "mac_append_points_dev_f64", "mac_mads_run",
     "mac_fire_last_error", "mac_fire_thresholds", "mac_fire_create", "mac_fire_destroy",
     "mac_fire_initial_points", "mac_fire_step", "mac_fire_last_points", "mac_fire_get_grid",
@@ -136,6 +140,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mac_cover_threshold": ([ctypes.c_double], ctypes.c_double),
         "mac_profile_read": ([_vp, _dp, _i64p, _i64p, ctypes.POINTER(_i32), _i32], _i32),
         "mac_profile_split": ([_vp, _dp, _dp, _dp, _i64p], _i32),
+        "mac_profile_kernels": ([_vp, _dp, _i64p, _i32], _i32),
         "mac_append_points_f64": ([_vp, _dp, _dp, _dp, _i64], _i32),
         "mac_mads_run": ([_vp, _dp, _i64, _dp, ctypes.c_double, _dp, _dp, ctypes.c_double,
                           ctypes.POINTER(MadsParams), _dp, ctypes.POINTER(MadsStats)], _i32),
@@ -306,6 +311,15 @@ class Context:
         _check(self._L.mac_profile_split(self._h, ctypes.byref(p1), ctypes.byref(p2),
                                          ctypes.byref(gap), ctypes.byref(n)))
         return p1.value, p2.value, gap.value, int(n.value)
+
+    def profile_kernels(self):
+        """Poll chains since the last reset, per launch role (mac_profile_kernels): {kernel name:
+        (summed launch spans in ms, launches)}. Call before profile_read(reset=True)."""
+        n = len(PROF_ROLES)
+        ms = (ctypes.c_double * n)()
+        cnt = (ctypes.c_int64 * n)()
+        _check(self._L.mac_profile_kernels(self._h, ms, cnt, n))
+        return {name: (ms[r], int(cnt[r])) for r, name in enumerate(PROF_ROLES)}
 
     # -- point list
     def set_points(self, x, y, w) -> None:
@@ -542,7 +556,12 @@ class Context:
 
     def best_fetch(self, d_best, stream=None):
         """The (objective, index) the latest device poll on d_best wrote (mac_best_fetch).
-        Thread-safe: the output words are per call."""
+        Thread-safe: the output words are per call.
+
+        Returns as soon as the poll's mapped result slot lands, while the poll's finalize launch
+        may still be retiring: d_best itself is then valid for device work on any stream, but
+        later host reads of d_obj / d_area, and reuse of the poll's inputs (candidates, d_prev,
+        d_rmax), must be ordered on ``stream`` or follow a synchronisation of it."""
         bo, bi = ctypes.c_double(), ctypes.c_int64()
         _check(self._L.mac_best_fetch(self._h, _devptr(d_best), _devptr(stream),
                                       ctypes.byref(bo), ctypes.byref(bi)))

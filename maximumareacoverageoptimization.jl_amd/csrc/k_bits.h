@@ -152,7 +152,7 @@ __device__ __forceinline__ int run_entry(const int* run_s, const int* run_pre, i
 // spart[i*K + k]: uint32 counts (kCounts: every entry weighs the same) or fp64 weights.
 template <bool kCounts>
 __global__ __launch_bounds__(kBitsThreads) void shared_bits_kernel(
-    const double2* __restrict__ xy, const double* __restrict__ w, const int32_t* __restrict__ off,
+    uint64_t* ts, const double2* __restrict__ xy, const double* __restrict__ w, const int32_t* __restrict__ off,
     Grid g, const DiskRec* __restrict__ urec, const int* __restrict__ umap,
     const int* __restrict__ ucount, const int4* __restrict__ region,
     const uint16_t* __restrict__ nbrT, const float4* __restrict__ lane4,
@@ -175,8 +175,12 @@ __global__ __launch_bounds__(kBitsThreads) void shared_bits_kernel(
     __shared__ int slive[kBitsGrp], sg_toff[kBitsGrp], sg_bp[kBitsGrp + 1], sg_np, sg_next[2];
     __shared__ int sg_m[kBitsGrp], sg_lo[kBitsGrp], sg_hi[kBitsGrp];
 
-    if (mode && *mode != kModePoll) return;                     // uniform
-    if (dcount[kDcBits] + dcount[kDcOther] <= min_disks) return;   // the poll kernel's jobs
+    ts_begin(ts);   // profiling only (k_common.h)
+    if ((mode && *mode != kModePoll) ||                            // uniform
+        dcount[kDcBits] + dcount[kDcOther] <= min_disks) {         // the poll kernel's jobs
+        ts_end(ts);
+        return;
+    }
     const int tid = threadIdx.x, lane = tid & (kWave - 1);
     const int wid = __builtin_amdgcn_readfirstlane(tid / kWave);   // wave-uniform (scalar loads)
 #ifdef MAC_DIAG
@@ -497,6 +501,7 @@ __global__ __launch_bounds__(kBitsThreads) void shared_bits_kernel(
         for (int q = 0; q < 16; ++q) g_diag_bits[16 * blockIdx.x + q] = dg[q];
     }
 #endif
+    ts_end(ts);
 }
 
 }  // namespace mac

@@ -190,13 +190,17 @@ __device__ __forceinline__ void finalize_argmin(const FinBest& fb, double o, int
     }
     if (fb.st) mads_step(fb, bo, gidx, ell, fcur);
     if (lane == 0) {
-        fb.best[0] = bo;
-        fb.best[1] = __builtin_bit_cast(double, gidx);
+        // d_best with agent-scope (sc1, write-through) stores: a host that has read the mirror may
+        // hand d_best to device work on another stream (an RCCL all-gather, dist.DeviceGather)
+        // while this launch retires, and a plain store would sit in this XCD's L2 only
+        unsigned long long* const bw = reinterpret_cast<unsigned long long*>(fb.best);
+        __hip_atomic_store(bw, __builtin_bit_cast(unsigned long long, bo), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(bw + 1, (unsigned long long)gidx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(fb.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (fb.mirror) {
-            // d_best's stores acknowledged by L2 first (a host that has read the mirror may hand
-            // d_best to device work on another stream), then the slot: plain stores to the
-            // mapped words, validated on the host by seq + check (no system-scope fence)
+            // d_best's stores acknowledged first, then the slot: plain stores to the mapped
+            // words, validated on the host by seq + check (no system-scope fence)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const uint64_t o = __builtin_bit_cast(uint64_t, bo);
             const uint64_t ix = (uint64_t)gidx;

@@ -157,7 +157,11 @@ struct CandSrc {
 constexpr int kPrepC = MAC_PREP_C;   // candidates per workgroup (a multiple of 4)
 constexpr int kPrepU = 512;      // UAVs per block = threads per workgroup
 
-// keysP / keysT row pitch: rows start on 128-B boundaries (and hold every workgroup's kPrepC keys)
+// keysP / keysT row pitch: rows start on 128-B boundaries (and hold every workgroup's kPrepC keys:
+// a workgroup writes kPrepC keys from k0 = its index * kPrepC, so 32 must be a multiple of kPrepC
+// or the last workgroup's keys would spill into the next row); the chain fold is one wave
+static_assert(kPrepC % 4 == 0 && 32 % kPrepC == 0 && kPrepC <= 64,
+              "MAC_PREP_C must divide 32 and be a multiple of 4");
 __host__ __device__ inline int keys_ld(int K) { return (K + 31) & ~31; }
 
 struct PrepArgs {

@@ -175,8 +175,11 @@ struct mac_ctx {
     // launch when the device picks the walk (mode != null): the launch that ran is read.
     // c / f: the chain's first launch (the prep) and its last (finalize), whose
     // stamps give the whole poll chain's device span (-1: not stamped)
+    // (role stamps, mac_profile_kernels: [r] = {first slot, slots} of launch role r, -1: none)
     struct Prof { int64_t a, na, b, nb; int64_t K; const int* mode; int algo;
-                  int64_t c = -1, nc = 0, f = -1, nf = 0; };
+                  int64_t c = -1, nc = 0, f = -1, nf = 0;
+                  int64_t role[MAC_PROF_ROLES][2] = {{-1, 0}, {-1, 0}, {-1, 0}, {-1, 0}, {-1, 0},
+                                                     {-1, 0}, {-1, 0}}; };
     std::vector<Prof> prof;                          // recorded launches (guarded by mu)
     DevBuf stamps;
     int64_t stamp_cap = 0, stamp_used = 0;           // in workgroup slots (guarded by mu)
@@ -484,6 +487,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
     // Profiling: the measured walk launches stamp their own workgroups' start / end times
     // (k_common.h), so measuring adds no packet, event or dependency to the stream.
     int64_t ts_a = -1, ts_na = 0, ts_b = -1, ts_nb = 0, ts_c = -1, ts_nc = 0, ts_f = -1, ts_nf = 0;
+    int64_t ts_i = -1, ts_ni = 0, ts_s = -1, ts_ns = 0, ts_g = -1, ts_ng = 0;   // index, set-up, bits
     auto take_ts = [&](int64_t nwg, int64_t& base, int64_t& n) -> uint64_t* {
         if (!ctx->profile) return nullptr;
         std::lock_guard<std::mutex> lk(ctx->mu);
@@ -516,8 +520,18 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
     auto prof_end = [&]() {
         if (!ctx->profile || (ts_a < 0 && ts_b < 0)) return;
         std::lock_guard<std::mutex> lk(ctx->mu);
-        ctx->prof.push_back({ts_a, ts_na, ts_b, ts_nb, (int64_t)K, d_mode,
-                             tiled ? MAC_ALGO_TILED : MAC_ALGO_SCAN, ts_c, ts_nc, ts_f, ts_nf});
+        mac_ctx::Prof p{ts_a, ts_na, ts_b, ts_nb, (int64_t)K, d_mode,
+                        tiled ? MAC_ALGO_TILED : MAC_ALGO_SCAN, ts_c, ts_nc, ts_f, ts_nf};
+        if (ts_c >= 0) {   // a poll chain: every launch's stamps by role (mac_profile_kernels)
+            const int64_t r[MAC_PROF_ROLES][2] = {{ts_c, ts_nc}, {ts_i, ts_ni}, {ts_s, ts_ns},
+                                                  {ts_a, ts_na}, {ts_b, ts_nb}, {ts_g, ts_ng},
+                                                  {ts_f, ts_nf}};
+            for (int q = 0; q < MAC_PROF_ROLES; ++q) {
+                p.role[q][0] = r[q][0];
+                p.role[q][1] = r[q][1];
+            }
+        }
+        ctx->prof.push_back(p);
     };
 
     CandSrc isrc = src;
@@ -622,18 +636,19 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                               ctx->off.as<int32_t>()};
             const unsigned nidx = 8 * ((N + 7) / 8);
             const int dedup = iper ? 1 : 0;
+            uint64_t* tsi = ts_c >= 0 ? take_ts(nidx, ts_i, ts_ni) : nullptr;
             if (isrc.keysT && iper == kIdxPerWide)
                 hipLaunchKernelGGL((disk_index_kernel<true, kIdxPerWide>), dim3(nidx), dim3(kIdxThreads),
-                                   0, s, nullptr, isrc, N, K, ctx->grid, dedup, io);
+                                   0, s, tsi, isrc, N, K, ctx->grid, dedup, io);
             else if (isrc.keysT)
                 hipLaunchKernelGGL((disk_index_kernel<true, kIdxPer>), dim3(nidx), dim3(kIdxThreads), 0, s,
-                                   nullptr, isrc, N, K, ctx->grid, dedup, io);
+                                   tsi, isrc, N, K, ctx->grid, dedup, io);
             else if (iper == kIdxPerWide)
                 hipLaunchKernelGGL((disk_index_kernel<false, kIdxPerWide>), dim3(nidx), dim3(kIdxThreads),
-                                   0, s, nullptr, isrc, N, K, ctx->grid, dedup, io);
+                                   0, s, tsi, isrc, N, K, ctx->grid, dedup, io);
             else
                 hipLaunchKernelGGL((disk_index_kernel<false, kIdxPer>), dim3(nidx), dim3(kIdxThreads), 0,
-                                   s, nullptr, isrc, N, K, ctx->grid, dedup, io);
+                                   s, tsi, isrc, N, K, ctx->grid, dedup, io);
             HCK(hipGetLastError());
             // launch hints from the lane's previous polls (mapped host memory the poll kernel
             // writes): disks with neighbours, most positions of a disk, the walk AUTO would choose
@@ -667,7 +682,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             L->qual.reserve(sizeof(int) * (size_t)N);
             L->nboxT.reserve(sizeof(int4) * (size_t)N * kPollNbr);
             L->partial.reserve(sizeof(double) * (size_t)K * std::max(G, N));
-            hipLaunchKernelGGL(walk_setup_kernel, dim3((unsigned)N), dim3(kBlock), 0, s, nullptr, N,
+            uint64_t* tss = ts_c >= 0 ? take_ts(N, ts_s, ts_ns) : nullptr;
+            hipLaunchKernelGGL(walk_setup_kernel, dim3((unsigned)N), dim3(kBlock), 0, s, tss, N,
                                L->region.as<int4>(), L->nbr.as<uint16_t>(), L->nboxT.as<int4>(),
                                L->ncount.as<int>(), L->dlist.as<int>(), L->mode.as<int>() + 1,
                                L->mode.as<int>(), L->qual.as<int>(), src.mst);
@@ -731,18 +747,19 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             // the shared entries of crowded polls: bit-words per distinct position (k_bits.h);
             // returns at once when few disks have neighbours (the poll kernel took them)
             const unsigned nbits = (unsigned)std::max(1, std::min(N, ctx->cus));
+            uint64_t* tsg = bits_on && ts_c >= 0 ? take_ts(nbits, ts_g, ts_ng) : nullptr;
             if (!bits_on)
                 ;
             else if (counts)
                 hipLaunchKernelGGL(shared_bits_kernel<true>, dim3(nbits), dim3(kBitsThreads), 0, s,
-                                   ctx->xys.as<double2>(), ctx->ws.as<double>(), ctx->off.as<int32_t>(),
+                                   tsg, ctx->xys.as<double2>(), ctx->ws.as<double>(), ctx->off.as<int32_t>(),
                                    ctx->grid, d_urec, d_map, L->ucount.as<int>(), L->region.as<int4>(),
                                    L->nbr.as<uint16_t>(), L->lane4.as<float4>(), L->lanexp.as<float>(),
                                    L->ncount.as<int>(), L->qual.as<int>(), L->mode.as<int>() + 1, d_mode,
                                    N, K, L->spart.as<double>(), bits_on == 2 ? 0 : kBitsMinDisks);
             else
                 hipLaunchKernelGGL(shared_bits_kernel<false>, dim3(nbits), dim3(kBitsThreads), 0, s,
-                                   ctx->xys.as<double2>(), ctx->ws.as<double>(), ctx->off.as<int32_t>(),
+                                   tsg, ctx->xys.as<double2>(), ctx->ws.as<double>(), ctx->off.as<int32_t>(),
                                    ctx->grid, d_urec, d_map, L->ucount.as<int>(), L->region.as<int4>(),
                                    L->nbr.as<uint16_t>(), L->lane4.as<float4>(), L->lanexp.as<float>(),
                                    L->ncount.as<int>(), L->qual.as<int>(), L->mode.as<int>() + 1, d_mode,
@@ -1051,6 +1068,41 @@ int32_t mac_profile_split(mac_ctx* ctx, double* prep_ms, double* walk_ms, double
     if (walk_ms) *walk_ms = a2;
     if (gap_ms) *gap_ms = gap;
     if (polls) *polls = n;
+    return MAC_OK;
+    ABI_END
+}
+
+int32_t mac_profile_kernels(mac_ctx* ctx, double* ms_out, int64_t* launches_out, int32_t n_roles)
+{
+    ABI_BEGIN
+    if (!ctx) return fail(MAC_E_INVAL, "null context");
+    if (n_roles < 0 || (n_roles > 0 && (!ms_out || !launches_out)))
+        return fail(MAC_E_INVAL, "null output / negative role count");
+    set_device(ctx);
+    HCK(hipDeviceSynchronize());
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::vector<uint64_t> st((size_t)(2 * ctx->stamp_used));
+    if (!st.empty())
+        HCK(hipMemcpy(st.data(), ctx->stamps.p, sizeof(uint64_t) * st.size(), hipMemcpyDeviceToHost));
+    const int nr = std::min<int32_t>(n_roles, MAC_PROF_ROLES);
+    for (int r = 0; r < n_roles; ++r) {
+        ms_out[r] = 0.0;
+        launches_out[r] = 0;
+    }
+    for (auto& p : ctx->prof) {
+        for (int r = 0; r < nr; ++r) {
+            const int64_t base = p.role[r][0], nwg = p.role[r][1];
+            if (base < 0 || nwg <= 0) continue;
+            uint64_t t0 = ~(uint64_t)0, t1 = 0;
+            for (int64_t q = base; q < base + nwg; ++q) {
+                t0 = std::min(t0, st[(size_t)(2 * q)]);
+                t1 = std::max(t1, st[(size_t)(2 * q + 1)]);
+            }
+            if (!(t1 > t0)) continue;
+            ms_out[r] += (double)(t1 - t0) / kRealtimeHz * 1e3;
+            ++launches_out[r];
+        }
+    }
     return MAC_OK;
     ABI_END
 }

@@ -66,6 +66,52 @@ def gather_best(best16, group=None):
     return reduce_best(objs, idxs)
 
 
+class PollGather:
+    """The strong-split poll's exchange without per-poll allocations or pageable copies: the
+    poll's 16-B d_best (device) goes into ONE all-gather into a persistent (world x 2) buffer,
+    ordered after the poll on torch's current stream (the caller's poll stream), and ONE pinned
+    host read of the world x 16 B result follows (the next poll's candidates depend on it).
+    RCCL (device buffers) on a GPU backend; on gloo (CPU rehearsal) d_best is first copied into
+    a persistent pinned CPU record. ``seconds`` / ``calls``: host time spent here per poll."""
+
+    def __init__(self, device, group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.device = torch.device(device)
+        self.on_device = self.device.type == "cuda"
+        pin = torch.cuda.is_available()
+        self.out = torch.empty((self.world, 2), dtype=torch.float64, device=self.device)
+        self.host = (torch.empty((self.world, 2), dtype=torch.float64, pin_memory=pin)
+                     if self.on_device else self.out)
+        self.rec = None if self.on_device else torch.empty(2, dtype=torch.float64, pin_memory=pin)
+        self.done = torch.cuda.Event() if self.on_device else None
+        self.seconds = 0.0
+        self.calls = 0
+
+    def __call__(self, best16):
+        import time
+        import torch
+        import torch.distributed as dist
+
+        t0 = time.perf_counter()
+        if self.on_device:
+            dist.all_gather_into_tensor(self.out, best16.reshape(1, 2), group=self.group)
+            self.host.copy_(self.out, non_blocking=True)
+            self.done.record()
+            self.done.synchronize()
+        else:
+            self.rec.copy_(best16)   # (synchronous: d_best to the CPU record)
+            dist.all_gather_into_tensor(self.out, self.rec.reshape(1, 2), group=self.group)
+        h = self.host
+        r = reduce_best(h[:, 0].numpy(), h.view(torch.int64)[:, 1].numpy())
+        self.seconds += time.perf_counter() - t0
+        self.calls += 1
+        return r
+
+
 class DeviceGather:
     """The per-iteration exchange of the sharded MADS loop without per-iteration allocations:
     on a GPU backend (RCCL) the stepper's polls write their 16-B shard best straight into a
@@ -91,6 +137,10 @@ class DeviceGather:
 
     def bind(self, stepper) -> None:
         if self.on_device:
+            import torch
+            # the zero-fill of self.best (torch's current stream) lands before the stepper's
+            # own writes to it (an empty shard's {+inf, -1} record is written at bind)
+            torch.cuda.current_stream(self.device).synchronize()
             stepper.best_buffer(self.best)
 
     def __call__(self, obj, idx):

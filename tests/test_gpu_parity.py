@@ -908,6 +908,68 @@ def test_native_mads_sharded_steppers(ctx, pkg, world):
         assert st["evaluations"] == want["evaluations"]
 
 
+def test_mads_best_buffer_device_exchange(ctx, pkg):
+    """dist.DeviceGather's device path (mac_mads_best_buffer): every poll of a sharded stepper
+    also writes its 16-B shard best into the bound device buffer, and once poll() has returned
+    the buffer holds exactly that poll's (objective, index) — read here on ANOTHER torch stream
+    with no event (what the RCCL all-gather does) — including an empty shard's {+inf, -1}
+    record. The steppers then follow mac_mads_run's iterates."""
+    import torch
+    from importlib import import_module
+    d = import_module(pkg.__name__ + ".dist")
+    wl = pkg.workloads
+    x, y, w = wl.grid_points(160)
+    ctx.set_points(x, y, w)
+    rng = wl.SplitMix64(4242)
+    N = 9
+    x0 = np.concatenate([np.round(200 + rng.uniform(N) * 350), np.round(200 + rng.uniform(N) * 350),
+                         np.full(N, 30.0)])
+    r_max = np.full(N, 30.0 * TAN50)
+    kw = dict(prev=x0, d_lim=np.full(N, 10.0), tan_half_fov=TAN50, n_iter=20, ell0=2, ell_max=5,
+              seed=31337)
+    want_x, want = ctx.mads_run(x0, r_max, 1e5, **kw)
+    K = 2 * x0.size
+    shards = [(0, 20), (20, 20), (20, K)]   # the middle one is empty
+    dev = torch.device("cuda", ctx.device)
+    side = torch.cuda.Stream(dev)
+    steppers, bufs = [], []
+    for sh in shards:
+        s_ = ctx.mads_stepper(x0, r_max, 1e5, shard=sh, **kw)
+        b = torch.full((2,), 7.0, dtype=torch.float64, device=dev)   # not the record
+        torch.cuda.current_stream(dev).synchronize()
+        s_.best_buffer(b)
+        steppers.append(s_)
+        bufs.append(b)
+    host = torch.empty((len(shards), 2), dtype=torch.float64, pin_memory=True)
+    polls = 0
+    while True:
+        res = [s_.poll() for s_ in steppers]
+        if res[0][0]:
+            break
+        polls += 1
+        with torch.cuda.stream(side):   # no event: ordered only by poll()'s return
+            for q, b in enumerate(bufs):
+                host[q].copy_(b, non_blocking=True)
+        side.synchronize()
+        for q, (done, bo, bi) in enumerate(res):
+            got_o = float(host[q, 0])
+            got_i = int(host[q].view(torch.int64)[1])
+            if shards[q][0] == shards[q][1]:
+                assert (got_o, got_i) == (math.inf, -1), (polls, q)
+            else:
+                assert got_i == bi and (got_o == bo or (math.isinf(got_o) and math.isinf(bo))), \
+                    (polls, q, got_o, got_i, bo, bi)
+        bo, bi = d.reduce_best([r[1] for r in res], [r[2] for r in res])
+        for s_ in steppers:
+            s_.update(bo, bi)
+    assert polls == want["iterations"] > 3
+    for s_ in steppers:
+        xs, st = s_.result()
+        s_.best_buffer(None)
+        s_.close()
+        assert np.array_equal(xs, want_x) and st["f"] == want["f"]
+
+
 @pytest.mark.parametrize("N,n_iter,ell0,ell_max,cons3,stall", [
     (40, 60, 2, 5, True, False),     # iteration limit, cons3
     (40, 200, 2, 4, False, True),    # mesh precision limit after 3 polls: later polls already enqueued

@@ -59,6 +59,11 @@ for s in $STEPS; do
         MAXCOVER_BENCH_DEVICE=0 run weak2 300 python -m torch.distributed.run --nnodes=1 \
             --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 \
             --no-cpu --dist-backend gloo --steps 20 ; rc=$? ;;
+    self2)   # bench.py --gpus 2 with no external launcher: it starts its two ranks itself (gloo; both on device 0)
+        MAXCOVER_BENCH_DEVICE=0 run self2 300 python bench.py --gpus 2 --no-cpu --dist-backend gloo --steps 20 ; rc=$?
+        grep '^{' gpurun_out/self2.log > gpurun_out/self2_${TAG}.json ;;
+    c5polls)  # per-poll kernel times of the config-5 loop; the slowest polls saved for analysis
+        run c5polls 600 python tools/c5_polls.py ; rc=$? ;;
     c5x2)    # rehearsal of the N=2 config-5 path (sharded MADS) on one GPU (gloo; both ranks on device 0)
         MAXCOVER_BENCH_DEVICE=0 run c5x2 400 python -m torch.distributed.run --nnodes=1 \
             --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 \
