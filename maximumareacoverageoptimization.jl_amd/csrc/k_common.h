@@ -27,8 +27,12 @@ constexpr int kBitsTab = 2048;     // bit-word kernel: positions per table group
 constexpr int kBitsMinDisks = 16;  // bit-word kernel: used above this many disks with neighbours
 // poll walk counters (dcount[]): [0] disks with neighbours the bit-word kernel can take (dlist
 // from the front), [1] poll-kernel jobs taken, [2] the other disks with neighbours (dlist from the
-// back), [3] bit-word jobs taken; cleared by the index kernel
-constexpr int kDcBits = 0, kDcPollJobs = 1, kDcOther = 2, kDcBitsJobs = 3;
+// back), [3] bit-word / union-pass jobs taken, [4] union-pass jobs listed (k_or.h), [5] disks with
+// lower neighbours whose upper list overflowed (the union pass stands down); cleared by the index
+// kernel (the lane's mode buffer holds [walk, dcount[0..6]])
+constexpr int kDcBits = 0, kDcPollJobs = 1, kDcOther = 2, kDcBitsJobs = 3, kDcOrJobs = 4,
+              kDcOrBad = 5;
+constexpr int kDcCount = 6;
 
 constexpr int kModePoll = 1;
 constexpr int kModeTiled = 2;

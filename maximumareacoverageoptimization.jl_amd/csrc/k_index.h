@@ -134,7 +134,7 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
     }
     MAC_IDX_STAMP(0);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        for (int q = 0; q < 4; ++q) o.dcount[q] = 0;   // the poll walk's counters (k_common.h)
+        for (int q = 0; q < kDcCount; ++q) o.dcount[q] = 0;   // the poll walk's counters (k_common.h)
     }
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
     const int64_t row = (int64_t)i * K;

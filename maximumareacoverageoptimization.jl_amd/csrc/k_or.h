@@ -1,0 +1,406 @@
+// k_or.h — shared entries by per-entry union (equal weights): the shared-entry pass of crowded
+// polls (config 5's clustered disks over the fire, config 4 "clustered").
+//
+// Ownership recap (k_poll.h): the walk of disk d credits every entry of region d that lies in no
+// LOWER neighbour's box; an entry e that lies in several region boxes ("shared") has its disk set
+// D_e = {d : tile(e) in box d}, and the walk of j0 = min D_e credits it when disk j0 of the
+// candidate covers it (no lower box holds e, so it is not shared for j0). The reference counts
+// e once when ANY disk covers it (src/AreaCoverageCalculation.jl:67-78, first hit + break), so
+// the missing part of e's count is
+//     [OR_{d in D_e} cov_d(e, k)] AND NOT cov_{j0}(e, k).
+// This pass adds exactly that, once per shared entry: e belongs to the job list of i = max D_e
+// (the entries of region i in some lower box and in no UPPER box, so D_e is {i} plus lower
+// neighbours of i, the lists walk_setup builds), split in blocks of 64 entries (walk_setup lists
+// the jobs). Per job:
+//   1. stage the 64 entries; per disk slot m ({i} + lower neighbours) the 64-bit mask live[m] of
+//      entries inside its box, and lmask[m] of entries whose j0 is that disk;
+//   2. per disk with live entries, per distinct position u of that disk (k_index.h), the 64-bit
+//      word T[u] of the entries it covers — the walk's exact fp32 filter (k_poll.h header), band
+//      entries re-decided in fp64 — then per candidate k: Y |= T[u_d(k)], Z |= T[u_d(k)] & lmask;
+//   3. per candidate: popcount(Y & ~Z) added (integer atomics: exact in any order) to spart row i.
+// Tests: sum over shared entries of sum over d in D_e of U_d (distinct positions), against the
+// bit-word kernel's per-owner (U_i + sum over ALL neighbours of U_j) x |S_i|: the owner form tests
+// each shared entry once per owner and against every neighbour's positions (3.4e9 tests on the
+// slowest config-5 poll, 6e8 here).
+// Used when every disk with neighbours fits the lists (at most kPollNbr lower and upper
+// neighbours, regions at most 64 x 64 tiles) and the list is not weighted; otherwise the poll
+// kernel's fp64 jobs take every disk (k_poll.h shared_route).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "predicate.h"
+#include "k_common.h"
+#include "k_lane.h"
+
+#pragma clang fp contract(off)
+
+namespace mac {
+
+constexpr int kOrThreads = 512;                 // 8 waves
+constexpr int kOrPT = 8;                        // candidates per thread per candidate chunk
+constexpr int kOrKC = kOrPT * kOrThreads;       // 4096 candidates per chunk
+constexpr int kOrE = 64;                        // entries per job
+constexpr int kOrTab = 4096;                    // positions per table chunk (32 KB of words)
+constexpr int kOrRuns = 64 * 32;                // tile runs of a region (64 rows x 32 runs)
+
+// Which shared-entry pass a poll takes (device side, uniform; the host's hint bits_on: 0 none,
+// 1 above kBitsMinDisks disks with neighbours, 2 always): 0 the poll kernel's fp64 jobs for
+// every disk with neighbours; 1 the bit-word kernel (k_bits.h, weighted lists) for the disks it
+// qualifies + fp64 jobs for the others; 2 this union pass for every disk (equal weights).
+__device__ __forceinline__ int shared_route(const int* __restrict__ dcount, int bits_on, int counts)
+{
+    const int nA = dcount[kDcBits], nB = dcount[kDcOther];
+    if (!bits_on || nA + nB <= (bits_on == 2 ? 0 : kBitsMinDisks)) return 0;
+    if (!counts) return 1;
+    return nB == 0 && dcount[kDcOrBad] == 0 ? 2 : 0;
+}
+
+// Row r's tiles of region R (at most 64 x 64 tiles) that lie in some lower box and in no upper
+// box, as a mask of tile columns relative to R.x.
+__device__ __forceinline__ uint64_t or_row_mask(const int4& R, int r, const int4* lbox, int nl,
+                                                const int4* ubox, int nu)
+{
+    if (r < R.z || r > R.w) return 0;
+    auto span = [&](const int4& Q) -> uint64_t {
+        if (r < Q.z || r > Q.w) return 0;
+        const int a = max(R.x, Q.x) - R.x, b = min(R.y, Q.y) - R.x;
+        if (a > b) return 0;
+        return (b - a == 63 ? ~0ull : ((1ull << (b - a + 1)) - 1)) << a;
+    };
+    uint64_t lo = 0, up = 0;
+    for (int m = 0; m < nl; ++m) lo |= span(lbox[m]);
+    for (int m = 0; m < nu; ++m) up |= span(ubox[m]);
+    const int tw = R.y - R.x + 1;
+    uint64_t mask = lo & ~up;
+    if (tw < 64) mask &= (1ull << tw) - 1;
+    return mask;
+}
+
+// Entries of row r's masked runs (wave 0: lane = row; off loads of every run in flight).
+__device__ __forceinline__ int or_row_count(const int32_t* __restrict__ off, const Grid& g,
+                                            const int4& R, int r, uint64_t mask)
+{
+    const int64_t rowbase = (int64_t)r * g.nTx + R.x;
+    int n = 0;
+    for (uint64_t m2 = mask; m2;) {
+        const int a = __builtin_ctzll(m2);
+        const uint64_t from = m2 >> a;
+        const int len = ~from ? __builtin_ctzll(~from) : 64 - a;
+        n += off[rowbase + a + len] - off[rowbase + a];
+        m2 &= len + a >= 64 ? 0ull : (~0ull << (a + len));
+    }
+    return n;
+}
+
+// walk_setup's part (block i, after neighbors_block with the lists in LDS): the number of entries
+// of region i that this pass owns (lower box, no upper box) and one job per 64 of them, appended
+// to jobs[] ({i, block}) from the counter dcount[kDcOrJobs]. A list past `cap` (cannot happen:
+// the owned sets are disjoint, cap >= M / 64 + N) makes the pass stand down (kDcOrBad).
+__device__ __forceinline__ void or_list_jobs(int i, const int4& R, const int4* lbox, int nl,
+                                             const int4* ubox, int nu, const int32_t* __restrict__ off,
+                                             const Grid& g, int2* __restrict__ jobs, int cap,
+                                             int* __restrict__ dcount)
+{
+    __shared__ int s_base, s_nblk;
+    const int tid = threadIdx.x;
+    if (nl == 0 || nl > kPollNbr || nu > kPollNbr || R.y - R.x + 1 > 64 || R.w - R.z + 1 > 64)
+        return;   // (uniform) nothing owned, or the pass stands down for this poll
+    if (tid < kWave) {
+        const int r = R.z + tid;
+        const uint64_t mask = or_row_mask(R, r, lbox, nl, ubox, nu);
+        int n = or_row_count(off, g, R, r, mask);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) n += __shfl_xor(n, o, kWave);
+        if (tid == 0) {
+            const int nblk = (n + kOrE - 1) / kOrE;
+            s_nblk = nblk;
+            s_base = nblk ? atomicAdd(dcount + kDcOrJobs, nblk) : 0;
+            if (nblk && s_base + nblk > cap) atomicAdd(dcount + kDcOrBad, 1);
+        }
+    }
+    __syncthreads();
+    const int base = s_base, nblk = s_nblk;
+    for (int b = tid; b < nblk; b += kBlock)
+        if (base + b < cap) jobs[base + b] = make_int2(i, b);
+}
+
+struct OrArgs {
+    const double2* xy;
+    const int32_t* off;
+    Grid g;
+    const DiskRec* urec;
+    const int* umap;
+    const int* ucount;
+    const int4* region;
+    const uint16_t* nbrT;
+    const int4* nboxT;
+    const int* ncount;
+    const int4* nboxU;
+    const int* ncountU;
+    const float4* lane4;
+    const float* lanexp;
+    const int2* jobs;
+    int* dcount;
+    const int* mode;
+    unsigned* spart;   // uint32 count rows [N][K] (the poll kernel zeroed the rows of disks with neighbours)
+    int N, K, bits_on;
+};
+
+// (cur << 1) | sign bit of v (v_alignbit_b32 {cur, v} >> 31)
+__device__ __forceinline__ uint32_t or_shift_sign(uint32_t cur, float v)
+{
+    uint32_t r;
+    asm("v_alignbit_b32 %0, %1, %2, 31" : "=v"(r) : "v"(cur), "v"(v));
+    return r;
+}
+
+__global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4))) void shared_or_kernel(uint64_t* ts, OrArgs a)
+{
+    __shared__ int sid[kPollNbr + 1], sU[kPollNbr + 1];
+    __shared__ int4 sbox[kPollNbr + 1], subox[kPollNbr];
+    __shared__ int run_s[kOrRuns], run_pre[kOrRuns + 1], run_row[kOrRuns];
+    __shared__ int wrun[kWave];
+    __shared__ double2 s64[kOrE];
+    __shared__ int2 stile[kOrE];
+    __shared__ int js[kOrE];
+    __shared__ uint64_t live[kPollNbr + 1], lmask[kPollNbr + 1];
+    __shared__ int rel[kPollNbr + 1];
+    __shared__ __attribute__((aligned(16))) float4 ent[kOrE / 2];   // {U0, U1, V0, V1} per entry pair
+    __shared__ f32x2 entq[kOrE / 2];                                 // {Q0, Q1}
+    __shared__ uint2 tab[kOrTab];
+    __shared__ int s_nrel, s_total, s_job;
+
+    ts_begin(ts);
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+    constexpr int kWaves = kOrThreads / kWave;
+    if ((a.mode && *a.mode != kModePoll) || shared_route(a.dcount, a.bits_on, 1) != 2) {   // uniform
+        ts_end(ts);
+        return;
+    }
+    const int njobs = a.dcount[kDcOrJobs];
+    const int K = a.K;
+    const Grid g = a.g;
+    for (int job = blockIdx.x; job < njobs;) {
+        const int2 jb = a.jobs[job];
+        const int i = jb.x, blk = jb.y;
+        // disk i's lists (slot 0: disk i itself, slots 1..nc: its lower neighbours)
+        const int nc = a.ncount[i], ncU = a.ncountU[i];
+        if (tid < nc) {
+            sid[1 + tid] = a.nbrT[i * kPollNbr + tid];
+            sbox[1 + tid] = a.nboxT[i * kPollNbr + tid];
+        }
+        if (tid < ncU) subox[tid] = a.nboxU[i * kPollNbr + tid];
+        if (tid == 0) {
+            sid[0] = i;
+            sbox[0] = a.region[i];
+        }
+        __syncthreads();
+        const int4 R = sbox[0];
+        // the owned runs of region i (wave 0: lane = row), and the disks' position counts
+        if (tid < kWave) {
+            const int r = R.z + lane;
+            const uint64_t mask = or_row_mask(R, r, sbox + 1, nc, subox, ncU);
+            const int64_t rowbase = (int64_t)r * g.nTx + R.x;
+            const int cnt = __popcll(mask & ~(mask << 1));   // runs of the row
+            const int qi = wave_incl_scan_i32(cnt, lane);
+            // the row's runs: first entry and length (every off load in flight), then the
+            // lengths turned into the exclusive prefix over the region's runs
+            int qq = qi - cnt, len_row = 0;
+            for (uint64_t m2 = mask; m2;) {
+                const int a0 = __builtin_ctzll(m2);
+                const uint64_t from = m2 >> a0;
+                const int len = ~from ? __builtin_ctzll(~from) : 64 - a0;
+                const int s0 = a.off[rowbase + a0];
+                const int n0 = a.off[rowbase + a0 + len] - s0;
+                run_s[qq] = s0;
+                run_pre[qq] = n0;
+                run_row[qq] = r;
+                len_row += n0;
+                ++qq;
+                m2 &= len + a0 >= 64 ? 0ull : (~0ull << (a0 + len));
+            }
+            const int ei = wave_incl_scan_i32(len_row, lane);
+            int pre = ei - len_row;
+            for (int z = qi - cnt; z < qi; ++z) {
+                const int n0 = run_pre[z];
+                run_pre[z] = pre;
+                pre += n0;
+            }
+            if (lane == kWave - 1) {
+                wrun[0] = qi;
+                run_pre[qi] = ei;
+                s_total = ei;
+            }
+        } else if (tid - kWave <= nc) {
+            sU[tid - kWave] = a.ucount[sid[tid - kWave]];
+        }
+        __syncthreads();
+        const int nrun = wrun[0], total = s_total;
+        // the job's 64 entries: exact coordinates, tiles (x from the coordinate as the walk does,
+        // y = the run's row); past the owned list: NaN, tile -1 (in no box)
+        if (tid < kOrE) {
+            const int f = blk * kOrE + tid;
+            double2 p = make_double2(__builtin_nan(""), __builtin_nan(""));
+            int2 tl = make_int2(-1, -1);
+            if (f < total) {
+                int lo = 0, hi = nrun - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (run_pre[mid] <= f) lo = mid; else hi = mid - 1;
+                }
+                p = a.xy[run_s[lo] + (f - run_pre[lo])];
+                tl = make_int2(tile_of(p.x, g.gx0, g.invS, g.nTx), run_row[lo]);
+            }
+            s64[tid] = p;
+            stile[tid] = tl;
+            // j0: the lowest disk whose box holds the entry (slot index; -1: none)
+            int best = -1, bid = 0x7fffffff;
+            for (int m = 0; m <= nc; ++m)
+                if (tl.x >= 0 && box_has(sbox[m], tl.x, tl.y) && sid[m] < bid) {
+                    bid = sid[m];
+                    best = m;
+                }
+            js[tid] = best;
+        }
+        __syncthreads();
+        // per disk slot: live entries (inside its box) and the entries it is j0 of
+        for (int m = wid; m <= nc; m += kWaves) {
+            const int2 tl = stile[lane];
+            const uint64_t lv = __ballot(tl.x >= 0 && box_has(sbox[m], tl.x, tl.y));
+            const uint64_t lm = __ballot(js[lane] == m);
+            if (lane == 0) {
+                live[m] = lv;
+                lmask[m] = lm;
+            }
+        }
+        __syncthreads();
+        if (tid < kWave) {   // the disks with live entries, in slot order
+            int n = 0;
+            for (int m0 = 0; m0 <= nc; m0 += kWave) {
+                const int m = m0 + lane;
+                const bool has = m <= nc && live[m] != 0;
+                const uint64_t bal = __ballot(has);
+                if (has) rel[n + __popcll(bal & ((1ull << lane) - 1))] = m;
+                n += __popcll(bal);
+            }
+            if (lane == 0) s_nrel = n;
+        }
+        __syncthreads();
+        const int nrel = s_nrel;
+
+        for (int kc0 = 0; kc0 < K; kc0 += kOrKC) {
+            uint64_t Y[kOrPT], Z[kOrPT];
+#pragma unroll
+            for (int c = 0; c < kOrPT; ++c) Y[c] = Z[c] = 0;
+            for (int r = 0; r < nrel; ++r) {
+                const int m = rel[r];
+                const int d = sid[m], U = sU[m];
+                const int64_t row = (int64_t)d * K;
+                const uint64_t lv = live[m], lm = lmask[m];
+                // the candidates' positions of disk d (in flight during the tables)
+                int um[kOrPT];
+#pragma unroll
+                for (int c = 0; c < kOrPT; ++c) {
+                    const int k = kc0 + tid + c * kOrThreads;
+                    um[c] = k < K ? a.umap[row + k] : -1;
+                }
+                // the entries relative to region d's centre, as the walk stages them; entries
+                // outside box d, past the list or non-finite are inert (Q = +inf: d' = -inf)
+                if (tid < kOrE) {
+                    const int4 Rd = sbox[m];
+                    const double ox = g.gx0 + 0.5 * (double)(Rd.x + Rd.y + 1) * g.S;
+                    const double oy = g.gy0 + 0.5 * (double)(Rd.z + Rd.w + 1) * g.S;
+                    const double2 p = s64[tid];
+                    const float fu = (float)(p.x - ox), fv = (float)(p.y - oy);
+                    const bool f = ((lv >> tid) & 1) && __builtin_isfinite(fu) && __builtin_isfinite(fv);
+                    float* const eu = reinterpret_cast<float*>(&ent[tid >> 1]);
+                    eu[tid & 1] = f ? fu : 0.0f;
+                    eu[2 + (tid & 1)] = f ? fv : 0.0f;
+                    reinterpret_cast<float*>(&entq[tid >> 1])[tid & 1] =
+                        f ? __builtin_fmaf(fu, fu, fv * fv) : __builtin_inff();
+                }
+                __syncthreads();
+                const bool w0 = (uint32_t)lv != 0, w1 = (uint32_t)(lv >> 32) != 0;
+                for (int u0 = 0; u0 < U; u0 += kOrTab) {
+                    const int u1 = min(U, u0 + kOrTab);
+                    for (int p = u0 + tid; p < u1; p += kOrThreads) {
+                        const float4 c4 = a.lane4[row + p];
+                        const float xp = a.lanexp[row + p];
+                        const f32x2 sa = {c4.x, c4.x}, sb = {c4.y, c4.y}, st = {c4.z, c4.z},
+                                    ns = {c4.w, c4.w}, xp2 = {xp, xp};
+                        uint32_t cw[2] = {0u, 0u};
+                        float bmin = __builtin_inff();
+#pragma unroll
+                        for (int wv = 0; wv < 2; ++wv) {
+                            if (!(wv ? w1 : w0)) continue;   // uniform: no live entry in the word
+#pragma unroll 4
+                            for (int j = 0; j < 16; ++j) {
+                                const float4 uv = ent[16 * wv + j];
+                                const f32x2 qq = entq[16 * wv + j];
+                                const f32x2 U2 = {uv.x, uv.y}, V2 = {uv.z, uv.w};
+                                const f32x2 dd = __builtin_elementwise_fma(
+                                    qq, ns, __builtin_elementwise_fma(V2, sb, __builtin_elementwise_fma(U2, sa, st)));
+                                // covered iff d' > X' iff X' - d' < 0: its sign bit shifted in
+                                const f32x2 sd2 = xp2 - dd;
+                                cw[wv] = or_shift_sign(cw[wv], sd2.x);
+                                cw[wv] = or_shift_sign(cw[wv], sd2.y);
+                                bmin = __builtin_fminf(bmin, __builtin_fminf(__builtin_fabsf(dd.x),
+                                                                             __builtin_fabsf(dd.y)));
+                            }
+                        }
+                        uint32_t t0 = __builtin_bitreverse32(cw[0]), t1 = __builtin_bitreverse32(cw[1]);
+                        // X' < 2 for every normal position: no |d'| <= 2 means no band entry; a
+                        // band (or forced) position re-decides its live entries, band ones in fp64
+                        if (bmin <= 2.0f || !(xp < 2.0f)) {
+                            const DiskRec rr = a.urec[row + p];
+                            uint32_t t[2] = {0u, 0u};
+                            for (int e = 0; e < kOrE; ++e) {
+                                const float4 uv = ent[e >> 1];
+                                const float qv = reinterpret_cast<const f32x2*>(entq)[e >> 1][e & 1];
+                                const float U1 = (e & 1) ? uv.y : uv.x, V1 = (e & 1) ? uv.w : uv.z;
+                                const float dp = __builtin_fmaf(qv, c4.w, __builtin_fmaf(V1, c4.y, __builtin_fmaf(U1, c4.x, c4.z)));
+                                bool cov = dp > xp;
+                                if (__builtin_fabsf(dp) <= xp) {
+                                    const double2 q = s64[e];
+                                    cov = qv != __builtin_inff() && sqdist(q.x, q.y, rr.cx, rr.cy) <= rr.T;
+                                }
+                                if (cov) t[e >> 5] |= 1u << (e & 31);
+                            }
+                            t0 = t[0];
+                            t1 = t[1];
+                        }
+                        tab[p - u0] = make_uint2(t0, t1);
+                    }
+                    __syncthreads();
+                    // combine: the union word and the j0 word of every candidate
+#pragma unroll
+                    for (int c = 0; c < kOrPT; ++c) {
+                        const int u = um[c];
+                        if (u >= u0 && u < u1) {
+                            const uint2 t2 = tab[u - u0];
+                            const uint64_t t = (uint64_t)t2.x | ((uint64_t)t2.y << 32);
+                            Y[c] |= t;
+                            Z[c] |= t & lm;
+                        }
+                    }
+                    __syncthreads();   // the next chunk / disk overwrites the tables and entries
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < kOrPT; ++c) {
+                const int k = kc0 + tid + c * kOrThreads;
+                const int n = __popcll(Y[c] & ~Z[c]);
+                if (k < K && n) atomicAdd(a.spart + (int64_t)i * K + k, (unsigned)n);
+            }
+        }
+        // the next job
+        if (tid == 0) s_job = (int)gridDim.x + atomicAdd(a.dcount + kDcBitsJobs, 1);
+        __syncthreads();
+        job = s_job;
+    }
+    ts_end(ts);
+}
+
+}  // namespace mac

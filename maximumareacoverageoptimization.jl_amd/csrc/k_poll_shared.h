@@ -14,6 +14,7 @@
 #include "predicate.h"
 #include "k_common.h"
 #include "k_index.h"
+#include "k_or.h"
 
 #pragma clang fp contract(off)
 
@@ -26,6 +27,10 @@ namespace mac {
 // A disk with neighbours goes to the bit-word kernel's list (front of dlist, k_bits.h) when its
 // list did not overflow and its region is at most 64 x 64 tiles; otherwise to the back of dlist
 // (the poll kernel's fp64 jobs).
+// With nboxU (the shared-entry union pass, k_or.h): also the UPPER neighbours' boxes (j > i,
+// nboxU / ncountU, at most kPollNbr kept), and the lists in LDS for the caller (lbox / ubox,
+// counts in cnt2[0..1]); a disk with lower neighbours whose upper list overflows is counted in
+// dcount[kDcOrBad] (the union pass then stands down for the poll).
 // R: region i; Q[q]: region j = threadIdx.x + q * kBlock (j < i), loaded by the caller beside the
 // walk choice's costs (one round trip); further j are loaded here.
 constexpr int kNbrPre = 4;   // regions per thread loaded up front (i <= 1024)
@@ -34,10 +39,24 @@ __device__ __forceinline__ void neighbors_block(int i, int N, const int4& R, con
                                                 uint16_t* __restrict__ nbr, int4* __restrict__ nboxT,
                                                 int* __restrict__ ncount,
                                                 int* __restrict__ dlist, int* __restrict__ dcount,
-                                                int* __restrict__ qual)
+                                                int* __restrict__ qual,
+                                                int4* __restrict__ nboxU = nullptr,
+                                                int* __restrict__ ncountU = nullptr,
+                                                int4* lbox = nullptr, int4* ubox = nullptr,
+                                                int* cnt2 = nullptr)
 {
-    __shared__ int cnt;
-    if (threadIdx.x == 0) cnt = 0;
+    __shared__ int cnt, cntU;
+    if (threadIdx.x == 0) {
+        cnt = 0;
+        cntU = 0;
+    }
+    // the upper neighbours' regions in flight beside the lower ones' tests
+    int4 QU[kNbrPre];
+#pragma unroll
+    for (int q = 0; q < kNbrPre; ++q) {
+        const int j = i + 1 + (int)threadIdx.x + q * kBlock;
+        QU[q] = nboxU && j < N ? region[j] : make_int4(0x7fffffff, -1, 0x7fffffff, -1);
+    }
     __syncthreads();
     if (R.x <= R.y) {
         auto test = [&](int j, const int4& B) {
@@ -46,6 +65,7 @@ __device__ __forceinline__ void neighbors_block(int i, int N, const int4& R, con
                 if (p < kPollNbr) {
                     nbr[i * kPollNbr + p] = (uint16_t)j;
                     nboxT[i * kPollNbr + p] = B;   // the neighbour's region box
+                    if (lbox) lbox[p] = B;
                 }
             }
         };
@@ -55,6 +75,20 @@ __device__ __forceinline__ void neighbors_block(int i, int N, const int4& R, con
             if (j < i) test(j, Q[q]);
         }
         for (int j = threadIdx.x + kNbrPre * kBlock; j < i; j += kBlock) test(j, region[j]);
+        if (nboxU) {
+            auto testU = [&](const int4& B) {
+                if (box_overlap(B, R)) {
+                    const int p = atomicAdd(&cntU, 1);
+                    if (p < kPollNbr) {
+                        nboxU[i * kPollNbr + p] = B;
+                        ubox[p] = B;
+                    }
+                }
+            };
+#pragma unroll
+            for (int q = 0; q < kNbrPre; ++q) testU(QU[q]);
+            for (int j = i + 1 + (int)threadIdx.x + kNbrPre * kBlock; j < N; j += kBlock) testU(region[j]);
+        }
     }
     __syncthreads();
     const int nc = cnt;   // (uniform, as R is)
@@ -66,6 +100,14 @@ __device__ __forceinline__ void neighbors_block(int i, int N, const int4& R, con
             if (!bad) dlist[atomicAdd(dcount + kDcBits, 1)] = i;
             else dlist[N - 1 - atomicAdd(dcount + kDcOther, 1)] = i;
         }
+        if (nboxU) {
+            ncountU[i] = cntU;
+            if (nc > 0 && cntU > kPollNbr) atomicAdd(dcount + kDcOrBad, 1);
+        }
+    }
+    if (cnt2 && threadIdx.x == 0) {
+        cnt2[0] = nc;
+        cnt2[1] = cntU;
     }
 }
 

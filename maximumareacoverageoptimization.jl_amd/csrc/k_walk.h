@@ -287,11 +287,22 @@ __global__ __launch_bounds__(kBlock) void coverage_tiled_poll_kernel(
 // neighbors_block) for the poll kernel, the bit-word kernel, finalize and the per-candidate walk;
 // block 0 sets mode[0] to the poll walk (coverage_tiled_poll_kernel, when launched, makes the choice
 // after it), or to 0 when the pipelined MADS loop has stopped.
+// With orj (the union pass, k_or.h, will run on this poll): block i also builds disk i's UPPER
+// neighbour boxes and lists the union pass's jobs for the shared entries region i owns.
+struct OrSetup {
+    int4* nboxU;
+    int* ncountU;
+    int2* jobs;
+    int cap;
+    const int32_t* off;
+    Grid g;
+};
+
 __global__ __launch_bounds__(kBlock) void walk_setup_kernel(
     uint64_t* ts, int N, const int4* __restrict__ region, uint16_t* __restrict__ nbr,
     int4* __restrict__ nboxT, int* __restrict__ ncount, int* __restrict__ dlist,
     int* __restrict__ dcount, int* __restrict__ mode, int* __restrict__ qual,
-    const MadsState* __restrict__ halt)
+    const MadsState* __restrict__ halt, OrSetup orj)
 {
     ts_begin(ts);
     // the neighbour lists' regions, loaded beside the halt word (one round trip)
@@ -312,7 +323,16 @@ __global__ __launch_bounds__(kBlock) void walk_setup_kernel(
         return;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) mode[0] = kModePoll;
-    if (i < N) neighbors_block(i, N, R, Q, region, nbr, nboxT, ncount, dlist, dcount, qual);
+    if (i < N && !orj.jobs) {
+        neighbors_block(i, N, R, Q, region, nbr, nboxT, ncount, dlist, dcount, qual);
+    } else if (i < N) {
+        __shared__ int4 lbox[kPollNbr], ubox[kPollNbr];
+        __shared__ int cnt2[2];
+        neighbors_block(i, N, R, Q, region, nbr, nboxT, ncount, dlist, dcount, qual, orj.nboxU,
+                        orj.ncountU, lbox, ubox, cnt2);
+        __syncthreads();
+        or_list_jobs(i, R, lbox, cnt2[0], ubox, cnt2[1], orj.off, orj.g, orj.jobs, orj.cap, dcount);
+    }
     ts_end(ts);
 }
 

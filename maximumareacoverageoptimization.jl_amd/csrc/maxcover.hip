@@ -132,7 +132,7 @@ struct Lane {
     hipEvent_t done = nullptr;
     DevBuf cands, disks, partial, area, obj, best, rmax, prev, dlim, region, mode, nbr,
         ncount, dlist, spart, vp, xinc, perm, ucount, umap, keysT, lane4, lanexp, rows, nboxT,
-        cnt, dlimraw, finblk, finarrive, c32, p32, qual;
+        cnt, dlimraw, finblk, finarrive, c32, p32, qual, nboxU, ncountU, orjobs;
     std::vector<double> h_dlim;
     PinnedBuf h_stage;                         // native MADS driver: best, permutations, incumbent
     PinnedBuf h_io;                            // host-pointer calls: candidates in, results out
@@ -504,6 +504,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
     const int* d_umap = nullptr;       // poll walk: candidate -> distinct-disk position
     const int* d_ncount = nullptr;
     int counts = 0;                    // poll walk with equal weights: integer count rows
+    int bits_on = 0;                   // the shared-entry pass's launch hint (walk set-up)
     if (d_obj) {
         L->vp.reserve(sizeof(double) * (size_t)std::max(K, 1));
         d_vp = L->vp.as<double>();
@@ -628,7 +629,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         } else {
             L->region.reserve(sizeof(int4) * N);
             L->cost.reserve(sizeof(double2) * N);
-            L->mode.reserve(8 * sizeof(int));  // [0] walk, [1..4] the poll walk's counters (k_common.h)
+            L->mode.reserve(8 * sizeof(int));  // [0] walk, [1..kDcCount] the poll walk's counters (k_common.h)
             const IndexOut io{L->disks.as<DiskRec>(), L->umap.as<int>(), L->ucount.as<int>(),
                               L->region.as<int4>(), L->cost.as<double2>(), L->mode.as<int>() + 1,
                               L->prec.as<int4>(), nchain,
@@ -682,11 +683,38 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             L->qual.reserve(sizeof(int) * (size_t)N);
             L->nboxT.reserve(sizeof(int4) * (size_t)N * kPollNbr);
             L->partial.reserve(sizeof(double) * (size_t)K * std::max(G, N));
+            // the shared-entry pass of crowded polls, launched when one of the lane's last 8 polls
+            // had more than kBitsMinDisks disks with neighbours (the poll kernel writes the count to
+            // mapped host memory): a hint only, the poll kernel takes every disk when it is not
+            // launched (MADS alternates crowded and quiet polls, and a crowded poll without the
+            // pass costs several times its launch)
+            const int dc_now = *(volatile int*)L->h_dc.p;   // 1 << 30 until a poll wrote it
+            int dc_max = dc_now;
+            if (dc_now < (1 << 30)) {
+                for (int q = 7; q > 0; --q) L->dc_hist[q] = L->dc_hist[q - 1];
+                L->dc_hist[0] = dc_now;
+                for (int q = 0; q < 8; ++q) dc_max = std::max(dc_max, L->dc_hist[q]);
+            }
+            // 0: fp64 jobs; 1: above kBitsMinDisks disks with neighbours; 2: always
+            bits_on = ctx->shared_mode == MAC_SHARED_BITS ? 2
+                    : ctx->shared_mode == MAC_SHARED_FP64 ? 0
+                    : dc_max > kBitsMinDisks ? 1 : 0;
+            // equal weights: the union pass (k_or.h), whose jobs walk_setup lists with the upper
+            // neighbour boxes; weighted lists: the bit-word kernel (k_bits.h)
+            OrSetup orj{};
+            if (bits_on && counts) {
+                L->nboxU.reserve(sizeof(int4) * (size_t)N * kPollNbr);
+                L->ncountU.reserve(sizeof(int) * (size_t)N);
+                const int64_t cap = M / kOrE + N + 64;   // the owned sets are disjoint
+                L->orjobs.reserve(sizeof(int2) * (size_t)cap);
+                orj = OrSetup{L->nboxU.as<int4>(), L->ncountU.as<int>(), L->orjobs.as<int2>(), (int)cap,
+                              ctx->off.as<int32_t>(), ctx->grid};
+            }
             uint64_t* tss = ts_c >= 0 ? take_ts(N, ts_s, ts_ns) : nullptr;
             hipLaunchKernelGGL(walk_setup_kernel, dim3((unsigned)N), dim3(kBlock), 0, s, tss, N,
                                L->region.as<int4>(), L->nbr.as<uint16_t>(), L->nboxT.as<int4>(),
                                L->ncount.as<int>(), L->dlist.as<int>(), L->mode.as<int>() + 1,
-                               L->mode.as<int>(), L->qual.as<int>(), src.mst);
+                               L->mode.as<int>(), L->qual.as<int>(), src.mst, orj);
             HCK(hipGetLastError());
             if (run_tiled) {
                 // one workgroup per CU at most, grid-striding over the (candidate, slice) units
@@ -704,22 +732,6 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             d_umap = d_map;
         }
         if (poll_possible) {
-            // the bit-word kernel runs when the previous poll on this lane had more than
-            // kBitsMinDisks disks with neighbours (the poll kernel writes the count to mapped host
-            // memory): a hint only, the poll kernel takes every disk when it is not launched
-            // (the maximum over the last 8 polls: MADS alternates crowded and quiet polls, and a
-            // crowded poll without the bit-word kernel costs several times its launch)
-            const int dc_now = *(volatile int*)L->h_dc.p;   // 1 << 30 until a poll wrote it
-            int dc_max = dc_now;
-            if (dc_now < (1 << 30)) {
-                for (int q = 7; q > 0; --q) L->dc_hist[q] = L->dc_hist[q - 1];
-                L->dc_hist[0] = dc_now;
-                for (int q = 0; q < 8; ++q) dc_max = std::max(dc_max, L->dc_hist[q]);
-            }
-            // 0: fp64 jobs; 1: bit-word kernel above kBitsMinDisks disks with neighbours; 2: always
-            const int bits_on = ctx->shared_mode == MAC_SHARED_BITS ? 2
-                              : ctx->shared_mode == MAC_SHARED_FP64 ? 0
-                              : dc_max > kBitsMinDisks ? 1 : 0;
             // walk rows: the lane's last 8 polls' most distinct positions of a disk (poll kernel
             // hint), one row per kPollKPB-position slice up to 4 (further slices loop)
             const int um_now = ((volatile int*)L->h_dc.p)[2];
@@ -744,20 +756,39 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                                bits_on, L->d_dc, L->qual.as<int>(),
                                walk_forced == 0 ? L->cost.as<double2>() : nullptr, kPollCostRatio);
             HCK(hipGetLastError());
-            // the shared entries of crowded polls: bit-words per distinct position (k_bits.h);
-            // returns at once when few disks have neighbours (the poll kernel took them)
+            // the shared entries of crowded polls: the union pass (equal weights, k_or.h) or
+            // bit-words per distinct position (k_bits.h); both return at once when few disks have
+            // neighbours (the poll kernel took them)
             const unsigned nbits = (unsigned)std::max(1, std::min(N, ctx->cus));
-            uint64_t* tsg = bits_on && ts_c >= 0 ? take_ts(nbits, ts_g, ts_ng) : nullptr;
+            const unsigned nor = (unsigned)(2 * ctx->cus);   // grid-strides over the listed jobs
+            uint64_t* tsg = bits_on && ts_c >= 0 ? take_ts(counts ? nor : nbits, ts_g, ts_ng) : nullptr;
             if (!bits_on)
                 ;
-            else if (counts)
-                hipLaunchKernelGGL(shared_bits_kernel<true>, dim3(nbits), dim3(kBitsThreads), 0, s,
-                                   tsg, ctx->xys.as<double2>(), ctx->ws.as<double>(), ctx->off.as<int32_t>(),
-                                   ctx->grid, d_urec, d_map, L->ucount.as<int>(), L->region.as<int4>(),
-                                   L->nbr.as<uint16_t>(), L->lane4.as<float4>(), L->lanexp.as<float>(),
-                                   L->ncount.as<int>(), L->qual.as<int>(), L->mode.as<int>() + 1, d_mode,
-                                   N, K, L->spart.as<double>(), bits_on == 2 ? 0 : kBitsMinDisks);
-            else
+            else if (counts) {
+                OrArgs oa{};
+                oa.xy = ctx->xys.as<double2>();
+                oa.off = ctx->off.as<int32_t>();
+                oa.g = ctx->grid;
+                oa.urec = d_urec;
+                oa.umap = d_map;
+                oa.ucount = L->ucount.as<int>();
+                oa.region = L->region.as<int4>();
+                oa.nbrT = L->nbr.as<uint16_t>();
+                oa.nboxT = L->nboxT.as<int4>();
+                oa.ncount = L->ncount.as<int>();
+                oa.nboxU = L->nboxU.as<int4>();
+                oa.ncountU = L->ncountU.as<int>();
+                oa.lane4 = L->lane4.as<float4>();
+                oa.lanexp = L->lanexp.as<float>();
+                oa.jobs = L->orjobs.as<int2>();
+                oa.dcount = L->mode.as<int>() + 1;
+                oa.mode = d_mode;
+                oa.spart = L->spart.as<unsigned>();
+                oa.N = N;
+                oa.K = K;
+                oa.bits_on = bits_on;
+                hipLaunchKernelGGL(shared_or_kernel, dim3(nor), dim3(kOrThreads), 0, s, tsg, oa);
+            } else
                 hipLaunchKernelGGL(shared_bits_kernel<false>, dim3(nbits), dim3(kBitsThreads), 0, s,
                                    tsg, ctx->xys.as<double2>(), ctx->ws.as<double>(), ctx->off.as<int32_t>(),
                                    ctx->grid, d_urec, d_map, L->ucount.as<int>(), L->region.as<int4>(),
@@ -1157,7 +1188,8 @@ void mac_ctx_destroy(mac_ctx* ctx)
                           &l->ncount, &l->dlist, &l->qual, &l->spart, &l->vp, &l->xinc,
                           &l->perm, &l->ucount, &l->umap, &l->keysT, &l->lane4,
                           &l->lanexp, &l->rows, &l->nboxT, &l->cnt, &l->dlimraw, &l->finblk, &l->finarrive, &l->c32, &l->p32,
-                          &l->cpart, &l->carrive, &l->ctot, &l->prec, &l->cost})
+                          &l->cpart, &l->carrive, &l->ctot, &l->prec, &l->cost, &l->nboxU,
+                          &l->ncountU, &l->orjobs})
             b->release();
         if (l->done) (void)hipEventDestroy(l->done);
 

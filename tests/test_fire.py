@@ -233,3 +233,67 @@ def test_config5_full_size_mpc_step(ctx, pkg, orc):
     assert np.all(want >= bo), (pick[want < bo], bo)
     assert bi == int(np.argmin(objs)) and bo == objs[bi]
     D.close()
+
+
+def _c5_poll293(pkg):
+    """The config-5 poll behind the bit-word kernel's 1.1-ms launch (tests/golden/c5_poll293.npz,
+    tests/golden/make_c5_poll_fixture.py): (x, y, w, candidates K x 3N, prev, r_max, ell)."""
+    import importlib.util
+    import os
+    root = os.path.dirname(os.path.abspath(__file__))
+    spec = importlib.util.spec_from_file_location(
+        "make_c5_poll_fixture", os.path.join(root, "golden", "make_c5_poll_fixture.py"))
+    mk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mk)
+    d = np.load(os.path.join(root, "golden", "c5_poll293.npz"))
+    seed, it, ell = (int(v) for v in d["meta"][:3])
+    cells = d["cells"].astype(np.float64)
+    x, y = cells[:, 0] * 5.0 - 2.5, cells[:, 1] * 5.0 - 2.5
+    w = np.full(x.size, 25.0)
+    X = mk.candidates(pkg.workloads, d["xinc"], seed, it, ell)
+    return x, y, w, X, d["prev"], d["rmax"], ell
+
+
+def test_c5_poll293_fixture_regenerates(pkg):
+    """CPU: the fixture's stream position reproduces a complete LTMADS poll (2n candidates on the
+    granular mesh around the incumbent, steps bounded by 2^ell)."""
+    x, y, w, X, prev, rmax, ell = _c5_poll293(pkg)
+    n = X.shape[1]
+    assert X.shape == (2 * n, n) and n == 3 * 512 and x.size == 192317
+    xc = (X[0] + X[n]) / 2                      # the incumbent
+    D = X[:n] - xc[None, :]
+    assert np.all(D == np.round(D)) and np.abs(D).max() == 2 ** ell
+    assert np.array_equal(X[n:], xc[None, :] - D)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shared", ["auto", "bits", "fp64"])
+def test_c5_poll293_against_oracle(ctx, pkg, orc, shared):
+    """The slowest config-5 poll of rounds 3-4 (ell = 5: ~1,460 distinct positions per UAV, 132K
+    shared entries): every shared-entry pass (auto = what the MADS loop runs, bits = the union
+    pass forced, fp64 = the poll kernel's jobs) gives the same K objectives, 64 sampled
+    candidates and the argmin equal the C oracle, and no sampled oracle objective is below the
+    device's best."""
+    x, y, w, X, prev, rmax, ell = _c5_poll293(pkg)
+    N = X.shape[1] // 3
+    tan50 = math.tan(100 / 180 * math.pi / 2)
+    ctx.set_points(x, y, w)
+    ctx.set_algo("auto")
+    ctx.set_shared(shared)
+    try:
+        res = [ctx.poll_best(X, rmax, 1e5, prev=prev, d_lim=np.full(N, 10.0), tan_half_fov=tan50,
+                             want_all=True) for _ in range(2)]   # (the second poll takes the hint)
+    finally:
+        ctx.set_shared("auto")
+    assert np.array_equal(res[0][2], res[1][2]) and res[0][:2] == res[1][:2]
+    bo, bi, objs = res[1]
+    rng = pkg.workloads.SplitMix64(293)
+    pick = np.unique(np.concatenate([[0, bi], np.floor(rng.uniform(64) * X.shape[0]).astype(np.int64)]))
+    lst = np.stack([x, y, w, w, np.zeros_like(x)], axis=1)
+    area = orc.PointerList(lst).area_batch(X[pick], 16)
+    viol = orc.violation_batch(X[pick], rmax)
+    ok3 = orc.cons3_batch(prev, X[pick], np.full(N, 10.0), tan50)
+    want = np.where(ok3, -area + viol * 1e5, np.inf)
+    assert np.array_equal(objs[pick], want), pick[objs[pick] != want]
+    assert bi == int(np.argmin(objs)) and bo == objs[bi]
+    assert np.all(want >= bo)
