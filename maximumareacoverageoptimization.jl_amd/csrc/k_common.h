@@ -27,12 +27,13 @@ constexpr int kBitsTab = 2048;     // bit-word kernel: positions per table group
 constexpr int kBitsMinDisks = 16;  // bit-word kernel: used above this many disks with neighbours
 // poll walk counters (dcount[]): [0] disks with neighbours the bit-word kernel can take (dlist
 // from the front), [1] poll-kernel jobs taken, [2] the other disks with neighbours (dlist from the
-// back), [3] bit-word / union-pass jobs taken, [4] union-pass jobs listed (k_or.h), [5] disks with
-// lower neighbours whose upper list overflowed (the union pass stands down); cleared by the index
-// kernel (the lane's mode buffer holds [walk, dcount[0..6]])
+// back), [3] bit-word / union-pass jobs taken, [4..7] union-pass jobs listed per weight bucket,
+// heaviest first (k_or.h), [8] disks with lower neighbours whose upper list overflowed (the union
+// pass stands down); cleared by the index kernel (the lane's mode buffer holds [walk, dcount])
+constexpr int kOrBuckets = 4;
 constexpr int kDcBits = 0, kDcPollJobs = 1, kDcOther = 2, kDcBitsJobs = 3, kDcOrJobs = 4,
-              kDcOrBad = 5;
-constexpr int kDcCount = 6;
+              kDcOrBad = kDcOrJobs + kOrBuckets;
+constexpr int kDcCount = kDcOrBad + 1;
 
 constexpr int kModePoll = 1;
 constexpr int kModeTiled = 2;

@@ -17,7 +17,8 @@
 //   2. per disk with live entries, per distinct position u of that disk (k_index.h), the 64-bit
 //      word T[u] of the entries it covers — the walk's exact fp32 filter (k_poll.h header), band
 //      entries re-decided in fp64 — then per candidate k: Y |= T[u_d(k)], Z |= T[u_d(k)] & lmask;
-//   3. per candidate: popcount(Y & ~Z) added (integer atomics: exact in any order) to spart row i.
+//   3. per candidate: popcount(Y & ~Z) added (integer atomics: exact in any order) to spart row i
+//      (kept as popcount(Y) - sum of popcount(T & lmask): the lmask sets are disjoint).
 // Tests: sum over shared entries of sum over d in D_e of U_d (distinct positions), against the
 // bit-word kernel's per-owner (U_i + sum over ALL neighbours of U_j) x |S_i|: the owner form tests
 // each shared entry once per owner and against every neighbour's positions (3.4e9 tests on the
@@ -38,9 +39,19 @@
 
 namespace mac {
 
+#ifdef MAC_DIAG
+// diagnostic build only: per workgroup, ticks (s_memrealtime, 10 ns) spent in each phase and counts
+__device__ uint64_t g_diag_or[1024 * 16];
+#define MAC_OR_T(q) do { if (threadIdx.x == 0) { const uint64_t t_ = __builtin_amdgcn_s_memrealtime(); dg[q] += t_ - dt; dt = t_; } } while (0)
+#define MAC_OR_N(q, v) do { if (threadIdx.x == 0) dg[q] += (v); } while (0)
+#else
+#define MAC_OR_T(q)
+#define MAC_OR_N(q, v)
+#endif
+
 constexpr int kOrThreads = 512;                 // 8 waves
-constexpr int kOrPT = 8;                        // candidates per thread per candidate chunk
-constexpr int kOrKC = kOrPT * kOrThreads;       // 4096 candidates per chunk
+constexpr int kOrPT = 7;                        // candidates per thread per candidate chunk (K = 3073: one)
+constexpr int kOrKC = kOrPT * kOrThreads;       // 3584 candidates per chunk
 constexpr int kOrE = 64;                        // entries per job
 constexpr int kOrTab = 4096;                    // positions per table chunk (32 KB of words)
 constexpr int kOrRuns = 64 * 32;                // tile runs of a region (64 rows x 32 runs)
@@ -94,14 +105,24 @@ __device__ __forceinline__ int or_row_count(const int32_t* __restrict__ off, con
     return n;
 }
 
+// A job's weight bucket (0 heaviest): its tables test about U_i * (1 + nl) positions (disk i's
+// positions and its lower neighbours'), so jobs are handed out heaviest first and the launch's
+// tail is made of light jobs (longest-processing-time order).
+__device__ __forceinline__ int or_bucket(int U, int nl)
+{
+    const int w = U * (1 + min(nl, 8));
+    return w >= 8192 ? 0 : w >= 4096 ? 1 : w >= 2048 ? 2 : 3;
+}
+
 // walk_setup's part (block i, after neighbors_block with the lists in LDS): the number of entries
 // of region i that this pass owns (lower box, no upper box) and one job per 64 of them, appended
-// to jobs[] ({i, block}) from the counter dcount[kDcOrJobs]. A list past `cap` (cannot happen:
-// the owned sets are disjoint, cap >= M / 64 + N) makes the pass stand down (kDcOrBad).
+// ({i, block}) to its weight bucket's list (jobs + bucket * cap) from the counter
+// dcount[kDcOrJobs + bucket]. A list past `cap` (cannot happen: the owned sets are disjoint,
+// cap >= M / 64 + N) makes the pass stand down (kDcOrBad).
 __device__ __forceinline__ void or_list_jobs(int i, const int4& R, const int4* lbox, int nl,
                                              const int4* ubox, int nu, const int32_t* __restrict__ off,
                                              const Grid& g, int2* __restrict__ jobs, int cap,
-                                             int* __restrict__ dcount)
+                                             int* __restrict__ dcount, int U)
 {
     __shared__ int s_base, s_nblk;
     const int tid = threadIdx.x;
@@ -115,15 +136,17 @@ __device__ __forceinline__ void or_list_jobs(int i, const int4& R, const int4* l
         for (int o = 32; o >= 1; o >>= 1) n += __shfl_xor(n, o, kWave);
         if (tid == 0) {
             const int nblk = (n + kOrE - 1) / kOrE;
+            const int bk = or_bucket(U, nl);
             s_nblk = nblk;
-            s_base = nblk ? atomicAdd(dcount + kDcOrJobs, nblk) : 0;
+            s_base = nblk ? atomicAdd(dcount + kDcOrJobs + bk, nblk) : 0;
             if (nblk && s_base + nblk > cap) atomicAdd(dcount + kDcOrBad, 1);
+            s_base += bk * cap;
         }
     }
     __syncthreads();
     const int base = s_base, nblk = s_nblk;
     for (int b = tid; b < nblk; b += kBlock)
-        if (base + b < cap) jobs[base + b] = make_int2(i, b);
+        if (base % cap + b < cap) jobs[base + b] = make_int2(i, b);
 }
 
 struct OrArgs {
@@ -146,6 +169,7 @@ struct OrArgs {
     const int* mode;
     unsigned* spart;   // uint32 count rows [N][K] (the poll kernel zeroed the rows of disks with neighbours)
     int N, K, bits_on;
+    int cap;           // jobs per bucket list (jobs + bucket * cap)
 };
 
 // (cur << 1) | sign bit of v (v_alignbit_b32 {cur, v} >> 31)
@@ -179,11 +203,28 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
         ts_end(ts);
         return;
     }
-    const int njobs = a.dcount[kDcOrJobs];
+    int nb[kOrBuckets], njobs = 0;   // the buckets' job counts, heaviest bucket first
+#pragma unroll
+    for (int b = 0; b < kOrBuckets; ++b) {
+        nb[b] = a.dcount[kDcOrJobs + b];
+        njobs += nb[b];
+    }
     const int K = a.K;
+#ifdef MAC_DIAG
+    uint64_t dg[16] = {};
+    uint64_t dt = __builtin_amdgcn_s_memrealtime();
+    const uint64_t dt0 = dt;
+#endif
     const Grid g = a.g;
     for (int job = blockIdx.x; job < njobs;) {
-        const int2 jb = a.jobs[job];
+        int q = job, bk = 0;
+#pragma unroll
+        for (int b = 0; b < kOrBuckets - 1; ++b)
+            if (bk == b && q >= nb[b]) {
+                q -= nb[b];
+                bk = b + 1;
+            }
+        const int2 jb = a.jobs[(int64_t)bk * a.cap + q];
         const int i = jb.x, blk = jb.y;
         // disk i's lists (slot 0: disk i itself, slots 1..nc: its lower neighbours)
         const int nc = a.ncount[i], ncU = a.ncountU[i];
@@ -289,11 +330,20 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
         }
         __syncthreads();
         const int nrel = s_nrel;
+        MAC_OR_T(0);
+        MAC_OR_N(8, 1);
+        MAC_OR_N(9, nrel);
 
         for (int kc0 = 0; kc0 < K; kc0 += kOrKC) {
-            uint64_t Y[kOrPT], Z[kOrPT];
+            // per candidate: Y = the union word; zc = the j0 part's count (the lmask sets of the
+            // disks are disjoint, so popcount(OR of (T & lmask)) is the sum of their popcounts)
+            uint64_t Y[kOrPT];
+            uint32_t zc[kOrPT];
 #pragma unroll
-            for (int c = 0; c < kOrPT; ++c) Y[c] = Z[c] = 0;
+            for (int c = 0; c < kOrPT; ++c) {
+                Y[c] = 0;
+                zc[c] = 0;
+            }
             for (int r = 0; r < nrel; ++r) {
                 const int m = rel[r];
                 const int d = sid[m], U = sU[m];
@@ -322,58 +372,92 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
                         f ? __builtin_fmaf(fu, fu, fv * fv) : __builtin_inff();
                 }
                 __syncthreads();
+                MAC_OR_T(1);
+                MAC_OR_N(10, U);
+                MAC_OR_N(11, __popcll(lv));
+                // work items (position, 32-entry half with live entries): both halves of a
+                // position are separate items, so the waves stay balanced and an item's lane
+                // constants load one item ahead of its tests
                 const bool w0 = (uint32_t)lv != 0, w1 = (uint32_t)(lv >> 32) != 0;
+                const int nh = (w0 ? 1 : 0) + (w1 ? 1 : 0), h1 = w0 ? 0 : 1;   // uniform
+                uint32_t* const tab32 = reinterpret_cast<uint32_t*>(tab);
                 for (int u0 = 0; u0 < U; u0 += kOrTab) {
                     const int u1 = min(U, u0 + kOrTab);
-                    for (int p = u0 + tid; p < u1; p += kOrThreads) {
-                        const float4 c4 = a.lane4[row + p];
-                        const float xp = a.lanexp[row + p];
+                    const int nit = (u1 - u0) * nh;
+                    int q = tid;
+                    float4 c4n = make_float4(0.0f, 0.0f, -1.0f, -1.0f);
+                    float xpn = -1.0f;
+                    if (q < nit) {
+                        const int p = u0 + (nh == 2 ? q >> 1 : q);
+                        c4n = a.lane4[row + p];
+                        xpn = a.lanexp[row + p];
+                    }
+                    for (; q < nit; q += kOrThreads) {
+                        const int p = u0 + (nh == 2 ? q >> 1 : q);
+                        const int hv = nh == 2 ? (q & 1) : h1;   // the half: entries 32 hv ..
+                        const float4 c4 = c4n;
+                        const float xp = xpn;
+                        const int qn = q + kOrThreads;
+                        if (qn < nit) {   // the next item's constants, in flight during the tests
+                            const int pn = u0 + (nh == 2 ? qn >> 1 : qn);
+                            c4n = a.lane4[row + pn];
+                            xpn = a.lanexp[row + pn];
+                        }
                         const f32x2 sa = {c4.x, c4.x}, sb = {c4.y, c4.y}, st = {c4.z, c4.z},
                                     ns = {c4.w, c4.w}, xp2 = {xp, xp};
-                        uint32_t cw[2] = {0u, 0u};
+                        uint32_t cw = 0u;
                         float bmin = __builtin_inff();
-#pragma unroll
-                        for (int wv = 0; wv < 2; ++wv) {
-                            if (!(wv ? w1 : w0)) continue;   // uniform: no live entry in the word
-#pragma unroll 4
-                            for (int j = 0; j < 16; ++j) {
-                                const float4 uv = ent[16 * wv + j];
-                                const f32x2 qq = entq[16 * wv + j];
+                        const float4* const eh = ent + 16 * hv;
+                        const f32x2* const qh = entq + 16 * hv;
+                        const uint32_t lvh = (uint32_t)(lv >> (32 * hv));   // the half's live entries
+                        // groups of 8 entries; a group with no live entry (uniform) only shifts
+                        // its 8 zero bits in (entries in tile order: live ones come in runs)
+                        for (int g8 = 0; g8 < 4; ++g8) {
+                            if (((lvh >> (8 * g8)) & 0xffu) == 0u) {
+                                cw <<= 8;
+                                continue;
+                            }
+#pragma unroll 1
+                            for (int j = 4 * g8; j < 4 * g8 + 4; ++j) {
+                                const float4 uv = eh[j];
+                                const f32x2 qq = qh[j];
                                 const f32x2 U2 = {uv.x, uv.y}, V2 = {uv.z, uv.w};
                                 const f32x2 dd = __builtin_elementwise_fma(
                                     qq, ns, __builtin_elementwise_fma(V2, sb, __builtin_elementwise_fma(U2, sa, st)));
                                 // covered iff d' > X' iff X' - d' < 0: its sign bit shifted in
                                 const f32x2 sd2 = xp2 - dd;
-                                cw[wv] = or_shift_sign(cw[wv], sd2.x);
-                                cw[wv] = or_shift_sign(cw[wv], sd2.y);
+                                cw = or_shift_sign(cw, sd2.x);
+                                cw = or_shift_sign(cw, sd2.y);
                                 bmin = __builtin_fminf(bmin, __builtin_fminf(__builtin_fabsf(dd.x),
                                                                              __builtin_fabsf(dd.y)));
                             }
                         }
-                        uint32_t t0 = __builtin_bitreverse32(cw[0]), t1 = __builtin_bitreverse32(cw[1]);
+                        uint32_t t = __builtin_bitreverse32(cw);
                         // X' < 2 for every normal position: no |d'| <= 2 means no band entry; a
-                        // band (or forced) position re-decides its live entries, band ones in fp64
+                        // band (or forced) position re-decides its half's entries, band ones in fp64
                         if (bmin <= 2.0f || !(xp < 2.0f)) {
                             const DiskRec rr = a.urec[row + p];
-                            uint32_t t[2] = {0u, 0u};
-                            for (int e = 0; e < kOrE; ++e) {
-                                const float4 uv = ent[e >> 1];
-                                const float qv = reinterpret_cast<const f32x2*>(entq)[e >> 1][e & 1];
+                            t = 0u;
+                            for (int e = 0; e < 32; ++e) {
+                                const float4 uv = eh[e >> 1];
+                                const float qv = qh[e >> 1][e & 1];
                                 const float U1 = (e & 1) ? uv.y : uv.x, V1 = (e & 1) ? uv.w : uv.z;
                                 const float dp = __builtin_fmaf(qv, c4.w, __builtin_fmaf(V1, c4.y, __builtin_fmaf(U1, c4.x, c4.z)));
                                 bool cov = dp > xp;
                                 if (__builtin_fabsf(dp) <= xp) {
-                                    const double2 q = s64[e];
-                                    cov = qv != __builtin_inff() && sqdist(q.x, q.y, rr.cx, rr.cy) <= rr.T;
+                                    const double2 qd = s64[32 * hv + e];
+                                    cov = qv != __builtin_inff() && sqdist(qd.x, qd.y, rr.cx, rr.cy) <= rr.T;
                                 }
-                                if (cov) t[e >> 5] |= 1u << (e & 31);
+                                if (cov) t |= 1u << e;
                             }
-                            t0 = t[0];
-                            t1 = t[1];
                         }
-                        tab[p - u0] = make_uint2(t0, t1);
+                        if (nh == 2)
+                            tab32[2 * (p - u0) + hv] = t;
+                        else
+                            tab[p - u0] = hv ? make_uint2(0u, t) : make_uint2(t, 0u);
                     }
                     __syncthreads();
+                    MAC_OR_T(2);
                     // combine: the union word and the j0 word of every candidate
 #pragma unroll
                     for (int c = 0; c < kOrPT; ++c) {
@@ -382,16 +466,17 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
                             const uint2 t2 = tab[u - u0];
                             const uint64_t t = (uint64_t)t2.x | ((uint64_t)t2.y << 32);
                             Y[c] |= t;
-                            Z[c] |= t & lm;
+                            zc[c] += (uint32_t)__popcll(t & lm);
                         }
                     }
                     __syncthreads();   // the next chunk / disk overwrites the tables and entries
+                    MAC_OR_T(3);
                 }
             }
 #pragma unroll
             for (int c = 0; c < kOrPT; ++c) {
                 const int k = kc0 + tid + c * kOrThreads;
-                const int n = __popcll(Y[c] & ~Z[c]);
+                const int n = __popcll(Y[c]) - (int)zc[c];   // popcount(Y & ~Z): Z is in Y
                 if (k < K && n) atomicAdd(a.spart + (int64_t)i * K + k, (unsigned)n);
             }
         }
@@ -399,7 +484,14 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
         if (tid == 0) s_job = (int)gridDim.x + atomicAdd(a.dcount + kDcBitsJobs, 1);
         __syncthreads();
         job = s_job;
+        MAC_OR_T(4);
     }
+#ifdef MAC_DIAG
+    if (tid == 0 && blockIdx.x < 1024) {
+        dg[12] = __builtin_amdgcn_s_memrealtime() - dt0;
+        for (int q = 0; q < 16; ++q) g_diag_or[16 * blockIdx.x + q] = dg[q];
+    }
+#endif
     ts_end(ts);
 }
 

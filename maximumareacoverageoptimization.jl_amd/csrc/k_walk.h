@@ -292,10 +292,11 @@ __global__ __launch_bounds__(kBlock) void coverage_tiled_poll_kernel(
 struct OrSetup {
     int4* nboxU;
     int* ncountU;
-    int2* jobs;
+    int2* jobs;        // kOrBuckets lists of cap jobs (k_or.h or_list_jobs)
     int cap;
     const int32_t* off;
     Grid g;
+    const int* ucount; // positions per disk (the index)
 };
 
 __global__ __launch_bounds__(kBlock) void walk_setup_kernel(
@@ -331,7 +332,8 @@ __global__ __launch_bounds__(kBlock) void walk_setup_kernel(
         neighbors_block(i, N, R, Q, region, nbr, nboxT, ncount, dlist, dcount, qual, orj.nboxU,
                         orj.ncountU, lbox, ubox, cnt2);
         __syncthreads();
-        or_list_jobs(i, R, lbox, cnt2[0], ubox, cnt2[1], orj.off, orj.g, orj.jobs, orj.cap, dcount);
+        or_list_jobs(i, R, lbox, cnt2[0], ubox, cnt2[1], orj.off, orj.g, orj.jobs, orj.cap, dcount,
+                     orj.ucount[i]);
     }
     ts_end(ts);
 }

@@ -629,7 +629,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         } else {
             L->region.reserve(sizeof(int4) * N);
             L->cost.reserve(sizeof(double2) * N);
-            L->mode.reserve(8 * sizeof(int));  // [0] walk, [1..kDcCount] the poll walk's counters (k_common.h)
+            L->mode.reserve((1 + kDcCount) * sizeof(int));  // [0] walk, [1..kDcCount] the poll walk's counters (k_common.h)
             const IndexOut io{L->disks.as<DiskRec>(), L->umap.as<int>(), L->ucount.as<int>(),
                               L->region.as<int4>(), L->cost.as<double2>(), L->mode.as<int>() + 1,
                               L->prec.as<int4>(), nchain,
@@ -706,9 +706,9 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                 L->nboxU.reserve(sizeof(int4) * (size_t)N * kPollNbr);
                 L->ncountU.reserve(sizeof(int) * (size_t)N);
                 const int64_t cap = M / kOrE + N + 64;   // the owned sets are disjoint
-                L->orjobs.reserve(sizeof(int2) * (size_t)cap);
+                L->orjobs.reserve(sizeof(int2) * (size_t)cap * kOrBuckets);   // a list per bucket
                 orj = OrSetup{L->nboxU.as<int4>(), L->ncountU.as<int>(), L->orjobs.as<int2>(), (int)cap,
-                              ctx->off.as<int32_t>(), ctx->grid};
+                              ctx->off.as<int32_t>(), ctx->grid, L->ucount.as<int>()};
             }
             uint64_t* tss = ts_c >= 0 ? take_ts(N, ts_s, ts_ns) : nullptr;
             hipLaunchKernelGGL(walk_setup_kernel, dim3((unsigned)N), dim3(kBlock), 0, s, tss, N,
@@ -787,6 +787,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                 oa.N = N;
                 oa.K = K;
                 oa.bits_on = bits_on;
+                oa.cap = (int)(M / kOrE + N + 64);
                 hipLaunchKernelGGL(shared_or_kernel, dim3(nor), dim3(kOrThreads), 0, s, tsg, oa);
             } else
                 hipLaunchKernelGGL(shared_bits_kernel<false>, dim3(nbits), dim3(kBitsThreads), 0, s,
@@ -969,6 +970,16 @@ int32_t mac_diag_bits_read(uint64_t* out, int64_t n)
 {
     if (n > 256 * 16) n = 256 * 16;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_bits), sizeof(uint64_t) * n, 0,
+                            hipMemcpyDeviceToHost) != hipSuccess)
+        return MAC_E_HIP;
+    return MAC_OK;
+}
+
+// diagnostic build only: per-workgroup phase ticks of shared_or_kernel (k_or.h)
+int32_t mac_diag_or_read(uint64_t* out, int64_t n)
+{
+    if (n > 1024 * 16) n = 1024 * 16;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_or), sizeof(uint64_t) * n, 0,
                             hipMemcpyDeviceToHost) != hipSuccess)
         return MAC_E_HIP;
     return MAC_OK;

@@ -280,9 +280,13 @@ def test_c5_poll293_against_oracle(ctx, pkg, orc, shared):
     ctx.set_points(x, y, w)
     ctx.set_algo("auto")
     ctx.set_shared(shared)
+    dl = np.full(N, 10.0)
     try:
-        res = [ctx.poll_best(X, rmax, 1e5, prev=prev, d_lim=np.full(N, 10.0), tan_half_fov=tan50,
-                             want_all=True) for _ in range(2)]   # (the second poll takes the hint)
+        # without cons3 (every objective finite), twice: the second poll takes the lane's hint
+        res = [ctx.poll_best(X, rmax, 1e5, want_all=True) for _ in range(2)]
+        # with cons3 against the MPC step's start, as the loop ran it
+        bo3, bi3, objs3 = ctx.poll_best(X, rmax, 1e5, prev=prev, d_lim=dl, tan_half_fov=tan50,
+                                        want_all=True)
     finally:
         ctx.set_shared("auto")
     assert np.array_equal(res[0][2], res[1][2]) and res[0][:2] == res[1][:2]
@@ -292,8 +296,13 @@ def test_c5_poll293_against_oracle(ctx, pkg, orc, shared):
     lst = np.stack([x, y, w, w, np.zeros_like(x)], axis=1)
     area = orc.PointerList(lst).area_batch(X[pick], 16)
     viol = orc.violation_batch(X[pick], rmax)
-    ok3 = orc.cons3_batch(prev, X[pick], np.full(N, 10.0), tan50)
-    want = np.where(ok3, -area + viol * 1e5, np.inf)
+    want = -area + viol * 1e5
     assert np.array_equal(objs[pick], want), pick[objs[pick] != want]
+    assert want[np.searchsorted(pick, bi)] == bo
     assert bi == int(np.argmin(objs)) and bo == objs[bi]
     assert np.all(want >= bo)
+    # cons3: the extreme barrier on top of the same objectives (the loop's poll: all infeasible
+    # at ell = 5, every step is 32 m against d_lim = 10 m)
+    ok3 = orc.cons3_batch(prev, X, dl, tan50)
+    assert np.array_equal(objs3, np.where(ok3, objs, np.inf))
+    assert bi3 == (int(np.argmin(objs3)) if np.isfinite(objs3).any() else -1)

@@ -62,6 +62,9 @@ for s in $STEPS; do
     self2)   # bench.py --gpus 2 with no external launcher: it starts its two ranks itself (gloo; both on device 0)
         MAXCOVER_BENCH_DEVICE=0 run self2 300 python bench.py --gpus 2 --no-cpu --dist-backend gloo --steps 20 ; rc=$?
         grep '^{' gpurun_out/self2.log > gpurun_out/self2_${TAG}.json ;;
+    diagor)   # phase times of the union pass on the config-5 regression poll at ell 5 / 4 / 3
+        MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
+            run diagor 300 python tools/diag_or.py ; rc=$? ;;
     c5polls)  # per-poll kernel times of the config-5 loop; the slowest polls saved for analysis
         run c5polls 600 python tools/c5_polls.py ; rc=$? ;;
     c5x2)    # rehearsal of the N=2 config-5 path (sharded MADS) on one GPU (gloo; both ranks on device 0)
