@@ -440,6 +440,11 @@ def main():
     ap.add_argument("--disks", default="uniform", choices=("uniform", "clustered"),
                     help="UAV disks: uniform over the domain (default) or SURVEY 8(d)'s "
                          "clustered variant (sqrt(N)*40 m around the centre, overlapping)")
+    ap.add_argument("--step-mode", default="armed", choices=("armed", "plain"),
+                    help="one GPU: armed (default) = each poll's chain is enqueued behind the "
+                         "context's doorbell while the previous poll runs and released once its "
+                         "result is read (mac_poll_arm_dev_f64 / mac_poll_fire); plain = enqueued "
+                         "after the previous result (mac_poll_best_dev_f64)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL on ROCm) for the real multi-GPU run; gloo only to rehearse "
                          "N>1 with several ranks sharing one GPU (MAXCOVER_BENCH_DEVICE)")
@@ -553,6 +558,30 @@ def main():
     # N > 1: the 16-B all-gather straight from d_best, ordered after the poll on its stream,
     # and one pinned host read of the world x 16-B result (dist.PollGather)
     gat = pdist.PollGather(coll_dev) if distributed else None
+    # one GPU, armed: poll j + 1 is enqueued behind the doorbell while poll j runs (its inputs are
+    # resident; a MADS driver fills them once poll j's result is known) and released right after
+    # that result is read, so no launch sits between dependent polls. Consecutive polls alternate
+    # two d_best buffers (each buffer's result slot follows its latest poll).
+    armed = args.step_mode == "armed" and not distributed and K > 1
+    if armed:
+        d_best2 = [d_best, torch.empty(2, dtype=torch.float64, device=dev)]
+        nb = len(d_polls) * 2 // np.gcd(len(d_polls), 2)
+        arm, fire, fetch = ctx.armed_steps(
+            [dict(d_cands=d_polls[j % len(d_polls)], three_n=3 * N, K=Kl, d_rmax=d_rmax,
+                  d_best=d_best2[j % 2], d_prev=d_prevs[j % len(d_polls)], d_dlim=d_dlim,
+                  tan_half_fov=tan_half, idx_base=idx_base) for j in range(nb)], stream=s_handle)
+
+    def run_armed(first, n):
+        """n dependent armed polls (poll sets first, first + 1, ...): fire j, arm j + 1 while
+        poll j runs, read j's result. Every armed poll is fired before returning."""
+        res = None
+        arm(first % nb)
+        for i in range(first, first + n):
+            fire(i % nb)
+            if i + 1 < first + n:
+                arm((i + 1) % nb)
+            res = fetch(i % nb)
+        return res
 
     def step(i):
         """One MADS poll. It ends with the best (objective, index) on the host, because the
@@ -566,8 +595,11 @@ def main():
                 return gat(d_best)
         return steps[i % len(steps)]()   # poll + the 16-B result from pinned host memory
 
-    for i in range(args.warmup):
-        step(i)
+    if armed:
+        run_armed(0, args.warmup)
+    else:
+        for i in range(args.warmup):
+            step(i)
     torch.cuda.synchronize(dev)
 
     # correctness guard on the timed workload: the timed poll (this rank's shard, the device's
@@ -601,10 +633,20 @@ def main():
     if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    if armed:   # (the first timed poll's chain is enqueued before the clock starts, as every
+                # later poll's is enqueued while its predecessor runs)
+        arm(args.warmup % nb)
     t0 = time.perf_counter()
     result = None
-    for i in range(args.steps):
-        result = step(args.warmup + i)
+    if armed:
+        for i in range(args.warmup, args.warmup + args.steps):
+            fire(i % nb)
+            if i + 1 < args.warmup + args.steps:
+                arm((i + 1) % nb)
+            result = fetch(i % nb)
+    else:
+        for i in range(args.steps):
+            result = step(args.warmup + i)
     if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -698,6 +740,7 @@ def main():
                                 f"one poll's candidates sharded over {world} GPU(s), "
                                 f"16-B argmin all-gather"),
                 "algo": args.algo,
+                "step_mode": "armed" if armed else "plain",
             },
             "roofline": {
                 "bound": "hbm",

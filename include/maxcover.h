@@ -246,6 +246,25 @@ int32_t mac_poll_best_dev_f32(mac_ctx* ctx, const float* d_cands, int64_t three_
 int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* best_obj,
                        int64_t* best_idx);
 
+/* Armed device polls: the host turnaround between dependent polls of a MADS loop (the next poll
+ * is known only after the previous one's result) taken off the device's critical path. The
+ * chain of mac_poll_best_dev_f64 is enqueued ahead of time behind a stream wait on the context's
+ * doorbell (signal memory the command processor watches), so its launches are already queued
+ * when the host decides; mac_poll_fire rings the doorbell and the chain starts without a launch.
+ * Its inputs (d_cands, d_prev, ...) may be written until the fire (device writes on other
+ * streams must have completed). Rules: tickets are fired in arming order (a fire releases every
+ * armed poll with a ticket <= it); a poll and the armed poll after it use different d_best
+ * buffers (each buffer's mapped slot follows its latest poll); nothing may wait for the stream
+ * (or the device) while an armed poll on it is not fired — mac_best_fetch of a fired poll never
+ * does, and mac_ctx_destroy fires every outstanding ticket first. MAC_E_HIP when the device
+ * cannot wait on stream values (hipDeviceAttributeCanUseStreamWaitValue). */
+int32_t mac_poll_arm_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three_n, int64_t K,
+                             const double* d_rmax, double penalty,
+                             const double* d_prev, const double* d_dlim, double tan_half_fov,
+                             int64_t idx_base, double* d_obj, void* d_best, void* stream,
+                             uint64_t* ticket);
+int32_t mac_poll_fire(mac_ctx* ctx, uint64_t ticket);
+
 /* ---- measurement ----------------------------------------------------------------- */
 /* With MAC_OPT_PROFILE = 1, the coverage-kernel launches (and the first and last launch of
  * each poll chain) stamp their workgroups' start / end times (s_memrealtime, k_common.h): no

@@ -51,7 +51,8 @@ EXPORTS = (
     "mac_set_points_dev_f64", "mac_num_points", "mac_get_points_f64",
     "mac_remove_covered_f64", "mac_covered_flags_f64", "mac_area_f64", "mac_area_batch_f64",
     "mac_objective_batch_f64", "mac_poll_best_f64", "mac_area_batch_dev_f64",
-    "mac_poll_best_dev_f64", "mac_best_fetch", "mac_cover_threshold", "mac_profile_read",
+    "mac_poll_best_dev_f64", "mac_best_fetch", "mac_poll_arm_dev_f64", "mac_poll_fire",
+    "mac_cover_threshold", "mac_profile_read",
     "mac_profile_split", "mac_profile_kernels",
     "mac_append_points_f64", "mac_append_points_dev_f64", "mac_mads_run",
     "mac_fire_last_error", "mac_fire_thresholds", "mac_fire_create", "mac_fire_destroy",
@@ -137,6 +138,10 @@ def _declare(L: ctypes.CDLL) -> None:
         "mac_poll_best_dev_f64": ([_vp, _vp, _i64, _i64, _vp, ctypes.c_double, _vp, _vp,
                                    ctypes.c_double, _i64, _vp, _vp, _vp], _i32),
         "mac_best_fetch": ([_vp, _vp, _vp, _dp, _i64p], _i32),
+        "mac_poll_arm_dev_f64": ([_vp, _vp, _i64, _i64, _vp, ctypes.c_double, _vp, _vp,
+                                  ctypes.c_double, _i64, _vp, _vp, _vp,
+                                  ctypes.POINTER(ctypes.c_uint64)], _i32),
+        "mac_poll_fire": ([_vp, ctypes.c_uint64], _i32),
         "mac_cover_threshold": ([ctypes.c_double], ctypes.c_double),
         "mac_profile_read": ([_vp, _dp, _i64p, _i64p, ctypes.POINTER(_i32), _i32], _i32),
         "mac_profile_split": ([_vp, _dp, _dp, _dp, _i64p], _i32),
@@ -553,6 +558,62 @@ class Context:
             return bo.value, bi.value
 
         return step
+
+    def poll_arm(self, d_cands, three_n: int, K: int, d_rmax, d_best, penalty: float = 1e5,
+                 d_prev=None, d_dlim=None, tan_half_fov: float = 1.0, idx_base: int = 0,
+                 d_obj=None, stream=None) -> int:
+        """mac_poll_arm_dev_f64: the device poll enqueued behind the context's doorbell; returns
+        its ticket (poll_fire releases it). See include/maxcover.h for the rules."""
+        t = ctypes.c_uint64()
+        _check(self._L.mac_poll_arm_dev_f64(
+            self._h, _devptr(d_cands), int(three_n), int(K), _devptr(d_rmax), float(penalty),
+            _devptr(d_prev), _devptr(d_dlim), float(tan_half_fov), int(idx_base),
+            _devptr(d_obj), _devptr(d_best), _devptr(stream), ctypes.byref(t)))
+        return int(t.value)
+
+    def poll_fire(self, ticket: int) -> None:
+        _check(self._L.mac_poll_fire(self._h, int(ticket)))
+
+    def armed_steps(self, polls, stream=None):
+        """Bound armed polls for a loop of dependent polls: ``polls`` = a list of dicts of
+        poll_best_dev arguments (d_cands, three_n, K, d_rmax, d_best, ...; consecutive polls on
+        different d_best buffers). Returns (arm(j), fire(j), fetch(j)): arm enqueues poll j
+        behind the doorbell, fire releases it, fetch returns its (objective, index) — with
+        prebuilt ctypes arguments, so a loop step is fire(j), arm(j + 1) (enqueued while poll j
+        runs), fetch(j)."""
+        h = _vp(self._h.value if isinstance(self._h, _vp) else self._h)
+        arm_f, fire_f, fetch_f = (self._L.mac_poll_arm_dev_f64, self._L.mac_poll_fire,
+                                  self._L.mac_best_fetch)
+        tickets = [ctypes.c_uint64() for _ in polls]
+        bo, bi = ctypes.c_double(), ctypes.c_int64()
+        sv = _vp(_devptr(stream))
+        arm_args, fetch_args = [], []
+        for p, t in zip(polls, tickets):
+            arm_args.append((h, _vp(_devptr(p["d_cands"])), _i64(int(p["three_n"])), _i64(int(p["K"])),
+                             _vp(_devptr(p["d_rmax"])), ctypes.c_double(float(p.get("penalty", 1e5))),
+                             _vp(_devptr(p.get("d_prev"))), _vp(_devptr(p.get("d_dlim"))),
+                             ctypes.c_double(float(p.get("tan_half_fov", 1.0))),
+                             _i64(int(p.get("idx_base", 0))), _vp(_devptr(p.get("d_obj"))),
+                             _vp(_devptr(p["d_best"])), sv, ctypes.byref(t)))
+            fetch_args.append((h, _vp(_devptr(p["d_best"])), sv, ctypes.byref(bo), ctypes.byref(bi)))
+
+        def arm(j):
+            rc = arm_f(*arm_args[j])
+            if rc != MAC_OK:
+                _check(rc)
+
+        def fire(j):
+            rc = fire_f(h, tickets[j].value)
+            if rc != MAC_OK:
+                _check(rc)
+
+        def fetch(j):
+            rc = fetch_f(*fetch_args[j])
+            if rc != MAC_OK:
+                _check(rc)
+            return bo.value, bi.value
+
+        return arm, fire, fetch
 
     def best_fetch(self, d_best, stream=None):
         """The (objective, index) the latest device poll on d_best wrote (mac_best_fetch).

@@ -164,12 +164,18 @@ static_assert(kPrepC % 4 == 0 && 32 % kPrepC == 0 && kPrepC <= 64,
               "MAC_PREP_C must divide 32 and be a multiple of 4");
 __host__ __device__ inline int keys_ld(int K) { return (K + 31) & ~31; }
 
+// vp word of a candidate whose penalty chain is folded later (prep_args.defer): a NaN payload no
+// arithmetic produces (a real vp is acc * penalty: a number, +-inf or the default quiet NaN)
+constexpr uint64_t kVpPending = 0x7FF4DEADBEEF0001ull;
+
 struct PrepArgs {
     CandSrc src;
     int N, K;
     PenArgs pa;
     double penalty;
     double* vp;                // per-candidate penalty (null: no objective)
+    int defer;                 // 1: only cons3 here (vp = +inf or kVpPending), the chains folded by
+                               // the poll kernel's shared workgroups beside the walks (fold_chains)
     int nchain;                // workgroups
     int4* prec;                // [nchain][N] records (null: no poll walk)
     Grid g;
@@ -307,7 +313,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
                     const double sq = ddx * ddx + ddy * ddy + ddz * ddz;
                     if (sq > T3) t = -1.0;
                 }
-                term[c][u] = t;
+                if (!a.defer) term[c][u] = t;
                 const uint64_t neg = __ballot(iv && t < 0.0);
                 if (lane == 0) wbad[wid][c] = neg != 0;
             }
@@ -373,6 +379,8 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
             if (u < kPrepC) {
 #pragma unroll
                 for (int w = 0; w < kPrepU / kWave; ++w) bad |= wbad[w][u] != 0;
+            }
+            if (u < kPrepC && !a.defer) {
                 int q = 0;
                 for (; q + 16 <= nb; q += 16) {
                     double t[16];
@@ -387,7 +395,48 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
         MAC_PREP_STAMP(3 + 3 * (ib / kPrepU));
         if (obj && ib + kPrepU < N) lds_barrier();   // the fold has read the terms
     }
-    if (obj && u < kPrepC && k0 + u < K) a.vp[k0 + u] = bad ? __builtin_inf() : acc * a.penalty;
+    if (obj && u < kPrepC && k0 + u < K)
+        a.vp[k0 + u] = bad ? __builtin_inf()
+                     : a.defer ? __builtin_bit_cast(double, kVpPending) : acc * a.penalty;
+}
+
+// The deferred penalty chains (prep_args.defer): the candidates whose vp is kVpPending get
+// vp = penalty * (((0 + t_0) + t_1) + ... + t_{N-1}), t_i = |R_i - rmax_i| — the prep's fold
+// (and src/TDM_STATIC_opt.jl:88-92) term for term, one thread per candidate, 16 loads in flight
+// per batch. Run by the poll kernel's shared-entry workgroups (idle while the walks run at every
+// poll that is not crowded) beside the walks, so the 512 dependent adds leave the chain's first
+// launch. No barriers: any thread may call it with its own candidates (first, first + stride, ...).
+struct FoldArgs {
+    CandSrc src;
+    int N, K;
+    const double* rmax;
+    double penalty;
+    double* vp;                // null: nothing deferred
+};
+
+__device__ __forceinline__ void fold_chains(const FoldArgs& f, int first, int stride)
+{
+    CandSrc src = f.src;
+    if (!f.vp || !src.resolve()) return;   // (a stopped pipelined MADS loop: no result)
+    const int N = f.N;
+    for (int k = first; k < f.K; k += stride) {
+        if (__builtin_bit_cast(uint64_t, f.vp[k]) != kVpPending) continue;
+        double acc = 0.0;
+        for (int i0 = 0; i0 < N; i0 += 16) {
+            double t[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int i = min(i0 + j, N - 1);
+                const double R2 = src.get(k, 2 * N + i, N);
+                t[j] = f.rmax ? __builtin_fabs(R2 - f.rmax[i]) : 0.0;
+            }
+            const int nj = min(16, N - i0);
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if (j < nj) acc += t[j];
+        }
+        f.vp[k] = acc * f.penalty;
+    }
 }
 
 __global__ __launch_bounds__(kPrepU) __attribute__((amdgpu_waves_per_eu(4))) void prep_kernel(uint64_t* ts, PrepArgs a)

@@ -166,6 +166,10 @@ struct mac_ctx {
     uint64_t mirror_used[kMirrorSlots] = {};
     uint64_t mirror_seq = 0, mirror_clock = 0;
     hipStream_t dev_stream = nullptr;   // ordered stream for *_dev calls passed stream = NULL
+    // armed polls (mac_poll_arm_dev_f64): the doorbell the streams wait on (signal memory), the
+    // last ticket armed and the last fired (guarded by mu)
+    uint64_t* doorbell = nullptr;
+    uint64_t armed = 0, fired = 0;
 
     int algo = MAC_ALGO_AUTO;
     int shared_mode = MAC_SHARED_AUTO;   // MAC_OPT_SHARED
@@ -551,6 +555,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         pr.pa = pa;
         pr.penalty = penalty;
         pr.vp = d_vp;
+        pr.defer = d_vp && poll_possible ? 1 : 0;   // the poll kernel folds the chains (k_prep.h)
         pr.nchain = nchain;
         pr.g = ctx->grid;
         if (poll_possible) {
@@ -754,7 +759,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                                L->mode.as<int>() + 2, N, K,
                                d_mode, L->partial.as<double>(), L->spart.as<double>(), n_shared, counts,
                                bits_on, L->d_dc, L->qual.as<int>(),
-                               walk_forced == 0 ? L->cost.as<double2>() : nullptr, kPollCostRatio);
+                               walk_forced == 0 ? L->cost.as<double2>() : nullptr, kPollCostRatio,
+                               FoldArgs{src, N, K, d_rmax, penalty, d_vp});
             HCK(hipGetLastError());
             // the shared entries of crowded polls: the union pass (equal weights, k_or.h) or
             // bit-words per distinct position (k_bits.h); both return at once when few disks have
@@ -1187,7 +1193,12 @@ void mac_ctx_destroy(mac_ctx* ctx)
 {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    if (ctx->doorbell) {   // every armed poll released first (else the synchronisation would wait)
+        __atomic_store_n(ctx->doorbell, ~(uint64_t)0 >> 1, __ATOMIC_RELEASE);
+        ctx->fired = ctx->armed;
+    }
     (void)hipDeviceSynchronize();
+    if (ctx->doorbell) (void)hipFree(ctx->doorbell);
     ctx->h_mirror.release();
     for (Lane* l : ctx->lanes_all) {
         l->h_stage.release();
@@ -2330,6 +2341,64 @@ int32_t mac_poll_best_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three
     ABI_END
 }
 
+int32_t mac_poll_arm_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three_n, int64_t K,
+                             const double* d_rmax, double penalty, const double* d_prev,
+                             const double* d_dlim, double tan_half_fov, int64_t idx_base,
+                             double* d_obj, void* d_best, void* stream, uint64_t* ticket)
+{
+    ABI_BEGIN
+    if (!ctx || !ticket) return fail(MAC_E_INVAL, "null context / ticket");
+    if (K <= 0) return fail(MAC_E_INVAL, "an armed poll needs K > 0");   // (K = 0 synchronises)
+    set_device(ctx);
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->dev_stream;
+    uint64_t t = 0;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        if (!ctx->doorbell) {
+            int ok = 0;
+            HCK(hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, ctx->device));
+            if (!ok) return fail(MAC_E_HIP, "the device cannot wait on stream values");
+            void* p = nullptr;
+            HCK(hipExtMallocWithFlags(&p, 64, hipMallocSignalMemory));
+            ctx->doorbell = (uint64_t*)p;
+            __atomic_store_n(ctx->doorbell, (uint64_t)0, __ATOMIC_RELEASE);
+            ctx->armed = ctx->fired = 0;
+        }
+        t = ++ctx->armed;
+    }
+    *ticket = t;
+    int32_t rc = MAC_OK;
+    try {
+        HCK(hipStreamWaitValue64(s, ctx->doorbell, t, hipStreamWaitValueGte, ~(uint64_t)0));
+        rc = poll_best_dev<double>(ctx, d_cands, three_n, K, d_rmax, penalty, d_prev, d_dlim,
+                                   tan_half_fov, idx_base, d_obj, d_best, stream);
+    } catch (...) {
+        rc = -1;
+    }
+    if (rc) {   // the poll did not go in: its ticket is released at once
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        if (t > ctx->fired) {
+            __atomic_store_n(ctx->doorbell, t, __ATOMIC_RELEASE);
+            ctx->fired = t;
+        }
+        if (rc < 0) return fail(MAC_E_HIP, "arming the poll failed");
+    }
+    return rc;
+    ABI_END
+}
+
+int32_t mac_poll_fire(mac_ctx* ctx, uint64_t ticket)
+{
+    if (!ctx) return fail(MAC_E_INVAL, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (!ctx->doorbell || ticket > ctx->armed) return fail(MAC_E_INVAL, "ticket was not armed");
+    if (ticket > ctx->fired) {
+        __atomic_store_n(ctx->doorbell, ticket, __ATOMIC_RELEASE);
+        ctx->fired = ticket;
+    }
+    return MAC_OK;
+}
+
 int32_t mac_poll_best_dev_f32(mac_ctx* ctx, const float* d_cands, int64_t three_n, int64_t K,
                               const double* d_rmax, double penalty, const float* d_prev,
                               const double* d_dlim, double tan_half_fov, int64_t idx_base,
@@ -2351,6 +2420,7 @@ int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* b
     hipStream_t s = stream ? (hipStream_t)stream : ctx->dev_stream;
     const uint64_t* slot = nullptr;
     uint64_t want = 0;
+    bool pending = false;   // an armed poll is not fired: the stream must not be waited for
     {
         std::lock_guard<std::mutex> lk(ctx->mu);   // (released before any wait)
         for (int q = 0; q < mac_ctx::kMirrorSlots; ++q)
@@ -2359,6 +2429,7 @@ int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* b
                 want = ctx->mirror_want[q];
                 break;
             }
+        pending = ctx->armed > ctx->fired;
     }
     if (slot) {
         // the latest device poll on d_best writes its result into this slot (the poll takes
@@ -2366,7 +2437,9 @@ int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* b
         // read the slot once more, else copy d_best
         double o = 0.0;
         int64_t i = -1;
-        bool ok = mirror_wait(slot, want, 2.0, &o, &i);
+        bool ok = mirror_wait(slot, want, pending ? 2000.0 : 2.0, &o, &i);
+        if (!ok && pending)
+            return fail(MAC_E_HIP, "poll result not written within 2 s (armed polls pending)");
         if (!ok) {
             HCK(hipStreamSynchronize(s));
             ok = mirror_read(slot, want, &o, &i);

@@ -1016,3 +1016,53 @@ def test_native_mads_pipelined_matches_stepper(ctx, pkg, N, n_iter, ell0, ell_ma
     if stall:
         assert want["status"] == 0 and want["iterations"] == ell0 + 1
         assert np.array_equal(want_x, x0)
+
+
+def test_armed_polls_match_plain_polls(pkg):
+    """mac_poll_arm_dev_f64 / mac_poll_fire: a loop of dependent polls armed one ahead (behind the
+    context's doorbell, released after the previous result is read, alternating d_best buffers)
+    returns every poll's (objective, index) exactly as mac_poll_best_dev_f64; a context destroyed
+    with an armed poll never fired releases it (no hang)."""
+    import torch
+    wl = pkg.workloads
+    x, y, w = wl.grid_points(192)
+    rng = wl.SplitMix64(808)
+    N = 16
+    x0 = wl.clustered_disks(N, 192, rng)
+    polls = [wl.poll_candidates(x0, rng) for _ in range(3)]
+    K = polls[0].shape[0]
+    r_max = np.full(N, 30.0 * TAN50)
+    dev = torch.device("cuda", 0)
+    d_polls = [torch.from_numpy(np.ascontiguousarray(p)).to(dev) for p in polls]
+    d_prev = [torch.from_numpy(np.ascontiguousarray(p[0])).to(dev) for p in polls]
+    d_rmax = torch.from_numpy(r_max).to(dev)
+    d_dlim = torch.full((N,), 10.0, dtype=torch.float64, device=dev)
+    bests = [torch.empty(2, dtype=torch.float64, device=dev) for _ in range(2)]
+    stream = torch.cuda.Stream(dev)
+    with pkg.Context(0) as ctx:
+        ctx.set_points(x, y, w)
+        want = []
+        for j in range(7):
+            ctx.poll_best_dev(d_polls[j % 3], 3 * N, K, d_rmax, bests[0], d_prev=d_prev[j % 3],
+                              d_dlim=d_dlim, tan_half_fov=TAN50, stream=stream.cuda_stream)
+            want.append(ctx.best_fetch(bests[0], stream=stream.cuda_stream))
+        torch.cuda.synchronize()
+        arm, fire, fetch = ctx.armed_steps(
+            [dict(d_cands=d_polls[j % 3], three_n=3 * N, K=K, d_rmax=d_rmax, d_best=bests[j % 2],
+                  d_prev=d_prev[j % 3], d_dlim=d_dlim, tan_half_fov=TAN50) for j in range(6)],
+            stream=stream.cuda_stream)
+        got = []
+        arm(0)
+        for j in range(7):
+            fire(j % 6)
+            if j + 1 < 7:
+                arm((j + 1) % 6)
+            got.append(fetch(j % 6))
+        assert got == want
+        assert len({o for o, _ in want}) > 1   # (different polls, different bests)
+        with pytest.raises(pkg.MaxCoverError):
+            ctx.poll_fire(10 ** 6)              # never armed
+    with pkg.Context(0) as ctx2:                # destroyed with an armed poll never fired
+        ctx2.set_points(x, y, w)
+        ctx2.poll_arm(d_polls[0], 3 * N, K, d_rmax, bests[1], stream=stream.cuda_stream)
+    torch.cuda.synchronize()
