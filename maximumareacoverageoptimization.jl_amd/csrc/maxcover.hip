@@ -555,7 +555,9 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         pr.pa = pa;
         pr.penalty = penalty;
         pr.vp = d_vp;
-        pr.defer = d_vp && poll_possible ? 1 : 0;   // the poll kernel folds the chains (k_prep.h)
+        // matrix polls: the poll kernel folds the chains (k_prep.h fold_chains) from the matrix's
+        // R rows; generated polls keep the fold here (a term there would be regenerated)
+        pr.defer = d_vp && poll_possible && src.cands ? 1 : 0;
         pr.nchain = nchain;
         pr.g = ctx->grid;
         if (poll_possible) {
