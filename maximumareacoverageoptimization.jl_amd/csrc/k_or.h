@@ -89,13 +89,36 @@ __device__ __forceinline__ uint64_t or_row_mask(const int4& R, int r, const int4
     return mask;
 }
 
-// Entries of row r's masked runs (wave 0: lane = row; off loads of every run in flight).
+// Entries of row r's masked runs (wave 0: lane = row). The first four runs' offsets are loaded
+// together (a row of a MADS poll's region has one to three), further runs one by one.
 __device__ __forceinline__ int or_row_count(const int32_t* __restrict__ off, const Grid& g,
                                             const int4& R, int r, uint64_t mask)
 {
     const int64_t rowbase = (int64_t)r * g.nTx + R.x;
+    int lo[4], hi[4];
+    uint64_t m2 = mask;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        lo[q] = hi[q] = 0;
+        if (m2) {
+            const int a = __builtin_ctzll(m2);
+            const uint64_t from = m2 >> a;
+            const int len = ~from ? __builtin_ctzll(~from) : 64 - a;
+            lo[q] = a;
+            hi[q] = a + len;
+            m2 &= len + a >= 64 ? 0ull : (~0ull << (a + len));
+        }
+    }
+    int v[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        v[2 * q] = hi[q] > lo[q] ? off[rowbase + lo[q]] : 0;
+        v[2 * q + 1] = hi[q] > lo[q] ? off[rowbase + hi[q]] : 0;
+    }
     int n = 0;
-    for (uint64_t m2 = mask; m2;) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) n += v[2 * q + 1] - v[2 * q];
+    while (m2) {
         const int a = __builtin_ctzll(m2);
         const uint64_t from = m2 >> a;
         const int len = ~from ? __builtin_ctzll(~from) : 64 - a;

@@ -65,6 +65,9 @@ for s in $STEPS; do
     diagor)   # phase times of the union pass on the config-5 regression poll at ell 5 / 4 / 3
         MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
             run diagor 300 python tools/diag_or.py ; rc=$? ;;
+    probeka)  # can a launch carry the 12-KB closure candidate as kernel arguments? (tools/probe)
+        [ -x tools/probe/kernarg_probe ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O2 tools/probe/kernarg_probe.hip -o tools/probe/kernarg_probe
+        run probeka 60 tools/probe/kernarg_probe ; rc=$? ;;
     c5polls)  # per-poll kernel times of the config-5 loop; the slowest polls saved for analysis
         run c5polls 600 python tools/c5_polls.py ; rc=$? ;;
     c5x2)    # rehearsal of the N=2 config-5 path (sharded MADS) on one GPU (gloo; both ranks on device 0)
