@@ -60,12 +60,23 @@ constexpr int kOrRuns = 64 * 32;                // tile runs of a region (64 row
 // 1 above kBitsMinDisks disks with neighbours, 2 always): 0 the poll kernel's fp64 jobs for
 // every disk with neighbours; 1 the bit-word kernel (k_bits.h, weighted lists) for the disks it
 // qualifies + fp64 jobs for the others; 2 this union pass for every disk (equal weights).
-__device__ __forceinline__ int shared_route(const int* __restrict__ dcount, int bits_on, int counts)
+__device__ __forceinline__ int shared_route(const int* __restrict__ dcount, int bits_on, int counts,
+                                            int K)
 {
     const int nA = dcount[kDcBits], nB = dcount[kDcOther];
     if (!bits_on || nA + nB <= (bits_on == 2 ? 0 : kBitsMinDisks)) return 0;
     if (!counts) return 1;
-    return nB == 0 && dcount[kDcOrBad] == 0 ? 2 : 0;
+    // (positions are staged as 16-bit words: K <= 65535)
+    return nB == 0 && dcount[kDcOrBad] == 0 && K <= 65535 ? 2 : 0;
+}
+
+// One wave's 64 16-bit words global -> LDS with no register (global_load_lds_ushort): lane l
+// reads g_lane (its own address, the low half of an int32 on little-endian) into l_wave + 2 l;
+// l_wave is wave-uniform. Drained by the next __syncthreads (hipcc waits vmcnt(0) there).
+__device__ __forceinline__ void glds_u16(const void* g_lane, void* l_wave)
+{
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g_lane,
+                                     (__attribute__((address_space(3))) void*)l_wave, 2, 0, 0);
 }
 
 // Row r's tiles of region R (at most 64 x 64 tiles) that lie in some lower box and in no upper
@@ -217,12 +228,13 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
     __shared__ __attribute__((aligned(16))) float4 ent[kOrE / 2];   // {U0, U1, V0, V1} per entry pair
     __shared__ f32x2 entq[kOrE / 2];                                 // {Q0, Q1}
     __shared__ uint2 tab[kOrTab];
+    __shared__ uint16_t um16[kOrKC];   // the current disk's position of every candidate of the chunk
     __shared__ int s_nrel, s_total, s_job;
 
     ts_begin(ts);
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
     constexpr int kWaves = kOrThreads / kWave;
-    if ((a.mode && *a.mode != kModePoll) || shared_route(a.dcount, a.bits_on, 1) != 2) {   // uniform
+    if ((a.mode && *a.mode != kModePoll) || shared_route(a.dcount, a.bits_on, 1, a.K) != 2) {   // uniform
         ts_end(ts);
         return;
     }
@@ -372,12 +384,13 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
                 const int d = sid[m], U = sU[m];
                 const int64_t row = (int64_t)d * K;
                 const uint64_t lv = live[m], lm = lmask[m];
-                // the candidates' positions of disk d (in flight during the tables)
-                int um[kOrPT];
+                // the candidates' positions of disk d straight into LDS (no registers), in flight
+                // during the tables; the barrier after the tables drains them
 #pragma unroll
                 for (int c = 0; c < kOrPT; ++c) {
-                    const int k = kc0 + tid + c * kOrThreads;
-                    um[c] = k < K ? a.umap[row + k] : -1;
+                    const int kw = kc0 + c * kOrThreads + wid * kWave;   // the wave's first candidate
+                    if (kw < K)
+                        glds_u16(a.umap + row + min(kw + lane, K - 1), um16 + c * kOrThreads + wid * kWave);
                 }
                 // the entries relative to region d's centre, as the walk stages them; entries
                 // outside box d, past the list or non-finite are inert (Q = +inf: d' = -inf)
@@ -440,7 +453,7 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
                                 cw <<= 8;
                                 continue;
                             }
-#pragma unroll 1
+#pragma unroll 2
                             for (int j = 4 * g8; j < 4 * g8 + 4; ++j) {
                                 const float4 uv = eh[j];
                                 const f32x2 qq = qh[j];
@@ -484,7 +497,8 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
                     // combine: the union word and the j0 word of every candidate
 #pragma unroll
                     for (int c = 0; c < kOrPT; ++c) {
-                        const int u = um[c];
+                        const int k = kc0 + tid + c * kOrThreads;
+                        const int u = k < K ? (int)um16[c * kOrThreads + tid] : -1;
                         if (u >= u0 && u < u1) {
                             const uint2 t2 = tab[u - u0];
                             const uint64_t t = (uint64_t)t2.x | ((uint64_t)t2.y << 32);

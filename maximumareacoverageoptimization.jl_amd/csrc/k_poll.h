@@ -177,7 +177,7 @@ __device__ __forceinline__ void coverage_poll_body(
         const int nA = dcount[kDcBits], nB = dcount[kDcOther];
         // (k_or.h shared_route) 0: every disk with neighbours here; 1: the bit-word kernel takes
         // the qualifying disks (the rest here); 2: the union pass takes every disk
-        const int route = lane4 != nullptr ? shared_route(dcount, bits_on, counts) : 0;
+        const int route = lane4 != nullptr ? shared_route(dcount, bits_on, counts, K) : 0;
         const int nlist = route == 1 ? nB : route == 2 ? 0 : nA + nB;   // list position q: dlist[N-1-q], then dlist[q-nB]
         const int C = nlist * ((K + kShC - 1) / kShC) > 2 * (int)gridDim.x ? kShCWide : kShC;
         const int nsub = (K + C - 1) / C;
@@ -276,7 +276,7 @@ __device__ __forceinline__ void coverage_poll_body(
     if (mv != kModePoll) return;       // (after the first loads: the check costs no round trip)
     // the union pass (launched next, k_or.h) adds its counts into spart row i of every disk
     // with neighbours (finalize reads those rows)
-    if (by == 0 && counts && nc > 0 && shared_route(dcount, bits_on, counts) == 2)
+    if (by == 0 && counts && nc > 0 && shared_route(dcount, bits_on, counts, K) == 2)
         for (int k = tid; k < K; k += kPollThreads) reinterpret_cast<unsigned*>(spart)[row + k] = 0u;
     if (R.x > R.y) {  // disk i covers nothing in any candidate (uniform across the block)
         if (by > 0)
