@@ -179,3 +179,41 @@ def test_gloo_world2_broadcast_points():
         assert p.exitcode == 0
     for rank, same, n_empty in res:
         assert same and n_empty == 0, rank
+
+
+def _pollgather_worker(rank, world, port, q):
+    """dist.PollGather on gloo (the bench's strong-mode exchange, CPU records): every rank's
+    16-B {objective, index} record in, the lexicographic minimum over ranks out, per call, with
+    ties to the lowest index and empty shards ({+inf, -1}) ignored."""
+    import sys
+    import torch.distributed as dist
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    from importlib import import_module
+    d = import_module(pkg.__name__ + ".dist")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = d.PollGather("cpu")
+    cases = [((5.0, 10), (4.0, 700)), ((3.0, 12), (3.0, 9)), ((np.inf, -1), (7.5, 1500)),
+             ((np.inf, -1), (np.inf, -1)), ((-2.0, 3), (-2.0, 2000))]
+    out = [g(d.pack_best(*c[rank])) for c in cases]
+    q.put((rank, out, g.calls))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_poll_gather():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pollgather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = [(4.0, 700), (3.0, 9), (7.5, 1500), (np.inf, -1), (-2.0, 3)]
+    for rank, out, calls in res:
+        assert out == want and calls == 5, rank
