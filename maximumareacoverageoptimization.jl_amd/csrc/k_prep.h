@@ -176,6 +176,9 @@ struct PrepArgs {
     double* vp;                // per-candidate penalty (null: no objective)
     int defer;                 // 1: only cons3 here (vp = +inf or kVpPending), the chains folded by
                                // the poll kernel's shared workgroups beside the walks (fold_chains)
+    int pair;                  // generated complete polls (K = 2n, n % 4 == 0): workgroup cw takes
+                               // x + B[:, k] and x - B[:, k] for k in [4cw, 4cw + 4) (one draw of
+                               // each B entry for both: prep_cand)
     int nchain;                // workgroups
     int4* prec;                // [nchain][N] records (null: no poll walk)
     Grid g;
@@ -269,6 +272,10 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
     const int N = a.N, K = a.K;
     const int u = threadIdx.x, lane = u & (kWave - 1), wid = u / kWave;
     const int k0 = cw * kPrepC;
+    const int n3 = 3 * N;
+    // candidate c of the workgroup: k0 + c, or (pairs) the plus / minus candidates of B's columns
+    // [4cw, 4cw + 4): c < 4 -> 4cw + c, c >= 4 -> n + 4cw + c - 4
+    auto cand = [&](int c) { return a.pair ? (c < 4 ? 4 * cw + c : n3 + 4 * cw + c - 4) : k0 + c; };
     const bool obj = a.vp != nullptr;
     const PenArgs& pa = a.pa;
     MAC_PREP_STAMP(0);
@@ -280,13 +287,28 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
         const bool iv = u < nb;
         const int ii = min(i, N - 1);
         double v[kPrepC][3];
+        if (!kMat && a.pair) {
+            // x +- B[v][col]: each draw once for the candidate pair (kPrepC == 8: four columns)
 #pragma unroll
-        for (int c = 0; c < kPrepC; ++c) {
-            const int k = min(k0 + c, K - 1);
+            for (int c = 0; c < 4; ++c) {
+                const int col = 4 * cw + c;
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                if constexpr (kMat) v[c][q] = a.src.cands[(int64_t)k * a.src.ldc + q * N + ii];
-                else v[c][q] = a.src.get(k, q * N + ii, N);
+                for (int q = 0; q < 3; ++q) {
+                    const int vv = q * N + ii;
+                    const double d = ltmads_entry(a.src.state, n3, a.src.b, a.src.rp[vv], a.src.cp[col]);
+                    v[c][q] = a.src.xinc[vv] + d;
+                    v[c + 4][q] = a.src.xinc[vv] - d;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < kPrepC; ++c) {
+                const int k = min(cand(c), K - 1);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    if constexpr (kMat) v[c][q] = a.src.cands[(int64_t)k * a.src.ldc + q * N + ii];
+                    else v[c][q] = a.src.get(k, q * N + ii, N);
+                }
             }
         }
         double base[3] = {0.0, 0.0, 0.0};   // candidate 0's values: the keys' base
@@ -327,7 +349,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
             for (int c = 0; c < kPrepC; ++c) {
                 const double x = v[c][0], y = v[c][1], r = v[c][2];
                 // span_of's cases: r <= 0 or NaN, or a non-finite centre, covers nothing
-                if (k0 + c < K && r > 0.0 && __builtin_isfinite(x) && __builtin_isfinite(y)) {
+                if (cand(c) < K && r > 0.0 && __builtin_isfinite(x) && __builtin_isfinite(y)) {
                     any = true;
                     xa = fmin(xa, x - r);
                     xb = fmax(xb, x + r);
@@ -354,14 +376,14 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
                         for (int q = 0; q < 3; ++q) {
                             const float f = (float)(v[c][q] - base[q]);
                             kb |= __builtin_bit_cast(uint64_t, base[q] + (double)f) != __builtin_bit_cast(uint64_t, v[c][q]);
-                            a.keysT[(int64_t)(q * N + i) * a.ldk + k0 + c] = f;
+                            a.keysT[(int64_t)(q * N + i) * a.ldk + cand(c)] = f;
                         }
                     }
                 }
-                uint4* dst = reinterpret_cast<uint4*>(a.keysP + (int64_t)i * a.ldk + k0);
 #pragma unroll
-                for (int h = 0; h < kPrepC / 4; ++h)
-                    dst[h] = make_uint4(pk[4 * h], pk[4 * h + 1], pk[4 * h + 2], pk[4 * h + 3]);
+                for (int h = 0; h < kPrepC / 4; ++h)   // candidates cand(4h) .. cand(4h) + 3
+                    *reinterpret_cast<uint4*>(a.keysP + (int64_t)i * a.ldk + cand(4 * h)) =
+                        make_uint4(pk[4 * h], pk[4 * h + 1], pk[4 * h + 2], pk[4 * h + 3]);
             }
             int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
             any = any && partial_range(xa, xb, xm, a.g.gx0, a.g.invS, a.g.nTx, x0, x1) &&
@@ -395,8 +417,8 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
         MAC_PREP_STAMP(3 + 3 * (ib / kPrepU));
         if (obj && ib + kPrepU < N) lds_barrier();   // the fold has read the terms
     }
-    if (obj && u < kPrepC && k0 + u < K)
-        a.vp[k0 + u] = bad ? __builtin_inf()
+    if (obj && u < kPrepC && cand(u) < K)
+        a.vp[cand(u)] = bad ? __builtin_inf()
                      : a.defer ? __builtin_bit_cast(double, kVpPending) : acc * a.penalty;
 }
 

@@ -544,7 +544,10 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
     const int G = (int)std::max<int64_t>(
         1, std::min<int64_t>((target + K - 1) / K, std::max(1, N / kWavesPerBlock)));
     const int64_t units = (int64_t)K * G;
-    const int nchain = (K + kPrepC - 1) / kPrepC;
+    // generated complete polls (the native MADS loop: K = 2n): the prep draws each B entry once
+    // for its plus and minus candidates (k_prep.h PrepArgs.pair)
+    const bool pair = !src.cands && src.k0 == 0 && K == 6 * N && (3 * N) % 4 == 0 && kPrepC == 8;
+    const int nchain = pair ? (3 * N) / 4 : (K + kPrepC - 1) / kPrepC;
     if ((d_obj || poll_possible) && K > 0) {
         // the prep launch (k_prep.h): penalty chains + cons3 into vp, the poll walk's partial
         // regions, and the index's fp32 keys
@@ -559,6 +562,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         // R rows; generated polls keep the fold here (a term there would be regenerated)
         pr.defer = d_vp && poll_possible && src.cands ? 1 : 0;
         pr.nchain = nchain;
+        pr.pair = pair ? 1 : 0;
         pr.g = ctx->grid;
         if (poll_possible) {
             L->prec.reserve(sizeof(int4) * (size_t)nchain * N);
