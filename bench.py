@@ -147,9 +147,12 @@ def pmc_traffic(config, disks, world, algo):
     for name, v in d.get("kernels", {}).items():
         base = name.split("<")[0]
         if base.startswith("mac::"):
-            per[base[5:]] = v.get("hbm_bytes_per_launch")
-    return (d.get("hbm_bytes_per_poll"), os.path.relpath(path, ROOT) + f" (src_sha {d['src_sha']})",
-            per)
+            per[base[5:]] = {"hbm_bytes": v.get("hbm_bytes_per_launch"),
+                             "hbm_bytes_raw": v.get("hbm_bytes_per_launch_raw")}
+    src = os.path.relpath(path, ROOT) + f" (src_sha {d['src_sha']})"
+    if d.get("hbm_bytes_per_poll_raw") is not None:
+        src += f"; uncorrected FETCH (lower bound): {d['hbm_bytes_per_poll_raw']:.4g} B per poll"
+    return d.get("hbm_bytes_per_poll"), src, per
 
 
 def kernel_table(kern, pmc_per=None):
@@ -161,7 +164,7 @@ def kernel_table(kern, pmc_per=None):
         if n:
             out[name] = {"avg_us": ms / n * 1e3, "launches": n}
             if pmc_per and pmc_per.get(name) is not None:
-                out[name]["hbm_bytes"] = pmc_per[name]
+                out[name].update({k: v for k, v in pmc_per[name].items() if v is not None})
     dom = max(out, key=lambda k: out[k]["avg_us"]) if out else None
     return out, dom
 

@@ -9,7 +9,10 @@ pass) with --kernel-trace-free counter collection only. Corrections, per
   * the counters are in KiB (rocprofv3 derived metrics: TCC_EA0_*REQ x 64 B / 1024);
   * on gfx950 FETCH_SIZE reports 1/2 of the bytes of wide coalesced reads, so it is doubled;
   * Infinity-Cache hits are counted by the memory-side counters, not excluded.
-Per kernel: 2 * FETCH + WRITE averaged over its launches. "hbm_bytes_per_poll" sums the kernels
+Per kernel: 2 * FETCH + WRITE averaged over its launches (and, uncorrected, FETCH + WRITE: the
+doubling is calibrated for 16-B-per-lane streaming reads only, so for gather- and hash-heavy
+kernels the corrected figure is an upper bound and the raw one a lower bound; both are kept,
+per kernel and per poll). "hbm_bytes_per_poll" sums the kernels
 of one poll chain (--chain; the default launch chain by default), which bench.py reports as
 roofline.traffic — only while the library sources hash to "src_sha" (bench.src_hash), i.e. the
 build that was profiled. Run the passes with `bench.py --no-extras` so that only the poll chain
@@ -65,6 +68,7 @@ def main():
             "fetch_kib_raw": fk,
             "write_kib_raw": wk,
             "hbm_bytes_per_launch": 2.0 * fk * 1024.0 + wk * 1024.0,
+            "hbm_bytes_per_launch_raw": fk * 1024.0 + wk * 1024.0,
         }
     chain = a.chain.split(";")
     missing = [k for k in chain if k not in kernels]
@@ -79,10 +83,12 @@ def main():
         "src_sha": bench.src_hash(),
         "chain": chain,
         "hbm_bytes_per_poll": sum(kernels[k]["hbm_bytes_per_launch"] for k in chain),
+        "hbm_bytes_per_poll_raw": sum(kernels[k]["hbm_bytes_per_launch_raw"] for k in chain),
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
                   "`python3 bench.py --steps 5 --warmup 1 --no-cpu --no-extras`; bytes = "
                   "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH correction, "
-                  "MI355X_MICROARCH.md)",
+                  "MI355X_MICROARCH.md: calibrated for wide streaming reads, so an upper bound "
+                  "for gathers); *_raw = FETCH_SIZE*1024 + WRITE_SIZE*1024 (a lower bound)",
         "kernels": kernels,
     }
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
