@@ -9,6 +9,12 @@ The static N = 5 run of src/FullSimulation.jl (defaults :725-803) wrote
 Only x, y, z are kept. Output: tests/golden/quadrotor_run.csv, one line per MPC step:
   tx, ty, tz (UAV 1's target), then x, y, z of UAVs 1..5's end-of-step states.
 
+A second, longer recording sits under src/: src/Quadrotor_Targets.xlsx holds 120 MPC steps of
+UAV 1's targets, but its state files come from different runs (src/Quadrotor_States1.xlsx has
+40 rows starting near (2, 10), States2/3 120 rows, States4 60), so UAV 1's start of each step is
+not recorded for it. Only its targets are kept: tests/golden/quadrotor_run_src.csv, tx, ty, tz
+per step — enough to pin the mesh (integer x, y and R = z tan(FOV/2)), not cons3.
+
 Usage: python tests/golden/make_quadrotor_fixture.py
 """
 from __future__ import annotations
@@ -44,6 +50,14 @@ def main() -> None:
         for row in data:
             f.write(",".join(repr(float(v)) for v in row) + "\n")
     print(path, data.shape)
+
+    T2 = read_sheet(os.path.join(REF, "src", "Quadrotor_Targets.xlsx"))[:, :3]
+    path = os.path.join(HERE, "quadrotor_run_src.csv")
+    with open(path, "w") as f:
+        f.write("# src/Quadrotor_Targets.xlsx (120 MPC steps): UAV 1 target x,y,z\n")
+        for row in T2:
+            f.write(",".join(repr(float(v)) for v in row) + "\n")
+    print(path, T2.shape)
 
 
 if __name__ == "__main__":

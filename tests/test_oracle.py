@@ -131,3 +131,19 @@ def test_reference_mads_outputs_on_mesh_and_cons3_feasible(orc, pkg, quadrotor_s
         assert pkg.TDM_Constraints.create_cons3(prev, fov, np.array([10.0]))(cand)
         far = np.array([prev[0] + 10.5, prev[1], prev[2]])   # 10.5 m from the start
         assert not orc.ref_cons3(prev, far, np.array([10.0]), tan)
+
+
+def test_reference_second_recording_targets_on_mesh():
+    """The longer recording under src/ (src/Quadrotor_Targets.xlsx, 120 MPC steps of UAV 1's
+    MADS targets; converted by tests/golden/make_quadrotor_fixture.py). Its state files come
+    from other runs (40/120/120/60 rows), so the start of each step is unknown and only the mesh
+    is pinned: integer x, y and R = z tan(FOV/2) integral (granularity 1.0,
+    src/TDM_STATIC_opt.jl:131-137) — the lattice the build's poll candidates are generated on."""
+    D = np.loadtxt(os.path.join(os.path.dirname(__file__), "golden", "quadrotor_run_src.csv"),
+                   delimiter=",", comments="#")
+    assert D.shape == (120, 3)
+    tan = math.tan(100 / 180 * math.pi / 2)
+    assert np.array_equal(D[:, :2], np.round(D[:, :2]))
+    R = D[:, 2] * tan
+    assert np.abs(R - np.round(R)).max() < 1e-9
+    assert (np.round(R) >= 1).all()
