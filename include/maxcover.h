@@ -249,7 +249,7 @@ int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* b
 /* Armed device polls: the host turnaround between dependent polls of a MADS loop (the next poll
  * is known only after the previous one's result) taken off the device's critical path. The
  * chain of mac_poll_best_dev_f64 is enqueued ahead of time behind a stream wait on the context's
- * doorbell (signal memory the command processor watches), so its launches are already queued
+ * doorbell (a coherent host word the stream waits on), so its launches are already queued
  * when the host decides; mac_poll_fire rings the doorbell and the chain starts without a launch.
  * Its inputs (d_cands, d_prev, ...) may be written until the fire (device writes on other
  * streams must have completed). Rules: tickets are fired in arming order (a fire releases every

@@ -66,17 +66,17 @@ __device__ __forceinline__ int shared_route(const int* __restrict__ dcount, int 
     const int nA = dcount[kDcBits], nB = dcount[kDcOther];
     if (!bits_on || nA + nB <= (bits_on == 2 ? 0 : kBitsMinDisks)) return 0;
     if (!counts) return 1;
-    // (positions are staged as 16-bit words: K <= 65535)
-    return nB == 0 && dcount[kDcOrBad] == 0 && K <= 65535 ? 2 : 0;
+    (void)K;
+    return nB == 0 && dcount[kDcOrBad] == 0 ? 2 : 0;
 }
 
-// One wave's 64 16-bit words global -> LDS with no register (global_load_lds_ushort): lane l
-// reads g_lane (its own address, the low half of an int32 on little-endian) into l_wave + 2 l;
-// l_wave is wave-uniform. Drained by the next __syncthreads (hipcc waits vmcnt(0) there).
-__device__ __forceinline__ void glds_u16(const void* g_lane, void* l_wave)
+// One wave's 64 32-bit words global -> LDS with no register (global_load_lds_dword): lane l
+// reads g_lane (its own address) into l_wave + 4 l; l_wave is wave-uniform. Drained by the next
+// __syncthreads (hipcc waits vmcnt(0) there).
+__device__ __forceinline__ void glds_u32(const void* g_lane, void* l_wave)
 {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g_lane,
-                                     (__attribute__((address_space(3))) void*)l_wave, 2, 0, 0);
+                                     (__attribute__((address_space(3))) void*)l_wave, 4, 0, 0);
 }
 
 // Row r's tiles of region R (at most 64 x 64 tiles) that lie in some lower box and in no upper
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
     __shared__ __attribute__((aligned(16))) float4 ent[kOrE / 2];   // {U0, U1, V0, V1} per entry pair
     __shared__ f32x2 entq[kOrE / 2];                                 // {Q0, Q1}
     __shared__ uint2 tab[kOrTab];
-    __shared__ uint16_t um16[kOrKC];   // the current disk's position of every candidate of the chunk
+    __shared__ int um32[kOrKC];   // the current disk's position of every candidate of the chunk
     __shared__ int s_nrel, s_total, s_job;
 
     ts_begin(ts);
@@ -390,7 +390,7 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
                 for (int c = 0; c < kOrPT; ++c) {
                     const int kw = kc0 + c * kOrThreads + wid * kWave;   // the wave's first candidate
                     if (kw < K)
-                        glds_u16(a.umap + row + min(kw + lane, K - 1), um16 + c * kOrThreads + wid * kWave);
+                        glds_u32(a.umap + row + min(kw + lane, K - 1), um32 + c * kOrThreads + wid * kWave);
                 }
                 // the entries relative to region d's centre, as the walk stages them; entries
                 // outside box d, past the list or non-finite are inert (Q = +inf: d' = -inf)
@@ -498,7 +498,7 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
 #pragma unroll
                     for (int c = 0; c < kOrPT; ++c) {
                         const int k = kc0 + tid + c * kOrThreads;
-                        const int u = k < K ? (int)um16[c * kOrThreads + tid] : -1;
+                        const int u = k < K ? um32[c * kOrThreads + tid] : -1;
                         if (u >= u0 && u < u1) {
                             const uint2 t2 = tab[u - u0];
                             const uint64_t t = (uint64_t)t2.x | ((uint64_t)t2.y << 32);

@@ -166,7 +166,7 @@ struct mac_ctx {
     uint64_t mirror_used[kMirrorSlots] = {};
     uint64_t mirror_seq = 0, mirror_clock = 0;
     hipStream_t dev_stream = nullptr;   // ordered stream for *_dev calls passed stream = NULL
-    // armed polls (mac_poll_arm_dev_f64): the doorbell the streams wait on (signal memory), the
+    // armed polls (mac_poll_arm_dev_f64): the doorbell the streams wait on (coherent host memory), the
     // last ticket armed and the last fired (guarded by mu)
     uint64_t* doorbell = nullptr;
     uint64_t armed = 0, fired = 0;
@@ -1204,7 +1204,7 @@ void mac_ctx_destroy(mac_ctx* ctx)
         ctx->fired = ctx->armed;
     }
     (void)hipDeviceSynchronize();
-    if (ctx->doorbell) (void)hipFree(ctx->doorbell);
+    if (ctx->doorbell) (void)hipHostFree(ctx->doorbell);
     ctx->h_mirror.release();
     for (Lane* l : ctx->lanes_all) {
         l->h_stage.release();
@@ -2364,8 +2364,10 @@ int32_t mac_poll_arm_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three_
             int ok = 0;
             HCK(hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, ctx->device));
             if (!ok) return fail(MAC_E_HIP, "the device cannot wait on stream values");
+            // coherent host memory: the host rings it with a plain atomic store, the stream's
+            // wait polls it (a signal-memory doorbell would need the HSA signal API to wake it)
             void* p = nullptr;
-            HCK(hipExtMallocWithFlags(&p, 64, hipMallocSignalMemory));
+            HCK(hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped));
             ctx->doorbell = (uint64_t*)p;
             __atomic_store_n(ctx->doorbell, (uint64_t)0, __ATOMIC_RELEASE);
             ctx->armed = ctx->fired = 0;

@@ -31,6 +31,9 @@ for s in $STEPS; do
     case $s in
     tests)
         run pytest_gpu 600 python -u -m pytest tests -m gpu -x -v -rfE -p no:cacheprovider --timeout 120 --timeout-method thread ; rc=$? ;;
+    testsall)   # every GPU test, no stop at the first failure
+        run pytest_gpu_all 900 python -u -m pytest tests -m gpu -v -rfE -p no:cacheprovider --timeout 120 --timeout-method thread ; rc=$?
+        [ $rc -eq 1 ] && rc=0 ;;
     smoke)
         run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ; rc=$? ;;
     benchq)
