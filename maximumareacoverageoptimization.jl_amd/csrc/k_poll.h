@@ -130,7 +130,7 @@ __device__ __forceinline__ void coverage_poll_body(
     const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
     int* __restrict__ jobctr, int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
     double* __restrict__ spart, int n_shared, int counts, int bits_on, int* __restrict__ dc_out,
-    const int* __restrict__ qual, const double2* __restrict__ cost, double ratio, const FoldArgs& fa)
+    const int* __restrict__ qual, const double2* __restrict__ cost, double ratio)
 {
     static_assert(kPollSlots == 2 * kPollPairs, "the hot loop pairs candidate slots");
 #ifdef MAC_DIAG
@@ -199,10 +199,6 @@ __device__ __forceinline__ void coverage_poll_body(
         }
     };
     if (bx >= nwalk) {  // then: the shared entries
-        // the deferred penalty chains (k_prep.h fold_chains), whatever walk runs: the last
-        // shared workgroups, one thread per candidate, beside the walks
-        fold_chains(fa, (n_shared - 1 - (bx - nwalk)) * kPollThreads + (int)threadIdx.x,
-                    n_shared * kPollThreads);
         if (mv != kModePoll) return;
         if (bx == nwalk && cost && dc_out) {
             // launch hint for the next poll: the walk AUTO would choose now that the neighbour
@@ -523,12 +519,12 @@ __global__ __launch_bounds__(kPollThreads) __attribute__((amdgpu_waves_per_eu(3)
     const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
     int* __restrict__ jobctr, int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
     double* __restrict__ spart, int n_shared, int counts, int bits_on, int* __restrict__ dc_out,
-    const int* __restrict__ qual, const double2* __restrict__ cost, double ratio, FoldArgs fa)
+    const int* __restrict__ qual, const double2* __restrict__ cost, double ratio)
 {
     ts_begin(ts);
     coverage_poll_body(xy, w, off, g, urec, umap, ucount, region, nbrT, nboxT, lane4, lanexp, rows,
                        ncount, dlist, dcount, jobctr, N, K, mode, partial, spart, n_shared, counts,
-                       bits_on, dc_out, qual, cost, ratio, fa);
+                       bits_on, dc_out, qual, cost, ratio);
     ts_end(ts);
 }
 

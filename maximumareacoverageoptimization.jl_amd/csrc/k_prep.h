@@ -164,18 +164,12 @@ static_assert(kPrepC % 4 == 0 && 32 % kPrepC == 0 && kPrepC <= 64,
               "MAC_PREP_C must divide 32 and be a multiple of 4");
 __host__ __device__ inline int keys_ld(int K) { return (K + 31) & ~31; }
 
-// vp word of a candidate whose penalty chain is folded later (prep_args.defer): a NaN payload no
-// arithmetic produces (a real vp is acc * penalty: a number, +-inf or the default quiet NaN)
-constexpr uint64_t kVpPending = 0x7FF4DEADBEEF0001ull;
-
 struct PrepArgs {
     CandSrc src;
     int N, K;
     PenArgs pa;
     double penalty;
     double* vp;                // per-candidate penalty (null: no objective)
-    int defer;                 // 1: only cons3 here (vp = +inf or kVpPending), the chains folded by
-                               // the poll kernel's shared workgroups beside the walks (fold_chains)
     int pair;                  // generated complete polls (K = 2n, n % 4 == 0): workgroup cw takes
                                // x + B[:, k] and x - B[:, k] for k in [4cw, 4cw + 4) (one draw of
                                // each B entry for both: prep_cand)
@@ -269,6 +263,8 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
 {
     __shared__ double term[kPrepC][kPrepU + 1];   // [candidate][UAV] (+1: lanes on distinct banks)
     __shared__ int wbad[kPrepU / kWave][kPrepC];  // per wave: a term of the candidate is negative
+    __shared__ int wexact[kPrepU / kWave][kPrepC];   // ... every term is on the exact grid (below)
+    __shared__ double wsum[kPrepU / kWave][kPrepC];  // ... the wave's terms summed (exact then)
     const int N = a.N, K = a.K;
     const int u = threadIdx.x, lane = u & (kWave - 1), wid = u / kWave;
     const int k0 = cw * kPrepC;
@@ -281,6 +277,14 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
     MAC_PREP_STAMP(0);
     double acc = 0.0;   // the chain (lane c of wave 0: candidate k0 + c)
     bool bad = false;   // ... and whether a term of it is negative (cons3)
+    bool on_grid = true;   // ... and whether every term so far was on the exact grid
+    // The exact grid: terms t = m * 2^-10 (m a non-negative integer) with t <= 2^43 / N. Every
+    // partial sum of such terms is a multiple of 2^-10 below 2^43, so exactly representable: the
+    // sequential chain of src/TDM_STATIC_opt.jl:88-92 then equals the exact sum, whatever order it
+    // is added in — a tree over the workgroup instead of 512 dependent adds. (MADS polls on the
+    // reference's granularity-1 mesh with an integral r_max give integer terms; any other term
+    // sends its candidate down the sequential chain, from that block of UAVs on.)
+    const double grid_lim = 8796093022208.0 / (double)N;   // 2^43 / N
     for (int ib = 0; ib < N; ib += kPrepU) {
         const int nb = min(kPrepU, N - ib);
         const int i = ib + u;
@@ -335,9 +339,19 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
                     const double sq = ddx * ddx + ddy * ddy + ddz * ddz;
                     if (sq > T3) t = -1.0;
                 }
-                if (!a.defer) term[c][u] = t;
+                term[c][u] = t;
                 const uint64_t neg = __ballot(iv && t < 0.0);
-                if (lane == 0) wbad[wid][c] = neg != 0;
+                const double ts = t * 1024.0;
+                const uint64_t off_grid =
+                    __ballot(iv && !(t >= 0.0 && t <= grid_lim && ts == __builtin_rint(ts)));
+                double sw = iv ? t : 0.0;   // the wave's sum (used only when exact)
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) sw += __shfl_xor(sw, o, kWave);
+                if (lane == 0) {
+                    wbad[wid][c] = neg != 0;
+                    wexact[wid][c] = off_grid == 0;
+                    wsum[wid][c] = sw;
+                }
             }
             MAC_PREP_STAMP(1 + 3 * (ib / kPrepU));
         }
@@ -396,69 +410,39 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
         MAC_PREP_STAMP(2 + 3 * (ib / kPrepU));
         if (obj) {
             // the chains, after every wave's other work (the adds are the critical path: the
-            // folding wave then has its SIMD to itself), sequential in UAV order
+            // folding wave then has its SIMD to itself), sequential in UAV order — or, for a
+            // candidate whose terms are all on the exact grid, the waves' sums (exact)
             lds_barrier();
             if (u < kPrepC) {
+                bool ex = on_grid;
+                double sb = 0.0;
 #pragma unroll
-                for (int w = 0; w < kPrepU / kWave; ++w) bad |= wbad[w][u] != 0;
-            }
-            if (u < kPrepC && !a.defer) {
-                int q = 0;
-                for (; q + 16 <= nb; q += 16) {
-                    double t[16];
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) t[j] = term[u][q + j];
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) acc += t[j];
+                for (int w = 0; w < kPrepU / kWave; ++w) {
+                    bad |= wbad[w][u] != 0;
+                    ex = ex && wexact[w][u] != 0;
+                    sb += wsum[w][u];
                 }
-                for (; q < nb; ++q) acc += term[u][q];
+                on_grid = ex;
+                if (ex) {
+                    acc += sb;
+                } else {
+                    int q = 0;
+                    for (; q + 16 <= nb; q += 16) {
+                        double t[16];
+#pragma unroll
+                        for (int j = 0; j < 16; ++j) t[j] = term[u][q + j];
+#pragma unroll
+                        for (int j = 0; j < 16; ++j) acc += t[j];
+                    }
+                    for (; q < nb; ++q) acc += term[u][q];
+                }
             }
         }
         MAC_PREP_STAMP(3 + 3 * (ib / kPrepU));
         if (obj && ib + kPrepU < N) lds_barrier();   // the fold has read the terms
     }
     if (obj && u < kPrepC && cand(u) < K)
-        a.vp[cand(u)] = bad ? __builtin_inf()
-                     : a.defer ? __builtin_bit_cast(double, kVpPending) : acc * a.penalty;
-}
-
-// The deferred penalty chains (prep_args.defer): the candidates whose vp is kVpPending get
-// vp = penalty * (((0 + t_0) + t_1) + ... + t_{N-1}), t_i = |R_i - rmax_i| — the prep's fold
-// (and src/TDM_STATIC_opt.jl:88-92) term for term, one thread per candidate, 16 loads in flight
-// per batch. Run by the poll kernel's shared-entry workgroups (idle while the walks run at every
-// poll that is not crowded) beside the walks, so the 512 dependent adds leave the chain's first
-// launch. No barriers: any thread may call it with its own candidates (first, first + stride, ...).
-struct FoldArgs {
-    CandSrc src;
-    int N, K;
-    const double* rmax;
-    double penalty;
-    double* vp;                // null: nothing deferred
-};
-
-__device__ __forceinline__ void fold_chains(const FoldArgs& f, int first, int stride)
-{
-    CandSrc src = f.src;
-    if (!f.vp || !src.resolve()) return;   // (a stopped pipelined MADS loop: no result)
-    const int N = f.N;
-    for (int k = first; k < f.K; k += stride) {
-        if (__builtin_bit_cast(uint64_t, f.vp[k]) != kVpPending) continue;
-        double acc = 0.0;
-        for (int i0 = 0; i0 < N; i0 += 16) {
-            double t[16];
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const int i = min(i0 + j, N - 1);
-                const double R2 = src.get(k, 2 * N + i, N);
-                t[j] = f.rmax ? __builtin_fabs(R2 - f.rmax[i]) : 0.0;
-            }
-            const int nj = min(16, N - i0);
-#pragma unroll
-            for (int j = 0; j < 16; ++j)
-                if (j < nj) acc += t[j];
-        }
-        f.vp[k] = acc * f.penalty;
-    }
+        a.vp[cand(u)] = bad ? __builtin_inf() : acc * a.penalty;
 }
 
 __global__ __launch_bounds__(kPrepU) __attribute__((amdgpu_waves_per_eu(4))) void prep_kernel(uint64_t* ts, PrepArgs a)

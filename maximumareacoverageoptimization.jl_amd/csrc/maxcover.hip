@@ -558,9 +558,6 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         pr.pa = pa;
         pr.penalty = penalty;
         pr.vp = d_vp;
-        // matrix polls: the poll kernel folds the chains (k_prep.h fold_chains) from the matrix's
-        // R rows; generated polls keep the fold here (a term there would be regenerated)
-        pr.defer = d_vp && poll_possible && src.cands ? 1 : 0;
         pr.nchain = nchain;
         pr.pair = pair ? 1 : 0;
         pr.g = ctx->grid;
@@ -765,8 +762,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                                L->mode.as<int>() + 2, N, K,
                                d_mode, L->partial.as<double>(), L->spart.as<double>(), n_shared, counts,
                                bits_on, L->d_dc, L->qual.as<int>(),
-                               walk_forced == 0 ? L->cost.as<double2>() : nullptr, kPollCostRatio,
-                               FoldArgs{src, N, K, d_rmax, penalty, d_vp});
+                               walk_forced == 0 ? L->cost.as<double2>() : nullptr, kPollCostRatio);
             HCK(hipGetLastError());
             // the shared entries of crowded polls: the union pass (equal weights, k_or.h) or
             // bit-words per distinct position (k_bits.h); both return at once when few disks have
@@ -2102,9 +2098,11 @@ static int32_t closure_eval(mac_ctx* ctx, const double* circles, int64_t three_n
     Lane* L = lg.lane;
     hipStream_t s = L->stream;
     const size_t in_bytes = sizeof(double) * (size_t)three_n;
-    L->h_io.reserve(std::max<size_t>(in_bytes, 64));
-    std::memcpy(L->h_io.p, circles, in_bytes);
-    L->cands.reserve(in_bytes);
+    if (N > kClosureArgN[2]) {   // (smaller candidates travel as the launch's arguments)
+        L->h_io.reserve(std::max<size_t>(in_bytes, 64));
+        std::memcpy(L->h_io.p, circles, in_bytes);
+        L->cands.reserve(in_bytes);
+    }
     L->area.reserve(sizeof(double));
     L->cpart.reserve(sizeof(unsigned long long) * (size_t)N);
     // zero once; the last block of each launch resets them
@@ -2118,7 +2116,8 @@ static int32_t closure_eval(mac_ctx* ctx, const double* circles, int64_t three_n
         L->d_cl = (uint64_t*)dp;
     }
     const uint64_t seq = ++L->cl_seq;
-    HCK(hipMemcpyAsync(L->cands.p, L->h_io.p, in_bytes, hipMemcpyHostToDevice, s));
+    const bool by_args = N <= kClosureArgN[2];
+    if (!by_args) HCK(hipMemcpyAsync(L->cands.p, L->h_io.p, in_bytes, hipMemcpyHostToDevice, s));
     int64_t ts_a = -1;
     uint64_t* ts = nullptr;
     if (ctx->profile) {
@@ -2131,9 +2130,26 @@ static int32_t closure_eval(mac_ctx* ctx, const double* circles, int64_t three_n
     }
     const ClosureOut co{L->cpart.as<unsigned long long>(), L->ctot.as<unsigned long long>(),
                         L->carrive.as<unsigned>(), L->area.as<double>(), L->d_cl, seq};
-    hipLaunchKernelGGL(closure_kernel, dim3((unsigned)N), dim3(kBlock), (uint32_t)closure_lds_bytes(N), s,
-                       ts, L->cands.as<double>(), N, ctx->grid, ctx->xys.as<double2>(),
-                       ctx->ws.as<double>(), ctx->off.as<int32_t>(), ctx->w_uniform ? 1 : 0, ctx->w0, co);
+    const dim3 grid((unsigned)N), block(kBlock);
+    const uint32_t lds = (uint32_t)closure_lds_bytes(N);
+    const int cnt = ctx->w_uniform ? 1 : 0;
+    // the candidate as the launch's arguments: the smallest block that holds it (the rest zero)
+    auto launch_args = [&](auto tag) {
+        using A = decltype(tag);
+        A c;
+        std::memcpy(c.v, circles, in_bytes);
+        std::memset(c.v + three_n, 0, sizeof(c.v) - in_bytes);
+        hipLaunchKernelGGL(closure_kernel<A>, grid, block, lds, s, ts, c, N, ctx->grid,
+                           ctx->xys.as<double2>(), ctx->ws.as<double>(), ctx->off.as<int32_t>(), cnt,
+                           ctx->w0, co);
+    };
+    if (N <= kClosureArgN[0]) launch_args(ClosureArgs<3 * kClosureArgN[0]>{});
+    else if (N <= kClosureArgN[1]) launch_args(ClosureArgs<3 * kClosureArgN[1]>{});
+    else if (by_args) launch_args(ClosureArgs<3 * kClosureArgN[2]>{});
+    else
+        hipLaunchKernelGGL(closure_kernel<ClosureBuf>, grid, block, lds, s, ts, ClosureBuf{L->cands.as<double>()},
+                           N, ctx->grid, ctx->xys.as<double2>(), ctx->ws.as<double>(),
+                           ctx->off.as<int32_t>(), cnt, ctx->w0, co);
     HCK(hipGetLastError());
     if (ts) {
         std::lock_guard<std::mutex> lk(ctx->mu);

@@ -508,6 +508,49 @@ def test_many_uav_full_poll_auto(ctx, pkg, orc, N):
     assert bi == k and bo == want[k]
 
 
+def test_penalty_chain_exact_grid_and_sequential(ctx, pkg, orc):
+    """The prep launch folds a candidate's penalty chain (src/TDM_STATIC_opt.jl:88-92) as a tree
+    when every term |R_i - r_max_i| is a multiple of 2^-10 below 2^43 / N (exact in any order),
+    else sequentially from the first off-grid block of 512 UAVs on (k_prep.h). N = 1100 (three
+    blocks): integer terms, 2^-10 fractions, an off-grid term in block 0, 1 or 2 only, terms
+    past 2^43 / N, and non-finite R. Every objective == -area + 1e5 x the C oracle's sequential
+    chain, bit for bit."""
+    wl = pkg.workloads
+    rng = wl.SplitMix64(1100)
+    G = 256
+    x, y, w = wl.grid_points(G)
+    ctx.set_points(x, y, w)
+    N = 1100
+    base = wl.uniform_disks(N, G, rng)
+    rmax = np.floor(rng.uniform(N) * 40.0) + 1.0
+    rows = []
+    for case in range(12):
+        c = base.copy()
+        R = np.floor(rng.uniform(N) * 40.0) + 1.0
+        if case in (1, 2):
+            R = R + np.floor(rng.uniform(N) * 1024.0) / 1024.0
+        elif case in (3, 4, 5):
+            blk = case - 3
+            R[blk * 512 + 7] += 0.1
+        elif case == 6:
+            R[600] = 2.0 ** 40
+        elif case == 7:
+            R[1099] = 2.0 ** 43 / N + 1.0
+        elif case == 8:
+            R[10] = np.nan
+        elif case == 9:
+            R[520] = np.inf
+        elif case == 10:
+            R = R * 1.5 + 0.25 / 3.0
+        c[2 * N:] = R
+        rows.append(c)
+    C = np.array(rows)
+    area = ctx.area_batch(C)
+    got = ctx.objective_batch(C, rmax)
+    want = -area + orc.violation_batch(C, rmax) * 1e5
+    assert np.array_equal(got, want, equal_nan=True), np.nonzero(got != want)
+
+
 @pytest.mark.parametrize("algo", ["auto", "poll"])
 def test_config4_clustered_full_poll(ctx, pkg, orc, algo):
     """SURVEY 8(d)'s "clustered" variant at full size: 512 R=36 disks within sqrt(N)*40 m of the
