@@ -4,9 +4,7 @@
 // src/TDM_STATIC_opt.jl:125; AreaMaxObjective :82-100 -> calculateArea
 // src/AreaCoverageCalculation.jl:63-78). For that path a batch chain (index, walk, finalize) is
 // all latency, so mac_area_f64 runs one kernel instead: workgroup i = disk i of the candidate.
-//   1. every workgroup stages the candidate's N disks (x, y, r) in LDS (one coalesced read), from
-//      the kernel arguments when 3N doubles fit the largest argument block (N <= 512: the
-//      launch carries the candidate, no copy is enqueued before it), else from the lane's copy;
+//   1. every workgroup stages the candidate's N disks (x, y, r) in LDS (one coalesced read);
 //   2. disk i's lower-index neighbours: the disks j < i that may share a covered entry with it
 //      (disks_may_overlap, conservative), their exact thresholds T(r_j) in LDS;
 //   3. the entries of disk i's tile span (CSR rows of the tile-sorted list, their offsets loaded
@@ -48,21 +46,7 @@ struct ClosureOut {
     uint64_t seq;
 };
 
-// Where the candidate comes from: a device buffer (the lane's copy), or the launch's own kernel
-// arguments (up to kCap doubles: no copy before the launch, the argument block is the copy)
-struct ClosureBuf {
-    const double* p;
-    __device__ __forceinline__ double get(int j) const { return p[j]; }
-};
-template <int kCap>
-struct ClosureArgs {
-    double v[kCap];
-    __device__ __forceinline__ double get(int j) const { return v[j]; }
-};
-constexpr int kClosureArgN[3] = {32, 128, 512};   // N of the argument-block sizes (3N doubles)
-
-template <class Src>
-__global__ __launch_bounds__(kBlock) void closure_kernel(uint64_t* ts, const Src cand,
+__global__ __launch_bounds__(kBlock) void closure_kernel(uint64_t* ts, const double* __restrict__ cand,
                                                          int N, Grid g, const double2* __restrict__ xy,
                                                          const double* __restrict__ w,
                                                          const int32_t* __restrict__ off, int counts,
@@ -81,9 +65,9 @@ __global__ __launch_bounds__(kBlock) void closure_kernel(uint64_t* ts, const Src
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
     const int i = blockIdx.x;
     for (int j = tid; j < N; j += kBlock) {
-        sx[j] = cand.get(j);
-        sy[j] = cand.get(N + j);
-        sr[j] = cand.get(2 * N + j);
+        sx[j] = cand[j];
+        sy[j] = cand[N + j];
+        sr[j] = cand[2 * N + j];
     }
     if (tid == 0) ncnt = 0;
     __syncthreads();

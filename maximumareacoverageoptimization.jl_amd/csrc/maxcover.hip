@@ -2098,11 +2098,9 @@ static int32_t closure_eval(mac_ctx* ctx, const double* circles, int64_t three_n
     Lane* L = lg.lane;
     hipStream_t s = L->stream;
     const size_t in_bytes = sizeof(double) * (size_t)three_n;
-    if (N > kClosureArgN[2]) {   // (smaller candidates travel as the launch's arguments)
-        L->h_io.reserve(std::max<size_t>(in_bytes, 64));
-        std::memcpy(L->h_io.p, circles, in_bytes);
-        L->cands.reserve(in_bytes);
-    }
+    L->h_io.reserve(std::max<size_t>(in_bytes, 64));
+    std::memcpy(L->h_io.p, circles, in_bytes);
+    L->cands.reserve(in_bytes);
     L->area.reserve(sizeof(double));
     L->cpart.reserve(sizeof(unsigned long long) * (size_t)N);
     // zero once; the last block of each launch resets them
@@ -2116,8 +2114,7 @@ static int32_t closure_eval(mac_ctx* ctx, const double* circles, int64_t three_n
         L->d_cl = (uint64_t*)dp;
     }
     const uint64_t seq = ++L->cl_seq;
-    const bool by_args = N <= kClosureArgN[2];
-    if (!by_args) HCK(hipMemcpyAsync(L->cands.p, L->h_io.p, in_bytes, hipMemcpyHostToDevice, s));
+    HCK(hipMemcpyAsync(L->cands.p, L->h_io.p, in_bytes, hipMemcpyHostToDevice, s));
     int64_t ts_a = -1;
     uint64_t* ts = nullptr;
     if (ctx->profile) {
@@ -2130,26 +2127,9 @@ static int32_t closure_eval(mac_ctx* ctx, const double* circles, int64_t three_n
     }
     const ClosureOut co{L->cpart.as<unsigned long long>(), L->ctot.as<unsigned long long>(),
                         L->carrive.as<unsigned>(), L->area.as<double>(), L->d_cl, seq};
-    const dim3 grid((unsigned)N), block(kBlock);
-    const uint32_t lds = (uint32_t)closure_lds_bytes(N);
-    const int cnt = ctx->w_uniform ? 1 : 0;
-    // the candidate as the launch's arguments: the smallest block that holds it (the rest zero)
-    auto launch_args = [&](auto tag) {
-        using A = decltype(tag);
-        A c;
-        std::memcpy(c.v, circles, in_bytes);
-        std::memset(c.v + three_n, 0, sizeof(c.v) - in_bytes);
-        hipLaunchKernelGGL(closure_kernel<A>, grid, block, lds, s, ts, c, N, ctx->grid,
-                           ctx->xys.as<double2>(), ctx->ws.as<double>(), ctx->off.as<int32_t>(), cnt,
-                           ctx->w0, co);
-    };
-    if (N <= kClosureArgN[0]) launch_args(ClosureArgs<3 * kClosureArgN[0]>{});
-    else if (N <= kClosureArgN[1]) launch_args(ClosureArgs<3 * kClosureArgN[1]>{});
-    else if (by_args) launch_args(ClosureArgs<3 * kClosureArgN[2]>{});
-    else
-        hipLaunchKernelGGL(closure_kernel<ClosureBuf>, grid, block, lds, s, ts, ClosureBuf{L->cands.as<double>()},
-                           N, ctx->grid, ctx->xys.as<double2>(), ctx->ws.as<double>(),
-                           ctx->off.as<int32_t>(), cnt, ctx->w0, co);
+    hipLaunchKernelGGL(closure_kernel, dim3((unsigned)N), dim3(kBlock), (uint32_t)closure_lds_bytes(N), s,
+                       ts, L->cands.as<double>(), N, ctx->grid, ctx->xys.as<double2>(),
+                       ctx->ws.as<double>(), ctx->off.as<int32_t>(), ctx->w_uniform ? 1 : 0, ctx->w0, co);
     HCK(hipGetLastError());
     if (ts) {
         std::lock_guard<std::mutex> lk(ctx->mu);
