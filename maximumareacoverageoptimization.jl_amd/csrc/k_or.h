@@ -218,7 +218,6 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
 {
     __shared__ int sid[kPollNbr + 1], sU[kPollNbr + 1];
     __shared__ int4 sbox[kPollNbr + 1], subox[kPollNbr];
-    __shared__ int run_s[kOrRuns], run_pre[kOrRuns + 1], run_row[kOrRuns];
     __shared__ int wrun[kWave];
     __shared__ double2 s64[kOrE];
     __shared__ int2 stile[kOrE];
@@ -227,9 +226,13 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
     __shared__ int rel[kPollNbr + 1];
     __shared__ __attribute__((aligned(16))) float4 ent[kOrE / 2];   // {U0, U1, V0, V1} per entry pair
     __shared__ f32x2 entq[kOrE / 2];                                 // {Q0, Q1}
-    __shared__ uint2 tab[kOrTab];
-    __shared__ int um32[kOrKC];   // the current disk's position of every candidate of the chunk
-    __shared__ int s_nrel, s_total, s_job;
+    __shared__ __attribute__((aligned(16))) uint2 tab[kOrTab];   // the tables (the set-up's runs alias them)
+    static_assert((3 * kOrRuns + 1) * sizeof(int) <= sizeof(uint2) * kOrTab, "runs fit the tables");
+    int* const run_s = reinterpret_cast<int*>(tab);
+    int* const run_pre = run_s + kOrRuns;
+    int* const run_row = run_pre + kOrRuns + 1;
+    __shared__ int um32[2][kOrKC];   // a disk's position of every candidate of the chunk (two buffers)
+    __shared__ int s_nrel, s_total, s_next[2];
 
     ts_begin(ts);
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
@@ -251,7 +254,18 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
     const uint64_t dt0 = dt;
 #endif
     const Grid g = a.g;
-    for (int job = blockIdx.x; job < njobs;) {
+    // the candidates' positions of slot m's disk (chunk kc0) straight into LDS buffer bb (no
+    // registers); the barrier after the next staging drains them
+    auto issue_pos = [&](int m, int bb, int kc0) {
+        const int64_t row = (int64_t)sid[m] * K;
+#pragma unroll
+        for (int c = 0; c < kOrPT; ++c) {
+            const int kw = kc0 + c * kOrThreads + wid * kWave;   // the wave's first candidate
+            if (kw < K) glds_u32(a.umap + row + min(kw + lane, K - 1), &um32[bb][c * kOrThreads + wid * kWave]);
+        }
+    };
+    int it = 0;
+    for (int job = blockIdx.x; job < njobs; ++it) {
         int q = job, bk = 0;
 #pragma unroll
         for (int b = 0; b < kOrBuckets - 1; ++b)
@@ -259,6 +273,9 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
                 q -= nb[b];
                 bk = b + 1;
             }
+        // the next job's counter add, in flight during this job (two slots: a wave still reading
+        // this job's slot never sees the next job's write)
+        if (tid == 0) s_next[it & 1] = (int)gridDim.x + atomicAdd(a.dcount + kDcBitsJobs, 1);
         const int2 jb = a.jobs[(int64_t)bk * a.cap + q];
         const int i = jb.x, blk = jb.y;
         // disk i's lists (slot 0: disk i itself, slots 1..nc: its lower neighbours)
@@ -379,19 +396,12 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
                 Y[c] = 0;
                 zc[c] = 0;
             }
+            if (nrel > 0) issue_pos(rel[0], 0, kc0);
             for (int r = 0; r < nrel; ++r) {
-                const int m = rel[r];
+                const int m = rel[r], bb = r & 1;
                 const int d = sid[m], U = sU[m];
                 const int64_t row = (int64_t)d * K;
                 const uint64_t lv = live[m], lm = lmask[m];
-                // the candidates' positions of disk d straight into LDS (no registers), in flight
-                // during the tables; the barrier after the tables drains them
-#pragma unroll
-                for (int c = 0; c < kOrPT; ++c) {
-                    const int kw = kc0 + c * kOrThreads + wid * kWave;   // the wave's first candidate
-                    if (kw < K)
-                        glds_u32(a.umap + row + min(kw + lane, K - 1), um32 + c * kOrThreads + wid * kWave);
-                }
                 // the entries relative to region d's centre, as the walk stages them; entries
                 // outside box d, past the list or non-finite are inert (Q = +inf: d' = -inf)
                 if (tid < kOrE) {
@@ -407,7 +417,9 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
                     reinterpret_cast<float*>(&entq[tid >> 1])[tid & 1] =
                         f ? __builtin_fmaf(fu, fu, fv * fv) : __builtin_inff();
                 }
-                __syncthreads();
+                __syncthreads();   // (this disk's positions have landed too)
+                // the next disk's positions into the other buffer, in flight during this disk
+                if (r + 1 < nrel) issue_pos(rel[r + 1], bb ^ 1, kc0);
                 MAC_OR_T(1);
                 MAC_OR_N(10, U);
                 MAC_OR_N(11, __popcll(lv));
@@ -498,7 +510,7 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
 #pragma unroll
                     for (int c = 0; c < kOrPT; ++c) {
                         const int k = kc0 + tid + c * kOrThreads;
-                        const int u = k < K ? um32[c * kOrThreads + tid] : -1;
+                        const int u = k < K ? um32[bb][c * kOrThreads + tid] : -1;
                         if (u >= u0 && u < u1) {
                             const uint2 t2 = tab[u - u0];
                             const uint64_t t = (uint64_t)t2.x | ((uint64_t)t2.y << 32);
@@ -517,10 +529,9 @@ __global__ __launch_bounds__(kOrThreads) __attribute__((amdgpu_waves_per_eu(4)))
                 if (k < K && n) atomicAdd(a.spart + (int64_t)i * K + k, (unsigned)n);
             }
         }
-        // the next job
-        if (tid == 0) s_job = (int)gridDim.x + atomicAdd(a.dcount + kDcBitsJobs, 1);
+        // the next job (its counter add went out at the start of this one)
         __syncthreads();
-        job = s_job;
+        job = s_next[it & 1];
         MAC_OR_T(4);
     }
 #ifdef MAC_DIAG

@@ -114,32 +114,35 @@ __device__ __forceinline__ void neighbors_block(int i, int N, const int4& R, con
 // The device-side walk choice, both costs in one unit (poll-walk tests): the poll walk tests
 // every entry of region i against every candidate's disk i (A = sum of cost[i].x = K * |region i|
 // entry visits, broadcast LDS reads); the per-candidate walk visits each candidate's span entries
-// (cost[i].y summed) with scattered global loads and, per candidate, tests disk c against the
-// disks of its poll-level neighbour list (ncount[c]; an overflowed list: every lower-index disk,
-// c of them, k_walk.h) in fp64 — a visit and a pair test each cost about `ratio` poll-walk tests
-// (4: measured) — so B = ratio * (sum of spans + K * sum_c pairs_c). Poll when A <= B, or
-// `forced`. Every block sums in the same fixed order, so every block gets the same choice.
-// Block-uniform result. (Round 2's choice, made before the lists existed, priced every pair,
-// K N(N-1)/2: a crowded config-5 poll had picked the per-candidate walk on visits alone and
-// rebuilt all pairs in every unit, 3.96 ms; tests/test_gpu_parity.py pins both choices.)
+// (cost[i].y summed) with scattered global loads and tests each covered one against the disks of
+// disk i's poll-level neighbour list (ncount[i]; an overflowed list: every lower-index disk, i of
+// them, k_walk.h) in fp64 — a visit and a pair test each cost about `ratio` poll-walk tests
+// (4: measured) — so B = ratio * sum_i spans_i * (1 + list_i). Poll when A <= B, or `forced`.
+// Every block sums in the same fixed order, so every block gets the same choice. Block-uniform
+// result. (Round 2's choice, made before the lists existed, priced every pair, K N(N-1)/2: a
+// crowded config-5 poll had picked the per-candidate walk on visits alone and rebuilt all pairs
+// in every unit, 3.96 ms. Round 3 priced the pairs once per candidate, K * sum_i list_i, not per
+// visited entry: the config-5 regression poll at ell 5 then picked the per-candidate walk, 7.1 ms
+// against 0.69 ms for the poll walk and the union pass (tools/c5_walks.py); tests/test_gpu_parity.py
+// pins both choices.)
 __device__ __forceinline__ int walk_choice(int N, int K, const double2* __restrict__ cost,
                                            const int* __restrict__ ncount, double ratio, int forced)
 {
     __shared__ double red[kWavesPerBlock];
     __shared__ int smode;
     if (forced) return forced;
-    double a = 0.0, b = 0.0, pr = 0.0;
+    // the per-candidate walk visits every span entry of disk j and tests each covered one
+    // against the disk's listed neighbours: span tiles x (1 + list length)
+    double a = 0.0, b = 0.0;
     for (int j = threadIdx.x; j < N; j += kBlock) {
         a += cost[j].x;
-        b += cost[j].y;
         const int nc = ncount[j];
-        pr += (double)(nc <= kPollNbr ? nc : j);
+        b += cost[j].y * (1.0 + (double)(nc <= kPollNbr ? nc : j));
     }
+    (void)K;
     const double A = block_sum_f64(a, red);
     __syncthreads();
-    const double Bv = block_sum_f64(b, red);
-    __syncthreads();
-    const double B = Bv + (double)K * block_sum_f64(pr, red);
+    const double B = block_sum_f64(b, red);
     __syncthreads();
     if (threadIdx.x == 0) smode = A <= ratio * B ? kModePoll : kModeTiled;
     __syncthreads();

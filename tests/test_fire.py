@@ -235,9 +235,10 @@ def test_config5_full_size_mpc_step(ctx, pkg, orc):
     D.close()
 
 
-def _c5_poll293(pkg):
+def _c5_poll293(pkg, ell_at=None):
     """The config-5 poll behind the bit-word kernel's 1.1-ms launch (tests/golden/c5_poll293.npz,
-    tests/golden/make_c5_poll_fixture.py): (x, y, w, candidates K x 3N, prev, r_max, ell)."""
+    tests/golden/make_c5_poll_fixture.py): (x, y, w, candidates K x 3N, prev, r_max, ell); with
+    ell_at, the same stream position's poll at mesh index ell_at."""
     import importlib.util
     import os
     root = os.path.dirname(os.path.abspath(__file__))
@@ -247,6 +248,7 @@ def _c5_poll293(pkg):
     spec.loader.exec_module(mk)
     d = np.load(os.path.join(root, "golden", "c5_poll293.npz"))
     seed, it, ell = (int(v) for v in d["meta"][:3])
+    ell = ell if ell_at is None else ell_at
     cells = d["cells"].astype(np.float64)
     x, y = cells[:, 0] * 5.0 - 2.5, cells[:, 1] * 5.0 - 2.5
     w = np.full(x.size, 25.0)
@@ -306,3 +308,23 @@ def test_c5_poll293_against_oracle(ctx, pkg, orc, shared):
     ok3 = orc.cons3_batch(prev, X, dl, tan50)
     assert np.array_equal(objs3, np.where(ok3, objs, np.inf))
     assert bi3 == (int(np.argmin(objs3)) if np.isfinite(objs3).any() else -1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ell", [5, 4, 3])
+def test_c5_poll293_takes_the_poll_walk(ctx, pkg, ell):
+    """AUTO's walk choice on the crowded config-5 poll (k_poll_shared.h walk_choice): the poll walk
+    at every mesh step. The per-candidate walk tests each visited entry against the disk's whole
+    neighbour list; priced once per candidate (round 3) it was chosen at ell = 5 and took 7.1 ms
+    against 0.69 ms (tools/c5_walks.py). Twice: the second call runs on the lane's hint."""
+    x, y, w, X, prev, rmax, _ = _c5_poll293(pkg, ell_at=ell)
+    ctx.set_points(x, y, w)
+    ctx.set_algo("auto")
+    walks = []
+    for _ in range(2):
+        ctx.profile(True)
+        ctx.profile_read(reset=True)
+        ctx.poll_best(X, rmax, 1e5)
+        walks.append(ctx.profile_read(reset=True)[3])
+        ctx.profile(False)
+    assert walks == ["poll", "poll"], walks

@@ -71,6 +71,8 @@ for s in $STEPS; do
     probeka)  # can a launch carry the 12-KB closure candidate as kernel arguments? (tools/probe)
         [ -x tools/probe/kernarg_probe ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O2 tools/probe/kernarg_probe.hip -o tools/probe/kernarg_probe
         run probeka 60 tools/probe/kernarg_probe ; rc=$? ;;
+    c5walks)  # the config-5 regression poll at ell 5..1 through each walk (per-kernel times)
+        run c5walks 300 python tools/c5_walks.py ; rc=$? ;;
     c5polls)  # per-poll kernel times of the config-5 loop; the slowest polls saved for analysis
         run c5polls 600 python tools/c5_polls.py ; rc=$? ;;
     c5x2)    # rehearsal of the N=2 config-5 path (sharded MADS) on one GPU (gloo; both ranks on device 0)
