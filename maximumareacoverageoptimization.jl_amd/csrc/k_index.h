@@ -86,7 +86,20 @@ struct IndexOut {
     float* lanexp;
     int2* rows;
     const int32_t* off;
+    // the poll's penalties (k_prep.h; null: none): a candidate with vp = +inf failed cons3, is not
+    // evaluated (its objective is +inf whatever it covers) and maps to one inert position
+    const double* vp;
 };
+
+// Key of a candidate that failed cons3: a signalling-NaN pattern, which no fp32 key can hold
+// (keys are small integers or fp32 conversions, and conversions produce quiet NaNs), so the
+// failed candidates share one position; its record covers nothing (T = -1, r = 0) and its lane
+// is inert.
+constexpr uint32_t kDeadKey = 0x7FBADEADu;
+__device__ __forceinline__ bool dead_cand(const double* vp, int k, int K)
+{
+    return vp && k < K && vp[k] == __builtin_inf();
+}
 
 // fp32 key of value v relative to the base b: exact when b + (double)key reproduces v bit for bit
 __device__ __forceinline__ float key_of(double v, double b, bool& ok)
@@ -220,6 +233,12 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
                 qr[j] = fx[(int64_t)2 * N * src.ldk + k];
             }
         }
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int k = j < kIdxPer ? tid + j * kIdxThreads : (tid == 0 ? kIndexMaxK : K);
+            if (dead_cand(o.vp, k, K))
+                qx[j] = qy[j] = qr[j] = __builtin_bit_cast(float, kDeadKey);
+        }
         const bool bad = pbad;   // a key of disk i is inexact (the records' flags)
         for (int q = tid; q < kIndexSlots; q += kIdxThreads) table[q] = -1;
         if (tid == 0) ucnt = 0;
@@ -278,7 +297,9 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
 #pragma unroll
         for (int j = 0; j < P; ++j) {
             const int k = j < kIdxPer ? tid + j * kIdxThreads : (tid == 0 ? kIndexMaxK : K);
-            if (k < K) {
+            if (dead_cand(o.vp, k, K)) {
+                kx[k] = ky[k] = kr[k] = __builtin_bit_cast(float, kDeadKey);
+            } else if (k < K) {
                 kx[k] = key_of(cx[j], bx, ok);
                 ky[k] = key_of(cy[j], by, ok);
                 kr[k] = key_of(cr[j], br, ok);
@@ -393,7 +414,12 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
             DiskRec d;
             if (hashed) {
                 const int k = owner_of[u];
-                d = make_disk(bx + (double)kx[k], by + (double)ky[k], br + (double)kr[k]);
+                if (__builtin_bit_cast(uint32_t, kr[k]) == kDeadKey) {   // the failed candidates
+                    d.cx = d.cy = d.r = 0.0;
+                    d.T = -1.0;
+                } else {
+                    d = make_disk(bx + (double)kx[k], by + (double)ky[k], br + (double)kr[k]);
+                }
                 o.urec[row + u] = d;
             } else {
                 double x, y, r;

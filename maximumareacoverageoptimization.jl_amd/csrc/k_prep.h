@@ -174,6 +174,7 @@ struct PrepArgs {
                                // x + B[:, k] and x - B[:, k] for k in [4cw, 4cw + 4) (one draw of
                                // each B entry for both: prep_cand)
     int nchain;                // workgroups
+    int skip_failed;           // 1: the records leave out cons3 failures (no area is reported for them)
     int4* prec;                // [nchain][N] records (null: no poll walk)
     Grid g;
     uint32_t* keysP;           // packed keys (null: none), one row per disk, pitch ldk
@@ -265,6 +266,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
     __shared__ int wbad[kPrepU / kWave][kPrepC];  // per wave: a term of the candidate is negative
     __shared__ int wexact[kPrepU / kWave][kPrepC];   // ... every term is on the exact grid (below)
     __shared__ double wsum[kPrepU / kWave][kPrepC];  // ... the wave's terms summed (exact then)
+    __shared__ uint32_t wbadm[kPrepU / kWave];       // ... wbad as a mask over the candidates
     const int N = a.N, K = a.K;
     const int u = threadIdx.x, lane = u & (kWave - 1), wid = u / kWave;
     const int k0 = cw * kPrepC;
@@ -285,6 +287,13 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
     // reference's granularity-1 mesh with an integral r_max give integer terms; any other term
     // sends its candidate down the sequential chain, from that block of UAVs on.)
     const double grid_lim = 8796093022208.0 / (double)N;   // 2^43 / N
+    // Candidates that fail cons3 (the extreme barrier, src/TDM_Constraints.jl:54-75) are not
+    // evaluated by the reference's DirectSearch poll, and their objective is +inf whatever they
+    // cover. With one block of UAVs (N <= kPrepU) their failure is known before the records are
+    // written, so the records leave them out (the regions, and with them the walks' work, shrink
+    // to the feasible candidates; the index maps them to an inert position, k_index.h). Uniform.
+    const bool excl = obj && pa.prev && a.prec && a.skip_failed && N <= kPrepU;
+    uint32_t dead = 0u;   // (excl) bit c: candidate c fails cons3 (0 otherwise)
     for (int ib = 0; ib < N; ib += kPrepU) {
         const int nb = min(kPrepU, N - ib);
         const int i = ib + u;
@@ -329,6 +338,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
             const double z1 = pa.prev ? pa.prev[2 * N + ii] / pa.tan_half_fov : 0.0;
             const double rm = pa.rmax ? pa.rmax[ii] : 0.0;
             const double T3 = pen_threshold(pa, ii);
+            uint32_t wdead = 0u;   // this wave's part of the failures
 #pragma unroll
             for (int c = 0; c < kPrepC; ++c) {
                 const double R2 = v[c][2];
@@ -352,8 +362,16 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
                     wexact[wid][c] = off_grid == 0;
                     wsum[wid][c] = sw;
                 }
+                wdead |= (neg != 0 ? 1u : 0u) << c;
             }
+            if (lane == 0) wbadm[wid] = wdead;
             MAC_PREP_STAMP(1 + 3 * (ib / kPrepU));
+        }
+        if (excl) {   // every wave's failures (the fold below needs no further barrier)
+            lds_barrier();
+            dead = 0u;
+#pragma unroll
+            for (int w = 0; w < kPrepU / kWave; ++w) dead |= wbadm[w];
         }
         if (a.prec && iv) {
             double xa = __builtin_inf(), xb = -__builtin_inf(), ya = __builtin_inf(), yb = -__builtin_inf();
@@ -363,7 +381,8 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
             for (int c = 0; c < kPrepC; ++c) {
                 const double x = v[c][0], y = v[c][1], r = v[c][2];
                 // span_of's cases: r <= 0 or NaN, or a non-finite centre, covers nothing
-                if (cand(c) < K && r > 0.0 && __builtin_isfinite(x) && __builtin_isfinite(y)) {
+                if (cand(c) < K && !((dead >> c) & 1u) && r > 0.0 && __builtin_isfinite(x) &&
+                    __builtin_isfinite(y)) {
                     any = true;
                     xa = fmin(xa, x - r);
                     xb = fmax(xb, x + r);
@@ -389,7 +408,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
 #pragma unroll
                         for (int q = 0; q < 3; ++q) {
                             const float f = (float)(v[c][q] - base[q]);
-                            kb |= __builtin_bit_cast(uint64_t, base[q] + (double)f) != __builtin_bit_cast(uint64_t, v[c][q]);
+                            kb |= !((dead >> c) & 1u) && __builtin_bit_cast(uint64_t, base[q] + (double)f) != __builtin_bit_cast(uint64_t, v[c][q]);
                             a.keysT[(int64_t)(q * N + i) * a.ldk + cand(c)] = f;
                         }
                     }
@@ -412,7 +431,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
             // the chains, after every wave's other work (the adds are the critical path: the
             // folding wave then has its SIMD to itself), sequential in UAV order — or, for a
             // candidate whose terms are all on the exact grid, the waves' sums (exact)
-            lds_barrier();
+            if (!excl) lds_barrier();   // (excl: passed above)
             if (u < kPrepC) {
                 bool ex = on_grid;
                 double sb = 0.0;

@@ -559,6 +559,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         pr.penalty = penalty;
         pr.vp = d_vp;
         pr.nchain = nchain;
+        pr.skip_failed = d_area ? 0 : 1;   // (the index maps them to an inert position likewise)
         pr.pair = pair ? 1 : 0;
         pr.g = ctx->grid;
         if (poll_possible) {
@@ -642,7 +643,10 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                               L->region.as<int4>(), L->cost.as<double2>(), L->mode.as<int>() + 1,
                               L->prec.as<int4>(), nchain,
                               L->lane4.as<float4>(), L->lanexp.as<float>(), L->rows.as<int2>(),
-                              ctx->off.as<int32_t>()};
+                              ctx->off.as<int32_t>(),
+                              // cons3 failures are not evaluated (objective +inf) unless the caller
+                              // also wants every candidate's area
+                              d_area ? nullptr : d_vp};
             const unsigned nidx = 8 * ((N + 7) / 8);
             const int dedup = iper ? 1 : 0;
             uint64_t* tsi = ts_c >= 0 ? take_ts(nidx, ts_i, ts_ni) : nullptr;

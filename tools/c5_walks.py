@@ -36,6 +36,22 @@ for ell in (5, 4, 3, 2, 1):
         us = {n: round(ms / c * 1e3, 1) for n, (ms, c) in k.items() if c}
         row[algo] = {"sum_us": round(sum(us.values()), 1), "kernels_us": us,
                      "same_objs": bool(np.array_equal(objs, ref))}
+    # as the MPC loop runs it: cons3 against the step's start (failing candidates not evaluated)
+    ctx.set_algo("auto")
+    dl = np.full(X.shape[1] // 3, 10.0)
+    tan50 = float(np.tan(100 / 180 * np.pi / 2))
+    for _ in range(4):
+        ctx.profile(True)
+        ctx.profile_read(reset=True)
+        bo, bi, objs3 = ctx.poll_best(X, d["rmax"], 1e5, prev=d["prev"], d_lim=dl, tan_half_fov=tan50,
+                                      want_all=True)
+        k = ctx.profile_kernels()
+        ctx.profile_read(reset=True)
+    us = {n: round(ms / c * 1e3, 1) for n, (ms, c) in k.items() if c}
+    row["auto_cons3"] = {"sum_us": round(sum(us.values()), 1), "kernels_us": us,
+                         "feasible": int(np.isfinite(objs3).sum()),
+                         "same_where_feasible": bool(np.array_equal(objs3[np.isfinite(objs3)],
+                                                                    ref[np.isfinite(objs3)]))}
     print(json.dumps(row), flush=True)
 ctx.profile(False)
 ctx.close()
