@@ -444,7 +444,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
                 on_grid = ex;
                 if (ex) {
                     acc += sb;
-                } else {
+                } else if (!bad) {   // (a cons3 failure's vp is +inf: no chain to fold)
                     int q = 0;
                     for (; q + 16 <= nb; q += 16) {
                         double t[16];
