@@ -479,6 +479,26 @@ def test_config4_full_poll(ctx, pkg, orc, algo):
         assert np.array_equal(got_scan, 25.0 * cnt[::384])
 
 
+@pytest.mark.parametrize("disks", ["uniform", "clustered"])
+def test_cons3_failures_not_evaluated(ctx, pkg, orc, disks):
+    """A poll at mesh step 8 (ell = 3): about half of the LTMADS candidates move some UAV more
+    than d_lim and fail cons3. With cons3 the prep leaves the failures out of the regions and the
+    index maps them to one inert position (k_prep.h, k_index.h): the feasible candidates'
+    objectives are still bit-exact (exact lattice counts) and the failures +inf, through every
+    walk; without cons3 (and for area_batch) nothing is left out."""
+    wl = pkg.workloads
+    rng = wl.SplitMix64(3003 if disks == "uniform" else 3004)
+    G, N = 512, 128
+    x, y, w = wl.grid_points(G)
+    ctx.set_points(x, y, w)
+    x0 = (wl.uniform_disks if disks == "uniform" else wl.clustered_disks)(N, G, rng)
+    C = wl.poll_candidates(x0, rng, ell=3)
+    feas = orc.cons3_batch(C[0], C, np.full(N, 10.0), TAN50)
+    assert 0 < int(feas.sum()) < C.shape[0], int(feas.sum())
+    _full_poll_check(ctx, orc, C, np.full(N, 30.0 * TAN50), G, ["auto", "poll", "tiled"],
+                     "ell3-" + disks)
+
+
 @pytest.mark.parametrize("N", [600, 2100])
 def test_many_uav_full_poll_auto(ctx, pkg, orc, N):
     """Polls past config 4's shape (src/TDM_STATIC_opt.jl:123: n = 3N, no cap). N = 600: K = 3601

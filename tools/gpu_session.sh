@@ -38,6 +38,8 @@ for s in $STEPS; do
         run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ; rc=$? ;;
     benchq)
         run benchq 300 python bench.py --no-cpu ; rc=$? ;;
+    benchplain)   # config 4, polls launched one after another (no doorbell)
+        run benchplain 300 python bench.py --no-cpu --step-mode plain ; rc=$? ;;
     bench)
         run bench 400 python bench.py ; rc=$?
         grep '^{' gpurun_out/bench.log > gpurun_out/bench_${TAG}.json ;;
