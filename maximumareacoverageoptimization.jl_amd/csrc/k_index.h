@@ -16,7 +16,7 @@
 // LDS hash table (exact keys, see "Keys" below) and writes per distinct disk u the record
 // urec[i*K + u], plus, for every candidate, the map umap[i*K + k] = u, and the count ucount[i].
 // Disk i's region (the union of its tile spans over the K candidates) and its walk costs
-// (K * |region|, the summed span areas) are reduced here from the prep launch's per-workgroup
+// (U_i * |region|, U_i its distinct positions, and the summed span areas) are reduced here from the prep launch's per-workgroup
 // partials (k_prep.h), while the keys load; its row descriptors are in flight during the hashing.
 // Consumers read disk i of candidate k as urec[i*K + umap[i*K + k]]: the result is bit-identical
 // to per-candidate records (same inputs, same arithmetic), and every candidate is still
@@ -74,7 +74,7 @@ struct IndexOut {
     int* umap;
     int* ucount;
     int4* region;           // disk i's region (written)
-    double2* cost;          // disk i's walk costs {K * |region|, summed span areas} (written)
+    double2* cost;          // disk i's walk costs {U_i * |region|, summed span areas} (written)
     int* dcount;            // the poll walk's counters (k_common.h kDc*), cleared here
     const int4* prec;       // the prep launch's records [nchain][N] (k_prep.h)
     int nchain;
@@ -327,11 +327,10 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
     }
     if (Rg.x > Rg.y || Rg.z > Rg.w) Rg = make_int4(0x7fffffff, -1, 0x7fffffff, -1);
     const bool any = Rg.x <= Rg.y;
-    if (tid == 0) {
-        o.region[i] = Rg;
-        const double rc = any ? (double)(Rg.y - Rg.x + 1) * (double)(Rg.w - Rg.z + 1) : 0.0;
-        o.cost[i] = make_double2(rc * (double)K, (double)psum);
-    }
+    // the walk costs: the poll walk tests region i against each DISTINCT position (written with
+    // the count below), the per-candidate walk visits the summed spans (k_poll_shared.h walk_choice)
+    const double rc = any ? (double)(Rg.y - Rg.x + 1) * (double)(Rg.w - Rg.z + 1) : 0.0;
+    if (tid == 0) o.region[i] = Rg;
     const bool want_rows = o.rows && any && Rg.w - Rg.z + 1 <= kRowInfo && tid < kWave;
     const int nr = Rg.w - Rg.z + 1;
     int rs0 = 0, rs1 = 0;
@@ -347,7 +346,10 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
             o.urec[row + k] = make_disk(x, y, r);
             o.umap[row + k] = k;
         }
-        if (tid == 0) o.ucount[i] = K;
+        if (tid == 0) {
+            o.ucount[i] = K;
+            o.cost[i] = make_double2(rc * (double)K, (double)psum);
+        }
     } else {
         // ---- insert (exact fp32 keys; linear probing)
         constexpr uint32_t mask = kIndexSlots - 1;
@@ -394,7 +396,10 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
             if (k >= K) continue;
             o.umap[row + k] = table[slot[j]] & ((1 << kIdBits) - 1);
         }
-        if (tid == 0) o.ucount[i] = ucnt;
+        if (tid == 0) {
+            o.ucount[i] = ucnt;
+            o.cost[i] = make_double2(rc * (double)ucnt, (double)psum);
+        }
     }
     MAC_IDX_STAMP(4);
     if (want_rows) {   // (wave-uniform)

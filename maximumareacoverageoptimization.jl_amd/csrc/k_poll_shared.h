@@ -112,7 +112,7 @@ __device__ __forceinline__ void neighbors_block(int i, int N, const int4& R, con
 }
 
 // The device-side walk choice, both costs in one unit (poll-walk tests): the poll walk tests
-// every entry of region i against every candidate's disk i (A = sum of cost[i].x = K * |region i|
+// every entry of region i against each distinct disk i (A = sum of cost[i].x = U_i * |region i|
 // entry visits, broadcast LDS reads); the per-candidate walk visits each candidate's span entries
 // (cost[i].y summed) with scattered global loads and tests each covered one against the disks of
 // disk i's poll-level neighbour list (ncount[i]; an overflowed list: every lower-index disk, i of

@@ -922,7 +922,8 @@ static int32_t host_eval(mac_ctx* ctx, const T* cands, int64_t three_n, int64_t 
     if constexpr (!f32) hc = cands;   // (AUTO's host-side walk estimate reads fp64 candidates)
     const bool tiled = use_tiled(ctx, N, hc, three_n);
     enqueue_eval(ctx, L, s, matrix_src(L->cands.as<double>(), N), N, (int)K, tiled, d_rmax, penalty, d_prev,
-                 d_dlimT, d_prev ? L->dlimraw.as<double>() : nullptr, tan_half_fov, L->area.as<double>(),
+                 d_dlimT, d_prev ? L->dlimraw.as<double>() : nullptr, tan_half_fov,
+                 area_out ? L->area.as<double>() : nullptr,
                  want_obj ? L->obj.as<double>() : nullptr,
                  (best_obj || best_idx) ? L->best.as<double>() : nullptr, 0);
     // results: into the pinned buffer (the upload has completed before the kernels ran), then
@@ -1668,7 +1669,7 @@ static void mads_best_of(mac_mads* m, const CandSrc& src, int Kc, int64_t idx_ba
     enqueue_eval(m->ctx, m->L, m->s, src, m->N, Kc, use_tiled(m->ctx, m->N, nullptr, m->n),
                  m->L->rmax.as<double>(), m->penalty, m->d_prev, m->d_dlimT,
                  m->d_prev ? m->L->dlimraw.as<double>() : nullptr, m->tan_half_fov,
-                 m->L->area.as<double>(), m->L->obj.as<double>(), mads_best_ptr(m), idx_base,
+                 nullptr, m->L->obj.as<double>(), mads_best_ptr(m), idx_base,
                  slot ? m->d_slot : nullptr, slot ? ++m->seq : 0);
     if (!slot) HCK(hipMemcpyAsync(m->hb, mads_best_ptr(m), 16, hipMemcpyDeviceToHost, m->s));
 }
@@ -2018,7 +2019,7 @@ static void mads_run_pipelined(mac_mads* m)
         fbm.done_seq = kMadsDoneSeq;
         enqueue_eval(m->ctx, m->L, s, src, m->N, m->K, true, m->L->rmax.as<double>(), m->penalty,
                      m->d_prev, m->d_dlimT, m->d_prev ? m->L->dlimraw.as<double>() : nullptr,
-                     m->tan_half_fov, m->L->area.as<double>(), m->L->obj.as<double>(),
+                     m->tan_half_fov, nullptr, m->L->obj.as<double>(),
                      m->L->best.as<double>(), 0, m->d_slot, (uint64_t)t, &fbm);
         const auto t3 = clk::now();
         if (computed < n_iter) {   // one iteration's permutations per poll, uploaded per chunk

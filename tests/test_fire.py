@@ -321,10 +321,12 @@ def test_c5_poll293_takes_the_poll_walk(ctx, pkg, ell):
     ctx.set_points(x, y, w)
     ctx.set_algo("auto")
     walks = []
-    for _ in range(2):
+    cons3 = dict(prev=prev, d_lim=np.full(X.shape[1] // 3, 10.0),
+                 tan_half_fov=math.tan(100 / 180 * math.pi / 2))
+    for kw in ({}, {}, cons3, cons3):   # without and with cons3 (failures left out), as the loop
         ctx.profile(True)
         ctx.profile_read(reset=True)
-        ctx.poll_best(X, rmax, 1e5)
+        ctx.poll_best(X, rmax, 1e5, **kw)
         walks.append(ctx.profile_read(reset=True)[3])
         ctx.profile(False)
-    assert walks == ["poll", "poll"], walks
+    assert walks == ["poll"] * 4, walks
