@@ -443,11 +443,13 @@ def main():
     ap.add_argument("--disks", default="uniform", choices=("uniform", "clustered"),
                     help="UAV disks: uniform over the domain (default) or SURVEY 8(d)'s "
                          "clustered variant (sqrt(N)*40 m around the centre, overlapping)")
-    ap.add_argument("--step-mode", default="armed", choices=("armed", "plain"),
-                    help="one GPU: armed (default) = each poll's chain is enqueued behind the "
+    ap.add_argument("--step-mode", default="plain", choices=("armed", "plain"),
+                    help="one GPU: plain (default) = each poll enqueued after the previous result "
+                         "(mac_poll_best_dev_f64); armed = each poll's chain enqueued behind the "
                          "context's doorbell while the previous poll runs and released once its "
-                         "result is read (mac_poll_arm_dev_f64 / mac_poll_fire); plain = enqueued "
-                         "after the previous result (mac_poll_best_dev_f64)")
+                         "result is read (mac_poll_arm_dev_f64 / mac_poll_fire). Measured at "
+                         "config 4: 0.0895 (plain) vs 0.0905 ms (armed): the stream's wait "
+                         "releases the chain no sooner than a fresh launch starts it")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL on ROCm) for the real multi-GPU run; gloo only to rehearse "
                          "N>1 with several ranks sharing one GPU (MAXCOVER_BENCH_DEVICE)")
