@@ -29,12 +29,11 @@ constexpr int kBitsMinDisks = 16;  // bit-word kernel: used above this many disk
 // from the front), [1] poll-kernel jobs taken, [2] the other disks with neighbours (dlist from the
 // back), [3] bit-word / union-pass jobs taken, [4..7] union-pass jobs listed per weight bucket,
 // heaviest first (k_or.h), [8] disks with lower neighbours whose upper list overflowed (the union
-// pass stands down), [9] deferred penalty-chain groups taken (k_prep.h fold_groups); cleared by
-// the index kernel (the lane's mode buffer holds [walk, dcount])
+// pass stands down); cleared by the index kernel (the lane's mode buffer holds [walk, dcount])
 constexpr int kOrBuckets = 4;
 constexpr int kDcBits = 0, kDcPollJobs = 1, kDcOther = 2, kDcBitsJobs = 3, kDcOrJobs = 4,
-              kDcOrBad = kDcOrJobs + kOrBuckets, kDcFold = kDcOrBad + 1;
-constexpr int kDcCount = kDcFold + 1;
+              kDcOrBad = kDcOrJobs + kOrBuckets;
+constexpr int kDcCount = kDcOrBad + 1;
 
 constexpr int kModePoll = 1;
 constexpr int kModeTiled = 2;

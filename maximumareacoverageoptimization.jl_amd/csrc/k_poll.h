@@ -130,18 +130,9 @@ __device__ __forceinline__ void coverage_poll_body(
     const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
     int* __restrict__ jobctr, int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
     double* __restrict__ spart, int n_shared, int counts, int bits_on, int* __restrict__ dc_out,
-    const int* __restrict__ qual, const double2* __restrict__ cost, double ratio, const FoldArgs& fa)
+    const int* __restrict__ qual, const double2* __restrict__ cost, double ratio)
 {
     static_assert(kPollSlots == 2 * kPollPairs, "the hot loop pairs candidate slots");
-    // s32: (Q, U, V, 0) per staged entry, (+inf, 0, 0) for shared / non-finite / pad; s64: exact
-    // coordinates (band decisions); red: per-wave credit of each position, used only between
-    // slices, over the staging area; the deferred chains' terms (k_prep.h fold_groups) outside a walk
-    constexpr int kStageBytes = (kPollCH + 4) * (int)sizeof(float4) + kPollCH * (int)sizeof(double2);
-    constexpr int kRedBytes = kPollWaves * kPollKPB * (int)sizeof(double);
-    static_assert(kRedBytes <= kStageBytes, "red aliases the staging arrays");
-    static_assert(kFoldC * kFoldMaxN * (int)sizeof(double) <= kStageBytes, "fold terms fit the staging");
-    __shared__ __attribute__((aligned(16))) unsigned char stage[kStageBytes];
-    __shared__ int sgrp[2];
 #ifdef MAC_DIAG
     const uint64_t diag_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -207,8 +198,7 @@ __device__ __forceinline__ void coverage_poll_body(
             job = -1;
         }
     };
-    if (bx >= nwalk) {  // then: the deferred penalty chains, the shared entries
-        fold_groups(fa, reinterpret_cast<double*>(stage), sgrp, kPollThreads);
+    if (bx >= nwalk) {  // then: the shared entries
         if (mv != kModePoll) return;
         if (bx == nwalk && cost && dc_out) {
             // launch hint for the next poll: the walk AUTO would choose now that the neighbour
@@ -225,6 +215,13 @@ __device__ __forceinline__ void coverage_poll_body(
 #ifdef MAC_DIAG
     int diag_entries = 0;
 #endif
+    // s32: (Q, U, V, 0) per staged entry, (+inf, 0, 0) for shared / non-finite / pad; s64: exact
+    // coordinates (band decisions); red: per-wave credit of each position, used only between
+    // slices, over the staging area
+    constexpr int kStageBytes = (kPollCH + 4) * (int)sizeof(float4) + kPollCH * (int)sizeof(double2);
+    constexpr int kRedBytes = kPollWaves * kPollKPB * (int)sizeof(double);
+    static_assert(kRedBytes <= kStageBytes, "red aliases the staging arrays");
+    __shared__ __attribute__((aligned(16))) unsigned char stage[kStageBytes];
     float4* const s32 = (float4*)stage;
     double2* const s64 = (double2*)(stage + (kPollCH + 4) * sizeof(float4));
     double (*const red)[kPollKPB] = (double (*)[kPollKPB])stage;
@@ -508,7 +505,6 @@ __device__ __forceinline__ void coverage_poll_body(
     }
     MAC_DIAG_STAMP(diag_t0, 3, ((uint64_t)nc << 40) | ((uint64_t)U << 20) | (uint64_t)diag_entries);
     } while (0);
-    fold_groups(fa, reinterpret_cast<double*>(stage), sgrp, kPollThreads);   // (the walk is done with stage)
     if (mv == kModePoll) shared_jobs(-1);
 }
 
@@ -523,12 +519,12 @@ __global__ __launch_bounds__(kPollThreads) __attribute__((amdgpu_waves_per_eu(3)
     const int* __restrict__ ncount, const int* __restrict__ dlist, const int* __restrict__ dcount,
     int* __restrict__ jobctr, int N, int K, const int* __restrict__ mode, double* __restrict__ partial,
     double* __restrict__ spart, int n_shared, int counts, int bits_on, int* __restrict__ dc_out,
-    const int* __restrict__ qual, const double2* __restrict__ cost, double ratio, FoldArgs fa)
+    const int* __restrict__ qual, const double2* __restrict__ cost, double ratio)
 {
     ts_begin(ts);
     coverage_poll_body(xy, w, off, g, urec, umap, ucount, region, nbrT, nboxT, lane4, lanexp, rows,
                        ncount, dlist, dcount, jobctr, N, K, mode, partial, spart, n_shared, counts,
-                       bits_on, dc_out, qual, cost, ratio, fa);
+                       bits_on, dc_out, qual, cost, ratio);
     ts_end(ts);
 }
 

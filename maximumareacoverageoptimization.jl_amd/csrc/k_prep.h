@@ -155,9 +155,6 @@ struct CandSrc {
 #define MAC_PREP_C 8
 #endif
 constexpr int kPrepC = MAC_PREP_C;   // candidates per workgroup (a multiple of 4)
-// vp word of a candidate whose penalty chain is folded later (PrepArgs.defer): a NaN payload no
-// arithmetic produces (a real vp is acc * penalty: a number, +-inf or the default quiet NaN)
-constexpr uint64_t kVpPending = 0x7FF4DEADBEEF0001ull;
 constexpr int kPrepU = 512;      // UAVs per block = threads per workgroup
 
 // keysP / keysT row pitch: rows start on 128-B boundaries (and hold every workgroup's kPrepC keys:
@@ -178,8 +175,6 @@ struct PrepArgs {
                                // each B entry for both: prep_cand)
     int nchain;                // workgroups
     int skip_failed;           // 1: the records leave out cons3 failures (no area is reported for them)
-    int defer;                 // 1: only cons3 here (vp = +inf or kVpPending); the chains are folded
-                               // by the poll kernel's workgroups beside the walks (fold_groups)
     int4* prec;                // [nchain][N] records (null: no poll walk)
     Grid g;
     uint32_t* keysP;           // packed keys (null: none), one row per disk, pitch ldk
@@ -447,9 +442,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
                     sb += wsum[w][u];
                 }
                 on_grid = ex;
-                if (a.defer) {
-                    // (the chain is folded by the poll kernel)
-                } else if (ex) {
+                if (ex) {
                     acc += sb;
                 } else if (!bad) {   // (a cons3 failure's vp is +inf: no chain to fold)
                     int q = 0;
@@ -468,63 +461,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
         if (obj && ib + kPrepU < N) lds_barrier();   // the fold has read the terms
     }
     if (obj && u < kPrepC && cand(u) < K)
-        a.vp[cand(u)] = bad ? __builtin_inf()
-                     : a.defer ? __builtin_bit_cast(double, kVpPending) : acc * a.penalty;
-}
-
-// The deferred penalty chains (PrepArgs.defer, matrix polls with N <= kFoldMaxN): the candidates
-// whose vp is kVpPending get vp = penalty * (((0 + t_0) + t_1) + ... + t_{N-1}),
-// t_i = |R_i - rmax_i| — the prep's chain (and src/TDM_STATIC_opt.jl:88-92) term for term. Run by
-// the poll kernel's workgroups beside the walks (the shared-entry workgroups first, walk workgroups
-// once their disk is done): groups of 4 candidates taken from a counter; a group's terms are
-// staged in LDS with one coalesced round trip (the R rows of the column-major matrix), then 4 lanes
-// fold them. Uniform per workgroup (barriers inside); buf holds 4 N doubles.
-constexpr int kFoldC = 4;
-constexpr int kFoldMaxN = 512;
-struct FoldArgs {
-    const double* cands;       // the 3N x K column-major matrix (null: nothing deferred)
-    int ldc, N, K;
-    const double* rmax;
-    double penalty;
-    double* vp;
-    int* ctr;                  // groups taken (dcount[kDcFold], cleared by the index kernel)
-};
-
-__device__ __forceinline__ void fold_groups(const FoldArgs& f, double* buf, int* sgrp, int nthreads)
-{
-    if (!f.cands) return;   // uniform
-    const int N = f.N, K = f.K, tid = threadIdx.x;
-    const int ngrp = (K + kFoldC - 1) / kFoldC;
-    for (int it = 0;; ++it) {
-        if (tid == 0) sgrp[it & 1] = atomicAdd(f.ctr, 1);
-        __syncthreads();
-        const int gq = sgrp[it & 1];
-        if (gq >= ngrp) break;   // uniform
-        const int k0 = gq * kFoldC;
-        for (int t = tid; t < kFoldC * N; t += nthreads) {
-            const int c = t / N, i = t - c * N;
-            const int k = min(k0 + c, K - 1);
-            const double R2 = f.cands[(int64_t)k * f.ldc + 2 * N + i];
-            buf[t] = f.rmax ? __builtin_fabs(R2 - f.rmax[i]) : 0.0;
-        }
-        __syncthreads();
-        if (tid < kFoldC && k0 + tid < K &&
-            __builtin_bit_cast(uint64_t, f.vp[k0 + tid]) == kVpPending) {
-            const double* t = buf + tid * N;
-            double acc = 0.0;
-            int q = 0;
-            for (; q + 16 <= N; q += 16) {
-                double v[16];
-#pragma unroll
-                for (int j = 0; j < 16; ++j) v[j] = t[q + j];
-#pragma unroll
-                for (int j = 0; j < 16; ++j) acc += v[j];
-            }
-            for (; q < N; ++q) acc += t[q];
-            f.vp[k0 + tid] = acc * f.penalty;
-        }
-        __syncthreads();   // the next group overwrites buf
-    }
+        a.vp[cand(u)] = bad ? __builtin_inf() : acc * a.penalty;
 }
 
 __global__ __launch_bounds__(kPrepU) __attribute__((amdgpu_waves_per_eu(4))) void prep_kernel(uint64_t* ts, PrepArgs a)

@@ -548,7 +548,6 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
     // for its plus and minus candidates (k_prep.h PrepArgs.pair)
     const bool pair = !src.cands && src.k0 == 0 && K == 6 * N && (3 * N) % 4 == 0 && kPrepC == 8;
     const int nchain = pair ? (3 * N) / 4 : (K + kPrepC - 1) / kPrepC;
-    bool pr_defer = false;   // the poll kernel folds the penalty chains (k_prep.h fold_groups)
     if ((d_obj || poll_possible) && K > 0) {
         // the prep launch (k_prep.h): penalty chains + cons3 into vp, the poll walk's partial
         // regions, and the index's fp32 keys
@@ -561,9 +560,6 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         pr.vp = d_vp;
         pr.nchain = nchain;
         pr.skip_failed = d_area ? 0 : 1;   // (the index maps them to an inert position likewise)
-        // matrix polls: the poll kernel's workgroups fold the chains beside the walks
-        pr.defer = d_vp && poll_possible && src.cands && N <= kFoldMaxN ? 1 : 0;
-        pr_defer = pr.defer != 0;
         pr.pair = pair ? 1 : 0;
         pr.g = ctx->grid;
         if (poll_possible) {
@@ -770,9 +766,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                                L->mode.as<int>() + 2, N, K,
                                d_mode, L->partial.as<double>(), L->spart.as<double>(), n_shared, counts,
                                bits_on, L->d_dc, L->qual.as<int>(),
-                               walk_forced == 0 ? L->cost.as<double2>() : nullptr, kPollCostRatio,
-                               FoldArgs{pr_defer ? src.cands : nullptr, src.ldc, N, K, d_rmax, penalty,
-                                        d_vp, L->mode.as<int>() + 1 + kDcFold});
+                               walk_forced == 0 ? L->cost.as<double2>() : nullptr, kPollCostRatio);
             HCK(hipGetLastError());
             // the shared entries of crowded polls: the union pass (equal weights, k_or.h) or
             // bit-words per distinct position (k_bits.h); both return at once when few disks have
