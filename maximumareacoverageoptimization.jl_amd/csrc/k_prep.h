@@ -264,8 +264,6 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
 {
     __shared__ double term[kPrepC][kPrepU + 1];   // [candidate][UAV] (+1: lanes on distinct banks)
     __shared__ int wbad[kPrepU / kWave][kPrepC];  // per wave: a term of the candidate is negative
-    __shared__ int wexact[kPrepU / kWave][kPrepC];   // ... every term is on the exact grid (below)
-    __shared__ double wsum[kPrepU / kWave][kPrepC];  // ... the wave's terms summed (exact then)
     __shared__ uint32_t wbadm[kPrepU / kWave];       // ... wbad as a mask over the candidates
     const int N = a.N, K = a.K;
     const int u = threadIdx.x, lane = u & (kWave - 1), wid = u / kWave;
@@ -279,14 +277,6 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
     MAC_PREP_STAMP(0);
     double acc = 0.0;   // the chain (lane c of wave 0: candidate k0 + c)
     bool bad = false;   // ... and whether a term of it is negative (cons3)
-    bool on_grid = true;   // ... and whether every term so far was on the exact grid
-    // The exact grid: terms t = m * 2^-10 (m a non-negative integer) with t <= 2^43 / N. Every
-    // partial sum of such terms is a multiple of 2^-10 below 2^43, so exactly representable: the
-    // sequential chain of src/TDM_STATIC_opt.jl:88-92 then equals the exact sum, whatever order it
-    // is added in — a tree over the workgroup instead of 512 dependent adds. (MADS polls on the
-    // reference's granularity-1 mesh with an integral r_max give integer terms; any other term
-    // sends its candidate down the sequential chain, from that block of UAVs on.)
-    const double grid_lim = 8796093022208.0 / (double)N;   // 2^43 / N
     // Candidates that fail cons3 (the extreme barrier, src/TDM_Constraints.jl:54-75) are not
     // evaluated by the reference's DirectSearch poll, and their objective is +inf whatever they
     // cover. With one block of UAVs (N <= kPrepU) their failure is known before the records are
@@ -351,17 +341,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
                 }
                 term[c][u] = t;
                 const uint64_t neg = __ballot(iv && t < 0.0);
-                const double ts = t * 1024.0;
-                const uint64_t off_grid =
-                    __ballot(iv && !(t >= 0.0 && t <= grid_lim && ts == __builtin_rint(ts)));
-                double sw = iv ? t : 0.0;   // the wave's sum (used only when exact)
-#pragma unroll
-                for (int o = 32; o >= 1; o >>= 1) sw += __shfl_xor(sw, o, kWave);
-                if (lane == 0) {
-                    wbad[wid][c] = neg != 0;
-                    wexact[wid][c] = off_grid == 0;
-                    wsum[wid][c] = sw;
-                }
+                if (lane == 0) wbad[wid][c] = neg != 0;
                 wdead |= (neg != 0 ? 1u : 0u) << c;
             }
             if (lane == 0) wbadm[wid] = wdead;
@@ -429,22 +409,12 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
         MAC_PREP_STAMP(2 + 3 * (ib / kPrepU));
         if (obj) {
             // the chains, after every wave's other work (the adds are the critical path: the
-            // folding wave then has its SIMD to itself), sequential in UAV order — or, for a
-            // candidate whose terms are all on the exact grid, the waves' sums (exact)
+            // folding wave then has its SIMD to itself), sequential in UAV order
             if (!excl) lds_barrier();   // (excl: passed above)
             if (u < kPrepC) {
-                bool ex = on_grid;
-                double sb = 0.0;
 #pragma unroll
-                for (int w = 0; w < kPrepU / kWave; ++w) {
-                    bad |= wbad[w][u] != 0;
-                    ex = ex && wexact[w][u] != 0;
-                    sb += wsum[w][u];
-                }
-                on_grid = ex;
-                if (ex) {
-                    acc += sb;
-                } else if (!bad) {   // (a cons3 failure's vp is +inf: no chain to fold)
+                for (int w = 0; w < kPrepU / kWave; ++w) bad |= wbad[w][u] != 0;
+                if (!bad) {   // (a cons3 failure's vp is +inf: no chain to fold)
                     int q = 0;
                     for (; q + 16 <= nb; q += 16) {
                         double t[16];

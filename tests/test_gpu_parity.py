@@ -529,12 +529,10 @@ def test_many_uav_full_poll_auto(ctx, pkg, orc, N):
 
 
 def test_penalty_chain_exact_grid_and_sequential(ctx, pkg, orc):
-    """The prep launch folds a candidate's penalty chain (src/TDM_STATIC_opt.jl:88-92) as a tree
-    when every term |R_i - r_max_i| is a multiple of 2^-10 below 2^43 / N (exact in any order),
-    else sequentially from the first off-grid block of 512 UAVs on (k_prep.h). N = 1100 (three
-    blocks): integer terms, 2^-10 fractions, an off-grid term in block 0, 1 or 2 only, terms
-    past 2^43 / N, and non-finite R. Every objective == -area + 1e5 x the C oracle's sequential
-    chain, bit for bit."""
+    """The prep launch folds a candidate's penalty chain (src/TDM_STATIC_opt.jl:88-92) in UAV
+    order across blocks of 512 UAVs (k_prep.h). N = 1100 (three blocks): integer terms, 2^-10
+    fractions, one odd term in block 0, 1 or 2 only, huge terms, and non-finite R. Every
+    objective == -area + 1e5 x the C oracle's sequential chain, bit for bit."""
     wl = pkg.workloads
     rng = wl.SplitMix64(1100)
     G = 256
