@@ -528,7 +528,7 @@ def test_many_uav_full_poll_auto(ctx, pkg, orc, N):
     assert bi == k and bo == want[k]
 
 
-def test_penalty_chain_exact_grid_and_sequential(ctx, pkg, orc):
+def test_penalty_chain_sequential_blocks(ctx, pkg, orc):
     """The prep launch folds a candidate's penalty chain (src/TDM_STATIC_opt.jl:88-92) in UAV
     order across blocks of 512 UAVs (k_prep.h). N = 1100 (three blocks): integer terms, 2^-10
     fractions, one odd term in block 0, 1 or 2 only, huge terms, and non-finite R. Every
