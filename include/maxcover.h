@@ -139,7 +139,9 @@ int32_t mac_objective_batch_f64(mac_ctx* ctx, const double* cands, int64_t three
  * `prev` [x;y;r] > d_lim[i], z = R / tan_half_fov; src/TDM_Constraints.jl:54-75) when prev
  * is non-null, and return the lowest-index minimiser (ties -> lowest index, the order a
  * sequential poll keeps its first best). best_idx = -1 when no candidate is feasible.
- * obj_out (nullable, K doubles) receives every objective (+inf for infeasible). */
+ * obj_out (nullable, K doubles) receives every objective (+inf for infeasible). As in
+ * DirectSearch's extreme barrier, an infeasible candidate is not evaluated: its coverage is never
+ * computed (the walks leave it out when N <= 512), only its +inf objective reported. */
 int32_t mac_poll_best_f64(mac_ctx* ctx, const double* cands, int64_t three_n, int64_t K,
                           const double* r_max, double penalty,
                           const double* prev, const double* d_lim, double tan_half_fov,

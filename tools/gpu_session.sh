@@ -130,6 +130,9 @@ for s in $STEPS; do
         fatal $rc || python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write --config 4 \
             --chain 'mac::prep_kernel;mac::disk_index_kernel<true, 3>;mac::walk_setup_kernel;mac::coverage_poll_kernel;mac::finalize_kernel' \
             --out gpurun_out/pmc_traffic_config4.json ;;
+    diagprep)   # prep launch: per-workgroup spans; phases of the first 64 (diagnostic build)
+        MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
+            run diagprep 300 python tools/diag_prep.py ; rc=$? ;;
     pmccp)   # the fresh PMC file where bench.py looks for it (attached while src_sha matches)
         cp gpurun_out/pmc_traffic_config4.json profiles/pmc_traffic_config4.json ; rc=$? ;;
     *) echo "unknown step $s"; rc=0 ;;
