@@ -96,6 +96,17 @@ struct IndexOut {
 // failed candidates share one position; its record covers nothing (T = -1, r = 0) and its lane
 // is inert.
 constexpr uint32_t kDeadKey = 0x7FBADEADu;
+// ... and in word mode (every key of the disk packed, k_prep.h): an escape pattern with a nonzero
+// offset field, which the prep never writes (its escapes are exactly kKeyEsc)
+constexpr uint32_t kDeadWord = kKeyEsc | 1u;
+
+__device__ __forceinline__ uint32_t word_hash(uint32_t w)
+{
+    w *= 0x9E3779B1u;
+    w ^= w >> 15;
+    w *= 0x85EBCA77u;
+    return w ^ (w >> 13);
+}
 __device__ __forceinline__ bool dead_cand(const double* vp, int k, int K)
 {
     return vp && k < K && vp[k] == __builtin_inf();
@@ -206,6 +217,7 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
     };
 
     bool hashed = false;
+    bool words = false;   // every key of the disk is a packed word: one-word keys (kx holds the bits)
     constexpr int P = kIdxPer + 1;
     int slot[P];
     double bx = 0.0, by = 0.0, br = 0.0;   // candidate 0's disk: the key base
@@ -233,22 +245,29 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
                 qr[j] = fx[(int64_t)2 * N * src.ldk + k];
             }
         }
+        bool dj[P], any_esc = false;
 #pragma unroll
         for (int j = 0; j < P; ++j) {
             const int k = j < kIdxPer ? tid + j * kIdxThreads : (tid == 0 ? kIndexMaxK : K);
-            if (dead_cand(o.vp, k, K))
-                qx[j] = qy[j] = qr[j] = __builtin_bit_cast(float, kDeadKey);
+            dj[j] = dead_cand(o.vp, k, K);
+            if (dj[j]) qx[j] = qy[j] = qr[j] = __builtin_bit_cast(float, kDeadKey);
+            any_esc |= k < K && !dj[j] && pq[j] == kKeyEsc;
         }
         const bool bad = pbad;   // a key of disk i is inexact (the records' flags)
         for (int q = tid; q < kIndexSlots; q += kIdxThreads) table[q] = -1;
         if (tid == 0) ucnt = 0;
+        words = !__syncthreads_or(any_esc);
 #pragma unroll
         for (int j = 0; j < P; ++j) {
             const int k = j < kIdxPer ? tid + j * kIdxThreads : (tid == 0 ? kIndexMaxK : K);
             if (k < K) {
-                kx[k] = qx[j];
-                ky[k] = qy[j];
-                kr[k] = qr[j];
+                if (words) {
+                    kx[k] = __builtin_bit_cast(float, dj[j] ? kDeadWord : pq[j]);
+                } else {
+                    kx[k] = qx[j];
+                    ky[k] = qy[j];
+                    kr[k] = qr[j];
+                }
             }
         }
         publish_partials();
@@ -359,9 +378,9 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
             slot[j] = 0;
             if (k >= K) continue;
             const uint32_t bx = __builtin_bit_cast(uint32_t, kx[k]);
-            const uint32_t by = __builtin_bit_cast(uint32_t, ky[k]);
-            const uint32_t br = __builtin_bit_cast(uint32_t, kr[k]);
-            uint32_t s = key_hash(bx, by, br) & mask;
+            const uint32_t by = words ? 0u : __builtin_bit_cast(uint32_t, ky[k]);
+            const uint32_t br = words ? 0u : __builtin_bit_cast(uint32_t, kr[k]);
+            uint32_t s = (words ? word_hash(bx) : key_hash(bx, by, br)) & mask;
             for (;;) {
                 int cur = table[s];
                 if (cur < 0) {
@@ -369,8 +388,8 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
                     if (cur < 0) break;                      // claimed an empty slot
                 }
                 if (__builtin_bit_cast(uint32_t, kx[cur]) == bx &&
-                    __builtin_bit_cast(uint32_t, ky[cur]) == by &&
-                    __builtin_bit_cast(uint32_t, kr[cur]) == br)
+                    (words || (__builtin_bit_cast(uint32_t, ky[cur]) == by &&
+                               __builtin_bit_cast(uint32_t, kr[cur]) == br)))
                     break;                                   // same disk: share the slot
                 s = (s + 1) & mask;                          // another disk: probe on
             }
@@ -419,11 +438,23 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
             DiskRec d;
             if (hashed) {
                 const int k = owner_of[u];
-                if (__builtin_bit_cast(uint32_t, kr[k]) == kDeadKey) {   // the failed candidates
+                float fx = 0.0f, fy = 0.0f, fr = 0.0f;
+                bool dead;
+                if (words) {
+                    const uint32_t wk = __builtin_bit_cast(uint32_t, kx[k]);
+                    dead = wk == kDeadWord;
+                    key_unpack(wk, fx, fy, fr);
+                } else {
+                    dead = __builtin_bit_cast(uint32_t, kr[k]) == kDeadKey;
+                    fx = kx[k];
+                    fy = ky[k];
+                    fr = kr[k];
+                }
+                if (dead) {   // the failed candidates
                     d.cx = d.cy = d.r = 0.0;
                     d.T = -1.0;
                 } else {
-                    d = make_disk(bx + (double)kx[k], by + (double)ky[k], br + (double)kr[k]);
+                    d = make_disk(bx + (double)fx, by + (double)fy, br + (double)fr);
                 }
                 o.urec[row + u] = d;
             } else {
