@@ -181,6 +181,20 @@ def _declare(L: ctypes.CDLL) -> None:
         f.restype = res
 
 
+def _one_hip_runtime() -> None:
+    """PyTorch-ROCm ships its own HIP and HSA runtimes, which its libraries load by file name. If
+    libmaxcover.so (NEEDED libamdhip64.so.7) were loaded first, it would bind the system runtime
+    and torch would then load a second one in the same process, whose device initialisation fails
+    ("No HIP GPUs are available"; measured on the MI355X box). torch loaded first makes its
+    runtime the process's libamdhip64.so.7, which libmaxcover then shares: one runtime, so the
+    device tensors, streams and RCCL collectives of the torch plumbing (dist.py, bench.py) and
+    the library's launches live in one context. Without torch nothing changes."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # pragma: no cover - torch is in this image
+        pass
+
+
 def load_library(path: str | None = None) -> ctypes.CDLL:
     """Load libmaxcover.so (raises MaxCoverError if absent: there is no fallback path)."""
     global _lib
@@ -190,6 +204,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         p = path or LIB_PATH
         if not os.path.exists(p):
             raise MaxCoverError(MAC_E_HIP, f"{p} not built (run __graft_entry__.build())")
+        _one_hip_runtime()
         try:
             L = ctypes.CDLL(p)
         except OSError as e:  # pragma: no cover - depends on the host

@@ -1,0 +1,102 @@
+"""GPU: the RCCL side of the multi-GPU exchanges (dist.py) on the one GPU a box has — a world of
+one rank with the nccl (= RCCL) backend, so the device collectives, events and pinned reads of
+the strong step (PollGather), of the sharded MADS loop (DeviceGather bound to a stepper) and of
+the point broadcast run as they do on the 8-GPU node (the gloo tests in test_dist.py cover two
+ranks on the CPU). Reference: src/TDM_STATIC_opt.jl:129 (the poll the ranks split)."""
+import math
+import os
+import socket
+from importlib import import_module
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+TAN50 = math.tan(100 / 180 * math.pi / 2)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture(scope="module")
+def nccl1(ctx):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
+                            world_size=1, device_id=dev)
+    assert dist.get_backend() == "nccl"
+    yield dev
+    dist.destroy_process_group()
+
+
+def test_poll_gather_over_rccl(nccl1, ctx, pkg):
+    """PollGather (bench.py's strong step): each device poll's d_best goes through the RCCL
+    all-gather and the pinned record; the result equals the poll's own (objective, index) from
+    mac_poll_best_f64, poll after poll, with no allocation in between."""
+    import torch
+
+    d = import_module(pkg.__name__ + ".dist")
+    wl = pkg.workloads
+    x, y, w = wl.grid_points(256)
+    ctx.set_points(x, y, w)
+    rng = wl.SplitMix64(71)
+    N = 16
+    rmax = np.full(N, 30.0 * TAN50)
+    d_rmax = torch.from_numpy(rmax).to(nccl1)
+    d_best = torch.empty(2, dtype=torch.float64, device=nccl1)
+    gather = d.PollGather(nccl1)
+    out_ptr = gather.out.data_ptr()
+    for t in range(5):
+        C = wl.poll_candidates(wl.uniform_disks(N, 256, rng), rng)
+        want = ctx.poll_best(C, rmax)
+        d_c = torch.from_numpy(np.ascontiguousarray(C)).to(nccl1)
+        ctx.poll_best_dev(d_c, 3 * N, C.shape[0], d_rmax, d_best,
+                          stream=torch.cuda.current_stream(nccl1).cuda_stream)
+        got = gather(d_best)
+        assert got == (want[0], want[1]), (t, got, want)
+    assert gather.calls == 5 and gather.out.data_ptr() == out_ptr
+
+
+def test_sharded_mads_loop_over_rccl(nccl1, ctx, pkg):
+    """dist.mads_loop with the RCCL DeviceGather bound to the stepper's device best buffer (the
+    config-5 multi-GPU loop's exchange): the same iterate, objective and counts as mac_mads_run."""
+    d = import_module(pkg.__name__ + ".dist")
+    wl = pkg.workloads
+    x, y, w = wl.grid_points(200)
+    ctx.set_points(x, y, w)
+    rng = wl.SplitMix64(404)
+    N = 9
+    x0 = np.concatenate([np.round(250 + rng.uniform(N) * 400), np.round(250 + rng.uniform(N) * 400),
+                         np.full(N, 30.0)])
+    r_max = np.full(N, 30.0 * TAN50)
+    kw = dict(prev=x0, d_lim=np.full(N, 10.0), tan_half_fov=TAN50, n_iter=25, ell0=2, ell_max=5,
+              seed=909)
+    want_x, want = ctx.mads_run(x0, r_max, 1e5, **kw)
+    # (make_gather is the identity for a world of one: the RCCL gather is bound explicitly)
+    gather = d.DeviceGather(nccl1)
+    st = ctx.mads_stepper(x0, r_max, 1e5, shard=(0, 2 * x0.size), **kw)
+    xs, stats = d.mads_loop(st, gather)
+    st.close()
+    assert np.array_equal(xs, want_x)
+    assert stats["f"] == want["f"] and stats["iterations"] == want["iterations"]
+    assert gather.calls == want["iterations"]
+
+
+def test_broadcast_points_over_rccl(nccl1, pkg):
+    """broadcast_points over RCCL from rank 0's host arrays to device tensors, bit for bit."""
+    d = import_module(pkg.__name__ + ".dist")
+    rng = np.random.default_rng(5)
+    x, y, w = rng.normal(size=1000), rng.normal(size=1000), rng.uniform(size=1000)
+    gx, gy, gw = d.broadcast_points(x, y, w, src=0, device=nccl1)
+    assert gx.device.type == "cuda"
+    for a, b in ((gx, x), (gy, y), (gw, w)):
+        assert np.array_equal(a.cpu().numpy(), b)
