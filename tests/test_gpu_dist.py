@@ -55,14 +55,17 @@ def test_poll_gather_over_rccl(nccl1, ctx, pkg):
     d_best = torch.empty(2, dtype=torch.float64, device=nccl1)
     gather = d.PollGather(nccl1)
     out_ptr = gather.out.data_ptr()
-    for t in range(5):
-        C = wl.poll_candidates(wl.uniform_disks(N, 256, rng), rng)
-        want = ctx.poll_best(C, rmax)
-        d_c = torch.from_numpy(np.ascontiguousarray(C)).to(nccl1)
-        ctx.poll_best_dev(d_c, 3 * N, C.shape[0], d_rmax, d_best,
-                          stream=torch.cuda.current_stream(nccl1).cuda_stream)
-        got = gather(d_best)
-        assert got == (want[0], want[1]), (t, got, want)
+    # the polls and the gather on one stream of the caller's (as bench.py's ranks do; stream NULL
+    # would mean the context's own stream, include/maxcover.h, not torch's legacy default stream)
+    s = torch.cuda.Stream(nccl1)
+    with torch.cuda.stream(s):
+        for t in range(5):
+            C = wl.poll_candidates(wl.uniform_disks(N, 256, rng), rng)
+            want = ctx.poll_best(C, rmax)
+            d_c = torch.from_numpy(np.ascontiguousarray(C)).to(nccl1)
+            ctx.poll_best_dev(d_c, 3 * N, C.shape[0], d_rmax, d_best, stream=s.cuda_stream)
+            got = gather(d_best)
+            assert got == (want[0], want[1]), (t, got, want)
     assert gather.calls == 5 and gather.out.data_ptr() == out_ptr
 
 
