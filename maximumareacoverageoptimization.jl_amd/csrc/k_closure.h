@@ -3,7 +3,7 @@
 // DirectSearch calls the objective closure once per trial point (SetObjective,
 // src/TDM_STATIC_opt.jl:125; AreaMaxObjective :82-100 -> calculateArea
 // src/AreaCoverageCalculation.jl:63-78). For that path a batch chain (index, walk, finalize) is
-// all latency, so mac_area_f64 runs one kernel instead: workgroup i = disk i of the candidate.
+// all latency, so mac_area_f64 runs one kernel instead: wave w of workgroup b = disk 4b + w.
 //   1. every workgroup stages the candidate's N disks (x, y, r) in LDS (one coalesced read);
 //   2. disk i's lower-index neighbours: the disks j < i that may share a covered entry with it
 //      (disks_may_overlap, conservative), their exact thresholds T(r_j) in LDS;
@@ -46,6 +46,9 @@ struct ClosureOut {
     uint64_t seq;
 };
 
+// Disks per workgroup: one wave per disk (the candidate is staged once per 4 disks).
+constexpr int kClosureDisksPerWG = kWavesPerBlock;
+
 __global__ __launch_bounds__(kBlock) void closure_kernel(uint64_t* ts, const double* __restrict__ cand,
                                                          int N, Grid g, const double2* __restrict__ xy,
                                                          const double* __restrict__ w,
@@ -57,55 +60,62 @@ __global__ __launch_bounds__(kBlock) void closure_kernel(uint64_t* ts, const dou
     double* sx = (double*)lds_raw;
     double* sy = sx + N;
     double* sr = sy + N;
-    __shared__ int nb[kClosureNbr];
-    __shared__ double nT[kClosureNbr];
-    __shared__ int ncnt;
-    __shared__ double dred[kWavesPerBlock];
-    __shared__ unsigned long long ired[kWavesPerBlock];
+    __shared__ int nb[kClosureDisksPerWG][kClosureNbr];
+    __shared__ double nT[kClosureDisksPerWG][kClosureNbr];
+    __shared__ int rs[kClosureDisksPerWG][kWave], rpre[kClosureDisksPerWG][kWave + 1];
+    __shared__ unsigned long long wcnt[kClosureDisksPerWG];
+    __shared__ int sarr;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
-    const int i = blockIdx.x;
+    const int i = blockIdx.x * kClosureDisksPerWG + wid;   // this wave's disk
+    const bool valid = i < N;                                // (wave-uniform)
     for (int j = tid; j < N; j += kBlock) {
         sx[j] = cand[j];
         sy[j] = cand[N + j];
         sr[j] = cand[2 * N + j];
     }
-    if (tid == 0) ncnt = 0;
     __syncthreads();
-    const double cx = sx[i], cy = sy[i], r = sr[i];
-    const double T = cover_threshold(r);
+    double cx = 0.0, cy = 0.0, r = 0.0, T = -1.0;
     int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
-    const bool any = T >= 0.0 && tile_span(cx, r, g.gx0, g.invS, g.nTx, x0, x1) &&
-                     tile_span(cy, r, g.gy0, g.invS, g.nTy, y0, y1);
-    // the span's row runs (a row of tiles is a contiguous run of the sorted list): every row's
-    // offsets loaded at once by wave 0, in flight during the neighbour tests, then flattened with
-    // a prefix (one memory round trip for the offsets and one for the entries, instead of two per
-    // row); spans of more than 64 rows walk row by row below
-    __shared__ int rs[kWave], rpre[kWave + 1];
+    bool any = false;
+    if (valid) {
+        cx = sx[i];
+        cy = sy[i];
+        r = sr[i];
+        T = cover_threshold(r);
+        any = T >= 0.0 && tile_span(cx, r, g.gx0, g.invS, g.nTx, x0, x1) &&
+              tile_span(cy, r, g.gy0, g.invS, g.nTy, y0, y1);
+    }
+    // the span's row runs (a row of tiles is a contiguous run of the sorted list): lane = row,
+    // every offset in flight during the neighbour tests, then a wave prefix; spans of more than
+    // 64 rows walk row by row below
     const int nrows = any ? y1 - y0 + 1 : 0;
     const bool flat = nrows <= kWave;
     int rs0 = 0, rlen = 0;
-    if (any && flat && tid < nrows) {
-        const int64_t rb = (int64_t)(y0 + tid) * g.nTx;
+    if (any && flat && lane < nrows) {
+        const int64_t rb = (int64_t)(y0 + lane) * g.nTx;
         rs0 = off[rb + x0];
         rlen = off[rb + x1 + 1] - rs0;
     }
+    // disk i's lower-index neighbours, compacted by ballot (list order is irrelevant: an OR)
+    int nc = 0;
     if (any) {
-        for (int j = tid; j < i; j += kBlock) {
-            if (sr[j] > 0.0 && disks_may_overlap(cx, cy, r, sx[j], sy[j], sr[j])) {
-                const int q = atomicAdd(&ncnt, 1);   // list order is irrelevant (a boolean OR)
-                if (q < kClosureNbr) nb[q] = j;
-            }
+        for (int j0 = 0; j0 < i; j0 += kWave) {
+            const int j = j0 + lane;
+            const bool hit = j < i && sr[j] > 0.0 && disks_may_overlap(cx, cy, r, sx[j], sy[j], sr[j]);
+            const uint64_t bal = __ballot(hit);
+            const int q = nc + __popcll(bal & ((1ull << lane) - 1));
+            if (hit && q < kClosureNbr) nb[wid][q] = j;
+            nc += __popcll(bal);
         }
     }
-    if (any && flat && tid < kWave) {   // wave 0: the rows' prefix
-        const int incl = wave_incl_scan_i32(rlen, tid);
-        if (tid < nrows) rs[tid] = rs0;
-        rpre[tid + 1] = incl;
-        if (tid == 0) rpre[0] = 0;
+    if (any && flat) {
+        const int incl = wave_incl_scan_i32(rlen, lane);
+        if (lane < nrows) rs[wid][lane] = rs0;
+        rpre[wid][lane + 1] = incl;
+        if (lane == 0) rpre[wid][0] = 0;
     }
     __syncthreads();
-    const int nc = ncnt;
-    if (tid < min(nc, kClosureNbr)) nT[tid] = cover_threshold(sr[nb[tid]]);
+    if (any && lane < min(nc, kClosureNbr)) nT[wid][lane] = cover_threshold(sr[nb[wid][lane]]);
     __syncthreads();
     uint64_t cnt = 0;
     double acc = 0.0;
@@ -116,8 +126,8 @@ __global__ __launch_bounds__(kBlock) void closure_kernel(uint64_t* ts, const dou
         bool owned = true;
         if (nc <= kClosureNbr) {
             for (int q = 0; q < nc && owned; ++q) {
-                const int c2 = nb[q];
-                owned = !(sqdist(p.x, p.y, sx[c2], sy[c2]) <= nT[q]);
+                const int c2 = nb[wid][q];
+                owned = !(sqdist(p.x, p.y, sx[c2], sy[c2]) <= nT[wid][q]);
             }
         } else {   // overflowed list: every lower-index disk
             for (int c2 = 0; c2 < i && owned; ++c2)
@@ -129,30 +139,32 @@ __global__ __launch_bounds__(kBlock) void closure_kernel(uint64_t* ts, const dou
         }
     };
     if (any && flat) {
-        const int total = rpre[nrows];
-        for (int f = tid; f < total; f += kBlock) {
+        const int total = rpre[wid][nrows];
+        for (int f = lane; f < total; f += kWave) {
             int lo = 0, hi = nrows - 1;
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
-                if (rpre[mid] <= f) lo = mid; else hi = mid - 1;
+                if (rpre[wid][mid] <= f) lo = mid; else hi = mid - 1;
             }
-            credit(rs[lo] + (f - rpre[lo]));
+            credit(rs[wid][lo] + (f - rpre[wid][lo]));
         }
     } else if (any) {
         for (int ty = y0; ty <= y1; ++ty) {
             const int64_t rowbase = (int64_t)ty * g.nTx;
-            const int s = off[rowbase + x0], e = off[rowbase + x1 + 1];
-            for (int j = s + tid; j < e; j += kBlock) credit(j);
+            const int s0 = off[rowbase + x0], e0 = off[rowbase + x1 + 1];
+            for (int j = s0 + lane; j < e0; j += kWave) credit(j);
         }
     }
     // the area
     if (counts) {
 #pragma unroll
         for (int off2 = 32; off2 >= 1; off2 >>= 1) cnt += __shfl_xor(cnt, off2, kWave);
-        if (lane == 0) ired[wid] = cnt;
+        if (lane == 0) wcnt[wid] = cnt;
         __syncthreads();
         if (tid == 0) {
-            const uint64_t mine = ired[0] + ired[1] + ired[2] + ired[3];
+            uint64_t mine = 0;
+#pragma unroll
+            for (int q = 0; q < kClosureDisksPerWG; ++q) mine += wcnt[q];
             const uint64_t old = __hip_atomic_fetch_add(o.total, (1ull << 40) | mine, __ATOMIC_RELAXED,
                                                         __HIP_MEMORY_SCOPE_AGENT);
             if ((old >> 40) == (uint64_t)(gridDim.x - 1)) {   // the last arrival: the total
@@ -172,22 +184,23 @@ __global__ __launch_bounds__(kBlock) void closure_kernel(uint64_t* ts, const dou
         ts_end(ts);
         return;
     }
-    const double v = block_sum_f64(acc, dred);   // valid in thread 0
-    unsigned old = 0;
-    if (tid == 0) {
+    const double v = wave_sum_f64(acc);   // disk i's credit (fixed butterfly)
+    if (valid && lane == 0)
         __hip_atomic_store(o.part + i, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (tid == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        old = __hip_atomic_fetch_add(o.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ncnt = (int)old;   // (LDS broadcast of the arrival rank)
+        sarr = (int)__hip_atomic_fetch_add(o.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    if ((unsigned)ncnt != gridDim.x - 1) {   // uniform: not the last workgroup
+    if ((unsigned)sarr != gridDim.x - 1) {   // uniform: not the last workgroup
         ts_end(ts);
         return;
     }
     // the last workgroup: the area over every disk's credit, in disk order per thread then in
     // thread order (fixed), from agent-scope loads of the published credits
+    __shared__ double dred[kWavesPerBlock];
     double a = 0.0;
     for (int j = tid; j < N; j += kBlock)
         a += __builtin_bit_cast(double, __hip_atomic_load(o.part + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));

@@ -2120,25 +2120,26 @@ static int32_t closure_eval(mac_ctx* ctx, const double* circles, int64_t three_n
     }
     const uint64_t seq = ++L->cl_seq;
     HCK(hipMemcpyAsync(L->cands.p, L->h_io.p, in_bytes, hipMemcpyHostToDevice, s));
+    const int nwg = (N + kClosureDisksPerWG - 1) / kClosureDisksPerWG;   // a wave per disk
     int64_t ts_a = -1;
     uint64_t* ts = nullptr;
     if (ctx->profile) {
         std::lock_guard<std::mutex> lk(ctx->mu);
-        if (ctx->stamp_used + N <= ctx->stamp_cap) {
+        if (ctx->stamp_used + nwg <= ctx->stamp_cap) {
             ts_a = ctx->stamp_used;
-            ctx->stamp_used += N;
+            ctx->stamp_used += nwg;
             ts = ctx->stamps.as<uint64_t>() + 2 * ts_a;
         }
     }
     const ClosureOut co{L->cpart.as<unsigned long long>(), L->ctot.as<unsigned long long>(),
                         L->carrive.as<unsigned>(), L->area.as<double>(), L->d_cl, seq};
-    hipLaunchKernelGGL(closure_kernel, dim3((unsigned)N), dim3(kBlock), (uint32_t)closure_lds_bytes(N), s,
+    hipLaunchKernelGGL(closure_kernel, dim3((unsigned)nwg), dim3(kBlock), (uint32_t)closure_lds_bytes(N), s,
                        ts, L->cands.as<double>(), N, ctx->grid, ctx->xys.as<double2>(),
                        ctx->ws.as<double>(), ctx->off.as<int32_t>(), ctx->w_uniform ? 1 : 0, ctx->w0, co);
     HCK(hipGetLastError());
     if (ts) {
         std::lock_guard<std::mutex> lk(ctx->mu);
-        ctx->prof.push_back({ts_a, N, -1, 0, 1, nullptr, MAC_ALGO_TILED});
+        ctx->prof.push_back({ts_a, nwg, -1, 0, 1, nullptr, MAC_ALGO_TILED});
     }
     double a = 0.0;
     int64_t unused = 0;
