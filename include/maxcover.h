@@ -222,7 +222,9 @@ int32_t mac_poll_best_f32(mac_ctx* ctx, const float* cands, int64_t three_n, int
 
 /* ---- device-pointer, stream-ordered variants (inputs already resident in HBM) ----- */
 /* d_cands: 3N x K column-major on the context's device; d_area: K doubles. `stream` is a
- * hipStream_t (NULL = the context's own stream). Returns after enqueueing. */
+ * hipStream_t; NULL is HIP's null stream (as in every HIP API: the work is ordered after the
+ * caller's default-stream work, e.g. torch's default stream, which produced d_cands). Returns
+ * after enqueueing. */
 int32_t mac_area_batch_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three_n, int64_t K,
                                double* d_area, void* stream);
 /* Device poll: d_best receives {best_obj (double), best_idx (int64 stored as double bits)}
@@ -243,7 +245,7 @@ int32_t mac_poll_best_dev_f32(mac_ctx* ctx, const float* d_cands, int64_t three_
  * result for device work, but the poll's launch may still be retiring on `stream` — order later
  * work that reads d_best or reuses the poll's inputs on `stream`, or synchronise it first.
  * Without a slot (a K = 0 poll, or the slot taken by 64 newer d_best buffers) or after 2 ms,
- * it waits for `stream` (NULL = the context's own stream) and copies d_best. Polls on different
+ * it waits for `stream` (NULL: HIP's null stream) and copies d_best. Polls on different
  * d_best buffers may be issued and fetched concurrently from several host threads. */
 int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* best_obj,
                        int64_t* best_idx);
@@ -258,8 +260,12 @@ int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* b
  * armed poll with a ticket <= it); a poll and the armed poll after it use different d_best
  * buffers (each buffer's mapped slot follows its latest poll); nothing may wait for the stream
  * (or the device) while an armed poll on it is not fired — mac_best_fetch of a fired poll never
- * does, and mac_ctx_destroy fires every outstanding ticket first. MAC_E_HIP when the device
- * cannot wait on stream values (hipDeviceAttributeCanUseStreamWaitValue). */
+ * does, and mac_ctx_destroy fires every outstanding ticket first. Argument errors are reported
+ * before anything is enqueued; a poll that fails after its wait went in voids only its own ticket
+ * (released together with the earlier tickets, never ahead of them). Buffers an armed poll grows
+ * are released at the next device synchronisation (point-list changes, mac_ctx_destroy), since
+ * freeing them would wait for the unfired poll. MAC_E_HIP when the device cannot wait on stream
+ * values (hipDeviceAttributeCanUseStreamWaitValue). */
 int32_t mac_poll_arm_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three_n, int64_t K,
                              const double* d_rmax, double penalty,
                              const double* d_prev, const double* d_dlim, double tan_half_fov,

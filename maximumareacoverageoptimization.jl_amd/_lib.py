@@ -181,18 +181,34 @@ def _declare(L: ctypes.CDLL) -> None:
         f.restype = res
 
 
+_loaded_before_torch = False
+
+
 def _one_hip_runtime() -> None:
     """PyTorch-ROCm ships its own HIP and HSA runtimes, which its libraries load by file name. If
-    libmaxcover.so (NEEDED libamdhip64.so.7) were loaded first, it would bind the system runtime
-    and torch would then load a second one in the same process, whose device initialisation fails
-    ("No HIP GPUs are available"; measured on the MI355X box). torch loaded first makes its
-    runtime the process's libamdhip64.so.7, which libmaxcover then shares: one runtime, so the
-    device tensors, streams and RCCL collectives of the torch plumbing (dist.py, bench.py) and
-    the library's launches live in one context. Without torch nothing changes."""
-    try:
+    libmaxcover.so (NEEDED libamdhip64.so.7) is loaded first, it binds the system runtime and a
+    later torch import loads a second one in the same process, whose device initialisation fails
+    ("No HIP GPUs are available"; measured on the MI355X box). With torch loaded first, libmaxcover
+    shares torch's runtime: one context for torch tensors, streams, RCCL and the library.
+
+    So a process that uses both must import torch first. The library does not
+    import torch itself — a CPU-only user does not pay for it, and which runtime binds does not
+    depend silently on whether torch is importable — unless MAXCOVER_TORCH_FIRST=1 asks for it.
+    Whether torch was already loaded is recorded: `check_one_runtime` (called by dist.py before
+    its device collectives) fails loudly instead of letting two runtimes meet."""
+    global _loaded_before_torch
+    import sys
+    if "torch" not in sys.modules and os.environ.get("MAXCOVER_TORCH_FIRST") == "1":
         import torch  # noqa: F401
-    except ImportError:  # pragma: no cover - torch is in this image
-        pass
+    _loaded_before_torch = "torch" not in sys.modules
+
+
+def check_one_runtime() -> None:
+    """Raise if libmaxcover was loaded before torch in this process (two HIP runtimes: torch's
+    device work and the library's would not share a context; see _one_hip_runtime)."""
+    if _lib is not None and _loaded_before_torch:
+        raise MaxCoverError(MAC_E_HIP, "libmaxcover was loaded before torch: import torch before the "
+                            "first libmaxcover call (one HIP runtime per process, INTEGRATION.md)")
 
 
 def load_library(path: str | None = None) -> ctypes.CDLL:
@@ -260,6 +276,22 @@ def _devptr(t) -> int:
     if isinstance(t, int):
         return t
     return int(t.data_ptr())
+
+
+def _stream(stream, device: int) -> int:
+    """hipStream_t handle for a *_dev call. An int is a raw handle (0: HIP's null stream, the C
+    ABI's NULL); a torch stream gives its handle; None follows torch's convention — the current
+    torch stream of the context's device when this process has initialised torch's GPU side (so a
+    poll is ordered after the torch ops that produced its inputs), else HIP's null stream."""
+    if stream is None:
+        import sys
+        torch = sys.modules.get("torch")
+        if torch is not None and torch.cuda.is_initialized():
+            return int(torch.cuda.current_stream(device).cuda_stream)
+        return 0
+    if isinstance(stream, int):
+        return stream
+    return int(stream.cuda_stream)
 
 
 class Context:
@@ -503,7 +535,7 @@ class Context:
         _check(self._L.mac_poll_best_dev_f32(
             self._h, _devptr(d_cands), int(three_n), int(K), _devptr(d_rmax), float(penalty),
             _devptr(d_prev), _devptr(d_dlim), float(tan_half_fov), int(idx_base),
-            _devptr(d_obj), _devptr(d_best), _devptr(stream)))
+            _devptr(d_obj), _devptr(d_best), _stream(stream, self.device)))
 
     # -- native MADS driver
     def mads_run(self, x0, r_max, penalty: float = 1e5, prev=None, d_lim=None,
@@ -535,7 +567,7 @@ class Context:
     # -- device-resident, stream-ordered
     def area_batch_dev(self, d_cands, three_n: int, K: int, d_area, stream=None) -> None:
         _check(self._L.mac_area_batch_dev_f64(self._h, _devptr(d_cands), int(three_n), int(K),
-                                              _devptr(d_area), _devptr(stream)))
+                                              _devptr(d_area), _stream(stream, self.device)))
 
     def poll_best_dev(self, d_cands, three_n: int, K: int, d_rmax, d_best, penalty: float = 1e5,
                       d_prev=None, d_dlim=None, tan_half_fov: float = 1.0, idx_base: int = 0,
@@ -543,7 +575,7 @@ class Context:
         _check(self._L.mac_poll_best_dev_f64(
             self._h, _devptr(d_cands), int(three_n), int(K), _devptr(d_rmax), float(penalty),
             _devptr(d_prev), _devptr(d_dlim), float(tan_half_fov), int(idx_base),
-            _devptr(d_obj), _devptr(d_best), _devptr(stream)))
+            _devptr(d_obj), _devptr(d_best), _stream(stream, self.device)))
 
     def poll_step(self, d_cands, three_n: int, K: int, d_rmax, d_best, penalty: float = 1e5,
                   d_prev=None, d_dlim=None, tan_half_fov: float = 1.0, idx_base: int = 0,
@@ -557,9 +589,9 @@ class Context:
                      _vp(_devptr(d_rmax)), ctypes.c_double(float(penalty)),
                      _vp(_devptr(d_prev)), _vp(_devptr(d_dlim)),
                      ctypes.c_double(float(tan_half_fov)), _i64(int(idx_base)),
-                     _vp(_devptr(d_obj)), _vp(_devptr(d_best)), _vp(_devptr(stream)))
+                     _vp(_devptr(d_obj)), _vp(_devptr(d_best)), _vp(_stream(stream, self.device)))
         bo, bi = ctypes.c_double(), ctypes.c_int64()
-        fetch_args = (h, _vp(_devptr(d_best)), _vp(_devptr(stream)), ctypes.byref(bo),
+        fetch_args = (h, _vp(_devptr(d_best)), _vp(_stream(stream, self.device)), ctypes.byref(bo),
                       ctypes.byref(bi))
         poll, fetch = self._L.mac_poll_best_dev_f64, self._L.mac_best_fetch
 
@@ -583,7 +615,7 @@ class Context:
         _check(self._L.mac_poll_arm_dev_f64(
             self._h, _devptr(d_cands), int(three_n), int(K), _devptr(d_rmax), float(penalty),
             _devptr(d_prev), _devptr(d_dlim), float(tan_half_fov), int(idx_base),
-            _devptr(d_obj), _devptr(d_best), _devptr(stream), ctypes.byref(t)))
+            _devptr(d_obj), _devptr(d_best), _stream(stream, self.device), ctypes.byref(t)))
         return int(t.value)
 
     def poll_fire(self, ticket: int) -> None:
@@ -601,7 +633,7 @@ class Context:
                                   self._L.mac_best_fetch)
         tickets = [ctypes.c_uint64() for _ in polls]
         bo, bi = ctypes.c_double(), ctypes.c_int64()
-        sv = _vp(_devptr(stream))
+        sv = _vp(_stream(stream, self.device))
         arm_args, fetch_args = [], []
         for p, t in zip(polls, tickets):
             arm_args.append((h, _vp(_devptr(p["d_cands"])), _i64(int(p["three_n"])), _i64(int(p["K"])),
@@ -639,7 +671,7 @@ class Context:
         later host reads of d_obj / d_area, and reuse of the poll's inputs (candidates, d_prev,
         d_rmax), must be ordered on ``stream`` or follow a synchronisation of it."""
         bo, bi = ctypes.c_double(), ctypes.c_int64()
-        _check(self._L.mac_best_fetch(self._h, _devptr(d_best), _devptr(stream),
+        _check(self._L.mac_best_fetch(self._h, _devptr(d_best), _stream(stream, self.device),
                                       ctypes.byref(bo), ctypes.byref(bi)))
         return bo.value, bi.value
 

@@ -72,13 +72,23 @@ struct HipError {
 
 // ------------------------------------------------------------------ device buffers
 
+// hipFree / hipHostFree synchronise the device. While an armed poll's stream wait is enqueued
+// ahead of its own launches (mac_poll_arm_dev_f64), a buffer that grows must not be freed there:
+// the wait only opens after the arming call returns, so the device would never drain. Frees on
+// the arming thread go to this list instead ({pointer, pinned}) and are released at the next
+// call that synchronises the device anyway (point-list changes, mac_ctx_destroy).
+static thread_local std::vector<std::pair<void*, bool>>* t_defer_free = nullptr;
+
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
     void reserve(size_t bytes)
     {
         if (bytes <= cap) return;
-        if (p) HCK(hipFree(p));
+        if (p && t_defer_free)
+            t_defer_free->push_back({p, false});
+        else if (p)
+            HCK(hipFree(p));
         p = nullptr;
         cap = 0;
         size_t b = bytes < 256 ? 256 : bytes;
@@ -111,7 +121,10 @@ struct PinnedBuf {
     void reserve(size_t b, unsigned flags = hipHostMallocDefault)
     {
         if (b <= cap) return;
-        if (p) HCK(hipHostFree(p));
+        if (p && t_defer_free)
+            t_defer_free->push_back({p, true});
+        else if (p)
+            HCK(hipHostFree(p));
         p = nullptr;
         cap = 0;
         HCK(hipHostMalloc(&p, b, flags));
@@ -165,11 +178,16 @@ struct mac_ctx {
     uint64_t mirror_want[kMirrorSlots] = {};
     uint64_t mirror_used[kMirrorSlots] = {};
     uint64_t mirror_seq = 0, mirror_clock = 0;
-    hipStream_t dev_stream = nullptr;   // ordered stream for *_dev calls passed stream = NULL
     // armed polls (mac_poll_arm_dev_f64): the doorbell the streams wait on (coherent host memory), the
-    // last ticket armed and the last fired (guarded by mu)
+    // last ticket armed and the last released (the doorbell's value), tickets voided by a failed
+    // arm that are released once every earlier ticket is, and each stream's latest armed ticket
+    // (guarded by mu)
     uint64_t* doorbell = nullptr;
     uint64_t armed = 0, fired = 0;
+    std::vector<uint64_t> voided;
+    std::vector<std::pair<hipStream_t, uint64_t>> armed_on;
+    // buffers an arming call replaced (t_defer_free), freed at the next device synchronisation
+    std::vector<std::pair<void*, bool>> deferred;
 
     int algo = MAC_ALGO_AUTO;
     int shared_mode = MAC_SHARED_AUTO;   // MAC_OPT_SHARED
@@ -207,13 +225,26 @@ struct mac_ctx {
 
 static void set_device(mac_ctx* ctx) { HCK(hipSetDevice(ctx->device)); }
 
-// A lane's scratch may be reused at once by a call on the SAME stream (stream order protects
-// it); on another stream only after the lane's last work has completed.
-static Lane* acquire_lane(mac_ctx* ctx, hipStream_t want)
+// Free the buffers arming calls replaced; only after the device has been synchronised (every
+// armed poll fired and drained).
+static void free_deferred(mac_ctx* ctx)
+{
+    std::vector<std::pair<void*, bool>> v;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        v.swap(ctx->deferred);
+    }
+    for (auto& d : v) (void)(d.second ? hipHostFree(d.first) : hipFree(d.first));
+}
+
+// A lane's scratch may be reused at once by a call ordered on the SAME stream (stream order
+// protects it; `ordered`: the *_dev calls, where `want` may be the null stream 0); on another
+// stream only after the lane's last work has completed.
+static Lane* acquire_lane(mac_ctx* ctx, hipStream_t want, bool ordered = false)
 {
     {
         std::lock_guard<std::mutex> lk(ctx->mu);
-        if (want) {
+        if (ordered) {
             for (size_t i = 0; i < ctx->lanes_free.size(); ++i) {
                 Lane* l = ctx->lanes_free[i];
                 if (l->last == want) {
@@ -249,13 +280,38 @@ static void release_lane(mac_ctx* ctx, Lane* l, hipStream_t used)
 }
 
 // Host-pointer calls: a lane on its own stream (synchronised before return).
-// Device-pointer calls: the caller's stream, or the context's ordered dev stream for NULL.
+// Device-pointer calls: the caller's stream; NULL is HIP's null stream, as in every HIP API, so a
+// poll is ordered after the caller's default-stream work (torch's default stream is that stream).
+// While an armed poll is not fired, no call may free a buffer it outgrows (t_defer_free): the
+// free would wait for the device, which waits for the doorbell.
+struct DeferFrees {
+    mac_ctx* ctx;
+    std::vector<std::pair<void*, bool>> v;
+    bool on = false;
+    explicit DeferFrees(mac_ctx* c) : ctx(c)
+    {
+        {
+            std::lock_guard<std::mutex> lk(ctx->mu);
+            on = ctx->armed > ctx->fired && !t_defer_free;
+        }
+        if (on) t_defer_free = &v;
+    }
+    ~DeferFrees()
+    {
+        if (!on) return;
+        t_defer_free = nullptr;
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        ctx->deferred.insert(ctx->deferred.end(), v.begin(), v.end());
+    }
+};
+
 struct LaneGuard {
     mac_ctx* ctx;
+    DeferFrees df;
     Lane* lane;
     hipStream_t used;
-    explicit LaneGuard(mac_ctx* c) : ctx(c), lane(acquire_lane(c, nullptr)), used(lane->stream) {}
-    LaneGuard(mac_ctx* c, hipStream_t s) : ctx(c), lane(acquire_lane(c, s)), used(s) {}
+    explicit LaneGuard(mac_ctx* c) : ctx(c), df(c), lane(acquire_lane(c, nullptr)), used(lane->stream) {}
+    LaneGuard(mac_ctx* c, hipStream_t s) : ctx(c), df(c), lane(acquire_lane(c, s, true)), used(s) {}
     ~LaneGuard() { release_lane(ctx, lane, used); }
 };
 
@@ -1190,7 +1246,6 @@ int32_t mac_ctx_create(mac_ctx** out, int32_t device)
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         ctx->cus = prop.multiProcessorCount;
     HCK(hipStreamCreateWithFlags(&ctx->setup_stream, hipStreamNonBlocking));
-    HCK(hipStreamCreateWithFlags(&ctx->dev_stream, hipStreamNonBlocking));
     *out = ctx;
     return MAC_OK;
     ABI_END
@@ -1205,6 +1260,7 @@ void mac_ctx_destroy(mac_ctx* ctx)
         ctx->fired = ctx->armed;
     }
     (void)hipDeviceSynchronize();
+    free_deferred(ctx);
     if (ctx->doorbell) (void)hipHostFree(ctx->doorbell);
     ctx->h_mirror.release();
     for (Lane* l : ctx->lanes_all) {
@@ -1232,7 +1288,6 @@ void mac_ctx_destroy(mac_ctx* ctx)
         b->release();
     ctx->stamps.release();
     if (ctx->setup_stream) (void)hipStreamDestroy(ctx->setup_stream);
-    if (ctx->dev_stream) (void)hipStreamDestroy(ctx->dev_stream);
     delete ctx;
 }
 
@@ -1289,6 +1344,7 @@ static int32_t set_points_common(mac_ctx* ctx, int64_t M)
     if (rc) return rc;
     set_device(ctx);
     HCK(hipDeviceSynchronize());  // no evaluation may overlap a point-list change
+    free_deferred(ctx);
     ctx->M = M;
     ctx->has_points = false;
     const size_t b = sizeof(double) * (size_t)std::max<int64_t>(M, 1);
@@ -1395,6 +1451,7 @@ static int32_t append_common(mac_ctx* ctx, const void* x, const void* y, const v
     if (rc) return rc;
     set_device(ctx);
     HCK(hipDeviceSynchronize());  // no evaluation may overlap a point-list change
+    free_deferred(ctx);
     hipStream_t s = ctx->setup_stream;
     const size_t need = sizeof(double) * (size_t)std::max<int64_t>(M0 + m, 1);
     if (need > ctx->x.cap) {      // grow by 1.5x, keeping the existing entries
@@ -1499,6 +1556,7 @@ int32_t mac_covered_flags_f64(mac_ctx* ctx, const double* circles, int64_t three
     set_device(ctx);
     hipStream_t s = ctx->setup_stream;
     HCK(hipDeviceSynchronize());
+    free_deferred(ctx);
     compute_flags(ctx, s, circles, (int)(three_n / 3));
     if (ctx->M > 0 && flags_out)
         HCK(hipMemcpyAsync(flags_out, ctx->flags_o.p, ctx->M, hipMemcpyDeviceToHost, s));
@@ -1517,6 +1575,7 @@ int32_t mac_remove_covered_f64(mac_ctx* ctx, const double* circles, int64_t thre
     set_device(ctx);
     hipStream_t s = ctx->setup_stream;
     HCK(hipDeviceSynchronize());
+    free_deferred(ctx);
     const int64_t M = ctx->M;
     compute_flags(ctx, s, circles, (int)(three_n / 3));
     int64_t kept = M;
@@ -2239,7 +2298,7 @@ int32_t mac_area_batch_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t thre
     if (K == 0) return MAC_OK;
     if (!d_cands || !d_area) return fail(MAC_E_INVAL, "null device pointer");
     set_device(ctx);
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->dev_stream;
+    hipStream_t s = (hipStream_t)stream;   // NULL: HIP's null stream
     LaneGuard lg(ctx, s);
     const int N = (int)(three_n / 3);
     enqueue_eval(ctx, lg.lane, s, matrix_src(d_cands, N), N, (int)K, use_tiled(ctx, N, nullptr, three_n), nullptr,
@@ -2250,6 +2309,19 @@ int32_t mac_area_batch_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t thre
 
 }  // extern "C" (the template below has C++ linkage)
 
+// The argument checks of a device poll (every failure a device poll can report before it
+// enqueues anything but a HIP error): an armed poll runs them before its stream wait goes in.
+static int32_t poll_dev_check(mac_ctx* ctx, const void* d_cands, int64_t three_n, int64_t K,
+                              const void* d_prev, const double* d_dlim, const void* d_best)
+{
+    int32_t rc = check_common(ctx, three_n, K);
+    if (rc) return rc;
+    if (!d_best) return fail(MAC_E_INVAL, "null d_best");
+    if (K > 0 && !d_cands) return fail(MAC_E_INVAL, "null d_cands");
+    if (d_prev && !d_dlim) return fail(MAC_E_INVAL, "d_prev given without d_dlim");
+    return MAC_OK;
+}
+
 template <class T>
 static int32_t poll_best_dev(mac_ctx* ctx, const T* d_cands_in, int64_t three_n, int64_t K,
                              const double* d_rmax, double penalty, const T* d_prev_in,
@@ -2257,12 +2329,10 @@ static int32_t poll_best_dev(mac_ctx* ctx, const T* d_cands_in, int64_t three_n,
                              double* d_obj, void* d_best, void* stream)
 {
     constexpr bool f32 = std::is_same<T, float>::value;
-    int32_t rc = check_common(ctx, three_n, K);
+    int32_t rc = poll_dev_check(ctx, d_cands_in, three_n, K, d_prev_in, d_dlim, d_best);
     if (rc) return rc;
-    if (!d_best) return fail(MAC_E_INVAL, "null d_best");
-    if (K > 0 && !d_cands_in) return fail(MAC_E_INVAL, "null d_cands");
     set_device(ctx);
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->dev_stream;
+    hipStream_t s = (hipStream_t)stream;   // NULL: HIP's null stream
     LaneGuard lg(ctx, s);
     Lane* L = lg.lane;
     const int N = (int)(three_n / 3);
@@ -2297,7 +2367,6 @@ static int32_t poll_best_dev(mac_ctx* ctx, const T* d_cands_in, int64_t three_n,
     // cons3: the raw d_lim goes down the chain; the kernels that read it threshold it once per
     // UAV (k_prep.h pen_threshold)
     const double* d_dlimT = nullptr;
-    if (d_prev && !d_dlim) return fail(MAC_E_INVAL, "d_prev given without d_dlim");
     double* d_o = d_obj;
     if (!d_o) {
         L->obj.reserve(sizeof(double) * K);
@@ -2349,6 +2418,24 @@ int32_t mac_poll_best_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three
     ABI_END
 }
 
+// Release tickets up to t (the doorbell's value), then every voided ticket that follows
+// (guarded by mu).
+static void release_tickets(mac_ctx* ctx, uint64_t t)
+{
+    if (t > ctx->fired) ctx->fired = t;
+    for (bool more = true; more;) {
+        more = false;
+        for (size_t q = 0; q < ctx->voided.size(); ++q)
+            if (ctx->voided[q] <= ctx->fired + 1) {
+                ctx->fired = std::max(ctx->fired, ctx->voided[q]);
+                ctx->voided.erase(ctx->voided.begin() + (long)q);
+                more = true;
+                break;
+            }
+    }
+    __atomic_store_n(ctx->doorbell, ctx->fired, __ATOMIC_RELEASE);
+}
+
 int32_t mac_poll_arm_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three_n, int64_t K,
                              const double* d_rmax, double penalty, const double* d_prev,
                              const double* d_dlim, double tan_half_fov, int64_t idx_base,
@@ -2357,8 +2444,11 @@ int32_t mac_poll_arm_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three_
     ABI_BEGIN
     if (!ctx || !ticket) return fail(MAC_E_INVAL, "null context / ticket");
     if (K <= 0) return fail(MAC_E_INVAL, "an armed poll needs K > 0");   // (K = 0 synchronises)
+    // every argument failure is reported before the wait goes into the stream
+    int32_t rc = poll_dev_check(ctx, d_cands, three_n, K, d_prev, d_dlim, d_best);
+    if (rc) return rc;
     set_device(ctx);
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->dev_stream;
+    hipStream_t s = (hipStream_t)stream;   // NULL: HIP's null stream
     uint64_t t = 0;
     {
         std::lock_guard<std::mutex> lk(ctx->mu);
@@ -2375,22 +2465,38 @@ int32_t mac_poll_arm_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three_
             ctx->armed = ctx->fired = 0;
         }
         t = ++ctx->armed;
+        bool found = false;
+        for (auto& a : ctx->armed_on)
+            if (a.first == s) {
+                a.second = t;
+                found = true;
+            }
+        if (!found) ctx->armed_on.push_back({s, t});
     }
     *ticket = t;
-    int32_t rc = MAC_OK;
+    // buffers the poll grows are not freed here (hipFree would wait for the device, which waits
+    // for this ticket): they are kept until the next device synchronisation
+    std::vector<std::pair<void*, bool>> defer;
+    t_defer_free = &defer;
+    bool ok = false;
     try {
         HCK(hipStreamWaitValue64(s, ctx->doorbell, t, hipStreamWaitValueGte, ~(uint64_t)0));
         rc = poll_best_dev<double>(ctx, d_cands, three_n, K, d_rmax, penalty, d_prev, d_dlim,
                                    tan_half_fov, idx_base, d_obj, d_best, stream);
+        ok = rc == MAC_OK;
     } catch (...) {
         rc = -1;
     }
-    if (rc) {   // the poll did not go in: its ticket is released at once
-        std::lock_guard<std::mutex> lk(ctx->mu);
-        if (t > ctx->fired) {
-            __atomic_store_n(ctx->doorbell, t, __ATOMIC_RELEASE);
-            ctx->fired = t;
-        }
+    t_defer_free = nullptr;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->deferred.insert(ctx->deferred.end(), defer.begin(), defer.end());
+    if (!ok) {
+        // the poll did not go in: only its own ticket is released (now if every earlier one is,
+        // else together with the last of them), never an earlier armed poll's
+        if (t == ctx->fired + 1)
+            release_tickets(ctx, t);
+        else
+            ctx->voided.push_back(t);
         if (rc < 0) return fail(MAC_E_HIP, "arming the poll failed");
     }
     return rc;
@@ -2402,10 +2508,7 @@ int32_t mac_poll_fire(mac_ctx* ctx, uint64_t ticket)
     if (!ctx) return fail(MAC_E_INVAL, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (!ctx->doorbell || ticket > ctx->armed) return fail(MAC_E_INVAL, "ticket was not armed");
-    if (ticket > ctx->fired) {
-        __atomic_store_n(ctx->doorbell, ticket, __ATOMIC_RELEASE);
-        ctx->fired = ticket;
-    }
+    if (ticket > ctx->fired) release_tickets(ctx, ticket);
     return MAC_OK;
 }
 
@@ -2427,10 +2530,10 @@ int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* b
     if (!ctx) return fail(MAC_E_INVAL, "null context");
     if (!d_best) return fail(MAC_E_INVAL, "null d_best");
     set_device(ctx);
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->dev_stream;
+    hipStream_t s = (hipStream_t)stream;   // NULL: HIP's null stream
     const uint64_t* slot = nullptr;
     uint64_t want = 0;
-    bool pending = false;   // an armed poll is not fired: the stream must not be waited for
+    bool pending = false;   // an armed poll on `stream` is not fired: it must not be waited for
     {
         std::lock_guard<std::mutex> lk(ctx->mu);   // (released before any wait)
         for (int q = 0; q < mac_ctx::kMirrorSlots; ++q)
@@ -2439,7 +2542,8 @@ int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* b
                 want = ctx->mirror_want[q];
                 break;
             }
-        pending = ctx->armed > ctx->fired;
+        for (auto& a : ctx->armed_on)   // an armed poll on THIS stream is not fired
+            pending = pending || (a.first == s && a.second > ctx->fired);
     }
     if (slot) {
         // the latest device poll on d_best writes its result into this slot (the poll takes

@@ -19,6 +19,8 @@ from __future__ import annotations
 
 import numpy as np
 
+from ._lib import check_one_runtime
+
 
 def shard_range(K: int, rank: int, world: int) -> tuple[int, int]:
     """Contiguous slice of the K candidates owned by `rank` (balanced to within one)."""
@@ -82,6 +84,8 @@ class PollGather:
         self.world = dist.get_world_size(group)
         self.device = torch.device(device)
         self.on_device = self.device.type == "cuda"
+        if self.on_device:
+            check_one_runtime()
         pin = torch.cuda.is_available()
         self.out = torch.empty((self.world, 2), dtype=torch.float64, device=self.device)
         self.host = (torch.empty((self.world, 2), dtype=torch.float64, pin_memory=pin)
@@ -128,6 +132,8 @@ class DeviceGather:
         self.world = dist.get_world_size(group)
         self.device = torch.device(device)
         self.on_device = self.device.type == "cuda"
+        if self.on_device:
+            check_one_runtime()
         self.best = torch.zeros(2, dtype=torch.float64, device=self.device)
         self.out = torch.empty((self.world, 2), dtype=torch.float64, device=self.device)
         self.host = (torch.empty((self.world, 2), dtype=torch.float64, pin_memory=True)
@@ -173,6 +179,8 @@ def broadcast_points(x=None, y=None, w=None, src: int = 0, device="cpu", group=N
     import torch.distributed as dist
 
     dev = torch.device(device)
+    if dev.type == "cuda":
+        check_one_runtime()
     rank = dist.get_rank(group)
     n = torch.zeros(1, dtype=torch.int64, device=dev)
     if rank == src:

@@ -5,6 +5,9 @@ import sys
 
 import numpy as np
 import pytest
+# torch before libmaxcover: one HIP runtime per process (the GPU tests mix torch tensors and
+# streams with the library's launches; _lib.check_one_runtime)
+import torch  # noqa: F401,E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:

@@ -55,8 +55,8 @@ def test_poll_gather_over_rccl(nccl1, ctx, pkg):
     d_best = torch.empty(2, dtype=torch.float64, device=nccl1)
     gather = d.PollGather(nccl1)
     out_ptr = gather.out.data_ptr()
-    # the polls and the gather on one stream of the caller's (as bench.py's ranks do; stream NULL
-    # would mean the context's own stream, include/maxcover.h, not torch's legacy default stream)
+    # the polls and the gather on one stream of the caller's (as bench.py's ranks do); the
+    # default-stream variant is the next test
     s = torch.cuda.Stream(nccl1)
     with torch.cuda.stream(s):
         for t in range(5):
@@ -67,6 +67,38 @@ def test_poll_gather_over_rccl(nccl1, ctx, pkg):
             got = gather(d_best)
             assert got == (want[0], want[1]), (t, got, want)
     assert gather.calls == 5 and gather.out.data_ptr() == out_ptr
+
+
+def test_poll_gather_over_rccl_default_stream(nccl1, ctx, pkg):
+    """The same exchange with no stream of the caller's: the candidates are copied, the poll
+    enqueued (stream=None) and the all-gather issued on torch's default stream, with no
+    synchronisation in between. stream=None is torch's current stream, which here is HIP's null
+    stream — the C ABI's NULL (include/maxcover.h) — so the poll is ordered after the copy of its
+    candidates and before the all-gather that reads its d_best. (Round 4 mapped NULL to a private
+    stream of the context: this exact sequence returned another poll's argmin at poll 4.)"""
+    import torch
+
+    d = import_module(pkg.__name__ + ".dist")
+    wl = pkg.workloads
+    x, y, w = wl.grid_points(256)
+    ctx.set_points(x, y, w)
+    rng = wl.SplitMix64(71)
+    N = 16
+    rmax = np.full(N, 30.0 * TAN50)
+    d_rmax = torch.from_numpy(rmax).to(nccl1)
+    d_best = torch.empty(2, dtype=torch.float64, device=nccl1)
+    gather = d.PollGather(nccl1)
+    assert torch.cuda.current_stream(nccl1).cuda_stream == 0
+    for t in range(6):
+        C = wl.poll_candidates(wl.uniform_disks(N, 256, rng), rng)
+        want = ctx.poll_best(C, rmax)
+        d_c = torch.from_numpy(np.ascontiguousarray(C)).to(nccl1)
+        ctx.poll_best_dev(d_c, 3 * N, C.shape[0], d_rmax, d_best)          # stream=None
+        got = gather(d_best)
+        assert got == (want[0], want[1]), (t, got, want)
+        # the raw C NULL (an int 0 handle) is the same stream
+        ctx.poll_best_dev(d_c, 3 * N, C.shape[0], d_rmax, d_best, stream=0)
+        assert gather(d_best) == (want[0], want[1]), t
 
 
 def test_sharded_mads_loop_over_rccl(nccl1, ctx, pkg):

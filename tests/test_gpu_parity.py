@@ -322,6 +322,42 @@ def test_device_pointer_api(ctx, pkg, orc):
         assert st2() == (w2.min(), int(np.argmin(w2)))
 
 
+def test_null_stream_orders_after_default_stream_producer(ctx, pkg, orc):
+    """A caller that writes d_cands with torch ops on the default stream — queued behind a long
+    default-stream job, so the candidates land late — and then polls with stream=None and fetches
+    with stream=None, with no synchronisation anywhere: every poll reads the candidates the
+    default stream wrote (NULL / None = HIP's null stream, ordered with torch's default stream;
+    include/maxcover.h). Checked against the oracle's objectives."""
+    import torch
+    wl = pkg.workloads
+    rng = wl.SplitMix64(93)
+    x, y, w = wl.grid_points(160)
+    ctx.set_points(x, y, w)
+    dev = torch.device("cuda", ctx.device)
+    torch.cuda.synchronize(dev)
+    assert torch.cuda.current_stream(dev).cuda_stream == 0
+    rec = recs(x, y, w)
+    N = 12
+    rmax = np.full(N, 35.0)
+    tR = torch.from_numpy(rmax).to(dev)
+    tB = torch.empty(2, dtype=torch.float64, device=dev)
+    big = torch.randn(4096, 4096, device=dev)
+    for t in range(4):
+        C = wl.poll_candidates(wl.uniform_disks(N, 160, rng), rng)
+        wobj = np.array([orc.ref_objective(c, rec, rmax) for c in C])
+        src = torch.from_numpy(C).pin_memory()
+        tC = torch.zeros(C.shape, dtype=torch.float64, device=dev)
+        for _ in range(3):
+            big = big @ big.T / 4096.0                # keeps the default stream busy
+        tC.copy_(src, non_blocking=True)               # lands after the matmuls
+        tC.add_(big[0, 0] * 0.0)                       # a dependent kernel on the default stream
+        ctx.poll_best_dev(tC, 3 * N, C.shape[0], tR, tB)
+        got = ctx.best_fetch(tB)
+        k = int(np.argmin(wobj))
+        assert got == (wobj[k], k), (t, got, (wobj[k], k))
+        del tC                                         # (freed after the poll: stream order)
+
+
 def test_concurrent_device_polls(ctx, pkg, orc):
     """Two host threads, each with its own stream and d_best, issue mac_poll_best_dev_f64 +
     mac_best_fetch on one context (DirectSearch SetMaxEvals, src/TDM_STATIC_opt.jl:129): every
@@ -1127,3 +1163,48 @@ def test_armed_polls_match_plain_polls(pkg):
         ctx2.set_points(x, y, w)
         ctx2.poll_arm(d_polls[0], 3 * N, K, d_rmax, bests[1], stream=stream.cuda_stream)
     torch.cuda.synchronize()
+
+
+def test_armed_poll_grows_lane_buffers(pkg):
+    """An armed poll larger than anything its lane has run (more candidates and more UAVs: every
+    scratch buffer grows inside the arming call). Freeing the old buffers there would wait for the
+    device, which waits for the unfired ticket: the buffers are released at the next device
+    synchronisation instead (include/maxcover.h). The results equal plain polls'. An argument error
+    is reported before anything is enqueued and takes no ticket, and a plain poll on another
+    stream runs and is fetched while an armed poll is pending."""
+    import torch
+    wl = pkg.workloads
+    x, y, w = wl.grid_points(192)
+    rng = wl.SplitMix64(809)
+    dev = torch.device("cuda", 0)
+    shapes = (4, 24, 40)                                   # N, growing
+    polls = [wl.poll_candidates(wl.uniform_disks(n, 192, rng), rng) for n in shapes]
+    with pkg.Context(0) as ref:
+        ref.set_points(x, y, w)
+        want = [ref.poll_best(p, np.full(p.shape[1] // 3, 36.0)) for p in polls]
+    d_polls = [torch.from_numpy(np.ascontiguousarray(p)).to(dev) for p in polls]
+    d_rmax = [torch.full((p.shape[1] // 3,), 36.0, dtype=torch.float64, device=dev) for p in polls]
+    bests = [torch.empty(2, dtype=torch.float64, device=dev) for _ in polls]
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
+    with pkg.Context(0) as ctx:
+        ctx.set_points(x, y, w)
+        got = []
+        for j, p in enumerate(polls):
+            t = ctx.poll_arm(d_polls[j], p.shape[1], p.shape[0], d_rmax[j], bests[j],
+                             stream=s1.cuda_stream)
+            with pytest.raises(pkg.MaxCoverError):     # checked before anything is enqueued
+                ctx.poll_arm(d_polls[j], p.shape[1], p.shape[0], d_rmax[j], None,
+                             stream=s1.cuda_stream)
+            if j == 1:   # a plain poll on another stream while ticket t is pending
+                ctx.poll_best_dev(d_polls[0], polls[0].shape[1], polls[0].shape[0], d_rmax[0],
+                                  bests[0], stream=s2.cuda_stream)
+                assert ctx.best_fetch(bests[0], stream=s2.cuda_stream) == want[0]
+            ctx.poll_fire(t)
+            got.append(ctx.best_fetch(bests[j], stream=s1.cuda_stream))
+        assert got == want
+        ctx.set_points(x, y, w)          # (a device synchronisation: deferred frees released)
+        ctx.poll_best_dev(d_polls[2], polls[2].shape[1], polls[2].shape[0], d_rmax[2], bests[2],
+                          stream=s1.cuda_stream)
+        assert ctx.best_fetch(bests[2], stream=s1.cuda_stream) == want[2]
+    torch.cuda.synchronize(dev)
