@@ -61,6 +61,13 @@ extern "C" {
 #define MAC_OPT_SHARED       5  /* poll walk, entries two disks' regions share:
                                    MAC_SHARED_AUTO (default) | _FP64 | _BITS                      */
 
+#define MAC_OPT_CHAIN        6  /* the poll chain: MAC_CHAIN_AUTO (default) | _FIVE | _FUSED */
+
+#define MAC_CHAIN_AUTO   0  /* the fused three-launch chain unless one of the lane's last 8 polls was crowded,
+                               scattered or off the packed-key grid (then the five-launch chain)  */
+#define MAC_CHAIN_FIVE   1  /* always the five-launch chain (prep, index, set-up, walk, finalize)   */
+#define MAC_CHAIN_FUSED  2  /* the fused chain whenever it applies (K <= 3073, packed keys possible) */
+
 #define MAC_SHARED_AUTO  0  /* bit-word kernel when one of the lane's last 8 polls had more than 16
                                disks with neighbours, else fp64 jobs in the poll kernel         */
 #define MAC_SHARED_FP64  1  /* always the poll kernel's fp64 jobs                                */
@@ -294,8 +301,10 @@ int32_t mac_profile_split(mac_ctx* ctx, double* prep_ms, double* walk_ms, double
  * launch role r < n_roles, the summed launch spans (last workgroup end - first workgroup start,
  * in-kernel stamps) in ms_out[r] and the launches counted in launches_out[r]. Roles:
  *   0 prep_kernel, 1 disk_index_kernel, 2 walk_setup_kernel, 3 coverage_tiled_poll_kernel,
- *   4 coverage_poll_kernel, 5 shared_bits_kernel, 6 finalize_kernel (MAC_PROF_ROLES = 7). */
-#define MAC_PROF_ROLES 7
+ *   4 coverage_poll_kernel, 5 the crowded-poll shared-entry pass (shared_or_kernel on equal
+ *   weights, shared_bits_kernel otherwise), 6 finalize_kernel (five-launch chain), 7 fiw_kernel and
+ *   8 fin2_kernel (the fused chain) (MAC_PROF_ROLES = 9). */
+#define MAC_PROF_ROLES 9
 int32_t mac_profile_kernels(mac_ctx* ctx, double* ms_out, int64_t* launches_out, int32_t n_roles);
 
 /* ---- fire generator (src/DynamicArea.jl, config 5) ------------------------------ */

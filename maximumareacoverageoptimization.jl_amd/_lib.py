@@ -29,7 +29,9 @@ MAC_OPT_STORAGE = 2
 MAC_OPT_TILE_POINTS = 3
 MAC_OPT_PROFILE = 4
 MAC_OPT_SHARED = 5
+MAC_OPT_CHAIN = 6
 SHARED_MODES = {"auto": 0, "fp64": 1, "bits": 2}
+CHAINS = {"auto": 0, "five": 1, "fused": 2}
 MAC_ALGO_AUTO = 0
 MAC_ALGO_SCAN = 1
 MAC_ALGO_TILED = 2
@@ -37,9 +39,12 @@ MAC_ALGO_POLL = 3
 MAC_STORE_F64 = 0
 MAC_STORE_F32 = 1
 
-# mac_profile_kernels launch roles (include/maxcover.h MAC_PROF_ROLES)
+# mac_profile_kernels launch roles (include/maxcover.h MAC_PROF_ROLES). Role 5 is one stamp slot
+# for the crowded-poll shared-entry pass: the union pass (shared_or_kernel) on equal weights — every
+# reference data set — else the bit-word kernel (shared_bits_kernel)
 PROF_ROLES = ("prep_kernel", "disk_index_kernel", "walk_setup_kernel", "coverage_tiled_poll_kernel",
-              "coverage_poll_kernel", "shared_bits_kernel", "finalize_kernel")
+              "coverage_poll_kernel", "shared_or_kernel", "finalize_kernel", "fiw_kernel",
+              "fin2_kernel")
 
 ALGOS = {"auto": MAC_ALGO_AUTO, "scan": MAC_ALGO_SCAN, "tiled": MAC_ALGO_TILED,
          "poll": MAC_ALGO_POLL}
@@ -334,6 +339,12 @@ class Context:
         """How the poll walk decides the entries two disks' regions share (MAC_OPT_SHARED):
         "auto" (default), "fp64" (the poll kernel's jobs) or "bits" (the bit-word kernel)."""
         self.set_option(MAC_OPT_SHARED, SHARED_MODES[mode])
+
+    def set_chain(self, chain: str) -> None:
+        """The poll chain (MAC_OPT_CHAIN): "auto" (default: the fused three-launch chain unless the
+        lane's recent polls were crowded, scattered or off the packed-key grid), "five" (prep, index,
+        set-up, walk, finalize) or "fused" (prep, fiw, fin2 whenever it applies)."""
+        self.set_option(MAC_OPT_CHAIN, CHAINS[chain])
 
     def set_algo(self, algo: str) -> None:
         if algo not in ALGOS:

@@ -130,17 +130,20 @@ __device__ __forceinline__ void argmin_take(double& v1, int& i1, double v2, int 
 // waits for them (vmcnt(0)), then adds to ONE counter; the block whose add returns the last count
 // loads every minimum with sc1 loads, in the same wave. The lexicographic (objective, index)
 // minimum is order-independent (the sequential first-best order); NaN / +inf never selected.
-__device__ __forceinline__ void finalize_argmin(const FinBest& fb, double o, int k, bool have)
+// C: lanes holding the block's candidates (a power of two <= 64). Returns true in the last block.
+template <int C = kFinC>
+__device__ __forceinline__ bool finalize_argmin(const FinBest& fb, double o, int k, bool have)
 {
+    static_assert(C >= 1 && C <= kWave && (C & (C - 1)) == 0, "C: a power of two up to a wave");
     const int lane = threadIdx.x & (kWave - 1);
     double bv = __builtin_inf();
     int bi = -1;
-    if (have && lane < kFinC && o < bv) {
+    if (have && lane < C && o < bv) {
         bv = o;
         bi = k;
     }
 #pragma unroll
-    for (int off = kFinC / 2; off >= 1; off >>= 1)
+    for (int off = C / 2; off >= 1; off >>= 1)
         argmin_take(bv, bi, __shfl_xor(bv, off, kWave), __shfl_xor(bi, off, kWave));
     unsigned old = 0;
     if (lane == 0) {
@@ -152,7 +155,7 @@ __device__ __forceinline__ void finalize_argmin(const FinBest& fb, double o, int
         old = __hip_atomic_fetch_add(fb.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     old = __shfl(old, 0, kWave);
-    if (old != gridDim.x - 1) return;   // wave-uniform: not the last block
+    if (old != gridDim.x - 1) return false;   // wave-uniform: not the last block
     // the pipelined MADS loop's state, loaded beside the minima (a stopped loop: no result)
     const int ell = fb.st ? fb.st->ell : 0;
     const double fcur = fb.st ? fb.st->f : 0.0;
@@ -186,7 +189,7 @@ __device__ __forceinline__ void finalize_argmin(const FinBest& fb, double o, int
     const int64_t gidx = bi >= 0 ? fb.idx_base + bi : (int64_t)-1;
     if (fb.st && ell < 0) {   // the loop stopped before this poll
         if (lane == 0) __hip_atomic_store(fb.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
+        return true;
     }
     if (fb.st) mads_step(fb, bo, gidx, ell, fcur);
     if (lane == 0) {
@@ -213,6 +216,7 @@ __device__ __forceinline__ void finalize_argmin(const FinBest& fb, double o, int
             if (fb.st && !(gidx >= 0 && bo < fcur) && ell == 0) fb.mirror[2] = fb.done_seq;
         }
     }
+    return true;
 }
 
 __global__ __launch_bounds__(kFinThreads) void finalize_kernel(

@@ -80,7 +80,8 @@ __device__ uint64_t g_diag_walk[8 * 65536];   // walk role, grid row 0: per-disk
 // Hot loop of the poll walk over this wave's groups of 4 staged entries (q4 = w, w + 4, ...):
 // NP candidate pairs per entry pair, per 2 entries x 2 candidates six packed fmas, two packed
 // clamps (count), two packed adds and two v_min3 (band detector). h[j]: covered counts of pair j.
-template <int NP>
+// NW: the waves splitting the groups (wave w takes groups w, w + NW, ...).
+template <int NP, int NW = kPollWaves>
 __device__ __forceinline__ void poll_hot(const float4* __restrict__ s32, int ng, int w,
                                          const f32x2 (&sa)[kPollPairs], const f32x2 (&sb)[kPollPairs],
                                          const f32x2 (&st)[kPollPairs], const f32x2 (&ns)[kPollPairs],
@@ -100,7 +101,7 @@ __device__ __forceinline__ void poll_hot(const float4* __restrict__ s32, int ng,
         bmin[2 * J + 1] = __builtin_fminf(__builtin_fminf(bmin[2 * J + 1], __builtin_fabsf(d0.y)), \
                                           __builtin_fabsf(d1.y));                              \
     }
-    for (int q4 = w; q4 < ng; q4 += kPollWaves) {
+    for (int q4 = w; q4 < ng; q4 += NW) {
         const float4 e0 = s32[4 * q4], e1 = s32[4 * q4 + 1], e2 = s32[4 * q4 + 2], e3 = s32[4 * q4 + 3];
 #pragma unroll
         for (int j = 0; j < NP; ++j) {

@@ -180,6 +180,12 @@ struct PrepArgs {
     uint32_t* keysP;           // packed keys (null: none), one row per disk, pitch ldk
     float* keysT;              // fp32 keys of escaped values, 3N rows of pitch ldk
     int ldk;
+    // the fused chain (k_fiw.h; null: none): per workgroup the largest displacement of a disk from
+    // candidate 0's over its live candidates {max |x - x0|, max |y - y0|, max r - r0, max r0 - r}
+    // (keysP needed; a NaN difference counts as +inf),
+    // and one byte per candidate: 1 when it fails cons3 and is left out (skip_failed, N <= kPrepU)
+    double4* pd;
+    uint8_t* dead8;
 };
 
 // Packed keys. Disk i of candidate k is keyed by its offsets (dx, dy, dr) from candidate 0's
@@ -282,7 +288,9 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
     // cover. With one block of UAVs (N <= kPrepU) their failure is known before the records are
     // written, so the records leave them out (the regions, and with them the walks' work, shrink
     // to the feasible candidates; the index maps them to an inert position, k_index.h). Uniform.
-    const bool excl = obj && pa.prev && a.prec && a.skip_failed && N <= kPrepU;
+    const bool excl = obj && pa.prev && (a.prec || a.pd) && a.skip_failed && N <= kPrepU;
+    double dmx = -__builtin_inf(), dmy = -__builtin_inf(), dmr = -__builtin_inf();   // (pd)
+    double dml = -__builtin_inf();   // (pd) max r0 - r
     uint32_t dead = 0u;   // (excl) bit c: candidate c fails cons3 (0 otherwise)
     for (int ib = 0; ib < N; ib += kPrepU) {
         const int nb = min(kPrepU, N - ib);
@@ -353,7 +361,28 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
 #pragma unroll
             for (int w = 0; w < kPrepU / kWave; ++w) dead |= wbadm[w];
         }
-        if (a.prec && iv) {
+        if (a.pd && a.keysP && iv) {
+            // the fused chain's displacement bound (k_fiw.h sup_box): over this workgroup's live
+            // candidates (the ones the records below would take), a NaN difference counts as +inf
+#pragma unroll
+            for (int c = 0; c < kPrepC; ++c) {
+                const double x = v[c][0], y = v[c][1], r = v[c][2];
+                if (cand(c) < K && !((dead >> c) & 1u) && r > 0.0 && __builtin_isfinite(x) &&
+                    __builtin_isfinite(y)) {
+                    double ex = __builtin_fabs(x - base[0]), ey = __builtin_fabs(y - base[1]), er = r - base[2];
+                    double el = base[2] - r;
+                    if (!(ex <= kDblMax)) ex = __builtin_inf();
+                    if (!(ey <= kDblMax)) ey = __builtin_inf();
+                    if (!(er == er)) er = __builtin_inf();
+                    if (!(el == el)) el = __builtin_inf();
+                    dmx = fmax(dmx, ex);
+                    dmy = fmax(dmy, ey);
+                    dmr = fmax(dmr, er);
+                    dml = fmax(dml, el);
+                }
+            }
+        }
+        if ((a.prec || a.keysP) && iv) {
             double xa = __builtin_inf(), xb = -__builtin_inf(), ya = __builtin_inf(), yb = -__builtin_inf();
             double xm = 0.0, ym = 0.0, est = 0.0;
             bool any = false;
@@ -398,13 +427,15 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
                     *reinterpret_cast<uint4*>(a.keysP + (int64_t)i * a.ldk + cand(4 * h)) =
                         make_uint4(pk[4 * h], pk[4 * h + 1], pk[4 * h + 2], pk[4 * h + 3]);
             }
-            int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
-            any = any && partial_range(xa, xb, xm, a.g.gx0, a.g.invS, a.g.nTx, x0, x1) &&
-                  partial_range(ya, yb, ym, a.g.gy0, a.g.invS, a.g.nTy, y0, y1);
-            a.prec[(int64_t)cw * N + i] =
-                make_int4((int)range_pack(any, x0, x1, range_shift(a.g.nTx)),
-                          (int)range_pack(any, y0, y1, range_shift(a.g.nTy)),
-                          __builtin_bit_cast(int, (float)est), kb ? 1 : 0);
+            if (a.prec) {
+                int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
+                any = any && partial_range(xa, xb, xm, a.g.gx0, a.g.invS, a.g.nTx, x0, x1) &&
+                      partial_range(ya, yb, ym, a.g.gy0, a.g.invS, a.g.nTy, y0, y1);
+                a.prec[(int64_t)cw * N + i] =
+                    make_int4((int)range_pack(any, x0, x1, range_shift(a.g.nTx)),
+                              (int)range_pack(any, y0, y1, range_shift(a.g.nTy)),
+                              __builtin_bit_cast(int, (float)est), kb ? 1 : 0);
+            }
         }
         MAC_PREP_STAMP(2 + 3 * (ib / kPrepU));
         if (obj) {
@@ -430,8 +461,36 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
         MAC_PREP_STAMP(3 + 3 * (ib / kPrepU));
         if (obj && ib + kPrepU < N) lds_barrier();   // the fold has read the terms
     }
-    if (obj && u < kPrepC && cand(u) < K)
+    if (obj && u < kPrepC && cand(u) < K) {
         a.vp[cand(u)] = bad ? __builtin_inf() : acc * a.penalty;
+        if (a.dead8) a.dead8[cand(u)] = excl && bad ? 1 : 0;
+    }
+    if (a.pd) {   // the workgroup's displacement bound: wave butterflies, then waves in order
+        __shared__ double dred[kPrepU / kWave][4];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            dmx = fmax(dmx, __shfl_xor(dmx, o, kWave));
+            dmy = fmax(dmy, __shfl_xor(dmy, o, kWave));
+            dmr = fmax(dmr, __shfl_xor(dmr, o, kWave));
+            dml = fmax(dml, __shfl_xor(dml, o, kWave));
+        }
+        if (lane == 0) {
+            dred[wid][0] = dmx;
+            dred[wid][1] = dmy;
+            dred[wid][2] = dmr;
+            dred[wid][3] = dml;
+        }
+        __syncthreads();
+        if (u == 0) {
+            for (int q = 1; q < kPrepU / kWave; ++q) {
+                dmx = fmax(dmx, dred[q][0]);
+                dmy = fmax(dmy, dred[q][1]);
+                dmr = fmax(dmr, dred[q][2]);
+                dml = fmax(dml, dred[q][3]);
+            }
+            a.pd[cw] = make_double4(dmx, dmy, dmr, dml);
+        }
+    }
 }
 
 __global__ __launch_bounds__(kPrepU) __attribute__((amdgpu_waves_per_eu(4))) void prep_kernel(uint64_t* ts, PrepArgs a)

@@ -41,3 +41,4 @@
 #include "k_final.h"
 #include "k_setup.h"
 #include "k_closure.h"
+#include "k_fiw.h"

@@ -159,6 +159,11 @@ struct Lane {
     DevBuf prec, cost;                         // prep launch: per-disk records; walk costs
     int um_hist[8] = {};                       // most distinct positions of a disk, last 8 polls
     int walk_hist[8] = {};                     // the walk AUTO would have chosen, last 8 polls
+    // the fused chain (k_fiw.h): displacement partials, failure bytes, credit rows, hint words,
+    // the shared entries handed to fin2_kernel
+    DevBuf pd, dead8, frows, fwhint, fwrec, fwsxy, fwsw;
+    int fused_bad[8] = {};                     // 1: a recent poll did not suit the fused chain
+    int last_chain = 0;                        // the chain of the lane's last poll: 1 five-launch, 2 fused
 };
 
 struct mac_ctx {
@@ -191,6 +196,7 @@ struct mac_ctx {
 
     int algo = MAC_ALGO_AUTO;
     int shared_mode = MAC_SHARED_AUTO;   // MAC_OPT_SHARED
+    int chain = MAC_CHAIN_AUTO;          // MAC_OPT_CHAIN
     bool profile = false;
     // In-kernel launch timing (k_common.h ts_begin / ts_end): each profiled walk launch takes
     // nwg consecutive {start, end} slots of `stamps`. a: the scan / tiled launch, b: the poll
@@ -201,7 +207,7 @@ struct mac_ctx {
     struct Prof { int64_t a, na, b, nb; int64_t K; const int* mode; int algo;
                   int64_t c = -1, nc = 0, f = -1, nf = 0;
                   int64_t role[MAC_PROF_ROLES][2] = {{-1, 0}, {-1, 0}, {-1, 0}, {-1, 0}, {-1, 0},
-                                                     {-1, 0}, {-1, 0}}; };
+                                                     {-1, 0}, {-1, 0}, {-1, 0}, {-1, 0}}; };
     std::vector<Prof> prof;                          // recorded launches (guarded by mu)
     DevBuf stamps;
     int64_t stamp_cap = 0, stamp_used = 0;           // in workgroup slots (guarded by mu)
@@ -343,6 +349,27 @@ static bool mirror_wait(const uint64_t* h, uint64_t want, double ms, double* obj
 }
 
 static inline unsigned grid1d(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
+
+// The lane's launch hints, mapped host words the poll kernels write for the next poll's enqueue:
+// [0] disks with neighbours, [2] most positions of a disk, [4] the walk AUTO would choose (the
+// five-launch chain, k_poll.h); [8..11] the fused chain's report (k_fiw.h kFwHints; -1: none yet)
+static void ensure_hints(Lane* L)
+{
+    if (L->h_dc.p) return;
+    L->h_dc.reserve(64, hipHostMallocMapped | hipHostMallocCoherent);
+    volatile int* h = (volatile int*)L->h_dc.p;
+    for (int q = 0; q < 16; ++q) h[q] = 0;
+    h[0] = 1 << 30;   // first poll: launch
+    h[8] = -1;
+    void* dp = nullptr;
+    HCK(hipHostGetDevicePointer(&dp, L->h_dc.p, 0));
+    L->d_dc = (int*)dp;
+}
+
+// The largest shared-entry work of one disk (entries x lower neighbours) a fused poll may report
+// before the lane's next polls take the five-launch chain (its union pass spreads crowded shared
+// entries over the whole chip; the fused kernel decides a disk's in its own workgroup).
+static constexpr int kFwCrowdWork = 2048;
 
 // fp32 entry points (*_f32): every float is widened to the double of the same value (exact), and
 // the fp64 path then evaluates the reference predicate on those doubles.
@@ -548,6 +575,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
     // (k_common.h), so measuring adds no packet, event or dependency to the stream.
     int64_t ts_a = -1, ts_na = 0, ts_b = -1, ts_nb = 0, ts_c = -1, ts_nc = 0, ts_f = -1, ts_nf = 0;
     int64_t ts_i = -1, ts_ni = 0, ts_s = -1, ts_ns = 0, ts_g = -1, ts_ng = 0;   // index, set-up, bits
+    int64_t ts_w = -1, ts_nw = 0;                                               // the fused kernel
     auto take_ts = [&](int64_t nwg, int64_t& base, int64_t& n) -> uint64_t* {
         if (!ctx->profile) return nullptr;
         std::lock_guard<std::mutex> lk(ctx->mu);
@@ -582,11 +610,15 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         if (!ctx->profile || (ts_a < 0 && ts_b < 0)) return;
         std::lock_guard<std::mutex> lk(ctx->mu);
         mac_ctx::Prof p{ts_a, ts_na, ts_b, ts_nb, (int64_t)K, d_mode,
-                        tiled ? MAC_ALGO_TILED : MAC_ALGO_SCAN, ts_c, ts_nc, ts_f, ts_nf};
+                        ts_w >= 0 ? MAC_ALGO_POLL : tiled ? MAC_ALGO_TILED : MAC_ALGO_SCAN, ts_c, ts_nc,
+                        ts_f, ts_nf};
         if (ts_c >= 0) {   // a poll chain: every launch's stamps by role (mac_profile_kernels)
             const int64_t r[MAC_PROF_ROLES][2] = {{ts_c, ts_nc}, {ts_i, ts_ni}, {ts_s, ts_ns},
-                                                  {ts_a, ts_na}, {ts_b, ts_nb}, {ts_g, ts_ng},
-                                                  {ts_f, ts_nf}};
+                                                  {ts_w >= 0 ? -1 : ts_a, ts_w >= 0 ? 0 : ts_na},
+                                                  {ts_b, ts_nb}, {ts_g, ts_ng},
+                                                  {ts_w >= 0 ? -1 : ts_f, ts_w >= 0 ? 0 : ts_nf},
+                                                  {ts_w, ts_nw},
+                                                  {ts_w >= 0 ? ts_f : -1, ts_w >= 0 ? ts_nf : 0}};
             for (int q = 0; q < MAC_PROF_ROLES; ++q) {
                 p.role[q][0] = r[q][0];
                 p.role[q][1] = r[q][1];
@@ -604,6 +636,116 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
     // for its plus and minus candidates (k_prep.h PrepArgs.pair)
     const bool pair = !src.cands && src.k0 == 0 && K == 6 * N && (3 * N) % 4 == 0 && kPrepC == 8;
     const int nchain = pair ? (3 * N) / 4 : (K + kPrepC - 1) / kPrepC;
+
+    // The fused chain (k_fiw.h: prep -> fiw -> fin2) whenever the poll walk runs on packed keys of at
+    // most kFwMaxK + 1 candidates, unless one of the lane's last 8 polls did not suit it: a crowded
+    // poll (many shared entries: the five-launch chain's union pass), a scattered batch (the
+    // per-candidate walk) or escaped keys (fp32 keys). Either chain gives the same results.
+    if (poll_possible && want_keys && N > 0 && M > 0 && K > 0 && K <= kFwMaxK + 1 &&
+        ctx->chain != MAC_CHAIN_FIVE && walk_forced != kModeTiled) {
+        ensure_hints(L);
+        volatile int* hw = (volatile int*)L->h_dc.p;
+        int bad_now = -1;   // the lane's last poll's report (a hint: it may be an older poll's)
+        if (L->last_chain == 2 && hw[8] >= 0)
+            bad_now = hw[8] > kFwCrowdWork || hw[9] > 0 || hw[11] > 0 ? 1 : 0;   // (k_fiw.h kFwHints)
+        else if (L->last_chain == 1 && hw[0] < (1 << 30))
+            bad_now = hw[0] > kBitsMinDisks || hw[4] == kModeTiled ? 1 : 0;
+        if (bad_now >= 0) {
+            for (int q = 7; q > 0; --q) L->fused_bad[q] = L->fused_bad[q - 1];
+            L->fused_bad[0] = bad_now;
+        }
+        bool fused = true;
+        for (int q = 0; q < 8; ++q) fused = fused && !L->fused_bad[q];
+        if (fused || ctx->chain == MAC_CHAIN_FUSED) {
+            const int ldk = keys_ld(K);
+            counts = ctx->w_uniform ? 1 : 0;
+            L->keysT.reserve(sizeof(float) * (size_t)4 * N * ldk);
+            L->pd.reserve(sizeof(double4) * (size_t)nchain);
+            L->frows.reserve((counts ? sizeof(unsigned) : sizeof(double)) * (size_t)N * ldk);
+            if (L->fwhint.grow(sizeof(int) * kFwHints)) HCK(hipMemsetAsync(L->fwhint.p, 0, L->fwhint.cap, s));
+            // cons3 failures are left out of the walk when only objectives are asked for
+            const bool excl = d_obj && d_prev && !d_area && N <= kPrepU;
+            if (excl) L->dead8.reserve((size_t)ldk + 16);   // (the fused kernel reads 4-B words)
+            L->fwrec.reserve(sizeof(int4) * (size_t)N);
+            L->fwsxy.reserve(sizeof(double2) * (size_t)N * kFwShCap);
+            L->fwsw.reserve(sizeof(double) * (size_t)N * kFwShCap);
+            PrepArgs pr{};
+            pr.src = src;
+            pr.N = N;
+            pr.K = K;
+            pr.pa = pa;
+            pr.penalty = penalty;
+            pr.vp = d_vp;
+            pr.nchain = nchain;
+            pr.skip_failed = d_area ? 0 : 1;
+            pr.pair = pair ? 1 : 0;
+            pr.g = ctx->grid;
+            pr.keysP = L->keysT.as<uint32_t>();
+            pr.keysT = L->keysT.as<float>() + (size_t)N * ldk;
+            pr.ldk = ldk;
+            pr.pd = L->pd.as<double4>();
+            pr.dead8 = excl ? L->dead8.as<uint8_t>() : nullptr;
+            uint64_t* tsk = take_ts(nchain, ts_c, ts_nc);
+            hipLaunchKernelGGL(prep_kernel, dim3((unsigned)nchain), dim3(kPrepU), 0, s, tsk, pr);
+            HCK(hipGetLastError());
+            FwArgs fa{};
+            fa.src = src;
+            fa.src.keysP = pr.keysP;
+            fa.src.keysT = pr.keysT;
+            fa.src.ldk = ldk;
+            fa.N = N;
+            fa.K = K;
+            fa.g = ctx->grid;
+            fa.dead = pr.dead8;
+            fa.pd = pr.pd;
+            fa.npd = nchain;
+            fa.xy = ctx->xys.as<double2>();
+            fa.w = ctx->ws.as<double>();
+            fa.off = ctx->off.as<int32_t>();
+            fa.counts = counts;
+            fa.crow = L->frows.as<unsigned>();
+            fa.frow = L->frows.as<double>();
+            fa.ldk = ldk;
+            fa.hint = L->fwhint.as<int>();
+            fa.sh = FwShared{L->fwrec.as<int4>(), L->fwsxy.as<double2>(), L->fwsw.as<double>()};
+            const F2Shared f2s{fa.src, L->fwrec.as<int4>(), L->fwsxy.as<double2>(), L->fwsw.as<double>(), fa.dead};
+            const unsigned nfw = 8 * (unsigned)((N + 7) / 8);
+            uint64_t* tsw = take_ts(nfw, ts_w, ts_nw);
+            ts_a = ts_w;   // (mac_profile_read: the walk launch)
+            ts_na = ts_nw;
+            hipLaunchKernelGGL(fiw_kernel, dim3(nfw), dim3(kFwThreads), 0, s, tsw, fa);
+            HCK(hipGetLastError());
+            const unsigned nfin = 8 * (unsigned)((K + 8 * kF2C - 1) / (8 * kF2C));
+            FinBest fb{};
+            if (d_best) {
+                L->finblk.reserve(2 * sizeof(unsigned long long) * nfin);
+                if (L->finarrive.grow(sizeof(unsigned)))
+                    HCK(hipMemsetAsync(L->finarrive.p, 0, L->finarrive.cap, s));
+                if (fb_mads) fb = *fb_mads;
+                fb.best = d_best;
+                fb.mirror = d_mirror;
+                fb.seq = mirror_seq;
+                fb.idx_base = idx_base;
+                fb.blk = L->finblk.as<unsigned long long>();
+                fb.arrive = L->finarrive.as<unsigned>();
+            }
+            uint64_t* tsf = take_ts(nfin, ts_f, ts_nf);
+            if (counts)
+                hipLaunchKernelGGL(fin2_kernel<true>, dim3(nfin), dim3(kF2Threads), 0, s, L->frows.as<unsigned>(),
+                                   nullptr, ldk, N, K, ctx->w0, d_vp, d_area, d_obj, fb, L->fwhint.as<int>(),
+                                   L->d_dc + 8, f2s, tsf);
+            else
+                hipLaunchKernelGGL(fin2_kernel<false>, dim3(nfin), dim3(kF2Threads), 0, s, nullptr,
+                                   L->frows.as<double>(), ldk, N, K, ctx->w0, d_vp, d_area, d_obj, fb,
+                                   L->fwhint.as<int>(), L->d_dc + 8, f2s, tsf);
+            HCK(hipGetLastError());
+            L->last_chain = 2;
+            prof_end();
+            return;
+        }
+    }
+    if (poll_possible) L->last_chain = 1;
+
     if ((d_obj || poll_possible) && K > 0) {
         // the prep launch (k_prep.h): penalty chains + cons3 into vp, the poll walk's partial
         // regions, and the index's fp32 keys
@@ -721,15 +863,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             HCK(hipGetLastError());
             // launch hints from the lane's previous polls (mapped host memory the poll kernel
             // writes): disks with neighbours, most positions of a disk, the walk AUTO would choose
-            if (!L->h_dc.p) {
-                L->h_dc.reserve(64, hipHostMallocMapped | hipHostMallocCoherent);
-                *(volatile int*)L->h_dc.p = 1 << 30;   // first poll: launch
-                ((volatile int*)L->h_dc.p)[2] = 0;     // most positions: not reported yet
-                ((volatile int*)L->h_dc.p)[4] = 0;     // walk: not reported yet (launch)
-                void* dp = nullptr;
-                HCK(hipHostGetDevicePointer(&dp, L->h_dc.p, 0));
-                L->d_dc = (int*)dp;
-            }
+            ensure_hints(L);
             // neighbour lists (k_walk.h walk_setup_kernel), then — when the per-candidate walk is
             // forced, or AUTO chose it on one of the lane's last 8 polls — the walk choice and that
             // walk (coverage_tiled_poll_kernel). Otherwise the poll walk runs; its kernel records
@@ -1024,6 +1158,26 @@ int32_t mac_diag_walk_read(uint64_t* out, int64_t n)
     return MAC_OK;
 }
 
+// diagnostic build only: per-disk phase stamps of the fused kernel (k_fiw.h)
+int32_t mac_diag_fiw_read(uint64_t* out, int64_t n)
+{
+    if (n > (int64_t)(8 * 65536)) n = 8 * 65536;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_fiw), sizeof(uint64_t) * n, 0,
+                            hipMemcpyDeviceToHost) != hipSuccess)
+        return MAC_E_HIP;
+    return MAC_OK;
+}
+
+// diagnostic build only: per-block phase stamps of fin2_kernel (k_fiw.h)
+int32_t mac_diag_f2_read(uint64_t* out, int64_t n)
+{
+    if (n > (int64_t)(8 * 4096)) n = 8 * 4096;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_f2), sizeof(uint64_t) * n, 0,
+                            hipMemcpyDeviceToHost) != hipSuccess)
+        return MAC_E_HIP;
+    return MAC_OK;
+}
+
 // diagnostic build only: phase stamps of the prep launch's first 64 chain workgroups (k_prep.h)
 int32_t mac_diag_prep_read(uint64_t* out, int64_t n)
 {
@@ -1274,7 +1428,8 @@ void mac_ctx_destroy(mac_ctx* ctx)
                           &l->perm, &l->ucount, &l->umap, &l->keysT, &l->lane4,
                           &l->lanexp, &l->rows, &l->nboxT, &l->cnt, &l->dlimraw, &l->finblk, &l->finarrive, &l->c32, &l->p32,
                           &l->cpart, &l->carrive, &l->ctot, &l->prec, &l->cost, &l->nboxU,
-                          &l->ncountU, &l->orjobs})
+                          &l->ncountU, &l->orjobs, &l->pd, &l->dead8, &l->frows, &l->fwhint, &l->fwrec,
+                          &l->fwsxy, &l->fwsw})
             b->release();
         if (l->done) (void)hipEventDestroy(l->done);
 
@@ -1327,6 +1482,10 @@ int32_t mac_set_option(mac_ctx* ctx, int32_t option, int64_t value)
     case MAC_OPT_SHARED:
         if (value < MAC_SHARED_AUTO || value > MAC_SHARED_BITS) return fail(MAC_E_INVAL, "bad shared mode");
         ctx->shared_mode = (int)value;
+        return MAC_OK;
+    case MAC_OPT_CHAIN:
+        if (value < MAC_CHAIN_AUTO || value > MAC_CHAIN_FUSED) return fail(MAC_E_INVAL, "bad chain");
+        ctx->chain = (int)value;
         return MAC_OK;
     case MAC_OPT_TILE_POINTS:
         if (value < 1 || value > 4096) return fail(MAC_E_INVAL, "tile points out of range");

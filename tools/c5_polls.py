@@ -56,7 +56,7 @@ def mads_host(x_in, r_max, penalty, prev, d_lim, tan_half_fov, n_iter, ell0, ell
         rec = {"t": sim.t, "poll": len(polls), "ell": st.ell,
                **{name: (ms / n * 1e3 if n else None) for name, (ms, n) in k.items()}}
         polls.append(rec)
-        b = rec["shared_bits_kernel"] or 0.0
+        b = rec["shared_or_kernel"] or 0.0
         if len(slow) < args.keep or b > min(s[0] for s in slow):
             if pts is None:
                 pts = ctx.get_points()
@@ -83,7 +83,7 @@ ctx.profile(False)
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 with open(os.path.join(ROOT, "gpurun_out", "c5_polls.json"), "w") as f:
     json.dump(polls, f)
-b = np.array([p["shared_bits_kernel"] or 0.0 for p in polls])
+b = np.array([p["shared_or_kernel"] or 0.0 for p in polls])
 print(json.dumps({"polls": len(polls), "bits_us_mean": float(b.mean()), "bits_us_max": float(b.max()),
                   "bits_us_p50": float(np.median(b)), "slowest": [s[1] for s in slow]}), flush=True)
 save = {}

@@ -34,6 +34,8 @@ for s in $STEPS; do
     testsall)   # every GPU test, no stop at the first failure
         run pytest_gpu_all 900 python -u -m pytest tests -m gpu -v -rfE -p no:cacheprovider --timeout 120 --timeout-method thread ; rc=$?
         [ $rc -eq 1 ] && rc=0 ;;
+    fused)   # the fused chain's tests alone
+        run pytest_fused 400 python -u -m pytest tests/test_gpu_fused.py -x -v -rfE -p no:cacheprovider --timeout 120 --timeout-method thread ; rc=$? ;;
     smoke)
         run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ; rc=$? ;;
     benchq)
@@ -56,6 +58,10 @@ for s in $STEPS; do
         make -s -C maximumareacoverageoptimization.jl_amd/csrc diag
         MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
             run diag5 600 python tools/diag_poll.py --config 5 ; rc=$? ;;
+    diagfiw)
+        make -s -C maximumareacoverageoptimization.jl_amd/csrc diag
+        MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
+            run diagfiw 300 python tools/diag_fiw.py ; rc=$? ;;
     diagidx)
         make -s -C maximumareacoverageoptimization.jl_amd/csrc diag
         MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \
