@@ -181,6 +181,12 @@ typedef struct mac_mads_stats {
     double host_perm_s;    /*           next iteration's permutations (overlaps the device)    */
     double wait_s;         /*           waiting for the device                                 */
     double host_post_s;    /*           incumbent update after each poll                       */
+    int64_t feasible_evaluations; /* poll candidates that passed cons3 and were evaluated (this
+                                     stepper's shard; the start point's evaluation not counted) */
+    int64_t rejected_polls;       /* iterations cons3 rejected whole with no evaluation: every
+                                     variable's diagonal step +-2^ell alone breaks its UAV's d_lim
+                                     (src/TDM_Constraints.jl:67), so no candidate passes — a
+                                     failure (ell - 1), as the extreme barrier makes it         */
 } mac_mads_stats;
 int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const double* r_max,
                      double penalty, const double* prev, const double* d_lim, double tan_half_fov,

@@ -71,6 +71,11 @@ class Status:
         self.runtime_total = 0.0
         self.iteration = 0
         self.function_evaluations = 0
+        # poll candidates passing cons3 (mac_mads_stats.feasible_evaluations: every candidate
+        # without cons3) and polls where none does (a superset of mac_mads_stats.rejected_polls,
+        # which counts the polls rejected by their diagonal steps alone)
+        self.cons3_passed = 0
+        self.cons3_empty_polls = 0
         self.optimization_status = "Unoptimized"
 
 
@@ -110,6 +115,9 @@ def mads(input, obj, cons_ext=(), N_iter: int = 100, ell0: int = 2, ell_max: int
         it += 1
         B = ltmads_basis(n, ell, rng).astype(np.float64)
         X = np.concatenate([x[None, :] + B.T, x[None, :] - B.T], axis=0)
+        n3 = sum(bool(cons3(v)) for v in X) if cons3 is not None else X.shape[0]
+        res.status.cons3_passed += n3
+        res.status.cons3_empty_polls += n3 == 0
         if hasattr(obj, "poll"):
             mask = np.array([all(bool(c(v)) for c in others) for v in X]) if others else None
             if mask is not None and not mask.any():

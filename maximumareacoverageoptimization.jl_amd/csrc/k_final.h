@@ -55,6 +55,11 @@ struct FinBest {
     uint64_t state;            // the poll's stream state
     int n, ell_max;
     uint64_t done_seq;         // mirror seq word once the loop has stopped (the host's wait ends)
+    // launch-hint words (device ints; null: none): the last block copies the first nhint to the
+    // mapped host words hint_host (the lane's next enqueue reads them) and clears them
+    int* hint;
+    int* hint_host;
+    int nhint;
 };
 
 // Check word of a mirrored result (host: mirror_check in maxcover.hip): the host accepts the slot
@@ -159,6 +164,7 @@ __device__ __forceinline__ bool finalize_argmin(const FinBest& fb, double o, int
     // the pipelined MADS loop's state, loaded beside the minima (a stopped loop: no result)
     const int ell = fb.st ? fb.st->ell : 0;
     const double fcur = fb.st ? fb.st->f : 0.0;
+    const int rej = fb.st ? fb.st->skip : 0;   // the prep rejected the poll whole: a failure
     bv = __builtin_inf();
     bi = -1;
     // every block's minimum in flight at once (kFinMaxBlk / 64 per lane), then the reduction
@@ -172,6 +178,9 @@ __device__ __forceinline__ bool finalize_argmin(const FinBest& fb, double o, int
         ix[r] = q < gridDim.x ? __hip_atomic_load(fb.blk + 2 * q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                               : ~0ull;
     }
+    // the hint words, in the same round trip
+    const bool hl = fb.hint && lane < fb.nhint;
+    const int hv = hl ? __hip_atomic_load(fb.hint + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
 #pragma unroll
     for (int r = 0; r < kPer; ++r)
         if ((long long)ix[r] >= 0) argmin_take(bv, bi, __builtin_bit_cast(double, v[r]), (int)(long long)ix[r]);
@@ -185,13 +194,17 @@ __device__ __forceinline__ bool finalize_argmin(const FinBest& fb, double o, int
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1)
         argmin_take(bv, bi, __shfl_xor(bv, off, kWave), __shfl_xor(bi, off, kWave));
-    const double bo = bi >= 0 ? bv : __builtin_inf();
-    const int64_t gidx = bi >= 0 ? fb.idx_base + bi : (int64_t)-1;
+    const bool none = bi < 0 || rej;
+    const double bo = none ? __builtin_inf() : bv;
+    const int64_t gidx = none ? (int64_t)-1 : fb.idx_base + bi;
     if (fb.st && ell < 0) {   // the loop stopped before this poll
         if (lane == 0) __hip_atomic_store(fb.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return true;
     }
-    if (fb.st) mads_step(fb, bo, gidx, ell, fcur);
+    if (fb.st) {
+        mads_step(fb, bo, gidx, ell, fcur);
+        if (rej && lane == 0) fb.st->skipped += 1;
+    }
     if (lane == 0) {
         // d_best with agent-scope (sc1, write-through) stores: a host that has read the mirror may
         // hand d_best to device work on another stream (an RCCL all-gather, dist.DeviceGather)
@@ -215,6 +228,10 @@ __device__ __forceinline__ bool finalize_argmin(const FinBest& fb, double o, int
             // seq word jumps past every seq the host may wait for
             if (fb.st && !(gidx >= 0 && bo < fcur) && ell == 0) fb.mirror[2] = fb.done_seq;
         }
+    }
+    if (hl) {   // (read above; cleared for the next poll)
+        if (fb.hint_host) ((volatile int*)fb.hint_host)[lane] = hv;
+        __hip_atomic_store(fb.hint + lane, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return true;
 }

@@ -60,6 +60,7 @@ constexpr int kFwR = kFwCH / kFwThreads;         // ... per thread
 constexpr int kFwShE = 64;                       // shared entries per decision word (in place)
 constexpr int kFwNbr = kPollNbr;                 // lower neighbours kept (more: every lower disk)
 constexpr int kFwShCap = 1024;                   // shared entries a disk hands to fin2_kernel
+constexpr int kFwTT = 64;                        // direct mode: radius thresholds tabulated
 
 // Hint words (device ints, zero between polls: fin2_kernel's last block copies them to the lane's
 // mapped host memory and clears them): [0] the most shared entries x neighbours of one disk,
@@ -156,8 +157,8 @@ __device__ __forceinline__ DiskRec key_disk(const CandSrc& s, uint32_t key, int 
 }
 
 #ifdef MAC_DIAG
-__device__ uint64_t g_diag_fiw[8 * 65536];   // diagnostic build only: per-disk phase stamps
-#define MAC_FW_STAMP(q) if (threadIdx.x == 0 && i < 65536) g_diag_fiw[8 * i + (q)] = __builtin_amdgcn_s_memrealtime()
+__device__ uint64_t g_diag_fiw[16 * 65536];  // diagnostic build only: per-disk phase stamps
+#define MAC_FW_STAMP(q) if (threadIdx.x == 0 && i < 65536) g_diag_fiw[16 * i + (q)] = __builtin_amdgcn_s_memrealtime()
 __device__ uint64_t g_diag_f2[8 * 4096];      // per fin2 block
 #define MAC_F2_STAMP(q)                                                                      \
     if (threadIdx.x == 0 && blockIdx.x < 4096) {                                             \
@@ -202,12 +203,16 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
     __shared__ double2 shp[kFwShE];
     __shared__ double shw[kFwShE];
     __shared__ int shidx[kFwCH];
-    __shared__ int rs[kPollRB], rpre[kPollRB + 1], rf[2][kPollRB];
+    __shared__ int rs[kPollRB], rpre[kPollRB + 1];
     __shared__ int nb_id[kFwNbr];
     __shared__ int4 nb_box[kFwNbr];
     __shared__ double nb_b[kFwNbr][3];
     __shared__ double dred[kFwWaves][4];
     __shared__ double sbase[7];   // candidate 0's disk i, the displacement bound
+    __shared__ double ttab[kFwTT];   // direct mode: T(br + dr) per radius offset dr + Dl (ttn > 0)
+    __shared__ uint8_t scov[kFwKPB]; // per slice slot: its position's disk covers (finite, r > 0)
+    __shared__ int ttn, ttl;
+    __shared__ unsigned ninner;      // entries every position covers (the annulus, counts only)
     __shared__ int ucnt, ncnt;
     __shared__ int wkeep[kFwR][kFwWaves];
     __shared__ int wsum[kFwWaves];
@@ -233,6 +238,10 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
     // candidate 0's disk i, the displacement partials, the lower disks' bases (first two batches)
     int4 RG = make_int4(0, -1, 0, -1);
     bool ident;
+    int rf0 = 0, rf1 = 0;   // the first row batch's runs (thread tid: row RG.z + tid), kept in flight
+    double2 ppr[kFwR];      // the walk's first chunk of entries, loaded ahead (pjg: list index, -1 none)
+    double pwr[kFwR];
+    int pjg[kFwR];
     {
         const uint32_t* krow = src.keysP + (int64_t)i * src.ldk;
         uint32_t pq[P];
@@ -273,6 +282,8 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
         if (tid == 0) {
             ucnt = 0;
             ncnt = 0;
+            ttn = 0;
+            ninner = 0u;
         }
         bool esc = false;
 #pragma unroll
@@ -307,6 +318,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
             sbase[3] = dmx;
             sbase[4] = dmy;
             sbase[5] = dmr;
+            sbase[6] = dml;
         }
         const bool rany = sup_box(bx, by, br, dmx, dmy, dmr, g, RG);
         if (!rany) RG = make_int4(0, -1, 0, -1);
@@ -314,8 +326,8 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
         const int nrows = rany ? RG.w - RG.z + 1 : 0;
         if (tid < min(nrows, kPollRB)) {
             const int64_t rb = (int64_t)(RG.z + tid) * g.nTx;
-            rf[0][tid] = a.off[rb + RG.x];
-            rf[1][tid] = a.off[rb + RG.y + 1];
+            rf0 = a.off[rb + RG.x];
+            rf1 = a.off[rb + RG.y + 1];
         }
         // ---- lower neighbours: disks j < i whose boxes overlap box i
         if (rany) {
@@ -340,6 +352,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
             for (int j = tid + 2 * kFwThreads; j < i; j += kFwThreads)
                 test(j, src_val(src, 0, j, N), src_val(src, 0, N + j, N), src_val(src, 0, 2 * N + j, N));
         }
+        MAC_FW_STAMP(12);
         // ---- positions. Direct-mapped when the live candidates' key offsets fit a small box
         // (every live key packs to (dx, dy, dr) with |dx| <= Dx, |dy| <= Dy, -Dl <= dr <= Dr: the
         // displacement bound): one slot per offset triple, plain stores, positions numbered in slot
@@ -378,6 +391,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
             for (int j = 0; j < P; ++j)
                 if (kof(j) < K) table[slot[j]] = 1;
         }
+        MAC_FW_STAMP(13);
         {   // any miss: the hash (an LDS word, not __syncthreads_or: that would wait for the row runs)
             const uint64_t mb = __ballot(miss);
             if (lane == 0) wsum[wid] = mb != 0;
@@ -388,6 +402,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
             direct = direct && !any;
             lds_barrier();   // (wsum is reused below)
         }
+        MAC_FW_STAMP(14);
         if (direct) {
             // number the occupied slots in slot order: each thread a run of consecutive slots
             const int per = (nslot + 1 + kFwThreads - 1) / kFwThreads;
@@ -412,6 +427,13 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
                 }
             }
             if (tid == kFwThreads - 1) ucnt = id;
+            if (nrd <= kFwTT) {   // the positions' radii take nrd values: their thresholds once
+                if (tid < nrd) ttab[tid] = cover_threshold(br + (double)(tid - Dl));
+                if (tid == 0) {
+                    ttn = nrd;
+                    ttl = Dl;
+                }
+            }
         } else if (!ident) {
 #pragma unroll
             for (int j = 0; j < P; ++j)
@@ -449,6 +471,38 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
         }
         lds_barrier();
         MAC_FW_STAMP(2);
+        // the walk's first row batch (its runs have arrived by now) and the first chunk's entry
+        // loads, left in flight through the positions and the slice's lane constants
+        if (rany && tid < kWave) {
+            const int nr = min(kPollRB, RG.w - RG.z + 1);
+            const int len = tid < nr ? rf1 - rf0 : 0;
+            const int incl = wave_incl_scan_i32(len, tid);
+            if (tid < nr) {
+                rs[tid] = rf0;
+                rpre[tid + 1] = incl;
+            }
+            if (tid == 0) rpre[0] = 0;
+        }
+        lds_barrier();
+        if (rany) {
+            const int nr = min(kPollRB, RG.w - RG.z + 1);
+            const int nraw = min(kFwCH, rpre[nr]);
+#pragma unroll
+            for (int r = 0; r < kFwR; ++r) {
+                const int qd = tid + r * kFwThreads;
+                pjg[r] = -1;
+                if (qd < nraw) {
+                    int lo = 0, hi = nr - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (rpre[mid] <= qd) lo = mid; else hi = mid - 1;
+                    }
+                    pjg[r] = rs[lo] + (qd - rpre[lo]);
+                    ppr[r] = a.xy[pjg[r]];
+                    pwr[r] = a.w[pjg[r]];
+                }
+            }
+        }
         // per candidate its position; hash: per position its key word (through registers: the
         // buffers change roles at the barrier)
         const int U0 = ident ? K : ucnt;
@@ -494,6 +548,38 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
         return word_disk(poskey[u], sbase[0], sbase[1], sbase[2]);
     };
 
+    // the walk's disks: in direct mode from the key word and the tabulated threshold
+    const bool tabT = ttn > 0;
+    const int tl = ttl;
+    auto walk_disk = [&](int u) -> DiskRec {
+        if (!tabT) return pos_disk(u);
+        const uint32_t w = poskey[u];
+        if (w == kDeadWord) return inert_disk();
+        float fx, fy, fr;
+        key_unpack(w, fx, fy, fr);
+        DiskRec d;
+        d.cx = sbase[0] + (double)fx;
+        d.cy = sbase[1] + (double)fy;
+        d.r = sbase[2] + (double)fr;
+        d.T = ttab[(int)fr + tl];
+        return d;
+    };
+    // The annulus (equal weights): every position's disk (c, r) lies within the displacement
+    // bound of candidate 0's, |cx - x0| <= Dx, |cy - y0| <= Dy, r >= r0 - Dl, r <= r0 + Dr, so an
+    // entry at distance d from (x0, y0) is covered by all of them when d + hypot(Dx, Dy) < r0 - Dl
+    // and by none when d - hypot(Dx, Dy) > r0 + Dr; margins of 1e-9 (relative) dominate every
+    // rounding of d, the bound and the reference's sqrt(d^2) < r. Those entries skip the tests:
+    // the first are counted once and credited to every covering position, the second dropped.
+    double rin2 = -1.0, rout2 = __builtin_inf();
+    if (a.counts && rany) {
+        const double bx0 = sbase[2], ex = sbase[3], ey = sbase[4], er = sbase[5], el = sbase[6];
+        const double e = __builtin_sqrt(ex * ex + ey * ey) * (1.0 + 1e-9);
+        const double rin = (bx0 - el) - e - 1e-9 * (__builtin_fabs(bx0) + __builtin_fabs(el) + e + 1.0);
+        if (rin > 0.0 && rin < 1e150) rin2 = rin * rin * (1.0 - 1e-9);
+        const double rout = (bx0 + er) + e + 1e-9 * (__builtin_fabs(bx0) + __builtin_fabs(er) + e + 1.0);
+        if (rout > 0.0 && rout < 1e150) rout2 = rout * rout * (1.0 + 1e-9);
+    }
+
     // ---- the walk of box i over the entries no lower box holds (k_poll.h)
     if (rany) {
         const double ox = g.gx0 + 0.5 * (double)(RG.x + RG.y + 1) * g.S;
@@ -504,25 +590,30 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
             for (int t = tid; t < kFwKPB; t += kFwThreads) {   // the slice's lane constants
                 const int u = kb + t;
                 PollLane L = inert_lane();
+                bool cov = false;
                 if (u < ke) {
-                    const DiskRec d = pos_disk(u);
+                    const DiskRec d = walk_disk(u);
                     int4 sp;
-                    if (disk_span(d, g, sp)) L = poll_lane(d, ox, oy, Umax);
+                    cov = d.T >= 0.0 && __builtin_isfinite(d.cx) && __builtin_isfinite(d.cy);
+                    if (tabT ? cov : disk_span(d, g, sp)) L = poll_lane(d, ox, oy, Umax);
                 }
                 sl4[t] = make_float4(L.sa, L.sb, L.stm, L.ns);
                 slx[t] = L.xp;
+                scov[t] = cov ? 1 : 0;
             }
             __syncthreads();
+            if (kb == 0) MAC_FW_STAMP(8);
             f32x2 sa[kPollPairs], sb[kPollPairs], st[kPollPairs], ns[kPollPairs];
             float xp[kPollSlots];
             double acc[kPollSlots];
-            uint32_t live = 0;
+            uint32_t live = 0, covm = 0;
 #pragma unroll
             for (int u = 0; u < kPollSlots; ++u) {
                 const int p = u * kWave + lane;
                 const float4 c = sl4[p];
                 xp[u] = kb + p < ke ? slx[p] : -1.0f;
                 if (kb + p < ke) live |= 1u << u;
+                if (kb + p < ke && scov[p]) covm |= 1u << u;
                 acc[u] = 0.0;
                 const int j = u >> 1;
                 if (u & 1) {
@@ -534,33 +625,37 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
             const int np = (ke - kb + 2 * kWave - 1) / (2 * kWave);
             for (int rb = RG.z; rb <= RG.w; rb += kPollRB) {
                 const int nr = min(kPollRB, RG.w - rb + 1);
-                int rs0 = 0, rs1 = 0;
-                if (rb == RG.z) {
-                    if (tid < nr) {
-                        rs0 = rf[0][tid];
-                        rs1 = rf[1][tid];
+                const bool first_rb = kb == 0 && rb == RG.z;   // (its runs are scanned already)
+                if (!first_rb) {
+                    int rs0 = 0, rs1 = 0;
+                    if (rb == RG.z) {
+                        if (tid < nr) {
+                            rs0 = rf0;
+                            rs1 = rf1;
+                        }
+                    } else if (tid < nr) {   // later row batches (boxes over 64 rows): their runs now
+                        const int64_t rowb = (int64_t)(rb + tid) * g.nTx;
+                        rs0 = a.off[rowb + RG.x];
+                        rs1 = a.off[rowb + RG.y + 1];
                     }
-                } else if (tid < nr) {   // later row batches (boxes over 64 rows): their runs now
-                    const int64_t rowb = (int64_t)(rb + tid) * g.nTx;
-                    rs0 = a.off[rowb + RG.x];
-                    rs1 = a.off[rowb + RG.y + 1];
-                }
-                __syncthreads();   // (the previous batch's rows are read)
-                if (tid < kWave) {
-                    const int len = tid < nr ? rs1 - rs0 : 0;
-                    const int incl = wave_incl_scan_i32(len, tid);
-                    if (tid < nr) {
-                        rs[tid] = rs0;
-                        rpre[tid + 1] = incl;
+                    __syncthreads();   // (the previous batch's rows are read)
+                    if (tid < kWave) {
+                        const int len = tid < nr ? rs1 - rs0 : 0;
+                        const int incl = wave_incl_scan_i32(len, tid);
+                        if (tid < nr) {
+                            rs[tid] = rs0;
+                            rpre[tid + 1] = incl;
+                        }
+                        if (tid == 0) rpre[0] = 0;
                     }
-                    if (tid == 0) rpre[0] = 0;
+                    __syncthreads();
                 }
-                __syncthreads();
                 const int total = rpre[nr];
                 for (int base = 0; base < total; base += kFwCH) {
                     // the chunk's entries disk i may own (no lower box holds them, finite),
                     // compacted in a fixed order (round, wave, lane)
                     const int nraw = min(kFwCH, total - base);
+                    const bool pre = first_rb && base == 0;   // loaded ahead (ppr, pwr, pjg)
                     double2 pr[kFwR];
                     double wr[kFwR];
                     int jg[kFwR];
@@ -568,7 +663,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
 #pragma unroll
                     for (int r = 0; r < kFwR; ++r) {
                         const int qd = tid + r * kFwThreads;
-                        bool keep = false;
+                        bool keep = false, inner = false;
                         pr[r] = make_double2(0.0, 0.0);
                         wr[r] = 0.0;
                         jg[r] = 0;
@@ -579,13 +674,31 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
                                 const int mid = (lo + hi + 1) >> 1;
                                 if (rpre[mid] <= f) lo = mid; else hi = mid - 1;
                             }
-                            jg[r] = rs[lo] + (f - rpre[lo]);
-                            pr[r] = a.xy[jg[r]];
-                            wr[r] = a.w[jg[r]];
+                            if (pre) {
+                                jg[r] = pjg[r];
+                                pr[r] = ppr[r];
+                                wr[r] = pwr[r];
+                            } else {
+                                jg[r] = rs[lo] + (f - rpre[lo]);
+                                pr[r] = a.xy[jg[r]];
+                                wr[r] = a.w[jg[r]];
+                            }
                             const bool shared = nc > 0 &&
                                 entry_shared(nc, nb_box, tile_of(pr[r].x, g.gx0, g.invS, g.nTx), rb + lo);
                             keep = !shared && __builtin_isfinite(pr[r].x) && __builtin_isfinite(pr[r].y);
+                            if (keep) {   // the annulus: inside every disk / outside all
+                                const double ux = pr[r].x - sbase[0], uy = pr[r].y - sbase[1];
+                                const double d0 = ux * ux + uy * uy;
+                                if (d0 <= rin2) {
+                                    keep = false;
+                                    inner = true;
+                                } else if (d0 >= rout2) {
+                                    keep = false;
+                                }
+                            }
                         }
+                        const uint64_t ib = __ballot(inner);
+                        if (kb == 0 && lane == 0 && ib) atomicAdd(&ninner, (unsigned)__popcll(ib));
                         bal[r] = __ballot(keep);
                         if (lane == 0) wkeep[r][wid] = __popcll(bal[r]);
                     }
@@ -614,6 +727,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
                     bool mixed = false;
                     for (int e = tid; e < n; e += kFwThreads) mixed |= __builtin_bit_cast(uint64_t, sw[e]) != w0b;
                     const bool uniform = !__syncthreads_or(mixed);
+                    if (kb == 0 && rb == RG.z && base == 0) MAC_FW_STAMP(9);
                     const int ng = (n + 3) >> 2;
                     float bmin[kPollSlots];
 #pragma unroll
@@ -654,6 +768,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
                     // entries of the chunk in fp64 (the position's disk from its key; the slot's
                     // constants from the slice arrays). The weighted loop above added the slot's
                     // fp32 decisions already: they are replaced.
+                    if (kb == 0 && rb == RG.z && base == 0) MAC_FW_STAMP(10);
                     uint32_t bandm = 0;
 #pragma unroll
                     for (int u = 0; u < kPollSlots; ++u)
@@ -686,13 +801,17 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
                             if (u == ub) acc[u] += uniform ? cv : cv - fv;
                     }
                     __syncthreads();   // the staging is read
+                    if (kb == 0 && rb == RG.z && base == 0) MAC_FW_STAMP(11);
                 }
             }
-            // the slice's credit per position, the waves' shares added in wave order
+            // the slice's credit per position, the waves' shares added in wave order (wave 0
+            // adds the annulus' inner entries to every covering position)
             if (a.counts) {
+                const unsigned nin = wid == 0 ? ninner : 0u;
 #pragma unroll
                 for (int u = 0; u < kPollSlots; ++u)
-                    if (live & (1u << u)) atomicAdd(&pcnt[kb + u * kWave + lane], (unsigned)acc[u]);
+                    if (live & (1u << u))
+                        atomicAdd(&pcnt[kb + u * kWave + lane], (unsigned)acc[u] + ((covm >> u) & 1u ? nin : 0u));
             } else {
                 for (int w2 = 0; w2 < kFwWaves; ++w2) {
                     if (w2 == wid) {
@@ -916,7 +1035,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
     }
 #ifdef MAC_DIAG
     if (tid == 0 && i < 65536)
-        g_diag_fiw[8 * i + 7] = ((uint64_t)U << 32) | ((uint64_t)min(nc, 0xFFFF) << 16) |
+        g_diag_fiw[16 * i + 7] = ((uint64_t)U << 32) | ((uint64_t)min(nc, 0xFFFF) << 16) |
                                 (uint64_t)min((RG.y - RG.x + 1) * (RG.w - RG.z + 1), 0xFFFF);
 #endif
     MAC_FW_STAMP(6);
@@ -934,7 +1053,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
 // also copies the fused kernel's hint words to the lane's mapped host memory (maxcover.hip
 // enqueue_eval reads them before the next poll).
 constexpr int kF2Threads = 1024;
-constexpr int kF2C = 32;
+constexpr int kF2C = 16;
 constexpr int kF2G = kF2Threads / kF2C;
 constexpr int kF2Slots = 64;      // disk records per batch (handed-off disks, their <= kFwHand neighbours)
 constexpr int kF2Ent = 2048;      // shared entries staged at once
@@ -952,7 +1071,7 @@ template <bool kCounts>
 __global__ __launch_bounds__(kF2Threads) void fin2_kernel(
     const unsigned* __restrict__ crow, const double* __restrict__ frow, int ldk, int N, int K,
     double w0, const double* __restrict__ vp, double* __restrict__ area_out, double* __restrict__ obj_out,
-    FinBest fb, int* __restrict__ hint, int* __restrict__ hint_host, F2Shared sd, uint64_t* ts)
+    FinBest fb, F2Shared sd, uint64_t* ts)
 {
     ts_begin(ts);
     MAC_F2_STAMP(0);
@@ -1061,6 +1180,34 @@ __global__ __launch_bounds__(kF2Threads) void fin2_kernel(
             __syncthreads();
             const int q1 = nbat;
             const int sl0 = bslot[q0], ns = bslot[q1] - sl0;
+            const int e0all = bent[q0], e1all = bent[q1];
+            // the first chunk's entries, loaded before the records' keys (one round trip for both)
+            constexpr int kEPT = kF2Ent / kF2Threads;
+            double2 exy[kEPT];
+            double ew[kEPT];
+            int esl[kEPT];
+            {
+                const int ne = min(kF2Ent, e1all - e0all);
+#pragma unroll
+                for (int r = 0; r < kEPT; ++r) {
+                    const int e = t + r * kF2Threads;
+                    exy[r] = make_double2(0.0, 0.0);
+                    ew[r] = 0.0;
+                    esl[r] = 0;
+                    if (e < ne) {
+                        const int eg = e0all + e;   // the listed disk holding it
+                        int lo = q0, hi = q1 - 1;
+                        while (lo < hi) {
+                            const int mid = (lo + hi + 1) >> 1;
+                            if (bent[mid] <= eg) lo = mid; else hi = mid - 1;
+                        }
+                        const int64_t se = (int64_t)flist[lo] * kFwShCap + (eg - bent[lo]);
+                        exy[r] = sd.xy[se];
+                        ew[r] = sd.w[se];
+                        esl[r] = bslot[lo] - sl0;
+                    }
+                }
+            }
             // one round trip: per slot and candidate the disk (its key word, candidate 0's disk),
             // and the batch's first kF2Ent entries
             for (int q = t; q < ns * C; q += kF2Threads) {
@@ -1085,10 +1232,19 @@ __global__ __launch_bounds__(kF2Threads) void fin2_kernel(
                 srec[sl][1][cc] = d.cy;
                 srec[sl][2][cc] = d.T;
             }
-            const int e0all = bent[q0], e1all = bent[q1];
             for (int e0 = e0all; e0 < e1all; e0 += kF2Ent) {
                 const int ne = min(kF2Ent, e1all - e0);
-                for (int e = t; e < ne; e += kF2Threads) {
+                if (e0 == e0all) {
+#pragma unroll
+                    for (int r = 0; r < kEPT; ++r) {
+                        const int e = t + r * kF2Threads;
+                        if (e < ne) {
+                            sxy[e] = exy[r];
+                            swt[e] = ew[r];
+                            sslot[e] = esl[r];
+                        }
+                    }
+                } else for (int e = t; e < ne; e += kF2Threads) {
                     const int eg = e0 + e;   // the listed disk holding it
                     int lo = q0, hi = q1 - 1;
                     while (lo < hi) {
@@ -1151,14 +1307,7 @@ __global__ __launch_bounds__(kF2Threads) void fin2_kernel(
     }
     MAC_F2_STAMP(5);
     if (fb.best && t < kWave) {
-        const bool last = finalize_argmin<C>(fb, o, k, k < K);
-        if (last && t == 0 && hint) {   // (read, reported, cleared for the next poll)
-            for (int q = 0; q < kFwHints; ++q) {
-                const int v = __hip_atomic_load(hint + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (hint_host) ((volatile int*)hint_host)[q] = v;
-                __hip_atomic_store(hint + q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
+        const bool last = finalize_argmin<C>(fb, o, k, k < K);   // (+ the hint words, fb.hint)
 #ifdef MAC_DIAG
         if (t == 0 && blockIdx.x < 4096) g_diag_f2[8 * blockIdx.x + 7] = last;
 #endif

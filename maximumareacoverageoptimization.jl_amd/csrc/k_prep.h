@@ -48,6 +48,34 @@ __device__ __forceinline__ double pen_term(double x2, double y2, double R2, int 
     return pa.rmax ? __builtin_fabs(R2 - pa.rmax[i]) : 0.0;
 }
 
+// Whether UAV i's diagonal LTMADS steps reject every candidate that carries them: with the
+// incumbent's value v of one of UAV i's variables (q = 0 x, 1 y, 2 r), both v + b and v - b (b =
+// 2^ell; the generator's x +- entry with entry = +-b gives exactly these doubles) put that
+// variable's own term of cons3's sum above T3. The sum dx^2 + dy^2 + dz^2 in floating point is at
+// least each of its terms (adding non-negative terms is monotone under rounding), so the whole
+// candidate fails cons3 then, whatever its other entries. Every variable is the diagonal of one
+// column of B, so when this holds for all 3N variables no candidate of the poll passes cons3.
+// pen_term's arithmetic (x1 - x2, z = R / tan(FOV/2), z1 - z2).
+__host__ __device__ __forceinline__ bool diag_rejects(double v, double b, double p, int q,
+                                                      double tan_half_fov, double T3)
+{
+    bool all = true;
+#pragma unroll
+    for (int sg = 0; sg < 2; ++sg) {
+        const double c = sg == 0 ? v + b : v - b;
+        double d;
+        if (q < 2) {
+            d = p - c;
+        } else {
+            const double z1 = p / tan_half_fov, z2 = c / tan_half_fov;
+            d = z1 - z2;
+        }
+        const double sq = d * d;
+        all = all && sq > T3;
+    }
+    return all;
+}
+
 // ------------------------------------------------------------------ candidate sources
 
 // splitmix64 stream value number `idx` (1-based) after `state` (workloads.SplitMix64).
@@ -82,11 +110,17 @@ __host__ __device__ __forceinline__ double ltmads_entry(uint64_t state, int64_t 
 // mads_run_pipelined): the finalize of poll t applies poll t's update (k_final.h mads_step) and
 // poll t + 1's launches read the mesh index from here, so the host enqueues polls ahead of their
 // outcomes. ell < 0 (the mesh precision limit) stops the loop: every later launch returns at once.
+// A poll that cons3 rejects whole (skip = 1, written by the poll's prep launch: every variable's
+// diagonal step ±2^ell alone violates its UAV's d_lim, k_prep.h poll_rejected) is a failure with
+// no evaluation: the launches after the prep return at once and the finalize applies the failure
+// update. feas counts the candidates that pass cons3 (the evaluations the reference makes).
 struct MadsState {
     double f;      // objective at the incumbent
     int64_t it;    // polls applied
     int ell;       // mesh index of the next poll (step 2^ell)
-    int pad;
+    int skip;      // the current poll is rejected whole (set by its prep launch)
+    unsigned long long feas;   // candidates evaluated (passing cons3)
+    int64_t skipped;           // polls rejected whole
 };
 
 // Where candidate coordinates come from: a 3N x K column-major matrix (the batch APIs), or a
@@ -108,12 +142,13 @@ struct CandSrc {
                            // (a rank's shard of it)
     const MadsState* mst;  // generator, pipelined MADS loop: b from the device state (else null)
     // Called at the top of every launch that reads the source: b = 2^ell from the device state;
-    // false once the loop has stopped (the launch returns at once). Uniform per workgroup.
-    __device__ __forceinline__ bool resolve()
+    // false once the loop has stopped, or (launches after the prep: any_poll false) when the
+    // prep rejected the poll whole (the launch returns at once). Uniform per workgroup.
+    __device__ __forceinline__ bool resolve(bool any_poll = false)
     {
         if (!mst) return true;
         const int e = mst->ell;
-        if (e < 0) return false;
+        if (e < 0 || (!any_poll && mst->skip)) return false;
         b = (int64_t)1 << e;
         return true;
     }
@@ -186,6 +221,11 @@ struct PrepArgs {
     // and one byte per candidate: 1 when it fails cons3 and is left out (skip_failed, N <= kPrepU)
     double4* pd;
     uint8_t* dead8;
+    // the pipelined MADS loop with cons3 (null: none): the state whose skip word this launch
+    // writes (workgroup 0), the poll being rejected whole when every variable's diagonal step
+    // fails (diag_rejects); then every workgroup returns before its records
+    MadsState* mst_w;
+    unsigned long long* feas;  // += the candidates that pass cons3 (null: not counted)
 };
 
 // Packed keys. Disk i of candidate k is keyed by its offsets (dx, dy, dr) from candidate 0's
@@ -271,6 +311,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
     __shared__ double term[kPrepC][kPrepU + 1];   // [candidate][UAV] (+1: lanes on distinct banks)
     __shared__ int wbad[kPrepU / kWave][kPrepC];  // per wave: a term of the candidate is negative
     __shared__ uint32_t wbadm[kPrepU / kWave];       // ... wbad as a mask over the candidates
+    __shared__ int wrej[kPrepU / kWave];             // per wave: every UAV's diagonal steps fail (mst_w)
     const int N = a.N, K = a.K;
     const int u = threadIdx.x, lane = u & (kWave - 1), wid = u / kWave;
     const int k0 = cw * kPrepC;
@@ -353,6 +394,17 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
                 wdead |= (neg != 0 ? 1u : 0u) << c;
             }
             if (lane == 0) wbadm[wid] = wdead;
+            if (a.mst_w) {   // (excl, one block of UAVs: uniform) the whole-poll rejection
+                bool rej = true;
+                if (iv) {
+                    const double bb = (double)a.src.b;
+                    rej = diag_rejects(a.src.xinc[ii], bb, x1, 0, pa.tan_half_fov, T3) &&
+                          diag_rejects(a.src.xinc[N + ii], bb, y1, 1, pa.tan_half_fov, T3) &&
+                          diag_rejects(a.src.xinc[2 * N + ii], bb, pa.prev[2 * N + ii], 2, pa.tan_half_fov, T3);
+                }
+                const uint64_t keep = __ballot(!rej);
+                if (lane == 0) wrej[wid] = keep == 0;
+            }
             MAC_PREP_STAMP(1 + 3 * (ib / kPrepU));
         }
         if (excl) {   // every wave's failures (the fold below needs no further barrier)
@@ -360,6 +412,13 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
             dead = 0u;
 #pragma unroll
             for (int w = 0; w < kPrepU / kWave; ++w) dead |= wbadm[w];
+            if (a.mst_w) {
+                bool rej = true;
+#pragma unroll
+                for (int w = 0; w < kPrepU / kWave; ++w) rej = rej && wrej[w] != 0;
+                if (cw == 0 && u == 0) a.mst_w->skip = rej ? 1 : 0;
+                if (rej) return;   // (uniform) the later launches see skip and return
+            }
         }
         if (a.pd && a.keysP && iv) {
             // the fused chain's displacement bound (k_fiw.h sup_box): over this workgroup's live
@@ -465,6 +524,10 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
         a.vp[cand(u)] = bad ? __builtin_inf() : acc * a.penalty;
         if (a.dead8) a.dead8[cand(u)] = excl && bad ? 1 : 0;
     }
+    if (obj && a.feas && wid == 0) {   // the evaluations: candidates that pass cons3
+        const uint64_t ok = __ballot(u < kPrepC && cand(u) < K && !bad);
+        if (lane == 0 && ok) atomicAdd(a.feas, (unsigned long long)__popcll(ok));
+    }
     if (a.pd) {   // the workgroup's displacement bound: wave butterflies, then waves in order
         __shared__ double dred[kPrepU / kWave][4];
 #pragma unroll
@@ -496,7 +559,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
 __global__ __launch_bounds__(kPrepU) __attribute__((amdgpu_waves_per_eu(4))) void prep_kernel(uint64_t* ts, PrepArgs a)
 {
     ts_begin(ts);   // profiling only (the chain's first launch: k_common.h)
-    if (!a.src.resolve()) {
+    if (!a.src.resolve(true)) {
         ts_end(ts);
         return;
     }

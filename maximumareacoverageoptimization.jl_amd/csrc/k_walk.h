@@ -316,9 +316,10 @@ __global__ __launch_bounds__(kBlock) void walk_setup_kernel(
         const int j = threadIdx.x + q * kBlock;
         Q[q] = j < i && i < N ? region[j] : none;
     }
-    // a stopped pipelined MADS loop (k_prep.h MadsState): no walk; the poll kernel, the
-    // bit-word kernel and the finalize's argmin see mode 0 / the state and return
-    if (halt && halt->ell < 0) {
+    // a stopped pipelined MADS loop, or a poll its prep rejected whole (k_prep.h MadsState): no
+    // walk; the poll kernel, the shared-entry passes and the finalize's argmin see mode 0 / the
+    // state and return
+    if (halt && (halt->ell < 0 || halt->skip)) {
         if (blockIdx.x == 0 && threadIdx.x == 0) mode[0] = 0;
         ts_end(ts);
         return;

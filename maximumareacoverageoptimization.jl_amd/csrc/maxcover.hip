@@ -566,7 +566,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                          const double* d_prev, const double* d_dlimT, const double* d_dlim_raw,
                          double tan_half_fov, double* d_area, double* d_obj, double* d_best,
                          int64_t idx_base, uint64_t* d_mirror = nullptr, uint64_t mirror_seq = 0,
-                         const FinBest* fb_mads = nullptr)
+                         const FinBest* fb_mads = nullptr, unsigned long long* d_feas = nullptr)
 {
     const int64_t M = ctx->M;
     int n_poll = N, n_other = 1;
@@ -685,6 +685,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             pr.ldk = ldk;
             pr.pd = L->pd.as<double4>();
             pr.dead8 = excl ? L->dead8.as<uint8_t>() : nullptr;
+            pr.mst_w = excl && fb_mads ? fb_mads->st : nullptr;
+            pr.feas = d_feas;
             uint64_t* tsk = take_ts(nchain, ts_c, ts_nc);
             hipLaunchKernelGGL(prep_kernel, dim3((unsigned)nchain), dim3(kPrepU), 0, s, tsk, pr);
             HCK(hipGetLastError());
@@ -728,16 +730,17 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                 fb.idx_base = idx_base;
                 fb.blk = L->finblk.as<unsigned long long>();
                 fb.arrive = L->finarrive.as<unsigned>();
+                fb.hint = L->fwhint.as<int>();   // (read and cleared by the argmin's last block)
+                fb.hint_host = L->d_dc + 8;
+                fb.nhint = kFwHints;
             }
             uint64_t* tsf = take_ts(nfin, ts_f, ts_nf);
             if (counts)
                 hipLaunchKernelGGL(fin2_kernel<true>, dim3(nfin), dim3(kF2Threads), 0, s, L->frows.as<unsigned>(),
-                                   nullptr, ldk, N, K, ctx->w0, d_vp, d_area, d_obj, fb, L->fwhint.as<int>(),
-                                   L->d_dc + 8, f2s, tsf);
+                                   nullptr, ldk, N, K, ctx->w0, d_vp, d_area, d_obj, fb, f2s, tsf);
             else
                 hipLaunchKernelGGL(fin2_kernel<false>, dim3(nfin), dim3(kF2Threads), 0, s, nullptr,
-                                   L->frows.as<double>(), ldk, N, K, ctx->w0, d_vp, d_area, d_obj, fb,
-                                   L->fwhint.as<int>(), L->d_dc + 8, f2s, tsf);
+                                   L->frows.as<double>(), ldk, N, K, ctx->w0, d_vp, d_area, d_obj, fb, f2s, tsf);
             HCK(hipGetLastError());
             L->last_chain = 2;
             prof_end();
@@ -760,6 +763,11 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         pr.skip_failed = d_area ? 0 : 1;   // (the index maps them to an inert position likewise)
         pr.pair = pair ? 1 : 0;
         pr.g = ctx->grid;
+        pr.feas = d_feas;
+        // the pipelined MADS loop: a poll cons3 rejects whole is decided by the prep (k_prep.h
+        // MadsState.skip) when its failures are left out of the walk (the prep's excl)
+        pr.mst_w = fb_mads && poll_possible && d_obj && d_prev && !d_area && N <= kPrepU ? fb_mads->st
+                                                                                           : nullptr;
         if (poll_possible) {
             L->prec.reserve(sizeof(int4) * (size_t)nchain * N);
             pr.prec = L->prec.as<int4>();
@@ -1161,7 +1169,7 @@ int32_t mac_diag_walk_read(uint64_t* out, int64_t n)
 // diagnostic build only: per-disk phase stamps of the fused kernel (k_fiw.h)
 int32_t mac_diag_fiw_read(uint64_t* out, int64_t n)
 {
-    if (n > (int64_t)(8 * 65536)) n = 8 * 65536;
+    if (n > (int64_t)(16 * 65536)) n = 16 * 65536;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_fiw), sizeof(uint64_t) * n, 0,
                             hipMemcpyDeviceToHost) != hipSuccess)
         return MAC_E_HIP;
@@ -1836,8 +1844,10 @@ struct mac_mads {
     const double* d_dlimT = nullptr;
     std::vector<double> x;
     double f = INFINITY;
-    int64_t evals = 0, it = 0;
+    int64_t evals = 0, it = 0, rejected = 0;
     int ell = 0;
+    std::vector<double> h_prev;   // cons3's prev (host copy: whole-poll rejection, poll_rejected)
+    DevBuf d_feas;                // candidates that passed cons3 (the prep launches count them)
     uint64_t state = 0, T = 0, per_iter = 0;
     std::vector<int> rp, cp, rp_next, cp_next;
     double* hb = nullptr;
@@ -1860,6 +1870,7 @@ struct mac_mads {
     ~mac_mads()
     {
         d_x.release();
+        d_feas.release();
         d_st.release();
         d_ring.release();
         h_ring.release();
@@ -1867,6 +1878,22 @@ struct mac_mads {
 };
 
 static double* mads_best_ptr(mac_mads* m) { return m->ext_best ? m->ext_best : m->L->best.as<double>(); }
+
+// Whether cons3 rejects every candidate of the poll at mesh step b around x (k_prep.h
+// diag_rejects for each of the 3N variables: each is the diagonal of one column of B, so each
+// candidate carries one such step). Exact: the prep's cons3 would mark every candidate failed,
+// and the poll's result would be (+inf, -1).
+static bool poll_rejected(const mac_mads* m, int64_t b)
+{
+    if (!m->d_prev) return false;
+    const int N = m->N;
+    const std::vector<double>& T3 = m->L->h_dlim;
+    for (int v = 0; v < m->n; ++v) {
+        const int q = v / N, i = v % N;
+        if (!diag_rejects(m->x[v], (double)b, m->h_prev[v], q, m->tan_half_fov, T3[i])) return false;
+    }
+    return true;
+}
 
 // slot: the poll's best through the mapped slot finalize's last block writes (mads_wait_best),
 // else a 16-B copy
@@ -1888,7 +1915,8 @@ static void mads_best_of(mac_mads* m, const CandSrc& src, int Kc, int64_t idx_ba
                  m->L->rmax.as<double>(), m->penalty, m->d_prev, m->d_dlimT,
                  m->d_prev ? m->L->dlimraw.as<double>() : nullptr, m->tan_half_fov,
                  nullptr, m->L->obj.as<double>(), mads_best_ptr(m), idx_base,
-                 slot ? m->d_slot : nullptr, slot ? ++m->seq : 0);
+                 slot ? m->d_slot : nullptr, slot ? ++m->seq : 0, nullptr,
+                 slot ? m->d_feas.as<unsigned long long>() : nullptr);
     if (!slot) HCK(hipMemcpyAsync(m->hb, mads_best_ptr(m), 16, hipMemcpyDeviceToHost, m->s));
 }
 
@@ -1957,7 +1985,10 @@ int32_t mac_mads_begin(mac_ctx* ctx, const double* x0, int64_t three_n, const do
         L->best.reserve(16);
         L->rmax.reserve(sizeof(double) * N);
         HCK(hipMemcpyAsync(L->rmax.p, r_max, sizeof(double) * N, hipMemcpyHostToDevice, s));
+        m->d_feas.reserve(sizeof(unsigned long long));
+        HCK(hipMemsetAsync(m->d_feas.p, 0, sizeof(unsigned long long), s));
         if (prev) {
+            m->h_prev.assign(prev, prev + three_n);
             L->prev.reserve(sizeof(double) * three_n);
             L->dlim.reserve(sizeof(double) * N);
             L->dlimraw.reserve(sizeof(double) * N);
@@ -2019,7 +2050,18 @@ int32_t mac_mads_poll(mac_mads* m, int32_t* done, double* best_obj, int64_t* bes
     m->rp.swap(m->rp_next);
     m->cp.swap(m->cp_next);
     const int Kc = (int)(m->hi - m->lo);
-    if (Kc > 0) {
+    // a poll cons3 rejects whole: no launch, its result (+inf, -1) (every rank decides alike)
+    const bool rejected = Kc > 0 && poll_rejected(m, b);
+    if (rejected) {
+        ++m->rejected;
+        if (m->ext_best) {   // the buffer holds this poll's best once the call returns
+            m->hb[0] = INFINITY;
+            m->hb[1] = __builtin_bit_cast(double, (int64_t)-1);
+            HCK(hipMemcpyAsync(m->ext_best, m->hb, 16, hipMemcpyHostToDevice, m->s));
+            HCK(hipStreamSynchronize(m->s));
+        }
+    }
+    if (Kc > 0 && !rejected) {
         // (the staging is free: the previous iteration's copies completed at its sync)
         // one copy of the contiguous staging [incumbent 8n][permutations 4*2n] (n = 3N); the
         // staging is free: the previous poll's copy preceded its finalize, whose results were read
@@ -2045,7 +2087,7 @@ int32_t mac_mads_poll(mac_mads* m, int32_t* done, double* best_obj, int64_t* bes
         stream_permutation(ns, (uint64_t)n + m->T + n + 1, n, m->cp_next);
     }
     const auto tc = clk::now();
-    if (Kc > 0) {
+    if (Kc > 0 && !rejected) {
         mads_wait_best(m, best_obj, best_idx);
     } else {
         *best_obj = INFINITY;
@@ -2104,6 +2146,12 @@ int32_t mac_mads_result(mac_mads* m, double* x_out, mac_mads_stats* st)
         st->host_perm_s = m->h_perm;
         st->wait_s = m->h_wait;
         st->host_post_s = m->h_post;
+        unsigned long long fe = 0;
+        set_device(m->ctx);
+        HCK(hipMemcpyAsync(&fe, m->d_feas.p, sizeof(fe), hipMemcpyDeviceToHost, m->s));
+        HCK(hipStreamSynchronize(m->s));
+        st->feasible_evaluations = (int64_t)fe;
+        st->rejected_polls = m->rejected;
     }
     return MAC_OK;
     ABI_END
@@ -2191,7 +2239,7 @@ static void mads_run_pipelined(mac_mads* m)
     // the incumbent and the state: x0 (begin's pinned staging holds it), f(x0), ell0
     const auto ta = clk::now();
     HCK(hipMemcpyAsync(dx, m->hx, sizeof(double) * n, hipMemcpyHostToDevice, s));
-    const MadsState st0{m->f, 0, m->ell, 0};
+    const MadsState st0{m->f, 0, m->ell, 0, 0ull, 0};
     HCK(hipMemcpy(dst, &st0, sizeof(st0), hipMemcpyHostToDevice));
     int64_t computed = std::min<int64_t>(n_iter, kMadsAhead);
     for (int64_t t = 1; t <= computed; ++t) perms_of(t);
@@ -2238,7 +2286,7 @@ static void mads_run_pipelined(mac_mads* m)
         enqueue_eval(m->ctx, m->L, s, src, m->N, m->K, true, m->L->rmax.as<double>(), m->penalty,
                      m->d_prev, m->d_dlimT, m->d_prev ? m->L->dlimraw.as<double>() : nullptr,
                      m->tan_half_fov, nullptr, m->L->obj.as<double>(),
-                     m->L->best.as<double>(), 0, m->d_slot, (uint64_t)t, &fbm);
+                     m->L->best.as<double>(), 0, m->d_slot, (uint64_t)t, &fbm, &dst->feas);
         const auto t3 = clk::now();
         if (computed < n_iter) {   // one iteration's permutations per poll, uploaded per chunk
             perms_of(++computed);
@@ -2258,6 +2306,11 @@ static void mads_run_pipelined(mac_mads* m)
     m->it = st.it;
     m->ell = st.ell;
     m->evals = 1 + st.it * (int64_t)m->K;
+    m->rejected += st.skipped;
+    if (st.feas) {   // (the stepper's counter holds the polls' evaluations: none before this loop)
+        const unsigned long long fe = st.feas;
+        HCK(hipMemcpy(m->d_feas.p, &fe, sizeof(fe), hipMemcpyHostToDevice));
+    }
     m->state = state_of(st.it + 1);
     m->h_wait += std::chrono::duration<double>(clk::now() - t5).count();
 }

@@ -922,6 +922,12 @@ def test_native_mads_matches_python_driver(ctx, pkg, with_cons3):
     assert st["iterations"] == res.status.iteration
     assert st["evaluations"] == res.status.function_evaluations
     assert (st["status"] == 0) == (res.status.optimization_status == "MeshPrecisionLimit")
+    # the evaluations the reference makes (candidates passing cons3), and the polls cons3
+    # rejects whole with no launch (only ones where no candidate passes)
+    assert st["feasible_evaluations"] == res.status.cons3_passed
+    assert st["rejected_polls"] <= res.status.cons3_empty_polls
+    if not with_cons3:
+        assert st["rejected_polls"] == 0
 
 
 @pytest.mark.parametrize("algo", ["auto", "poll"])
@@ -1108,8 +1114,11 @@ def test_native_mads_pipelined_matches_stepper(ctx, pkg, N, n_iter, ell0, ell_ma
     finally:
         st_.close()
     assert np.array_equal(want_x, xs)
-    for key in ("f", "iterations", "evaluations", "status", "feasible"):
-        assert want[key] == got[key], key
+    for key in ("f", "iterations", "evaluations", "status", "feasible", "feasible_evaluations",
+                "rejected_polls"):
+        assert want[key] == got[key], key   # (rejections: device-side vs host-side, alike)
+    if cons3 and not stall and n_iter >= 40:   # (ell reaches 5: 2^5 - 12 > 12 on every axis)
+        assert want["rejected_polls"] > 0 and want["feasible_evaluations"] > 0
     if stall:
         assert want["status"] == 0 and want["iterations"] == ell0 + 1
         assert np.array_equal(want_x, x0)

@@ -35,11 +35,13 @@ def main():
     N = C.shape[1] // 3
     for _ in range(4):
         ctx.poll_best(C, rmax, 1e5, prev=C[0], d_lim=np.full(N, 10.0), tan_half_fov=tan)
-    buf = (ctypes.c_uint64 * (8 * N))()
-    assert L.mac_diag_fiw_read(buf, 8 * N) == 0
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(N, 8)
+    buf = (ctypes.c_uint64 * (16 * N))()
+    assert L.mac_diag_fiw_read(buf, 16 * N) == 0
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(N, 16)
     info = a[:, 7]
     t = a[:, :7].astype(np.int64)
+    # the walk's first slice / chunk: lane constants, staging + compaction, hot loop, band + rest
+    wk = np.concatenate([a[:, 3:4], a[:, 8:12], a[:, 4:5]], axis=1).astype(np.int64)
     ok = (t > 0).all(axis=1)
     t = t[ok]
     ph = np.diff(t, axis=1) / 100.0
@@ -53,6 +55,23 @@ def main():
            "neighbours_max": int(((info[ok] >> 16) & 0xFFFF).max()),
            "disks_with_neighbours": int((((info[ok] >> 16) & 0xFFFF) > 0).sum()),
            "box_tiles_median": float(np.median((info[ok] & 0xFFFF).astype(np.int64)))}
+    hk = np.concatenate([a[:, 1:2], a[:, 12:15], a[:, 2:3]], axis=1).astype(np.int64)[ok]
+    hok = (hk > 0).all(axis=1)
+    if hok.any():
+        hp = np.diff(hk[hok], axis=1) / 100.0
+        out["index_split"] = {"names": ["bound+box+neighbours", "table clear+mark", "miss vote",
+                                        "numbering"],
+                              "median_us": [round(float(v), 2) for v in np.median(hp, axis=0)],
+                              "max_us": [round(float(v), 2) for v in hp.max(axis=0)]}
+    wk = wk[ok]
+    wok = (wk > 0).all(axis=1)
+    if wok.any():
+        wp = np.diff(wk[wok], axis=1) / 100.0
+        out["walk_split"] = {"names": ["lane constants", "staging+compaction", "hot loop",
+                                       "band+sync", "rest (more chunks, credit write)"],
+                             "median_us": [round(float(v), 2) for v in np.median(wp, axis=0)],
+                             "max_us": [round(float(v), 2) for v in wp.max(axis=0)],
+                             "disks": int(wok.sum())}
     slow = np.argsort(-(t[:, 6] - t[:, 0]))[:5]
     out["slowest"] = [{"total_us": float((t[q, 6] - t[q, 0]) / 100.0),
                        "phases_us": [round(float(v), 2) for v in ph[q]],

@@ -36,6 +36,8 @@ for s in $STEPS; do
         [ $rc -eq 1 ] && rc=0 ;;
     fused)   # the fused chain's tests alone
         run pytest_fused 400 python -u -m pytest tests/test_gpu_fused.py -x -v -rfE -p no:cacheprovider --timeout 120 --timeout-method thread ; rc=$? ;;
+    mads)   # the native MADS loop's tests alone
+        run pytest_mads 400 python -u -m pytest tests -m gpu -k "mads" -x -v -rfE -p no:cacheprovider --timeout 120 --timeout-method thread ; rc=$? ;;
     smoke)
         run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ; rc=$? ;;
     benchq)
