@@ -60,7 +60,6 @@ constexpr int kFwR = kFwCH / kFwThreads;         // ... per thread
 constexpr int kFwShE = 64;                       // shared entries per decision word (in place)
 constexpr int kFwNbr = kPollNbr;                 // lower neighbours kept (more: every lower disk)
 constexpr int kFwShCap = 1024;                   // shared entries a disk hands to fin2_kernel
-constexpr int kFwTT = 64;                        // direct mode: radius thresholds tabulated
 
 // Hint words (device ints, zero between polls: fin2_kernel's last block copies them to the lane's
 // mapped host memory and clears them): [0] the most shared entries x neighbours of one disk,
@@ -170,9 +169,17 @@ __device__ uint64_t g_diag_f2[8 * 4096];      // per fin2 block
 #define MAC_F2_STAMP(q)
 #endif
 
+// per-position / per-candidate credit: exact integer counts (every entry weighs the same) or fp64
+template <bool C> struct FwAcc { typedef double T; };
+template <> struct FwAcc<true> { typedef unsigned T; };
+
+// kCounts == (a.counts != 0): the equal-weight build keeps its credits in 32-bit integers (half the
+// registers of the walk's accumulators and of the shared credits)
+template <bool kCounts>
 __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2))) void fiw_kernel(
     uint64_t* ts, FwArgs a)
 {
+    typedef typename FwAcc<kCounts>::T Acc;
     ts_begin(ts);
     CandSrc src = a.src;
     const int N = a.N, K = a.K;
@@ -188,7 +195,8 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
     // LDS, by phase (index | walk and shared entries):
     //   X: hash: key word per candidate        | key word per position (poskey)
     //   Y: dedup table (direct or hash)        | credit per position (u32 counts or f64)
-    //   Z: hash: a candidate of each position  | per candidate: position | failed << 15
+    //   Z: per candidate: slot | failed << 15  | per candidate: position | failed << 15
+    //   wbuf: hash: a candidate of each position (owner_of)
     //   wbuf: -                                | walk: slice lane constants + staging;
     //                                            in-place shared decisions: coverage words
     __shared__ uint32_t xbuf[kFwMaxK + 1];
@@ -209,9 +217,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
     __shared__ double nb_b[kFwNbr][3];
     __shared__ double dred[kFwWaves][4];
     __shared__ double sbase[7];   // candidate 0's disk i, the displacement bound
-    __shared__ double ttab[kFwTT];   // direct mode: T(br + dr) per radius offset dr + Dl (ttn > 0)
     __shared__ uint8_t scov[kFwKPB]; // per slice slot: its position's disk covers (finite, r > 0)
-    __shared__ int ttn, ttl;
     __shared__ unsigned ninner;      // entries every position covers (the annulus, counts only)
     __shared__ int ucnt, ncnt;
     __shared__ int wkeep[kFwR][kFwWaves];
@@ -221,7 +227,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
     int* const table = reinterpret_cast<int*>(tabbuf);
     unsigned* const pcnt = reinterpret_cast<unsigned*>(tabbuf);
     double* const pcred = tabbuf;
-    uint16_t* const owner_of = zbuf;
+    uint16_t* const owner_of = reinterpret_cast<uint16_t*>(wbuf);   // (hash numbering only)
     uint16_t* const cinfo = zbuf;
     float4* const sl4 = reinterpret_cast<float4*>(wbuf);
     float* const slx = reinterpret_cast<float*>(wbuf + kSl4);
@@ -282,12 +288,21 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
         if (tid == 0) {
             ucnt = 0;
             ncnt = 0;
-            ttn = 0;
             ninner = 0u;
         }
+        // the key words (failed: the dead word) and failure bits into LDS, this thread's own
+        // candidates (no barrier needed to read them back): no per-candidate registers stay live
+        // through the index (the walk needs every register it can get)
         bool esc = false;
 #pragma unroll
-        for (int j = 0; j < P; ++j) esc |= kof(j) < K && !dj[j] && pq[j] == kKeyEsc;
+        for (int j = 0; j < P; ++j) {
+            const int k = kof(j);
+            esc |= k < K && !dj[j] && pq[j] == kKeyEsc;
+            if (k < K) {
+                kx[k] = dj[j] ? kDeadWord : pq[j];
+                zbuf[k] = dj[j] ? (uint16_t)0x8000 : (uint16_t)0;
+            }
+        }
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
             dmx = fmax(dmx, __shfl_xor(dmx, o, kWave));
@@ -366,30 +381,28 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
         const int nslot = dfits && nrd >= 1 ? (2 * Dx + 1) * nyd * nrd : 0;
         bool direct = dfits && nrd >= 1 && (double)Dx == dmx && (double)Dy == dmy && (double)Dr == dmr &&
                       (double)Dl == dml && nslot + 1 <= kFwDirect;
-        int slot[P];
         if (direct) {
             for (int q = tid; q <= nslot; q += kFwThreads) table[q] = 0;
         }
         lds_barrier();   // (the table is cleared; the row runs' loads stay in flight)
+        MAC_FW_STAMP(15);
         bool miss = false;
-        if (direct) {
+        if (direct) {   // per candidate its slot (zbuf, beside the failure bit); branch-free
 #pragma unroll
             for (int j = 0; j < P; ++j) {
-                slot[j] = nslot;   // the dead slot
-                if (kof(j) >= K || dj[j]) continue;
-                float fx, fy, fr;
-                key_unpack(pq[j], fx, fy, fr);
-                const int dx = (int)fx, dy = (int)fy, dr = (int)fr;
-                if (!(br + (double)dr > 0.0)) continue;       // covers nothing: the dead slot
-                if (dx < -Dx || dx > Dx || dy < -Dy || dy > Dy || dr < -Dl || dr > Dr) {
-                    miss = true;
-                    continue;
+                const int k = kof(j);
+                const uint32_t w = pq[j];
+                const int dx = (int)(w << 21) >> 21, dy = (int)(w << 10) >> 21, dr = (int)w >> 22;
+                // (r <= 0 covers nothing: the dead slot, as a failed candidate)
+                const bool live = k < K && !dj[j] && br + (double)dr > 0.0;
+                const bool inr = dx >= -Dx && dx <= Dx && dy >= -Dy && dy <= Dy && dr >= -Dl && dr <= Dr;
+                miss |= live && !inr;
+                const int sl = live && inr ? ((dx + Dx) * nyd + (dy + Dy)) * nrd + (dr + Dl) : nslot;
+                if (k < K) {
+                    table[sl] = 1;
+                    zbuf[k] = (uint16_t)((dj[j] ? 0x8000 : 0) | sl);
                 }
-                slot[j] = ((dx + Dx) * nyd + (dy + Dy)) * nrd + (dr + Dl);
             }
-#pragma unroll
-            for (int j = 0; j < P; ++j)
-                if (kof(j) < K) table[slot[j]] = 1;
         }
         MAC_FW_STAMP(13);
         {   // any miss: the hash (an LDS word, not __syncthreads_or: that would wait for the row runs)
@@ -427,24 +440,13 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
                 }
             }
             if (tid == kFwThreads - 1) ucnt = id;
-            if (nrd <= kFwTT) {   // the positions' radii take nrd values: their thresholds once
-                if (tid < nrd) ttab[tid] = cover_threshold(br + (double)(tid - Dl));
-                if (tid == 0) {
-                    ttn = nrd;
-                    ttl = Dl;
-                }
-            }
         } else if (!ident) {
-#pragma unroll
-            for (int j = 0; j < P; ++j)
-                if (kof(j) < K) kx[kof(j)] = dj[j] ? kDeadWord : pq[j];
             for (int q = tid; q < kFwHash; q += kFwThreads) table[q] = -1;
             lds_barrier();
             constexpr uint32_t mask = kFwHash - 1;
 #pragma unroll
             for (int j = 0; j < P; ++j) {
                 const int k = kof(j);
-                slot[j] = 0;
                 if (k >= K) continue;
                 const uint32_t key = kx[k];
                 uint32_t s = word_hash(key) & mask;
@@ -457,7 +459,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
                     if (kx[cur] == key) break;
                     s = (s + 1) & mask;
                 }
-                slot[j] = (int)s;
+                zbuf[k] = (uint16_t)((zbuf[k] & 0x8000) | s);   // (the slot, beside the failure bit)
             }
             lds_barrier();
             for (int q = tid; q < kFwHash; q += kFwThreads) {
@@ -506,12 +508,6 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
         // per candidate its position; hash: per position its key word (through registers: the
         // buffers change roles at the barrier)
         const int U0 = ident ? K : ucnt;
-        int ukr[P];
-#pragma unroll
-        for (int j = 0; j < P; ++j)
-            ukr[j] = ident ? kof(j)
-                   : kof(j) >= K ? 0
-                   : direct ? table[slot[j]] : table[slot[j]] & ((1 << kFwIdBits) - 1);
         constexpr int PU = (kFwMaxK + 1 + kFwThreads - 1) / kFwThreads;
         uint32_t pkr[PU];
         const bool hashed = !direct && !ident;
@@ -520,17 +516,25 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
             const int u = tid + q * kFwThreads;
             pkr[q] = hashed && u < U0 ? kx[owner_of[u]] : 0u;
         }
-        lds_barrier();
+        // per candidate its position (this thread's own zbuf words: slot -> position), read
+        // before the barrier: the table's words become the position credits after it
 #pragma unroll
-        for (int j = 0; j < P; ++j)
-            if (kof(j) < K) cinfo[kof(j)] = (uint16_t)(ukr[j] | (dj[j] ? 0x8000 : 0));
+        for (int j = 0; j < P; ++j) {
+            const int k = kof(j);
+            if (k >= K) continue;
+            const uint16_t zb = zbuf[k];
+            const int sl = zb & 0x7FFF;
+            const int u = ident ? k : direct ? table[sl] : table[sl] & ((1 << kFwIdBits) - 1);
+            cinfo[k] = (uint16_t)(u | (zb & 0x8000));
+        }
+        lds_barrier();
         if (hashed) {
 #pragma unroll
             for (int q = 0; q < PU; ++q)
                 if (tid + q * kFwThreads < U0) poskey[tid + q * kFwThreads] = pkr[q];
         }
         for (int u = tid; u < U0; u += kFwThreads) {
-            if (a.counts) pcnt[u] = 0u;
+            if (kCounts) pcnt[u] = 0u;
             else pcred[u] = 0.0;
         }
         lds_barrier();
@@ -548,20 +552,28 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
         return word_disk(poskey[u], sbase[0], sbase[1], sbase[2]);
     };
 
-    // the walk's disks: in direct mode from the key word and the tabulated threshold
-    const bool tabT = ttn > 0;
-    const int tl = ttl;
+    // The walk's lane constants need T(r) only to within the fp32 filter's spare error budget
+    // (k_poll.h: the filter's error is below 38.1 eps M^2 S, the band half-width X' is 64 eps M^2 S,
+    // eps = 2^-24): fl(r * r) differs from T(r) by a few ulp of r^2 (2^-51 M^2), far inside it, and
+    // every entry in the band is re-decided with the exact T (pos_disk). So the lane constants take
+    // the disk from its key word and r * r, without the 128-bit threshold (cover_threshold).
     auto walk_disk = [&](int u) -> DiskRec {
-        if (!tabT) return pos_disk(u);
-        const uint32_t w = poskey[u];
-        if (w == kDeadWord) return inert_disk();
-        float fx, fy, fr;
-        key_unpack(w, fx, fy, fr);
         DiskRec d;
-        d.cx = sbase[0] + (double)fx;
-        d.cy = sbase[1] + (double)fy;
-        d.r = sbase[2] + (double)fr;
-        d.T = ttab[(int)fr + tl];
+        if (ident) {
+            if (cinfo[u] & 0x8000) return inert_disk();
+            d.cx = src_val(src, u, i, N);
+            d.cy = src_val(src, u, N + i, N);
+            d.r = src_val(src, u, 2 * N + i, N);
+        } else {
+            const uint32_t w = poskey[u];
+            if (w == kDeadWord) return inert_disk();
+            float fx, fy, fr;
+            key_unpack(w, fx, fy, fr);
+            d.cx = sbase[0] + (double)fx;
+            d.cy = sbase[1] + (double)fy;
+            d.r = sbase[2] + (double)fr;
+        }
+        d.T = d.r > 0.0 ? d.r * d.r : -1.0;
         return d;
     };
     // The annulus (equal weights): every position's disk (c, r) lies within the displacement
@@ -571,7 +583,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
     // rounding of d, the bound and the reference's sqrt(d^2) < r. Those entries skip the tests:
     // the first are counted once and credited to every covering position, the second dropped.
     double rin2 = -1.0, rout2 = __builtin_inf();
-    if (a.counts && rany) {
+    if (kCounts && rany) {
         const double bx0 = sbase[2], ex = sbase[3], ey = sbase[4], er = sbase[5], el = sbase[6];
         const double e = __builtin_sqrt(ex * ex + ey * ey) * (1.0 + 1e-9);
         const double rin = (bx0 - el) - e - 1e-9 * (__builtin_fabs(bx0) + __builtin_fabs(el) + e + 1.0);
@@ -593,9 +605,10 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
                 bool cov = false;
                 if (u < ke) {
                     const DiskRec d = walk_disk(u);
-                    int4 sp;
+                    // (a finite disk with r > 0 whose span misses the grid covers no entry: its
+                    // lane decides every staged entry "not covered", exactly as an inert lane)
                     cov = d.T >= 0.0 && __builtin_isfinite(d.cx) && __builtin_isfinite(d.cy);
-                    if (tabT ? cov : disk_span(d, g, sp)) L = poll_lane(d, ox, oy, Umax);
+                    if (cov) L = poll_lane(d, ox, oy, Umax);
                 }
                 sl4[t] = make_float4(L.sa, L.sb, L.stm, L.ns);
                 slx[t] = L.xp;
@@ -605,7 +618,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
             if (kb == 0) MAC_FW_STAMP(8);
             f32x2 sa[kPollPairs], sb[kPollPairs], st[kPollPairs], ns[kPollPairs];
             float xp[kPollSlots];
-            double acc[kPollSlots];
+            Acc acc[kPollSlots];
             uint32_t live = 0, covm = 0;
 #pragma unroll
             for (int u = 0; u < kPollSlots; ++u) {
@@ -614,7 +627,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
                 xp[u] = kb + p < ke ? slx[p] : -1.0f;
                 if (kb + p < ke) live |= 1u << u;
                 if (kb + p < ke && scov[p]) covm |= 1u << u;
-                acc[u] = 0.0;
+                acc[u] = 0;
                 const int j = u >> 1;
                 if (u & 1) {
                     sa[j].y = c.x; sb[j].y = c.y; st[j].y = c.z; ns[j].y = c.w;
@@ -723,10 +736,13 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
                     }
                     if (tid < ((4 - (n & 3)) & 3)) s32[n + tid] = make_float4(__builtin_inff(), 0.0f, 0.0f, 0.0f);
                     __syncthreads();
-                    const uint64_t w0b = __builtin_bit_cast(uint64_t, sw[0]);
-                    bool mixed = false;
-                    for (int e = tid; e < n; e += kFwThreads) mixed |= __builtin_bit_cast(uint64_t, sw[e]) != w0b;
-                    const bool uniform = !__syncthreads_or(mixed);
+                    bool uniform = true;   // (equal weights: always)
+                    if constexpr (!kCounts) {
+                        const uint64_t w0b = __builtin_bit_cast(uint64_t, sw[0]);
+                        bool mixed = false;
+                        for (int e = tid; e < n; e += kFwThreads) mixed |= __builtin_bit_cast(uint64_t, sw[e]) != w0b;
+                        uniform = !__syncthreads_or(mixed);
+                    }
                     if (kb == 0 && rb == RG.z && base == 0) MAC_FW_STAMP(9);
                     const int ng = (n + 3) >> 2;
                     float bmin[kPollSlots];
@@ -740,11 +756,14 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
                         case 3: poll_hot<3, kFwWaves>(s32, ng, wid, sa, sb, st, ns, h, bmin); break;
                         default: poll_hot<4, kFwWaves>(s32, ng, wid, sa, sb, st, ns, h, bmin); break;
                         }
-                        const double wu = a.counts ? 1.0 : sw[0];
+                        const double wu = kCounts ? 1.0 : sw[0];
 #pragma unroll
                         for (int u = 0; u < kPollSlots; ++u) {
                             const float hc = (u & 1) ? h[u >> 1].y : h[u >> 1].x;
-                            if ((live & (1u << u)) && !(bmin[u] <= xp[u])) acc[u] += (double)hc * wu;
+                            if ((live & (1u << u)) && !(bmin[u] <= xp[u])) {
+                                if constexpr (kCounts) acc[u] += (unsigned)hc;
+                                else acc[u] += (double)hc * wu;
+                            }
                         }
                     } else {
                         for (int q4 = wid; q4 < ng; q4 += kFwWaves) {
@@ -758,7 +777,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
                                     const float d = (u & 1)
                                         ? __builtin_fmaf(en.x, ns[j].y, __builtin_fmaf(en.z, sb[j].y, __builtin_fmaf(en.y, sa[j].y, st[j].y)))
                                         : __builtin_fmaf(en.x, ns[j].x, __builtin_fmaf(en.z, sb[j].x, __builtin_fmaf(en.y, sa[j].x, st[j].x)));
-                                    if ((live & (1u << u)) && d > 0.0f) acc[u] += wq;
+                                    if ((live & (1u << u)) && d > 0.0f) acc[u] += (Acc)wq;
                                     bmin[u] = __builtin_fminf(bmin[u], __builtin_fabsf(d));
                                 }
                             }
@@ -792,13 +811,13 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
                                 } else {
                                     cov = dp > 0.0f;
                                 }
-                                const double we = a.counts ? 1.0 : sw[e];
+                                const double we = kCounts ? 1.0 : sw[e];
                                 if (cov) cv += we;
                                 if (dp > 0.0f) fv += we;
                             }
 #pragma unroll
                         for (int u = 0; u < kPollSlots; ++u)
-                            if (u == ub) acc[u] += uniform ? cv : cv - fv;
+                            if (u == ub) acc[u] += (Acc)(uniform ? cv : cv - fv);
                     }
                     __syncthreads();   // the staging is read
                     if (kb == 0 && rb == RG.z && base == 0) MAC_FW_STAMP(11);
@@ -806,7 +825,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
             }
             // the slice's credit per position, the waves' shares added in wave order (wave 0
             // adds the annulus' inner entries to every covering position)
-            if (a.counts) {
+            if constexpr (kCounts) {
                 const unsigned nin = wid == 0 ? ninner : 0u;
 #pragma unroll
                 for (int u = 0; u < kPollSlots; ++u)
@@ -829,9 +848,9 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
 
     // ---- the shared entries (box i's entries inside a lower box): enumerated in a fixed order and
     // handed to fin2_kernel, or — past kFwShCap entries or kFwNbr neighbours — decided here
-    double sh[P];
+    Acc sh[P];
 #pragma unroll
-    for (int j = 0; j < P; ++j) sh[j] = 0.0;
+    for (int j = 0; j < P; ++j) sh[j] = 0;
     int swork = 0;
     bool handed = false;
     if (rany && nc > 0) {
@@ -964,8 +983,8 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
                         }
 #pragma unroll
                         for (int j = 0; j < P; ++j) {
-                            if (a.counts) {
-                                sh[j] += (double)__popcll(Mj[j]);
+                            if constexpr (kCounts) {
+                                sh[j] += (unsigned)__popcll(Mj[j]);
                             } else {
                                 for (uint64_t b = Mj[j]; b;) {
                                     const int e = __builtin_ctzll(b);
@@ -1000,7 +1019,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
     for (int c = 0; c < kFwPer / 4; ++c) {
         const int b0 = tid * kFwPer + 4 * c;
         if (b0 >= K) break;
-        if (a.counts) {
+        if constexpr (kCounts) {
             unsigned v[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -1022,7 +1041,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
     if (tid == 0 && K > kFwMaxK) {
         const uint16_t ci = cinfo[kFwMaxK];
         const bool dead = (ci & 0x8000) || !rany;
-        if (a.counts) a.crow[orow + kFwMaxK] = dead ? 0u : pcnt[ci & 0x7FFF] + (unsigned)sh[kFwPer];
+        if constexpr (kCounts) a.crow[orow + kFwMaxK] = dead ? 0u : pcnt[ci & 0x7FFF] + (unsigned)sh[kFwPer];
         else a.frow[orow + kFwMaxK] = dead ? 0.0 : pcred[ci & 0x7FFF] + sh[kFwPer];
     }
     if (tid == 0 && a.hint) {

@@ -715,7 +715,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             uint64_t* tsw = take_ts(nfw, ts_w, ts_nw);
             ts_a = ts_w;   // (mac_profile_read: the walk launch)
             ts_na = ts_nw;
-            hipLaunchKernelGGL(fiw_kernel, dim3(nfw), dim3(kFwThreads), 0, s, tsw, fa);
+            if (counts) hipLaunchKernelGGL(fiw_kernel<true>, dim3(nfw), dim3(kFwThreads), 0, s, tsw, fa);
+            else hipLaunchKernelGGL(fiw_kernel<false>, dim3(nfw), dim3(kFwThreads), 0, s, tsw, fa);
             HCK(hipGetLastError());
             const unsigned nfin = 8 * (unsigned)((K + 8 * kF2C - 1) / (8 * kF2C));
             FinBest fb{};

@@ -55,12 +55,12 @@ def main():
            "neighbours_max": int(((info[ok] >> 16) & 0xFFFF).max()),
            "disks_with_neighbours": int((((info[ok] >> 16) & 0xFFFF) > 0).sum()),
            "box_tiles_median": float(np.median((info[ok] & 0xFFFF).astype(np.int64)))}
-    hk = np.concatenate([a[:, 1:2], a[:, 12:15], a[:, 2:3]], axis=1).astype(np.int64)[ok]
+    hk = np.concatenate([a[:, 1:2], a[:, 12:13], a[:, 15:16], a[:, 13:15], a[:, 2:3]], axis=1).astype(np.int64)[ok]
     hok = (hk > 0).all(axis=1)
     if hok.any():
         hp = np.diff(hk[hok], axis=1) / 100.0
-        out["index_split"] = {"names": ["bound+box+neighbours", "table clear+mark", "miss vote",
-                                        "numbering"],
+        out["index_split"] = {"names": ["bound+box+neighbours", "table clear+barrier", "mark",
+                                        "miss vote", "numbering"],
                               "median_us": [round(float(v), 2) for v in np.median(hp, axis=0)],
                               "max_us": [round(float(v), 2) for v in hp.max(axis=0)]}
     wk = wk[ok]
