@@ -212,6 +212,19 @@ int32_t mac_mads_begin(mac_ctx* ctx, const double* x0, int64_t three_n, const do
 int32_t mac_mads_poll(mac_mads* m, int32_t* done, double* best_obj, int64_t* best_idx);
 int32_t mac_mads_update(mac_mads* m, double best_obj, int64_t best_idx);
 int32_t mac_mads_result(mac_mads* m, double* x_out, mac_mads_stats* stats);
+/* Speculation over failure branches (src/TDM_STATIC_opt.jl:162: the MADS iterations are
+ * serial, but a failed iteration's next poll is fully determined: the same incumbent, ell - 1, the
+ * stream's next position). Rank j of a P-GPU loop evaluates, beside rank 0's real poll, the poll
+ * that follows j consecutive failures; after one exchange every rank applies the results in
+ * order up to the first success, so a run of failures advances up to P iterations per round:
+ *   mac_mads_poll_ahead  evaluates (this stepper's shard of) the poll of the iteration `ahead`
+ *                        failures past the current one, without advancing; done = 1 when that
+ *                        poll does not exist (iteration limit or ell - ahead < 0);
+ *   mac_mads_advance     applies one iteration's result (the poll at ahead = 0) as
+ *                        mac_mads_update does, without a prior mac_mads_poll; moved = 1 when the
+ *                        incumbent moved (success). Same iterates as the sequential loop. */
+int32_t mac_mads_poll_ahead(mac_mads* m, int32_t ahead, int32_t* done, double* best_obj, int64_t* best_idx);
+int32_t mac_mads_advance(mac_mads* m, double best_obj, int64_t best_idx, int32_t* moved);
 void mac_mads_destroy(mac_mads* m);
 /* Every later poll of the stepper also writes its 16-byte shard best {objective, index as
  * int64 bits} to d_best16 (device memory of the context's device, 8-byte aligned; NULL: stop):

@@ -193,6 +193,40 @@ class PollStepper:
         else:
             self.ell -= 1
 
+    # speculation over failure branches (mac_mads_poll_ahead / mac_mads_advance)
+    def _draws(self) -> int:
+        n = self.n
+        return n + n * (n - 1) // 2 + 2 * n   # ltmads_basis's stream values per iteration
+
+    def _poll_matrix(self, ahead: int):
+        rng = SplitMix64()
+        with np.errstate(over="ignore"):
+            rng.state = self.rng.state + np.uint64(ahead * self._draws()) * np.uint64(0x9E3779B97F4A7C15)
+        B = ltmads_basis(self.n, self.ell - ahead, rng).astype(np.float64)
+        return np.concatenate([self.x[None, :] + B.T, self.x[None, :] - B.T], axis=0)
+
+    def poll_ahead(self, ahead: int):
+        if self.it + ahead >= self.N_iter or self.ell - ahead < 0:
+            return True, np.inf, -1
+        Xs = self._poll_matrix(ahead)[self.lo:self.hi]
+        if Xs.shape[0] == 0:
+            return False, np.inf, -1
+        bo, bi = self.poll_fn(Xs)
+        return False, float(bo), (self.lo + int(bi) if bi >= 0 else -1)
+
+    def advance(self, best_obj: float, best_idx: int) -> bool:
+        X = self._poll_matrix(0)
+        self.rng.next_u64(self._draws())   # the iteration's stream values
+        self.it += 1
+        self.evals += 2 * self.n
+        if best_idx >= 0 and best_obj < self.f:
+            self.x = X[best_idx].copy()
+            self.f = float(best_obj)
+            self.ell = min(self.ell + 1, self.ell_max)
+            return True
+        self.ell -= 1
+        return False
+
     def result(self):
         return self.x.copy(), {"f": self.f, "iterations": self.it, "evaluations": self.evals,
                                "status": 0 if self.ell < 0 else 1}

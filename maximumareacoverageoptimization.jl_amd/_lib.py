@@ -66,6 +66,7 @@ EXPORTS = (
     "mac_set_points_f32", "mac_set_points_dev_f32", "mac_area_f32", "mac_area_batch_f32",
     "mac_poll_best_f32", "mac_poll_best_dev_f32",
     "mac_mads_begin", "mac_mads_poll", "mac_mads_update", "mac_mads_result", "mac_mads_destroy",
+    "mac_mads_poll_ahead", "mac_mads_advance",
     "mac_mads_best_buffer",
 )
 
@@ -169,6 +170,8 @@ def _declare(L: ctypes.CDLL) -> None:
                             ctypes.POINTER(MadsParams), _i64, _i64, ctypes.POINTER(_vp)], _i32),
         "mac_mads_poll": ([_vp, ctypes.POINTER(_i32), _dp, _i64p], _i32),
         "mac_mads_update": ([_vp, ctypes.c_double, _i64], _i32),
+        "mac_mads_poll_ahead": ([_vp, _i32, ctypes.POINTER(_i32), _dp, _i64p], _i32),
+        "mac_mads_advance": ([_vp, ctypes.c_double, _i64, ctypes.POINTER(_i32)], _i32),
         "mac_mads_result": ([_vp, _dp, ctypes.POINTER(MadsStats)], _i32),
         "mac_mads_destroy": ([_vp], None),
         "mac_mads_best_buffer": ([_vp, _vp], _i32),
@@ -720,6 +723,19 @@ class MadsStepper:
 
     def update(self, best_obj: float, best_idx: int) -> None:
         _check(self._L.mac_mads_update(self._h, float(best_obj), int(best_idx)))
+
+    def poll_ahead(self, ahead: int):
+        """mac_mads_poll_ahead: (done, best_obj, best_idx) of the poll that follows `ahead`
+        failures of the current iteration, the stepper unchanged."""
+        _check(self._L.mac_mads_poll_ahead(self._h, int(ahead), ctypes.byref(self._done),
+                                           ctypes.byref(self._bo), ctypes.byref(self._bi)))
+        return bool(self._done.value), self._bo.value, int(self._bi.value)
+
+    def advance(self, best_obj: float, best_idx: int) -> bool:
+        """mac_mads_advance: apply one iteration's result; True when the incumbent moved."""
+        mv = _i32()
+        _check(self._L.mac_mads_advance(self._h, float(best_obj), int(best_idx), ctypes.byref(mv)))
+        return bool(mv.value)
 
     def best_buffer(self, d_best16) -> None:
         """Later polls also write their 16-B shard best into ``d_best16`` (a device tensor of

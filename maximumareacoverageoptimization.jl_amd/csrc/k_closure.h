@@ -49,7 +49,7 @@ struct ClosureOut {
 // Disks per workgroup: one wave per disk (the candidate is staged once per 4 disks).
 constexpr int kClosureDisksPerWG = kWavesPerBlock;
 
-__global__ __launch_bounds__(kBlock) void closure_kernel(uint64_t* ts, const double* __restrict__ cand,
+__global__ __launch_bounds__(kBlock) void closure_kernel(uint64_t* ts, const double* cand,
                                                          int N, Grid g, const double2* __restrict__ xy,
                                                          const double* __restrict__ w,
                                                          const int32_t* __restrict__ off, int counts,
@@ -65,6 +65,17 @@ __global__ __launch_bounds__(kBlock) void closure_kernel(uint64_t* ts, const dou
     __shared__ int rs[kClosureDisksPerWG][kWave], rpre[kClosureDisksPerWG][kWave + 1];
     __shared__ unsigned long long wcnt[kClosureDisksPerWG];
     __shared__ int sarr;
+    // grid.y: the candidates of a coalesced batch (mac_area_f64 callers arriving together), each
+    // with its own counters, credits, device word and slot (ts: null for batches)
+    {
+        const int b = (int)blockIdx.y;
+        cand += (size_t)b * 3 * (size_t)N;
+        o.part += (size_t)b * (size_t)N;
+        o.total += b;
+        o.arrive += b;
+        o.area += b;
+        if (o.slot) o.slot += 4 * b;
+    }
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
     const int i = blockIdx.x * kClosureDisksPerWG + wid;   // this wave's disk
     const bool valid = i < N;                                // (wave-uniform)

@@ -308,10 +308,12 @@ __device__ __forceinline__ void lds_barrier()
 template <bool kMat>
 __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
 {
-    __shared__ double term[kPrepC][kPrepU + 1];   // [candidate][UAV] (+1: lanes on distinct banks)
+    // [candidate][UAV]; rows 16-B aligned (the fold reads pairs) and 4 banks apart (+2)
+    __shared__ __attribute__((aligned(16))) double term[kPrepC][kPrepU + 2];
     __shared__ int wbad[kPrepU / kWave][kPrepC];  // per wave: a term of the candidate is negative
     __shared__ uint32_t wbadm[kPrepU / kWave];       // ... wbad as a mask over the candidates
     __shared__ int wrej[kPrepU / kWave];             // per wave: every UAV's diagonal steps fail (mst_w)
+    __shared__ double dred[kPrepU / kWave][4];       // per wave: its share of the displacement bound
     const int N = a.N, K = a.K;
     const int u = threadIdx.x, lane = u & (kWave - 1), wid = u / kWave;
     const int k0 = cw * kPrepC;
@@ -441,6 +443,22 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
                 }
             }
         }
+        if (a.pd && ib + kPrepU >= N) {   // (uniform) this wave's share of the bound, into LDS now:
+            // its registers are free before the fold (thread 0 combines the waves at the end)
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+                dmx = fmax(dmx, __shfl_xor(dmx, o, kWave));
+                dmy = fmax(dmy, __shfl_xor(dmy, o, kWave));
+                dmr = fmax(dmr, __shfl_xor(dmr, o, kWave));
+                dml = fmax(dml, __shfl_xor(dml, o, kWave));
+            }
+            if (lane == 0) {
+                dred[wid][0] = dmx;
+                dred[wid][1] = dmy;
+                dred[wid][2] = dmr;
+                dred[wid][3] = dml;
+            }
+        }
         if ((a.prec || a.keysP) && iv) {
             double xa = __builtin_inf(), xb = -__builtin_inf(), ya = __builtin_inf(), yb = -__builtin_inf();
             double xm = 0.0, ym = 0.0, est = 0.0;
@@ -505,15 +523,29 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
 #pragma unroll
                 for (int w = 0; w < kPrepU / kWave; ++w) bad |= wbad[w][u] != 0;
                 if (!bad) {   // (a cons3 failure's vp is +inf: no chain to fold)
-                    int q = 0;
-                    for (; q + 16 <= nb; q += 16) {
-                        double t[16];
+                    // batches of 2 kB terms (pair reads), the next batch's reads in flight while
+                    // this batch's adds run: the dependent adds, not the LDS latency, set the pace
+                    constexpr int kB = 6;
+                    const double2* row2 = reinterpret_cast<const double2*>(&term[u][0]);
+                    const int nfull = nb / (2 * kB);
+                    double2 cur[kB];
 #pragma unroll
-                        for (int j = 0; j < 16; ++j) t[j] = term[u][q + j];
+                    for (int j = 0; j < kB; ++j) cur[j] = nfull > 0 ? row2[j] : make_double2(0.0, 0.0);
+#pragma unroll 1
+                    for (int bt = 0; bt < nfull; ++bt) {
+                        const int nx = (bt + 1 < nfull ? bt + 1 : bt) * kB;   // (the last: a re-read)
+                        double2 nxt[kB];
 #pragma unroll
-                        for (int j = 0; j < 16; ++j) acc += t[j];
+                        for (int j = 0; j < kB; ++j) nxt[j] = row2[nx + j];
+#pragma unroll
+                        for (int j = 0; j < kB; ++j) {
+                            acc += cur[j].x;
+                            acc += cur[j].y;
+                        }
+#pragma unroll
+                        for (int j = 0; j < kB; ++j) cur[j] = nxt[j];
                     }
-                    for (; q < nb; ++q) acc += term[u][q];
+                    for (int q = nfull * 2 * kB; q < nb; ++q) acc += term[u][q];
                 }
             }
         }
@@ -528,30 +560,17 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
         const uint64_t ok = __ballot(u < kPrepC && cand(u) < K && !bad);
         if (lane == 0 && ok) atomicAdd(a.feas, (unsigned long long)__popcll(ok));
     }
-    if (a.pd) {   // the workgroup's displacement bound: wave butterflies, then waves in order
-        __shared__ double dred[kPrepU / kWave][4];
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            dmx = fmax(dmx, __shfl_xor(dmx, o, kWave));
-            dmy = fmax(dmy, __shfl_xor(dmy, o, kWave));
-            dmr = fmax(dmr, __shfl_xor(dmr, o, kWave));
-            dml = fmax(dml, __shfl_xor(dml, o, kWave));
-        }
-        if (lane == 0) {
-            dred[wid][0] = dmx;
-            dred[wid][1] = dmy;
-            dred[wid][2] = dmr;
-            dred[wid][3] = dml;
-        }
-        __syncthreads();
+    if (a.pd) {   // the workgroup's displacement bound: the waves' shares in order
+        lds_barrier();
         if (u == 0) {
+            double4 m = make_double4(dred[0][0], dred[0][1], dred[0][2], dred[0][3]);
             for (int q = 1; q < kPrepU / kWave; ++q) {
-                dmx = fmax(dmx, dred[q][0]);
-                dmy = fmax(dmy, dred[q][1]);
-                dmr = fmax(dmr, dred[q][2]);
-                dml = fmax(dml, dred[q][3]);
+                m.x = fmax(m.x, dred[q][0]);
+                m.y = fmax(m.y, dred[q][1]);
+                m.z = fmax(m.z, dred[q][2]);
+                m.w = fmax(m.w, dred[q][3]);
             }
-            a.pd[cw] = make_double4(dmx, dmy, dmr, dml);
+            a.pd[cw] = m;
         }
     }
 }

@@ -13,6 +13,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <new>
 #include <string>
@@ -170,6 +172,11 @@ struct mac_ctx {
     int device = 0;
     int cus = 256;
     std::mutex mu;
+    // mac_area_f64's combiner: queued single-candidate requests, one batch launch at a time
+    std::mutex cl_mu;
+    std::condition_variable cl_cv;
+    std::deque<struct ClReq*> cl_q;
+    bool cl_busy = false;
     std::vector<Lane*> lanes_free;
     std::vector<Lane*> lanes_all;
     hipStream_t setup_stream = nullptr;
@@ -2131,6 +2138,96 @@ int32_t mac_mads_update(mac_mads* m, double best_obj, int64_t best_idx)
     ABI_END
 }
 
+// Speculation over failure branches (the sharded loop's other mode, dist.mads_loop speculate):
+// a failed iteration's next poll is fully determined — the same incumbent, ell - 1 and the next
+// stream position — so rank j can evaluate, beside rank 0's real poll, the poll that follows j
+// consecutive failures. mac_mads_poll_ahead evaluates it (the whole poll, this stepper's shard)
+// without advancing the stepper; mac_mads_advance then applies the gathered results in order, one
+// iteration each, up to the first success. Same iterates as the sequential loop.
+int32_t mac_mads_poll_ahead(mac_mads* m, int32_t ahead, int32_t* done, double* best_obj, int64_t* best_idx)
+{
+    ABI_BEGIN
+    if (!m || !done || !best_obj || !best_idx) return fail(MAC_E_INVAL, "null argument");
+    if (ahead < 0) return fail(MAC_E_INVAL, "negative ahead");
+    if (m->polled_b) return fail(MAC_E_INVAL, "mac_mads_poll_ahead with a mac_mads_poll pending");
+    *done = 0;
+    *best_obj = INFINITY;
+    *best_idx = -1;
+    if (m->it + ahead >= m->prm.n_iter || m->ell - ahead < 0) {
+        *done = 1;
+        return MAC_OK;
+    }
+    set_device(m->ctx);
+    const int n = m->n;
+    const int ell = m->ell - ahead;
+    const int64_t b = (int64_t)1 << ell;
+    const uint64_t state = m->state + (uint64_t)ahead * m->per_iter * 0x9E3779B97F4A7C15ull;
+    const int Kc = (int)(m->hi - m->lo);
+    if (Kc == 0) return MAC_OK;
+    if (poll_rejected(m, b)) {
+        ++m->rejected;
+        return MAC_OK;
+    }
+    if (ahead == 0) {   // the current iteration's permutations are computed already
+        std::copy(m->rp_next.begin(), m->rp_next.end(), m->hperm);
+        std::copy(m->cp_next.begin(), m->cp_next.end(), m->hperm + n);
+    } else {
+        std::vector<int> rp, cp;
+        stream_permutation(state, (uint64_t)n + m->T + 1, n, rp);
+        stream_permutation(state, (uint64_t)n + m->T + n + 1, n, cp);
+        std::copy(rp.begin(), rp.end(), m->hperm);
+        std::copy(cp.begin(), cp.end(), m->hperm + n);
+    }
+    std::copy(m->x.begin(), m->x.end(), m->hx);
+    m->L->xinc.reserve(sizeof(double) * n + sizeof(int) * 2 * n);
+    HCK(hipMemcpyAsync(m->L->xinc.p, m->hx, sizeof(double) * n + sizeof(int) * 2 * n,
+                       hipMemcpyHostToDevice, m->s));
+    CandSrc src{};
+    src.xinc = m->L->xinc.as<double>();
+    src.rp = reinterpret_cast<int*>(m->L->xinc.as<double>() + n);
+    src.cp = src.rp + n;
+    src.state = state;
+    src.b = b;
+    src.k0 = (int)m->lo;
+    mads_best_of(m, src, Kc, m->lo, true);
+    mads_wait_best(m, best_obj, best_idx);
+    return MAC_OK;
+    ABI_END
+}
+
+int32_t mac_mads_advance(mac_mads* m, double best_obj, int64_t best_idx, int32_t* moved)
+{
+    ABI_BEGIN
+    if (!m) return fail(MAC_E_INVAL, "null stepper");
+    if (m->polled_b) return fail(MAC_E_INVAL, "mac_mads_advance with a mac_mads_poll pending (use mac_mads_update)");
+    if (best_idx >= m->K) return fail(MAC_E_INVAL, "best index outside the poll");
+    if (m->it >= m->prm.n_iter || m->ell < 0) return fail(MAC_E_INVAL, "mac_mads_advance past the loop's end");
+    const int n = m->n;
+    const int64_t b = (int64_t)1 << m->ell;
+    ++m->it;
+    m->evals += m->K;
+    const bool better = best_idx >= 0 && best_obj < m->f;
+    if (better) {   // the current iteration's permutations (rp_next / cp_next)
+        const int kk = best_idx < n ? (int)best_idx : (int)best_idx - n;
+        for (int v = 0; v < n; ++v) {
+            const double d = ltmads_entry(m->state, n, b, m->rp_next[v], m->cp_next[kk]);
+            m->x[v] = best_idx < n ? m->x[v] + d : m->x[v] - d;
+        }
+        m->f = best_obj;
+        m->ell = std::min(m->ell + 1, (int)m->prm.ell_max);
+    } else {
+        --m->ell;
+    }
+    m->state += m->per_iter * 0x9E3779B97F4A7C15ull;
+    if (m->it < m->prm.n_iter) {
+        stream_permutation(m->state, (uint64_t)n + m->T + 1, n, m->rp_next);
+        stream_permutation(m->state, (uint64_t)n + m->T + n + 1, n, m->cp_next);
+    }
+    if (moved) *moved = better ? 1 : 0;
+    return MAC_OK;
+    ABI_END
+}
+
 int32_t mac_mads_result(mac_mads* m, double* x_out, mac_mads_stats* st)
 {
     ABI_BEGIN
@@ -2351,51 +2448,46 @@ int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const doub
     ABI_END
 }
 
-// The single-candidate closure (k_closure.h): the candidate through the lane's pinned staging, one
-// kernel, the area from the lane's mapped slot (no copy back, no stream synchronisation). AUTO /
-// TILED walks, N <= kClosureMaxN; otherwise (or if the slot has not landed within 2 ms: a failed
-// launch) the batch chain / a stream synchronisation report it.
-static int32_t closure_eval(mac_ctx* ctx, const double* circles, int64_t three_n, double* area_out,
-                            bool* handled)
+// The single-candidate closure (k_closure.h): the candidates through the lane's pinned staging, one
+// kernel (grid.y = the batch), each area from its own mapped slot (no copy back, no stream
+// synchronisation). AUTO / TILED walks, N <= kClosureMaxN; if a slot has not landed within 2 ms (a
+// failed launch) a stream synchronisation reports it.
+static constexpr int kClBatch = 64;   // concurrent mac_area_f64 calls evaluated by one launch
+
+static bool closure_path(const mac_ctx* ctx, int64_t three_n)
 {
-    *handled = false;
-    int32_t rc = check_common(ctx, three_n, 1);
-    if (rc) return rc;
-    if (!circles) return fail(MAC_E_INVAL, "null circles");
+    return (ctx->algo == MAC_ALGO_AUTO || ctx->algo == MAC_ALGO_TILED) && three_n / 3 <= kClosureMaxN;
+}
+
+static void closure_batch(mac_ctx* ctx, int64_t three_n, const double* const* cands, double* const* outs, int B)
+{
     const int N = (int)(three_n / 3);
-    if (ctx->algo != MAC_ALGO_AUTO && ctx->algo != MAC_ALGO_TILED) return MAC_OK;
-    if (N > kClosureMaxN) return MAC_OK;
-    *handled = true;
-    if (N == 0 || ctx->M == 0) {
-        *area_out = 0.0;
-        return MAC_OK;
-    }
     set_device(ctx);
     LaneGuard lg(ctx);
     Lane* L = lg.lane;
     hipStream_t s = L->stream;
-    const size_t in_bytes = sizeof(double) * (size_t)three_n;
-    L->h_io.reserve(std::max<size_t>(in_bytes, 64));
-    std::memcpy(L->h_io.p, circles, in_bytes);
-    L->cands.reserve(in_bytes);
-    L->area.reserve(sizeof(double));
-    L->cpart.reserve(sizeof(unsigned long long) * (size_t)N);
-    // zero once; the last block of each launch resets them
-    if (L->carrive.grow(sizeof(unsigned))) HCK(hipMemsetAsync(L->carrive.p, 0, L->carrive.cap, s));
-    if (L->ctot.grow(sizeof(uint64_t))) HCK(hipMemsetAsync(L->ctot.p, 0, L->ctot.cap, s));
-    if (!L->h_cl.p) {
-        L->h_cl.reserve(64, hipHostMallocMapped | hipHostMallocCoherent);
-        std::memset(L->h_cl.p, 0, 64);
+    const size_t one = sizeof(double) * (size_t)three_n;
+    L->h_io.reserve(std::max<size_t>(one * B, 64));
+    for (int b = 0; b < B; ++b) std::memcpy((char*)L->h_io.p + one * b, cands[b], one);
+    L->cands.reserve(one * B);
+    L->area.reserve(sizeof(double) * B);
+    L->cpart.reserve(sizeof(unsigned long long) * (size_t)N * B);
+    // zero once; the last block of each candidate resets its words
+    if (L->carrive.grow(sizeof(unsigned) * kClBatch)) HCK(hipMemsetAsync(L->carrive.p, 0, L->carrive.cap, s));
+    if (L->ctot.grow(sizeof(uint64_t) * kClBatch)) HCK(hipMemsetAsync(L->ctot.p, 0, L->ctot.cap, s));
+    if (!L->h_cl.p) {   // a 32-B slot per batch candidate
+        L->h_cl.reserve(32 * kClBatch, hipHostMallocMapped | hipHostMallocCoherent);
+        std::memset(L->h_cl.p, 0, 32 * kClBatch);
         void* dp = nullptr;
         HCK(hipHostGetDevicePointer(&dp, L->h_cl.p, 0));
         L->d_cl = (uint64_t*)dp;
     }
     const uint64_t seq = ++L->cl_seq;
-    HCK(hipMemcpyAsync(L->cands.p, L->h_io.p, in_bytes, hipMemcpyHostToDevice, s));
+    HCK(hipMemcpyAsync(L->cands.p, L->h_io.p, one * B, hipMemcpyHostToDevice, s));
     const int nwg = (N + kClosureDisksPerWG - 1) / kClosureDisksPerWG;   // a wave per disk
     int64_t ts_a = -1;
     uint64_t* ts = nullptr;
-    if (ctx->profile) {
+    if (ctx->profile && B == 1) {
         std::lock_guard<std::mutex> lk(ctx->mu);
         if (ctx->stamp_used + nwg <= ctx->stamp_cap) {
             ts_a = ctx->stamp_used;
@@ -2405,34 +2497,117 @@ static int32_t closure_eval(mac_ctx* ctx, const double* circles, int64_t three_n
     }
     const ClosureOut co{L->cpart.as<unsigned long long>(), L->ctot.as<unsigned long long>(),
                         L->carrive.as<unsigned>(), L->area.as<double>(), L->d_cl, seq};
-    hipLaunchKernelGGL(closure_kernel, dim3((unsigned)nwg), dim3(kBlock), (uint32_t)closure_lds_bytes(N), s,
-                       ts, L->cands.as<double>(), N, ctx->grid, ctx->xys.as<double2>(),
-                       ctx->ws.as<double>(), ctx->off.as<int32_t>(), ctx->w_uniform ? 1 : 0, ctx->w0, co);
+    hipLaunchKernelGGL(closure_kernel, dim3((unsigned)nwg, (unsigned)B), dim3(kBlock),
+                       (uint32_t)closure_lds_bytes(N), s, ts, L->cands.as<double>(), N, ctx->grid,
+                       ctx->xys.as<double2>(), ctx->ws.as<double>(), ctx->off.as<int32_t>(),
+                       ctx->w_uniform ? 1 : 0, ctx->w0, co);
     HCK(hipGetLastError());
     if (ts) {
         std::lock_guard<std::mutex> lk(ctx->mu);
         ctx->prof.push_back({ts_a, nwg, -1, 0, 1, nullptr, MAC_ALGO_TILED});
     }
-    double a = 0.0;
-    int64_t unused = 0;
-    if (!mirror_wait((const uint64_t*)L->h_cl.p, seq, 2.0, &a, &unused)) {
-        HCK(hipStreamSynchronize(s));
-        if (!mirror_read((const uint64_t*)L->h_cl.p, seq, &a, &unused))
-            HCK(hipMemcpy(&a, L->area.p, sizeof(double), hipMemcpyDeviceToHost));
+    bool synced = false;
+    for (int b = 0; b < B; ++b) {
+        const uint64_t* slot = (const uint64_t*)L->h_cl.p + 4 * b;
+        double a = 0.0;
+        int64_t unused = 0;
+        if (!synced && mirror_wait(slot, seq, 2.0, &a, &unused)) {
+            *outs[b] = a;
+            continue;
+        }
+        if (!synced) {
+            HCK(hipStreamSynchronize(s));
+            synced = true;
+        }
+        if (!mirror_read(slot, seq, &a, &unused))
+            HCK(hipMemcpy(&a, L->area.as<double>() + b, sizeof(double), hipMemcpyDeviceToHost));
+        *outs[b] = a;
     }
-    *area_out = a;
-    return MAC_OK;
 }
+
+// Concurrent callers (DirectSearch's threaded poll, src/TDM_STATIC_opt.jl:129: one objective call
+// per trial point per thread) are combined: a caller queues its request; whoever finds no batch in
+// flight takes every queued request of the same size (up to kClBatch) and evaluates them in one
+// launch, then wakes the others. A lone caller runs its own request at once. Results per call are
+// exactly the single-candidate kernel's (the batch dimension only selects the candidate).
+struct ClReq {
+    const double* c;
+    int64_t three_n;
+    double* out;
+    int32_t rc;
+    bool done;
+    std::string err;
+};
 
 int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, double* area_out)
 {
     ABI_BEGIN
     if (!area_out) return fail(MAC_E_INVAL, "null area_out");
-    bool handled = false;
-    const int32_t rc = closure_eval(ctx, circles, three_n, area_out, &handled);
-    if (rc || handled) return rc;
-    return host_eval<double>(ctx, circles, three_n, 1, nullptr, 0.0, nullptr, nullptr, 1.0, area_out,
-                     nullptr, nullptr, nullptr);
+    int32_t rc = check_common(ctx, three_n, 1);
+    if (rc) return rc;
+    if (!circles) return fail(MAC_E_INVAL, "null circles");
+    if (!closure_path(ctx, three_n))
+        return host_eval<double>(ctx, circles, three_n, 1, nullptr, 0.0, nullptr, nullptr, 1.0, area_out,
+                                 nullptr, nullptr, nullptr);
+    if (three_n == 0 || ctx->M == 0) {
+        *area_out = 0.0;
+        return MAC_OK;
+    }
+    ClReq r{circles, three_n, area_out, MAC_OK, false, {}};
+    std::unique_lock<std::mutex> lk(ctx->cl_mu);
+    ctx->cl_q.push_back(&r);
+    while (!r.done) {
+        if (ctx->cl_busy) {
+            ctx->cl_cv.wait(lk);
+            continue;
+        }
+        ctx->cl_busy = true;
+        std::vector<ClReq*> batch;
+        const int64_t tn = ctx->cl_q.front()->three_n;
+        for (auto it = ctx->cl_q.begin(); it != ctx->cl_q.end() && (int)batch.size() < kClBatch;) {
+            if ((*it)->three_n == tn) {
+                batch.push_back(*it);
+                it = ctx->cl_q.erase(it);
+            } else {
+                ++it;
+            }
+        }
+        lk.unlock();
+        int32_t brc = MAC_OK;
+        std::string msg;
+        try {
+            std::vector<const double*> cs(batch.size());
+            std::vector<double*> os(batch.size());
+            for (size_t q = 0; q < batch.size(); ++q) {
+                cs[q] = batch[q]->c;
+                os[q] = batch[q]->out;
+            }
+            closure_batch(ctx, tn, cs.data(), os.data(), (int)batch.size());
+        } catch (const HipError& he) {
+            brc = he.e == hipErrorOutOfMemory ? MAC_E_NOMEM : MAC_E_HIP;
+            char buf[512];
+            snprintf(buf, sizeof buf, "HIP error %d (%s) at maxcover.hip:%d in %s", (int)he.e,
+                     hipGetErrorString(he.e), he.line, he.what);
+            msg = buf;
+        } catch (const std::bad_alloc&) {
+            brc = MAC_E_NOMEM;
+            msg = "host allocation failed";
+        } catch (...) {
+            brc = MAC_E_HIP;
+            msg = "unexpected exception";
+        }
+        lk.lock();
+        for (ClReq* q : batch) {
+            q->rc = brc;
+            q->err = msg;
+            q->done = true;
+        }
+        ctx->cl_busy = false;
+        ctx->cl_cv.notify_all();
+    }
+    lk.unlock();
+    if (r.rc) return fail(r.rc, r.err);
+    return MAC_OK;
     ABI_END
 }
 

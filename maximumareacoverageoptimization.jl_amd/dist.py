@@ -219,6 +219,77 @@ def make_gather(device="cpu", group=None):
     return DeviceGather(device, group)
 
 
+class SpecGather:
+    """The speculative loop's exchange: every rank's (done, best objective, best index) in rank
+    order — one all-gather of a 24-B record per rank (RCCL on a GPU device, gloo on CPU) and one
+    host read."""
+
+    def __init__(self, device="cpu", group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.device = torch.device(device)
+        self.on_device = self.device.type == "cuda"
+        if self.on_device:
+            check_one_runtime()
+        pin = self.on_device
+        self.stage = torch.zeros(3, dtype=torch.float64, pin_memory=pin)
+        self.rec = torch.zeros(3, dtype=torch.float64, device=self.device)
+        self.out = torch.empty((self.world, 3), dtype=torch.float64, device=self.device)
+        self.host = (torch.empty((self.world, 3), dtype=torch.float64, pin_memory=True)
+                     if self.on_device else self.out)
+
+    def __call__(self, done, obj, idx):
+        import torch
+        import torch.distributed as dist
+
+        self.stage[0] = 1.0 if done else 0.0
+        self.stage[1] = float(obj)
+        self.stage.view(torch.int64)[2] = int(idx)
+        self.rec.copy_(self.stage)
+        dist.all_gather_into_tensor(self.out, self.rec.reshape(1, 3), group=self.group)
+        if self.on_device:
+            self.host.copy_(self.out)
+        h = self.host
+        hi = h.view(torch.int64)
+        return [(bool(h[j, 0].item() != 0.0), float(h[j, 1].item()), int(hi[j, 2].item()))
+                for j in range(self.world)]
+
+
+def mads_loop_speculative(stepper, gather=None):
+    """The multi-GPU MADS loop by speculation over failure branches (mac_mads_poll_ahead /
+    mac_mads_advance, include/maxcover.h): rank j evaluates the whole poll that follows j
+    consecutive failures of the current iteration (rank 0: the real poll), one exchange gathers
+    all P results, and every rank applies them in order up to the first success — a run of
+    failures advances up to P iterations per round, a success one. The iterates are the
+    sequential loop's (src/TDM_STATIC_opt.jl:162). ``gather``: a SpecGather (None: one rank).
+    Returns stepper.result() with ``rounds`` (exchanges) added to the statistics."""
+    rank = gather.rank if gather is not None else 0
+    world = gather.world if gather is not None else 1
+    rounds = 0
+    while True:
+        mine = stepper.poll_ahead(rank)
+        recs = gather(*mine) if gather is not None else [mine]
+        rounds += 1
+        finished = False
+        for j in range(world):
+            done, obj, idx = recs[j]
+            if done:
+                finished = True
+                break
+            if stepper.advance(obj, idx):
+                break
+        if finished:
+            break
+    x, st = stepper.result()
+    st = dict(st)
+    st["rounds"] = rounds
+    return x, st
+
+
 def mads_loop(stepper, gather=None):
     """The sharded MADS loop's host side (mac_mads_poll / mac_mads_update, include/maxcover.h):
     per iteration the stepper polls its shard, ``gather`` combines the ranks' local bests and

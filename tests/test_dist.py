@@ -144,6 +144,70 @@ def test_gloo_world2_sharded_mads_loop():
     assert res[0][1] == res[1][1]
 
 
+def _spec_worker(rank, world, port, q):
+    """dist.mads_loop_speculative over gloo: rank j evaluates the whole poll that follows j
+    failures (TDM_STATIC_opt.PollStepper.poll_ahead on the C oracle), SpecGather exchanges the
+    results, every rank advances through them up to the first success."""
+    import sys
+    import torch.distributed as dist
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    orc = ge.load_oracle()
+    from importlib import import_module
+    d = import_module(pkg.__name__ + ".dist")
+    TS, TC = pkg.TDM_STATIC_opt, pkg.TDM_Constraints
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    wl = pkg.workloads
+    rng = wl.SplitMix64(616)
+    x, y, w = wl.grid_points(48)
+    rec = np.stack([x, y, w, w, np.zeros_like(x)], axis=1)
+    N = 4
+    x0 = np.concatenate([np.round(60 + rng.uniform(N) * 120), np.round(60 + rng.uniform(N) * 120),
+                         np.full(N, 20.0)])
+    rmax = np.full(N, 22.0)
+    c3 = TC.create_cons3(x0, 100 / 180 * np.pi, np.full(N, 6.0))
+
+    def obj(v):
+        return orc.ref_objective(v, rec, rmax)
+
+    def poll_fn(X):
+        f = np.array([obj(v) if c3(v) else np.inf for v in X])
+        k = int(np.argmin(f))
+        return (f[k], k) if np.isfinite(f[k]) else (np.inf, -1)
+
+    f0 = obj(x0) if c3(x0) else np.inf
+    st = TS.PollStepper(x0, f0, poll_fn, N_iter=30, ell0=3, ell_max=5, seed=41)
+    xs, info = d.mads_loop_speculative(st, d.SpecGather("cpu"))
+    ref = TS.mads(x0, obj, [c3], N_iter=30, ell0=3, ell_max=5, seed=41)
+    want_x = ref.x if ref.x is not None else ref.i
+    q.put((rank, xs.tolist(), info["f"], info["iterations"], info["rounds"], want_x.tolist(),
+           ref.x_cost, ref.status.iteration))
+    dist.destroy_process_group()
+
+
+def test_gloo_speculative_mads_loop():
+    """World sizes 2 and 3: the speculative loop (failure branches polled ahead on ranks
+    1..P-1) holds the sequential MADS iterate, objective and iteration count on every rank, in
+    fewer exchanges than iterations once failures run together."""
+    for world in (2, 3):
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_spec_worker, args=(r, world, port, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        res = [q.get(timeout=300) for _ in procs]
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        for rank, xs, f, it, rounds, want_x, want_f, want_it in res:
+            assert xs == want_x and f == want_f and it == want_it, (world, rank)
+            assert rounds < it, (world, rounds, it)
+
+
 def _bcast_worker(rank, world, port, q):
     import sys
     import torch.distributed as dist

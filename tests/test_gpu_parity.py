@@ -272,6 +272,41 @@ def test_concurrent_host_threads(ctx, pkg):
             assert np.array_equal(r, want[t::4])
 
 
+@pytest.mark.parametrize("threads", [2, 16])
+def test_concurrent_closure_calls(ctx, pkg, orc, threads):
+    """mac_area_f64 (the single-candidate closure) from many host threads at once, as
+    DirectSearch's threaded poll calls it (src/TDM_STATIC_opt.jl:129): concurrent calls are combined
+    into one batched closure launch (maxcover.hip ClReq), and every call still returns its own
+    candidate's area, equal to the C oracle's, for mixed disk counts and repeated candidates."""
+    wl = pkg.workloads
+    rng = wl.SplitMix64(2100 + threads)
+    x, y, w = wl.grid_points(220)
+    ctx.set_points(x, y, w)
+    polls = []
+    for N in (12, 12, 7):   # two threads' worth of N = 12 and one of N = 7: batches by size
+        x0 = wl.uniform_disks(N, 220, rng)
+        polls.append(wl.poll_candidates(x0, rng)[:24])
+    rec = recs(x, y, w)
+    pl = orc.PointerList(rec)
+    want = [pl.area_batch(C) for C in polls]
+    errs = []
+
+    def run(t):
+        C, A = polls[t % 3], want[t % 3]
+        for rep in range(6):
+            for k in range(t % 5, C.shape[0], 5):
+                got = ctx.area(np.ascontiguousarray(C[k]))
+                if got != A[k]:
+                    errs.append((t, k, got, A[k]))
+
+    th = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
+    for h in th:
+        h.start()
+    for h in th:
+        h.join()
+    assert not errs, errs[:5]
+
+
 # ---------------------------------------------------------------------------- device API
 
 def test_device_pointer_api(ctx, pkg, orc):
@@ -1003,6 +1038,50 @@ def test_native_mads_sharded_steppers(ctx, pkg, world):
         for s_ in steppers:
             s_.update(bo, bi)
     assert polls == want["iterations"] > 5
+    for s_ in steppers:
+        xs, st = s_.result()
+        s_.close()
+        assert np.array_equal(xs, want_x)
+        assert st["f"] == want["f"] and st["iterations"] == want["iterations"]
+        assert st["evaluations"] == want["evaluations"]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_native_mads_speculative_steppers(ctx, pkg, world):
+    """The speculative multi-GPU loop's native side in one process (mac_mads_poll_ahead /
+    mac_mads_advance): stepper j polls the whole poll that follows j failures, and every stepper
+    applies the P results in order up to the first success (what dist.mads_loop_speculative does
+    after its all-gather). Every stepper ends on mac_mads_run's iterate, objective, iteration and
+    evaluation counts, with cons3, in fewer rounds than iterations."""
+    wl = pkg.workloads
+    x, y, w = wl.grid_points(200)
+    ctx.set_points(x, y, w)
+    rng = wl.SplitMix64(919)
+    N = 9
+    x0 = np.concatenate([np.round(250 + rng.uniform(N) * 400), np.round(250 + rng.uniform(N) * 400),
+                         np.full(N, 30.0)])
+    r_max = np.full(N, 30.0 * TAN50)
+    kw = dict(prev=x0, d_lim=np.full(N, 10.0), tan_half_fov=TAN50, n_iter=40, ell0=2, ell_max=6,
+              seed=4711)
+    want_x, want = ctx.mads_run(x0, r_max, 1e5, **kw)
+    steppers = [ctx.mads_stepper(x0, r_max, 1e5, **kw) for _ in range(world)]
+    rounds = 0
+    while True:
+        res = [s_.poll_ahead(j) for j, s_ in enumerate(steppers)]
+        rounds += 1
+        finished = False
+        for j in range(world):
+            done, bo, bi = res[j]
+            if done:
+                finished = True
+                break
+            moved = [s_.advance(bo, bi) for s_ in steppers]
+            assert len(set(moved)) == 1
+            if moved[0]:
+                break
+        if finished:
+            break
+    assert rounds < want["iterations"]
     for s_ in steppers:
         xs, st = s_.result()
         s_.close()

@@ -38,6 +38,8 @@ for s in $STEPS; do
         run pytest_fused 400 python -u -m pytest tests/test_gpu_fused.py -x -v -rfE -p no:cacheprovider --timeout 120 --timeout-method thread ; rc=$? ;;
     mads)   # the native MADS loop's tests alone
         run pytest_mads 400 python -u -m pytest tests -m gpu -k "mads" -x -v -rfE -p no:cacheprovider --timeout 120 --timeout-method thread ; rc=$? ;;
+    gather)   # RCCL world-1 exchange costs (dist.PollGather / DeviceGather)
+        run gather 200 python tools/time_gather.py ; rc=$? ;;
     smoke)
         run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ; rc=$? ;;
     benchq)
