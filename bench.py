@@ -387,6 +387,7 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
     evals = sum(r["evaluations"] for r in recs)
     rejected = sum(r["rejected_polls"] for r in recs)
     iters = sum(r["iterations"] for r in recs)
+    succ = sum(r["successes"] for r in recs)
     M_avg = float(np.mean([r["points"] for r in recs]))
     b_eval = 24 * M_avg + 24 * cfg["N"] + 8
     avg_launch_ms = k_ms / max(k_launches, 1)
@@ -439,6 +440,8 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
                            "candidates_polled counts every generated candidate (1 + 2n per "
                            "iteration)",
             "mads_iterations": iters,
+            "mads_successes": succ,
+            "failure_fraction": (1.0 - succ / iters) if iters else None,
             "rejected_polls": rejected,
             "rejected_note": "iterations cons3 rejects whole (every variable's diagonal step "
                              "+-2^ell alone breaks d_lim): a failure with no launch (stepper) or "

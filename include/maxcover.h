@@ -187,6 +187,7 @@ typedef struct mac_mads_stats {
                                      variable's diagonal step +-2^ell alone breaks its UAV's d_lim
                                      (src/TDM_Constraints.jl:67), so no candidate passes — a
                                      failure (ell - 1), as the extreme barrier makes it         */
+    int64_t successes;            /* iterations whose poll moved the incumbent (the rest failed) */
 } mac_mads_stats;
 int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const double* r_max,
                      double penalty, const double* prev, const double* d_lim, double tan_half_fov,

@@ -76,6 +76,7 @@ class Status:
         # which counts the polls rejected by their diagonal steps alone)
         self.cons3_passed = 0
         self.cons3_empty_polls = 0
+        self.successes = 0   # polls that moved the incumbent (mac_mads_stats.successes)
         self.optimization_status = "Unoptimized"
 
 
@@ -140,6 +141,7 @@ def mads(input, obj, cons_ext=(), N_iter: int = 100, ell0: int = 2, ell_max: int
         if bi >= 0 and bo < f:
             x, f = X[bi].copy(), bo
             ell = min(ell + 1, ell_max)
+            res.status.successes += 1
         else:
             ell -= 1
     res.status.iteration = it

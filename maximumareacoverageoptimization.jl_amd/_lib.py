@@ -84,7 +84,8 @@ class MadsStats(ctypes.Structure):
                 ("feasible", ctypes.c_int32), ("seconds", ctypes.c_double),
                 ("host_enqueue_s", ctypes.c_double), ("host_perm_s", ctypes.c_double),
                 ("wait_s", ctypes.c_double), ("host_post_s", ctypes.c_double),
-                ("feasible_evaluations", ctypes.c_int64), ("rejected_polls", ctypes.c_int64)]
+                ("feasible_evaluations", ctypes.c_int64), ("rejected_polls", ctypes.c_int64),
+                ("successes", ctypes.c_int64)]
 
 
 class FireParams(ctypes.Structure):

@@ -118,6 +118,7 @@ __device__ __forceinline__ void mads_step(const FinBest& fb, double bo, int64_t 
         fb.st->f = better ? bo : f;
         fb.st->ell = e;
         fb.st->it += 1;
+        if (better) fb.st->succ += 1;
     }
 }
 

@@ -67,12 +67,15 @@ constexpr int kFwShCap = 1024;                   // shared entries a disk hands 
 // neighbours, [3] disks whose shared entries were decided in place (overflow)
 constexpr int kFwHints = 4;
 
-// The shared entries a disk hands to fin2_kernel: per disk one 16-B record {lower neighbours
-// (0: nothing handed off), shared entries, neighbour ids 0 | 1 << 16, 2 | 3 << 16} — a disk with at
-// most kFwHand neighbours and kFwShCap shared entries hands them off, else decides them in place
+// The shared entries a disk hands to fin2_kernel: a disk with at most kFwHand lower neighbours and
+// kFwShCap shared entries appends one 16-B record {disk, neighbours | entries << 8, neighbour ids
+// 0 | 1 << 16, 2 | 3 << 16} to a compact list (any order: fin2 sorts it by disk; the count is
+// zeroed by the next poll's prep launch), else decides them in place
 constexpr int kFwHand = 4;
+constexpr int kF2ListCap = 1024;   // listed disks fin2_kernel takes (the rest decide in place)
 struct FwShared {
-    int4* rec;        // [N]
+    int* count;       // listed disks
+    int4* list;       // [N] their records
     double2* xy;      // [N][kFwShCap] the entries' coordinates, in a fixed order
     double* w;        // [N][kFwShCap] and weights
 };
@@ -219,7 +222,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
     __shared__ double sbase[7];   // candidate 0's disk i, the displacement bound
     __shared__ uint8_t scov[kFwKPB]; // per slice slot: its position's disk covers (finite, r > 0)
     __shared__ unsigned ninner;      // entries every position covers (the annulus, counts only)
-    __shared__ int ucnt, ncnt;
+    __shared__ int ucnt, ncnt, lslot;
     __shared__ int wkeep[kFwR][kFwWaves];
     __shared__ int wsum[kFwWaves];
     uint32_t* const kx = xbuf;
@@ -999,18 +1002,23 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
             }
             if (pass == 0) {
                 swork = nsh_all;
-                if (nsh_all <= kFwShCap) {
-                    handed = true;
-                    break;
+                if (nsh_all <= kFwShCap) {   // (uniform) a place on the list, else in place
+                    if (tid == 0) lslot = atomicAdd(a.sh.count, 1);
+                    __syncthreads();
+                    if (lslot < kF2ListCap) {
+                        handed = true;
+                        break;
+                    }
                 }
             }
         }
     }
-    if (tid == 0) {
+    if (tid == 0 && handed) {
         int id[kFwHand];
 #pragma unroll
-        for (int m = 0; m < kFwHand; ++m) id[m] = handed && m < nc ? nb_id[m] : 0;
-        a.sh.rec[i] = make_int4(handed ? nc : 0, handed ? swork : 0, (int)((unsigned)id[0] | ((unsigned)id[1] << 16)), (int)((unsigned)id[2] | ((unsigned)id[3] << 16)));
+        for (int m = 0; m < kFwHand; ++m) id[m] = m < nc ? nb_id[m] : 0;
+        a.sh.list[lslot] = make_int4(i, nc | (swork << 8), (int)((unsigned)id[0] | ((unsigned)id[1] << 16)),
+                                     (int)((unsigned)id[2] | ((unsigned)id[3] << 16)));
     }
     MAC_FW_STAMP(5);
     // ---- the row: per candidate its position's credit (plus the shared credit decided in place)
@@ -1063,11 +1071,12 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
 
 // ------------------------------------------------------------------ finalize of the fused chain
 // Block = C candidates x (1024 / C) row groups: thread (c, g) sums rows g, g + G, ... of candidate
-// kb + c in batches of 8 (u32 counts: exact in any order; f64 credits: this fixed order), then the
-// G group sums in group order. Then the shared entries the disks handed off (FwShared), in batches
-// of whole disks (at most kF2Slots disk records): per slot and candidate the disk from its key word
-// (exact doubles), per (entry, candidate) the decision — disk i covers it, none of its listed lower
-// neighbours does — with entries split over the row groups and added in that group's fixed order.
+// kb + c, all of its rows in flight at once (u32 counts: exact in any order; f64 credits: this
+// fixed order), then the G group sums in group order. Then the shared entries the disks handed off
+// (FwShared's list, sorted by disk), in batches of whole disks (at most kF2Slots disk records): per
+// slot and candidate the disk from its key word (exact doubles), per (entry, candidate) the
+// decision — disk i covers it, none of its listed lower neighbours does — with each disk's entries
+// split over the row groups (its records held in registers) and added in that group's fixed order.
 // obj_k = -area_k + vp_k; the argmin by the last-arriving block (k_final.h finalize_argmin), which
 // also copies the fused kernel's hint words to the lane's mapped host memory (maxcover.hip
 // enqueue_eval reads them before the next poll).
@@ -1076,11 +1085,13 @@ constexpr int kF2C = 16;
 constexpr int kF2G = kF2Threads / kF2C;
 constexpr int kF2Slots = 64;      // disk records per batch (handed-off disks, their <= kFwHand neighbours)
 constexpr int kF2Ent = 2048;      // shared entries staged at once
-constexpr int kF2List = 1024;     // handed-off disks listed per scan of the flags
+constexpr int kF2List = kF2ListCap;   // listed disks taken (a disk past it decided in place)
+constexpr int kF2Pre = 64;        // list records loaded with the rows
 
 struct F2Shared {
     CandSrc src;                  // keys (keysP / ldk) and candidate 0's column (the bases)
-    const int4* rec;              // FwShared.rec
+    const int* count;             // FwShared's list
+    const int4* list;
     const double2* xy;
     const double* w;
     const uint8_t* dead;
@@ -1105,10 +1116,11 @@ __global__ __launch_bounds__(kF2Threads) void fin2_kernel(
     const bool run = src.resolve();   // (a stopped pipelined MADS loop: nothing to add)
     __shared__ double fred[G][C];
     __shared__ uint64_t ired[G][C];
-    // one round trip: the hand-off records of the first kF2List disks, the candidate's penalty and
+    // one round trip: the list's count and first kF2Pre records, the candidate's penalty and
     // failure byte, and its rows (kF2R per thread in flight at once; more in later batches)
     constexpr int kF2R = 16;
-    const int4 rec0 = t < N ? sd.rec[t] : make_int4(0, 0, 0, 0);
+    const int lc = min(*sd.count, min(kF2List, N));
+    const int4 lr0 = t < kF2Pre ? sd.list[min(t, N - 1)] : make_int4(0, 0, 0, 0);
     const double vpk = (vp && gq == 0 && k < K) ? vp[k] : 0.0;
     const bool cdead = !(k < K) || !run || (sd.dead && sd.dead[kc]);
     uint64_t s = 0;
@@ -1139,61 +1151,50 @@ __global__ __launch_bounds__(kF2Threads) void fin2_kernel(
         }
     }
     MAC_F2_STAMP(1);
-    // ---- the handed-off shared entries
-    __shared__ int flist[kF2List], fnc[kF2List];
-    __shared__ int wcnt[kF2Threads / kWave];
-    __shared__ int bslot[kF2List + 1], bent[kF2List + 1];   // per listed disk: first slot, entry
-    __shared__ int sdisk[kF2Slots], sown[kF2Slots];          // per slot: its disk, its listed disk's slot
-    __shared__ double srec[kF2Slots][3][C];                  // per slot and candidate: x, y, T
-    __shared__ double2 sxy[kF2Ent];
-    __shared__ double swt[kF2Ent];
-    __shared__ int sslot[kF2Ent];                            // per entry: its listed disk's slot
-    __shared__ int fids[kF2List][kFwHand];
-    __shared__ int fsh[kF2List];
-    __shared__ int nbat;
-    const int lane = t & (kWave - 1), wv = t / kWave;
-    for (int i0 = 0; i0 < N; i0 += kF2List) {
-        // the handed-off disks of [i0, i0 + kF2List), in disk order
-        const int ii = i0 + t;
-        const int4 rr = i0 == 0 ? rec0 : (ii < N ? sd.rec[ii] : make_int4(0, 0, 0, 0));
-        const bool f = ii < N && rr.x > 0;
-        const uint64_t bal = __ballot(f);
-        if (lane == 0) wcnt[wv] = __popcll(bal);
+    // ---- the handed-off shared entries (lc: uniform)
+    if (lc > 0 && run) {
+        __shared__ int4 lraw[kF2List];
+        __shared__ int flist[kF2List], fnc[kF2List], fsh[kF2List];
+        __shared__ int fids[kF2List][kFwHand];
+        __shared__ int bslot[kF2List + 1], bent[kF2List + 1];   // per listed disk: first slot, entry
+        __shared__ double srec[kF2Slots][3][C];                  // per slot and candidate: x, y, T
+        __shared__ double2 sxy[kF2Ent];
+        __shared__ double swt[kF2Ent];
+        __shared__ int nbat;
+        for (int q = t; q < lc; q += kF2Threads) lraw[q] = q < kF2Pre ? lr0 : sd.list[q];
         __syncthreads();
-        int pos = __popcll(bal & ((1ull << lane) - 1)), nl = 0;
-        for (int q = 0; q < kF2Threads / kWave; ++q) {
-            if (q < wv) pos += wcnt[q];
-            nl += wcnt[q];
-        }
-        if (f) {
-            flist[pos] = ii;
-            fnc[pos] = rr.x;
-            fsh[pos] = rr.y;
-            fids[pos][0] = rr.z & 0xFFFF;
-            fids[pos][1] = (int)((unsigned)rr.z >> 16);
-            fids[pos][2] = rr.w & 0xFFFF;
-            fids[pos][3] = (int)((unsigned)rr.w >> 16);
+        // sorted by disk: each record's rank among the listed disks (distinct ids)
+        for (int q = t; q < lc; q += kF2Threads) {
+            const int4 r = lraw[q];
+            int rk = 0;
+            for (int o = 0; o < lc; ++o) rk += lraw[o].x < r.x;
+            flist[rk] = r.x;
+            fnc[rk] = r.y & 0xFF;
+            fsh[rk] = r.y >> 8;
+            fids[rk][0] = r.z & 0xFFFF;
+            fids[rk][1] = (int)((unsigned)r.z >> 16);
+            fids[rk][2] = r.w & 0xFFFF;
+            fids[rk][3] = (int)((unsigned)r.w >> 16);
         }
         __syncthreads();
-        MAC_F2_STAMP(2);
-        if (nl == 0) continue;   // uniform
-        if (t == 0) {   // slots and entries per listed disk (one thread: the lists are short)
+        if (t == 0) {   // slots and entries per listed disk
             int sl = 0, en = 0;
-            for (int q = 0; q < nl; ++q) {
+            for (int q = 0; q < lc; ++q) {
                 bslot[q] = sl;
                 bent[q] = en;
                 sl += 1 + fnc[q];
                 en += fsh[q];
             }
-            bslot[nl] = sl;
-            bent[nl] = en;
+            bslot[lc] = sl;
+            bent[lc] = en;
         }
         __syncthreads();
-        for (int q0 = 0; q0 < nl;) {
+        MAC_F2_STAMP(2);
+        for (int q0 = 0; q0 < lc;) {
             // the batch: listed disks [q0, q1) whose records fit kF2Slots (one disk always fits)
             if (t == 0) {
                 int q1 = q0 + 1;
-                while (q1 < nl && bslot[q1 + 1] - bslot[q0] <= kF2Slots) ++q1;
+                while (q1 < lc && bslot[q1 + 1] - bslot[q0] <= kF2Slots) ++q1;
                 nbat = q1;
             }
             __syncthreads();
@@ -1204,7 +1205,6 @@ __global__ __launch_bounds__(kF2Threads) void fin2_kernel(
             constexpr int kEPT = kF2Ent / kF2Threads;
             double2 exy[kEPT];
             double ew[kEPT];
-            int esl[kEPT];
             {
                 const int ne = min(kF2Ent, e1all - e0all);
 #pragma unroll
@@ -1212,7 +1212,6 @@ __global__ __launch_bounds__(kF2Threads) void fin2_kernel(
                     const int e = t + r * kF2Threads;
                     exy[r] = make_double2(0.0, 0.0);
                     ew[r] = 0.0;
-                    esl[r] = 0;
                     if (e < ne) {
                         const int eg = e0all + e;   // the listed disk holding it
                         int lo = q0, hi = q1 - 1;
@@ -1222,13 +1221,11 @@ __global__ __launch_bounds__(kF2Threads) void fin2_kernel(
                         }
                         const int64_t se = (int64_t)flist[lo] * kFwShCap + (eg - bent[lo]);
                         exy[r] = sd.xy[se];
-                        ew[r] = sd.w[se];
-                        esl[r] = bslot[lo] - sl0;
+                        if constexpr (!kCounts) ew[r] = sd.w[se];
                     }
                 }
             }
-            // one round trip: per slot and candidate the disk (its key word, candidate 0's disk),
-            // and the batch's first kF2Ent entries
+            // per slot and candidate: the disk (its key word, candidate 0's disk)
             for (int q = t; q < ns * C; q += kF2Threads) {
                 const int sl = q / C, cc = q % C;
                 int lo = q0, hi = q1 - 1;   // the listed disk holding slot sl0 + sl
@@ -1238,15 +1235,10 @@ __global__ __launch_bounds__(kF2Threads) void fin2_kernel(
                 }
                 const int m = sl - (bslot[lo] - sl0);
                 const int jj = m == 0 ? flist[lo] : fids[lo][m - 1];
-                if (cc == 0) {
-                    sdisk[sl] = jj;
-                    sown[sl] = bslot[lo] - sl0;
-                }
                 const int kk = min(cb * C + cc, K - 1);
                 const uint32_t key = src.keysP[(int64_t)jj * src.ldk + kk];
-                const DiskRec d = run ? key_disk(src, key, jj, kk, N, src_val(src, 0, jj, N),
-                                                 src_val(src, 0, N + jj, N), src_val(src, 0, 2 * N + jj, N))
-                                      : inert_disk();
+                const DiskRec d = key_disk(src, key, jj, kk, N, src_val(src, 0, jj, N),
+                                           src_val(src, 0, N + jj, N), src_val(src, 0, 2 * N + jj, N));
                 srec[sl][0][cc] = d.cx;
                 srec[sl][1][cc] = d.cy;
                 srec[sl][2][cc] = d.T;
@@ -1260,36 +1252,50 @@ __global__ __launch_bounds__(kF2Threads) void fin2_kernel(
                         if (e < ne) {
                             sxy[e] = exy[r];
                             swt[e] = ew[r];
-                            sslot[e] = esl[r];
                         }
                     }
-                } else for (int e = t; e < ne; e += kF2Threads) {
-                    const int eg = e0 + e;   // the listed disk holding it
-                    int lo = q0, hi = q1 - 1;
-                    while (lo < hi) {
-                        const int mid = (lo + hi + 1) >> 1;
-                        if (bent[mid] <= eg) lo = mid; else hi = mid - 1;
+                } else {
+                    for (int e = t; e < ne; e += kF2Threads) {
+                        const int eg = e0 + e;
+                        int lo = q0, hi = q1 - 1;
+                        while (lo < hi) {
+                            const int mid = (lo + hi + 1) >> 1;
+                            if (bent[mid] <= eg) lo = mid; else hi = mid - 1;
+                        }
+                        const int64_t se = (int64_t)flist[lo] * kFwShCap + (eg - bent[lo]);
+                        sxy[e] = sd.xy[se];
+                        swt[e] = kCounts ? 0.0 : sd.w[se];
                     }
-                    const int64_t se = (int64_t)flist[lo] * kFwShCap + (eg - bent[lo]);
-                    sxy[e] = sd.xy[se];
-                    swt[e] = sd.w[se];
-                    sslot[e] = bslot[lo] - sl0;
                 }
                 __syncthreads();
                 MAC_F2_STAMP(3);
-                // (entry, candidate) decisions: thread (c, g) takes entries g, g + G, ...
+                // per listed disk: its records and its neighbours' in registers, then its entries
+                // of this chunk, split over the row groups (group gq: entries gq, gq + G, ...)
                 if (!cdead) {
-                    for (int e = gq; e < ne; e += G) {
-                        const int b = sslot[e];
-                        const double2 p = sxy[e];
-                        if (!(sqdist(p.x, p.y, srec[b][0][c], srec[b][1][c]) <= srec[b][2][c])) continue;
-                        // the listed disk's neighbours: the slots after b that it owns
-                        bool stolen = false;
-                        for (int sl = b + 1; sl < ns && sown[sl] == b && !stolen; ++sl)
-                            stolen = sqdist(p.x, p.y, srec[sl][0][c], srec[sl][1][c]) <= srec[sl][2][c];
-                        if (!stolen) {
-                            if constexpr (kCounts) s += 1;
-                            else sf += swt[e];
+                    for (int lq = q0; lq < q1; ++lq) {
+                        const int ea = max(bent[lq], e0) - e0, eb = min(bent[lq + 1], e0 + ne) - e0;
+                        if (ea >= eb) continue;
+                        const int b = bslot[lq] - sl0, ncq = fnc[lq];
+                        const double cx = srec[b][0][c], cy = srec[b][1][c], T = srec[b][2][c];
+                        double nx[kFwHand], ny[kFwHand], nT[kFwHand];
+#pragma unroll
+                        for (int m = 0; m < kFwHand; ++m) {
+                            const bool in = m < ncq;
+                            nx[m] = in ? srec[b + 1 + m][0][c] : 0.0;
+                            ny[m] = in ? srec[b + 1 + m][1][c] : 0.0;
+                            nT[m] = in ? srec[b + 1 + m][2][c] : -1.0;   // (never covers)
+                        }
+                        for (int e = ea + gq; e < eb; e += G) {
+                            const double2 p = sxy[e];
+                            if (!(sqdist(p.x, p.y, cx, cy) <= T)) continue;
+                            bool stolen = false;
+#pragma unroll
+                            for (int m = 0; m < kFwHand; ++m)
+                                stolen |= sqdist(p.x, p.y, nx[m], ny[m]) <= nT[m];
+                            if (!stolen) {
+                                if constexpr (kCounts) s += 1;
+                                else sf += swt[e];
+                            }
                         }
                     }
                 }

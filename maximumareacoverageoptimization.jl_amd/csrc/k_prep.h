@@ -121,6 +121,7 @@ struct MadsState {
     int skip;      // the current poll is rejected whole (set by its prep launch)
     unsigned long long feas;   // candidates evaluated (passing cons3)
     int64_t skipped;           // polls rejected whole
+    int64_t succ;              // successful polls (the incumbent moved)
 };
 
 // Where candidate coordinates come from: a 3N x K column-major matrix (the batch APIs), or a
@@ -226,6 +227,7 @@ struct PrepArgs {
     // fails (diag_rejects); then every workgroup returns before its records
     MadsState* mst_w;
     unsigned long long* feas;  // += the candidates that pass cons3 (null: not counted)
+    int* lreset;               // the fused chain's hand-off list count, zeroed for this poll (null: none)
 };
 
 // Packed keys. Disk i of candidate k is keyed by its offsets (dx, dy, dr) from candidate 0's
@@ -578,6 +580,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
 __global__ __launch_bounds__(kPrepU) __attribute__((amdgpu_waves_per_eu(4))) void prep_kernel(uint64_t* ts, PrepArgs a)
 {
     ts_begin(ts);   // profiling only (the chain's first launch: k_common.h)
+    if (a.lreset && blockIdx.x == 0 && threadIdx.x == 0) *a.lreset = 0;   // (read by fin2 after fiw)
     if (!a.src.resolve(true)) {
         ts_end(ts);
         return;

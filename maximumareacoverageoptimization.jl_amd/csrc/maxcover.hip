@@ -163,7 +163,7 @@ struct Lane {
     int walk_hist[8] = {};                     // the walk AUTO would have chosen, last 8 polls
     // the fused chain (k_fiw.h): displacement partials, failure bytes, credit rows, hint words,
     // the shared entries handed to fin2_kernel
-    DevBuf pd, dead8, frows, fwhint, fwrec, fwsxy, fwsw;
+    DevBuf pd, dead8, frows, fwhint, fwlist, fwcount, fwsxy, fwsw;
     int fused_bad[8] = {};                     // 1: a recent poll did not suit the fused chain
     int last_chain = 0;                        // the chain of the lane's last poll: 1 five-launch, 2 fused
 };
@@ -673,7 +673,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             // cons3 failures are left out of the walk when only objectives are asked for
             const bool excl = d_obj && d_prev && !d_area && N <= kPrepU;
             if (excl) L->dead8.reserve((size_t)ldk + 16);   // (the fused kernel reads 4-B words)
-            L->fwrec.reserve(sizeof(int4) * (size_t)N);
+            L->fwlist.reserve(sizeof(int4) * (size_t)std::max(N, kF2Pre));
+            if (L->fwcount.grow(sizeof(int))) HCK(hipMemsetAsync(L->fwcount.p, 0, L->fwcount.cap, s));
             L->fwsxy.reserve(sizeof(double2) * (size_t)N * kFwShCap);
             L->fwsw.reserve(sizeof(double) * (size_t)N * kFwShCap);
             PrepArgs pr{};
@@ -694,6 +695,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             pr.dead8 = excl ? L->dead8.as<uint8_t>() : nullptr;
             pr.mst_w = excl && fb_mads ? fb_mads->st : nullptr;
             pr.feas = d_feas;
+            pr.lreset = L->fwcount.as<int>();
             uint64_t* tsk = take_ts(nchain, ts_c, ts_nc);
             hipLaunchKernelGGL(prep_kernel, dim3((unsigned)nchain), dim3(kPrepU), 0, s, tsk, pr);
             HCK(hipGetLastError());
@@ -716,8 +718,10 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             fa.frow = L->frows.as<double>();
             fa.ldk = ldk;
             fa.hint = L->fwhint.as<int>();
-            fa.sh = FwShared{L->fwrec.as<int4>(), L->fwsxy.as<double2>(), L->fwsw.as<double>()};
-            const F2Shared f2s{fa.src, L->fwrec.as<int4>(), L->fwsxy.as<double2>(), L->fwsw.as<double>(), fa.dead};
+            fa.sh = FwShared{L->fwcount.as<int>(), L->fwlist.as<int4>(), L->fwsxy.as<double2>(),
+                             L->fwsw.as<double>()};
+            const F2Shared f2s{fa.src, L->fwcount.as<int>(), L->fwlist.as<int4>(), L->fwsxy.as<double2>(),
+                               L->fwsw.as<double>(), fa.dead};
             const unsigned nfw = 8 * (unsigned)((N + 7) / 8);
             uint64_t* tsw = take_ts(nfw, ts_w, ts_nw);
             ts_a = ts_w;   // (mac_profile_read: the walk launch)
@@ -1444,7 +1448,7 @@ void mac_ctx_destroy(mac_ctx* ctx)
                           &l->perm, &l->ucount, &l->umap, &l->keysT, &l->lane4,
                           &l->lanexp, &l->rows, &l->nboxT, &l->cnt, &l->dlimraw, &l->finblk, &l->finarrive, &l->c32, &l->p32,
                           &l->cpart, &l->carrive, &l->ctot, &l->prec, &l->cost, &l->nboxU,
-                          &l->ncountU, &l->orjobs, &l->pd, &l->dead8, &l->frows, &l->fwhint, &l->fwrec,
+                          &l->ncountU, &l->orjobs, &l->pd, &l->dead8, &l->frows, &l->fwhint, &l->fwlist, &l->fwcount,
                           &l->fwsxy, &l->fwsw})
             b->release();
         if (l->done) (void)hipEventDestroy(l->done);
@@ -1852,7 +1856,7 @@ struct mac_mads {
     const double* d_dlimT = nullptr;
     std::vector<double> x;
     double f = INFINITY;
-    int64_t evals = 0, it = 0, rejected = 0;
+    int64_t evals = 0, it = 0, rejected = 0, succ = 0;
     int ell = 0;
     std::vector<double> h_prev;   // cons3's prev (host copy: whole-poll rejection, poll_rejected)
     DevBuf d_feas;                // candidates that passed cons3 (the prep launches count them)
@@ -2129,6 +2133,7 @@ int32_t mac_mads_update(mac_mads* m, double best_obj, int64_t best_idx)
         }
         m->f = best_obj;
         m->ell = std::min(m->ell + 1, (int)m->prm.ell_max);
+        ++m->succ;
     } else {
         --m->ell;
     }
@@ -2215,6 +2220,7 @@ int32_t mac_mads_advance(mac_mads* m, double best_obj, int64_t best_idx, int32_t
         }
         m->f = best_obj;
         m->ell = std::min(m->ell + 1, (int)m->prm.ell_max);
+        ++m->succ;
     } else {
         --m->ell;
     }
@@ -2250,6 +2256,7 @@ int32_t mac_mads_result(mac_mads* m, double* x_out, mac_mads_stats* st)
         HCK(hipStreamSynchronize(m->s));
         st->feasible_evaluations = (int64_t)fe;
         st->rejected_polls = m->rejected;
+        st->successes = m->succ;
     }
     return MAC_OK;
     ABI_END
@@ -2337,7 +2344,7 @@ static void mads_run_pipelined(mac_mads* m)
     // the incumbent and the state: x0 (begin's pinned staging holds it), f(x0), ell0
     const auto ta = clk::now();
     HCK(hipMemcpyAsync(dx, m->hx, sizeof(double) * n, hipMemcpyHostToDevice, s));
-    const MadsState st0{m->f, 0, m->ell, 0, 0ull, 0};
+    const MadsState st0{m->f, 0, m->ell, 0, 0ull, 0, 0};
     HCK(hipMemcpy(dst, &st0, sizeof(st0), hipMemcpyHostToDevice));
     int64_t computed = std::min<int64_t>(n_iter, kMadsAhead);
     for (int64_t t = 1; t <= computed; ++t) perms_of(t);
@@ -2405,6 +2412,7 @@ static void mads_run_pipelined(mac_mads* m)
     m->ell = st.ell;
     m->evals = 1 + st.it * (int64_t)m->K;
     m->rejected += st.skipped;
+    m->succ += st.succ;
     if (st.feas) {   // (the stepper's counter holds the polls' evaluations: none before this loop)
         const unsigned long long fe = st.feas;
         HCK(hipMemcpy(m->d_feas.p, &fe, sizeof(fe), hipMemcpyHostToDevice));

@@ -960,6 +960,7 @@ def test_native_mads_matches_python_driver(ctx, pkg, with_cons3):
     # the evaluations the reference makes (candidates passing cons3), and the polls cons3
     # rejects whole with no launch (only ones where no candidate passes)
     assert st["feasible_evaluations"] == res.status.cons3_passed
+    assert st["successes"] == res.status.successes
     assert st["rejected_polls"] <= res.status.cons3_empty_polls
     if not with_cons3:
         assert st["rejected_polls"] == 0
@@ -1194,7 +1195,7 @@ def test_native_mads_pipelined_matches_stepper(ctx, pkg, N, n_iter, ell0, ell_ma
         st_.close()
     assert np.array_equal(want_x, xs)
     for key in ("f", "iterations", "evaluations", "status", "feasible", "feasible_evaluations",
-                "rejected_polls"):
+                "rejected_polls", "successes"):
         assert want[key] == got[key], key   # (rejections: device-side vs host-side, alike)
     if cons3 and not stall and n_iter >= 40:   # (ell reaches 5: 2^5 - 12 > 12 on every axis)
         assert want["rejected_polls"] > 0 and want["feasible_evaluations"] > 0
