@@ -334,12 +334,15 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
     rng = wl.SplitMix64(args.seed)
     fire_kw, x0 = wl.config5_setup(rng, cfg["G"], cfg["N"], cfg["ignition"])
     ctx = pkg.Context(dev_index, algo=args.algo)
+    ctx.set_chain(args.chain)
     t_set = time.perf_counter()
     D = pkg.DynamicArea.DynamicArea(**fire_kw, seed=args.seed, device=dev_index)
     shard = (rank, world) if world > 1 else None
-    gather = pdist.make_gather(coll_dev) if world > 1 else None
+    spec = world > 1 and args.mads_mode == "speculate"
+    gather = ((pdist.SpecGather(coll_dev) if spec else pdist.make_gather(coll_dev))
+              if world > 1 else None)
     sim = pkg.FullSimulation.Simulation(ctx, x0, fire=D, N_iter=args.mads_iters, seed=args.seed,
-                                        shard=shard, gather=gather)
+                                        shard=shard, gather=gather, speculate=spec)
     t_set = time.perf_counter() - t_set
     for _ in range(args.warmup):
         sim.step()
@@ -440,6 +443,7 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
                            "candidates_polled counts every generated candidate (1 + 2n per "
                            "iteration)",
             "mads_iterations": iters,
+            "exchange_rounds": sum(r["rounds"] for r in recs),
             "mads_successes": succ,
             "failure_fraction": (1.0 - succ / iters) if iters else None,
             "rejected_polls": rejected,
@@ -451,6 +455,9 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
             "mads_host_split_s": {k: float(np.sum([r.get("mads_host_s", {}).get(k, 0.0) for r in recs]))
                                   for k in ("host_enqueue_s", "host_perm_s", "wait_s", "host_post_s")},
             "parallelism": ("1 GPU" if world == 1 else
+                            (f"{world} GPUs: speculation over failure branches (rank j polls the "
+                             f"poll after j failures), one 24-B all-gather per round; fire stream "
+                             f"regenerated per GPU") if spec else
                             f"{world} GPUs: every poll's 2n candidates sharded, 16-B all-gather "
                             f"per MADS iteration; fire stream regenerated per GPU"),
             "ranks_in_lockstep": lockstep,
@@ -498,6 +505,12 @@ def main():
                     help="4 (default): one MADS poll per step; 5: one end-to-end MPC step "
                          "(CA fire stream + rmvCoveredPOI + a MADS run) per step")
     ap.add_argument("--mads-iters", type=int, default=100, help="config 5: N_iter per MPC step")
+    ap.add_argument("--chain", choices=["auto", "five", "fused"], default="auto",
+                    help="poll chain: the device's choice (auto), the five-launch chain or the "
+                         "fused three-launch chain (MAC_OPT_CHAIN)")
+    ap.add_argument("--mads-mode", choices=["shard", "speculate"], default="shard",
+                    help="config 5 on P GPUs: shard every poll's candidates, or speculate over "
+                         "failure branches (rank j polls the poll after j failures)")
     ap.add_argument("--algo", default="auto", choices=("auto", "tiled", "scan", "poll"))
     ap.add_argument("--polls", type=int, default=4, help="distinct poll sets cycled over steps")
     ap.add_argument("--tile-points", type=int, default=None,
@@ -608,6 +621,7 @@ def main():
     Kl = hi - lo
 
     ctx = pkg.Context(dev_index, algo=args.algo, tile_points=args.tile_points)
+    ctx.set_chain(args.chain)
     # once per MPC step (src/FullSimulation.jl:50-61), outside the per-poll step: the host upload
     # of the list, then the device tile index over it (mac_set_points_dev_f64: sort, offsets)
     t_set = time.perf_counter()
@@ -824,7 +838,7 @@ def main():
                                 if args.scaling == "weak" else
                                 f"one poll's candidates sharded over {world} GPU(s), "
                                 f"16-B argmin all-gather"),
-                "algo": args.algo,
+                "algo": args.algo, "chain": args.chain,
                 "step_mode": "armed" if armed else "plain",
             },
             "roofline": {

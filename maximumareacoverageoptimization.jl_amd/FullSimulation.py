@@ -67,7 +67,7 @@ class Simulation:
     def __init__(self, ctx: Context, starting_circles, *, fire: DynamicArea | None = None,
                  firepoints=None, initial_points=None, N_iter: int = N_iter, d_lim=None,
                  r_max=None, seed: int = 20250216, ell0: int = 2, ell_max: int = 6,
-                 shard=None, gather=None):
+                 shard=None, gather=None, speculate: bool = False):
         self.ctx = ctx
         self.x_prev = np.asarray(starting_circles, dtype=np.float64).copy()
         self.N = N = self.x_prev.size // 3
@@ -79,6 +79,9 @@ class Simulation:
         self.N_iter, self.seed, self.ell0, self.ell_max = N_iter, seed, ell0, ell_max
         self.shard = shard          # (rank, world) or None: the whole poll on this GPU
         self.gather = gather
+        # P GPUs: shard every poll's candidates (gather: dist.make_gather), or speculate over
+        # failure branches, rank j polling the poll after j failures (gather: dist.SpecGather)
+        self.speculate = speculate
         if fire is not None:
             ctx.set_points_records(fire.initial_points())
         elif firepoints is not None:
@@ -119,6 +122,13 @@ class Simulation:
                   ell0=self.ell0, ell_max=self.ell_max, seed=self.seed + t)
         if self.shard is None or self.shard[1] == 1:
             x_out, st = ctx.mads_run(single_input, self.r_max, 1e5, **kw)
+        elif self.speculate:
+            from .dist import mads_loop_speculative
+            stepper = ctx.mads_stepper(single_input, self.r_max, 1e5, **kw)
+            try:
+                x_out, st = mads_loop_speculative(stepper, self.gather)
+            finally:
+                stepper.close()
         else:
             from .dist import mads_loop, shard_range
             lo, hi = shard_range(2 * single_input.size, *self.shard)
@@ -134,6 +144,7 @@ class Simulation:
                    feasible_evaluations=int(st.get("feasible_evaluations", 0)),
                    rejected_polls=int(st.get("rejected_polls", 0)),
                    successes=int(st.get("successes", 0)),
+                   rounds=int(st.get("rounds", st["iterations"])),
                    fire_s=t1 - t0, remove_s=t2 - t1, mads_s=t3 - t2, step_s=t3 - t0,
                    mads_host_s={k: float(st.get(k, 0.0)) for k in
                                 ("host_enqueue_s", "host_perm_s", "wait_s", "host_post_s")},

@@ -224,6 +224,7 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
     __shared__ unsigned ninner;      // entries every position covers (the annulus, counts only)
     __shared__ int ucnt, ncnt, lslot;
     __shared__ int wkeep[kFwR][kFwWaves];
+    __shared__ int wshr[kFwR][kFwWaves];   // per round and wave: shared entries handed off
     __shared__ int wsum[kFwWaves];
     uint32_t* const kx = xbuf;
     uint32_t* const poskey = xbuf;
@@ -595,6 +596,10 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
         if (rout > 0.0 && rout < 1e150) rout2 = rout * rout * (1.0 + 1e-9);
     }
 
+    // the shared entries (box i's entries inside a lower box) are handed to fin2_kernel from the
+    // walk's own compaction (slice 0), in its fixed order, when the list can take the disk
+    const bool hand_ok = nc > 0 && nc <= kFwHand;
+    int nsh_walk = 0;
     // ---- the walk of box i over the entries no lower box holds (k_poll.h)
     if (rany) {
         const double ox = g.gx0 + 0.5 * (double)(RG.x + RG.y + 1) * g.S;
@@ -675,11 +680,11 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
                     double2 pr[kFwR];
                     double wr[kFwR];
                     int jg[kFwR];
-                    uint64_t bal[kFwR];
+                    uint64_t bal[kFwR], hbal[kFwR];
 #pragma unroll
                     for (int r = 0; r < kFwR; ++r) {
                         const int qd = tid + r * kFwThreads;
-                        bool keep = false, inner = false;
+                        bool keep = false, inner = false, hs = false;
                         pr[r] = make_double2(0.0, 0.0);
                         wr[r] = 0.0;
                         jg[r] = 0;
@@ -701,7 +706,9 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
                             }
                             const bool shared = nc > 0 &&
                                 entry_shared(nc, nb_box, tile_of(pr[r].x, g.gx0, g.invS, g.nTx), rb + lo);
-                            keep = !shared && __builtin_isfinite(pr[r].x) && __builtin_isfinite(pr[r].y);
+                            const bool fin = __builtin_isfinite(pr[r].x) && __builtin_isfinite(pr[r].y);
+                            keep = !shared && fin;
+                            hs = shared && fin;
                             if (keep) {   // the annulus: inside every disk / outside all
                                 const double ux = pr[r].x - sbase[0], uy = pr[r].y - sbase[1];
                                 const double d0 = ux * ux + uy * uy;
@@ -717,8 +724,25 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
                         if (kb == 0 && lane == 0 && ib) atomicAdd(&ninner, (unsigned)__popcll(ib));
                         bal[r] = __ballot(keep);
                         if (lane == 0) wkeep[r][wid] = __popcll(bal[r]);
+                        hbal[r] = __ballot(hs && kb == 0 && hand_ok);
+                        if (lane == 0) wshr[r][wid] = __popcll(hbal[r]);
                     }
                     __syncthreads();
+                    if (kb == 0 && hand_ok) {   // (uniform) hand-off copies, in the fixed order
+#pragma unroll
+                        for (int r = 0; r < kFwR; ++r) {
+                            int hd = nsh_walk + __popcll(hbal[r] & ((1ull << lane) - 1));
+#pragma unroll
+                            for (int w2 = 0; w2 < kFwWaves; ++w2) {
+                                if (w2 < wid) hd += wshr[r][w2];
+                                nsh_walk += wshr[r][w2];
+                            }
+                            if (((hbal[r] >> lane) & 1) && hd < kFwShCap) {
+                                a.sh.xy[(int64_t)i * kFwShCap + hd] = pr[r];
+                                a.sh.w[(int64_t)i * kFwShCap + hd] = wr[r];
+                            }
+                        }
+                    }
                     int n = 0;
 #pragma unroll
                     for (int r = 0; r < kFwR; ++r) {
@@ -856,11 +880,18 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
     for (int j = 0; j < P; ++j) sh[j] = 0;
     int swork = 0;
     bool handed = false;
-    if (rany && nc > 0) {
+    if (rany && hand_ok && nsh_walk <= kFwShCap) {   // (uniform) a place on the list, else in place
+        if (tid == 0) lslot = atomicAdd(a.sh.count, 1);
+        __syncthreads();
+        if (lslot < kF2ListCap) {
+            handed = true;
+            swork = nsh_walk;
+        }
+    }
+    if (rany && nc > 0 && !handed) {
         const int nclist = min(nc, kFwNbr);
-        // pass 0 hands off (stops copying at the cap), pass 1 decides in place
-        for (int pass = nc <= kFwHand ? 0 : 1; pass < 2; ++pass) {
-            int nsh_all = 0;
+        // decided in place: the entries enumerated again, in windows, per candidate in fp64
+        {
             for (int rb = RG.z; rb <= RG.w; rb += kPollRB) {
                 const int nr = min(kPollRB, RG.w - rb + 1);
                 int rs0 = 0, rs1 = 0;
@@ -919,18 +950,6 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
                         if ((bal[r] >> lane) & 1) shidx[dst] = jglob[r];
                     }
                     __syncthreads();
-                    if (pass == 0) {   // hand off: the entries' coordinates and weights, in order
-                        for (int e = tid; e < nsh; e += kFwThreads) {
-                            const int q = nsh_all + e;
-                            if (q < kFwShCap) {
-                                a.sh.xy[(int64_t)i * kFwShCap + q] = a.xy[shidx[e]];
-                                a.sh.w[(int64_t)i * kFwShCap + q] = a.w[shidx[e]];
-                            }
-                        }
-                        nsh_all += nsh;
-                        __syncthreads();   // (shidx is rewritten by the next window)
-                        continue;
-                    }
                     swork += nsh;
                     for (int e0 = 0; e0 < nsh; e0 += kFwShE) {
                         const int ne = min(kFwShE, nsh - e0);
@@ -997,17 +1016,6 @@ __global__ __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(2)))
                             }
                         }
                         __syncthreads();   // the chunk and the words are reused
-                    }
-                }
-            }
-            if (pass == 0) {
-                swork = nsh_all;
-                if (nsh_all <= kFwShCap) {   // (uniform) a place on the list, else in place
-                    if (tid == 0) lslot = atomicAdd(a.sh.count, 1);
-                    __syncthreads();
-                    if (lslot < kF2ListCap) {
-                        handed = true;
-                        break;
                     }
                 }
             }
@@ -1332,7 +1340,7 @@ __global__ __launch_bounds__(kF2Threads) void fin2_kernel(
     }
     MAC_F2_STAMP(5);
     if (fb.best && t < kWave) {
-        const bool last = finalize_argmin<C>(fb, o, k, k < K);   // (+ the hint words, fb.hint)
+        [[maybe_unused]] const bool last = finalize_argmin<C>(fb, o, k, k < K);   // (+ the hint words)
 #ifdef MAC_DIAG
         if (t == 0 && blockIdx.x < 4096) g_diag_f2[8 * blockIdx.x + 7] = last;
 #endif

@@ -91,6 +91,10 @@ for s in $STEPS; do
         MAXCOVER_BENCH_DEVICE=0 run c5x2 400 python -m torch.distributed.run --nnodes=1 \
             --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 \
             --config 5 --no-cpu --dist-backend gloo --steps 2 --warmup 1 ; rc=$? ;;
+    c5x2s)   # the speculative N=2 config-5 loop on one GPU (gloo; both ranks on device 0)
+        MAXCOVER_BENCH_DEVICE=0 run c5x2s 400 python -m torch.distributed.run --nnodes=1 \
+            --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 2 \
+            --config 5 --no-cpu --dist-backend gloo --steps 2 --warmup 1 --mads-mode speculate ; rc=$? ;;
     probe)
         { nproc; python3 -c "import os; print(os.cpu_count(), len(os.sched_getaffinity(0)))";
           cat /sys/fs/cgroup/cpu.max 2>/dev/null; lscpu | grep -E 'Model name|Socket|Core|Thread'; 
@@ -100,6 +104,16 @@ for s in $STEPS; do
         grep '^{' gpurun_out/benchc.log > gpurun_out/benchc_${TAG}.json ;;
     bench3)
         run bench3 600 python bench.py --config 3 --no-cpu ; rc=$? ;;
+    chains5)   # config 5 through each forced chain
+        for c in five fused; do
+            run bench5_$c 600 python bench.py --config 5 --steps 2 --warmup 1 --no-cpu --chain $c ; rc=$?
+            fatal $rc && break
+        done ;;
+    chains4)   # config 4 through each forced chain
+        for c in five fused; do
+            run bench4_$c 300 python bench.py --no-cpu --no-extras --chain $c ; rc=$?
+            fatal $rc && break
+        done ;;
     bench5)
         run bench5 600 python bench.py --config 5 --steps 3 --warmup 1 --no-cpu ; rc=$? ;;
     shards)   # per-rank chain floor of the strong split: rank 0's shard alone on one GPU
