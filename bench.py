@@ -224,46 +224,33 @@ def cpu_baseline(x, y, w, cands, seconds_target: float, threads: int):
 
 
 def closure_threads(ctx, cands, sweep, seconds=0.25):
-    """Aggregate mac_area_f64 calls/s with T host threads calling at once (DirectSearch's
+    """Aggregate mac_area_f64 calls/s with T native host threads calling at once (DirectSearch's
     SetMaxEvals threaded poll, src/TDM_STATIC_opt.jl:129: one objective call per trial point per
-    thread). Thread t evaluates candidates t, t + T, ... of the poll; every result is checked
+    thread), through csrc/closure_threads.cpp (Python threads would serialise on the GIL around
+    every call). Thread t evaluates candidates t, t + T, ... of the poll; every result is checked
     against the single-threaded area of the same candidate."""
-    import threading
-    K = cands.shape[0]
-    nc = min(K, 64)
-    want = [ctx.area(np.ascontiguousarray(cands[k])) for k in range(nc)]
+    import ctypes
+    path = os.path.join(os.path.dirname(ctx._L._name), "libmaxcover_threads.so")
+    if not os.path.exists(path):
+        return {"error": "libmaxcover_threads.so not built"}
+    H = ctypes.CDLL(path)
+    H.mac_closure_threads.restype = ctypes.c_double
+    H.mac_closure_threads.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                      ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32, ctypes.c_double,
+                                      ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                                      ctypes.POINTER(ctypes.c_int64)]
+    K = min(cands.shape[0], 64)
+    C = np.ascontiguousarray(cands[:K])
+    want = np.array([ctx.area(np.ascontiguousarray(C[k])) for k in range(K)])
+    fn = ctypes.cast(ctx._L.mac_area_f64, ctypes.c_void_p).value
     out = {}
     for T in sweep:
-        stop = time.perf_counter() + 3600.0
-        counts = [0] * T
-        bad = [0] * T
-        start = threading.Barrier(T + 1)
-
-        def work(t):
-            rows = [np.ascontiguousarray(cands[k]) for k in range(t % nc, nc, T)] or \
-                   [np.ascontiguousarray(cands[t % nc])]
-            ks = list(range(t % nc, nc, T)) or [t % nc]
-            start.wait()
-            q = 0
-            while time.perf_counter() < stop:
-                j = q % len(rows)
-                if ctx.area(rows[j]) != want[ks[j]]:
-                    bad[t] += 1
-                q += 1
-            counts[t] = q
-
-        th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
-        for h in th:
-            h.start()
-        t0 = time.perf_counter()
-        stop = t0 + seconds
-        start.wait()
-        t0 = time.perf_counter()
-        stop = t0 + seconds
-        for h in th:
-            h.join()
-        dt = time.perf_counter() - t0
-        out[str(T)] = {"calls_per_s": sum(counts) / dt, "calls": sum(counts), "mismatches": sum(bad)}
+        calls, bad, fail = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        dt = H.mac_closure_threads(fn, ctx._h, C.ctypes.data, K, C.shape[1], want.ctypes.data, int(T),
+                                   float(seconds), ctypes.byref(calls), ctypes.byref(bad),
+                                   ctypes.byref(fail))
+        out[str(T)] = {"calls_per_s": calls.value / dt, "calls": calls.value,
+                       "mismatches": bad.value, "failures": fail.value}
     base = out[str(sweep[0])]["calls_per_s"]
     for T in sweep:
         out[str(T)]["vs_1_thread"] = out[str(T)]["calls_per_s"] / base if base else None

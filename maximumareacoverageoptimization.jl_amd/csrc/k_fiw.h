@@ -1293,16 +1293,26 @@ __global__ __launch_bounds__(kF2Threads) void fin2_kernel(
                             ny[m] = in ? srec[b + 1 + m][1][c] : 0.0;
                             nT[m] = in ? srec[b + 1 + m][2][c] : -1.0;   // (never covers)
                         }
-                        for (int e = ea + gq; e < eb; e += G) {
-                            const double2 p = sxy[e];
-                            if (!(sqdist(p.x, p.y, cx, cy) <= T)) continue;
-                            bool stolen = false;
+                        // four entries per step, their LDS reads issued together
+                        constexpr int kU = 4;
+                        for (int e = ea + gq; e < eb; e += kU * G) {
+                            double2 pp[kU];
 #pragma unroll
-                            for (int m = 0; m < kFwHand; ++m)
-                                stolen |= sqdist(p.x, p.y, nx[m], ny[m]) <= nT[m];
-                            if (!stolen) {
-                                if constexpr (kCounts) s += 1;
-                                else sf += swt[e];
+                            for (int u = 0; u < kU; ++u)
+                                pp[u] = e + u * G < eb ? sxy[e + u * G] : make_double2(0.0, 0.0);
+#pragma unroll
+                            for (int u = 0; u < kU; ++u) {
+                                if (!(e + u * G < eb)) break;
+                                const double2 p = pp[u];
+                                if (!(sqdist(p.x, p.y, cx, cy) <= T)) continue;
+                                bool stolen = false;
+#pragma unroll
+                                for (int m = 0; m < kFwHand; ++m)   // (ncq: uniform; usually 1)
+                                    if (m < ncq && !stolen) stolen = sqdist(p.x, p.y, nx[m], ny[m]) <= nT[m];
+                                if (!stolen) {
+                                    if constexpr (kCounts) s += 1;
+                                    else sf += swt[e + u * G];
+                                }
                             }
                         }
                     }

@@ -467,6 +467,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
             bool any = false;
 #pragma unroll
             for (int c = 0; c < kPrepC; ++c) {
+                if (!a.prec) break;   // (the fused chain: keys only, no region records)
                 const double x = v[c][0], y = v[c][1], r = v[c][2];
                 // span_of's cases: r <= 0 or NaN, or a non-finite centre, covers nothing
                 if (cand(c) < K && !((dead >> c) & 1u) && r > 0.0 && __builtin_isfinite(x) &&
@@ -530,22 +531,33 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
                     constexpr int kB = 6;
                     const double2* row2 = reinterpret_cast<const double2*>(&term[u][0]);
                     const int nfull = nb / (2 * kB);
-                    double2 cur[kB];
+                    // ping-pong buffers (no register moves between batches); the reads past the
+                    // last batch re-read it (clamped) and are never added
+                    auto batch = [&](double2 (&buf)[kB], int bt) {
+                        const int at = (bt < nfull ? bt : nfull - 1) * kB;
 #pragma unroll
-                    for (int j = 0; j < kB; ++j) cur[j] = nfull > 0 ? row2[j] : make_double2(0.0, 0.0);
-#pragma unroll 1
-                    for (int bt = 0; bt < nfull; ++bt) {
-                        const int nx = (bt + 1 < nfull ? bt + 1 : bt) * kB;   // (the last: a re-read)
-                        double2 nxt[kB];
-#pragma unroll
-                        for (int j = 0; j < kB; ++j) nxt[j] = row2[nx + j];
+                        for (int j = 0; j < kB; ++j) buf[j] = row2[at + j];
+                    };
+                    auto add = [&](const double2 (&buf)[kB]) {
 #pragma unroll
                         for (int j = 0; j < kB; ++j) {
-                            acc += cur[j].x;
-                            acc += cur[j].y;
+                            acc += buf[j].x;
+                            acc += buf[j].y;
                         }
-#pragma unroll
-                        for (int j = 0; j < kB; ++j) cur[j] = nxt[j];
+                    };
+                    if (nfull > 0) {
+                        double2 A[kB], B[kB];
+                        batch(A, 0);
+#pragma unroll 1
+                        for (int bt = 0; bt < nfull; bt += 2) {
+                            batch(B, bt + 1);
+                            __builtin_amdgcn_sched_barrier(0);   // (the reads stay ahead of the adds)
+                            add(A);
+                            if (bt + 1 >= nfull) break;
+                            batch(A, bt + 2);
+                            __builtin_amdgcn_sched_barrier(0);
+                            add(B);
+                        }
                     }
                     for (int q = nfull * 2 * kB; q < nb; ++q) acc += term[u][q];
                 }

@@ -5,6 +5,9 @@
 // src/AreaCoverageCalculation.jl:63-110 (calculateArea). See DESIGN.md.
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -12,13 +15,14 @@
 #include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
-#include <condition_variable>
 #include <deque>
 #include <mutex>
 #include <new>
 #include <string>
 #include <type_traits>
+#include <thread>
 #include <vector>
 
 #include "kernels.h"
@@ -174,9 +178,10 @@ struct mac_ctx {
     std::mutex mu;
     // mac_area_f64's combiner: queued single-candidate requests, one batch launch at a time
     std::mutex cl_mu;
-    std::condition_variable cl_cv;
     std::deque<struct ClReq*> cl_q;
-    bool cl_busy = false;
+    int cl_busy = 0;   // batches in flight
+    int64_t cl_batches = 0, cl_reqs = 0;   // (MAXCOVER_CL_STATS=1: printed at destroy)
+    double cl_batch_s = 0.0;               // time inside the batches' evaluations
     std::vector<Lane*> lanes_free;
     std::vector<Lane*> lanes_all;
     hipStream_t setup_stream = nullptr;
@@ -1428,6 +1433,10 @@ int32_t mac_ctx_create(mac_ctx** out, int32_t device)
 void mac_ctx_destroy(mac_ctx* ctx)
 {
     if (!ctx) return;
+    if (const char* e = std::getenv("MAXCOVER_CL_STATS"); e && *e == '1' && ctx->cl_batches)
+        std::fprintf(stderr, "maxcover: closure batches %lld, requests %lld (%.2f per batch), %.1f us per batch\n",
+                     (long long)ctx->cl_batches, (long long)ctx->cl_reqs,
+                     (double)ctx->cl_reqs / (double)ctx->cl_batches, ctx->cl_batch_s / ctx->cl_batches * 1e6);
     (void)hipSetDevice(ctx->device);
     if (ctx->doorbell) {   // every armed poll released first (else the synchronisation would wait)
         __atomic_store_n(ctx->doorbell, ~(uint64_t)0 >> 1, __ATOMIC_RELEASE);
@@ -2495,11 +2504,11 @@ static void closure_batch(mac_ctx* ctx, int64_t three_n, const double* const* ca
     const int nwg = (N + kClosureDisksPerWG - 1) / kClosureDisksPerWG;   // a wave per disk
     int64_t ts_a = -1;
     uint64_t* ts = nullptr;
-    if (ctx->profile && B == 1) {
+    if (ctx->profile) {
         std::lock_guard<std::mutex> lk(ctx->mu);
-        if (ctx->stamp_used + nwg <= ctx->stamp_cap) {
+        if (ctx->stamp_used + (int64_t)nwg * B <= ctx->stamp_cap) {
             ts_a = ctx->stamp_used;
-            ctx->stamp_used += nwg;
+            ctx->stamp_used += (int64_t)nwg * B;
             ts = ctx->stamps.as<uint64_t>() + 2 * ts_a;
         }
     }
@@ -2512,7 +2521,7 @@ static void closure_batch(mac_ctx* ctx, int64_t three_n, const double* const* ca
     HCK(hipGetLastError());
     if (ts) {
         std::lock_guard<std::mutex> lk(ctx->mu);
-        ctx->prof.push_back({ts_a, nwg, -1, 0, 1, nullptr, MAC_ALGO_TILED});
+        ctx->prof.push_back({ts_a, (int64_t)nwg * B, -1, 0, (int64_t)B, nullptr, MAC_ALGO_TILED});
     }
     bool synced = false;
     for (int b = 0; b < B; ++b) {
@@ -2534,18 +2543,41 @@ static void closure_batch(mac_ctx* ctx, int64_t three_n, const double* const* ca
 }
 
 // Concurrent callers (DirectSearch's threaded poll, src/TDM_STATIC_opt.jl:129: one objective call
-// per trial point per thread) are combined: a caller queues its request; whoever finds no batch in
-// flight takes every queued request of the same size (up to kClBatch) and evaluates them in one
-// launch, then wakes the others. A lone caller runs its own request at once. Results per call are
-// exactly the single-candidate kernel's (the batch dimension only selects the candidate).
+// per trial point per thread) are combined: a caller queues its request; while fewer than
+// kClLeaders batches are in flight, a caller whose request is still queued takes every queued
+// request of the same size (up to kClBatch) and evaluates them in one launch on its own lane
+// (stream), marking each done; the others spin on their own request's state word (no lock, no
+// condition-variable wake-up chain) and lead a later batch if theirs is still queued when a slot
+// frees. A lone caller runs its own request at once. Results per call are exactly the
+// single-candidate kernel's (the batch dimension only selects the candidate).
+static constexpr int kClLeaders = 2;   // batches in flight at once (two lanes, two streams)
+
 struct ClReq {
     const double* c;
     int64_t three_n;
     double* out;
-    int32_t rc;
-    bool done;
+    std::atomic<int> state{0};   // 0 queued, 1 taken by a batch, 2 done
+    int32_t rc = MAC_OK;
     std::string err;
 };
+
+// Waiting on a request's state word: a short spin, then a futex sleep (no CPU taken from the
+// threads that lead batches); woken by the leader that completes the request, or by the leader
+// that frees a batch slot while the request is still queued (it may then lead), or after 1 ms.
+static void cl_wait(std::atomic<int>* w, int seen, int spin)
+{
+    if (spin < 64) {
+        __builtin_ia32_pause();
+        return;
+    }
+    struct timespec ts{0, 1000000};
+    syscall(SYS_futex, reinterpret_cast<int*>(w), FUTEX_WAIT_PRIVATE, seen, &ts, nullptr, 0);
+}
+
+static void cl_wake(std::atomic<int>* w)
+{
+    syscall(SYS_futex, reinterpret_cast<int*>(w), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+}
 
 int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, double* area_out)
 {
@@ -2561,26 +2593,39 @@ int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, doubl
         *area_out = 0.0;
         return MAC_OK;
     }
-    ClReq r{circles, three_n, area_out, MAC_OK, false, {}};
-    std::unique_lock<std::mutex> lk(ctx->cl_mu);
-    ctx->cl_q.push_back(&r);
-    while (!r.done) {
-        if (ctx->cl_busy) {
-            ctx->cl_cv.wait(lk);
-            continue;
-        }
-        ctx->cl_busy = true;
+    ClReq r;
+    r.c = circles;
+    r.three_n = three_n;
+    r.out = area_out;
+    {
+        std::lock_guard<std::mutex> lk(ctx->cl_mu);
+        ctx->cl_q.push_back(&r);
+    }
+    for (int spin = 0; r.state.load(std::memory_order_acquire) != 2; ++spin) {
         std::vector<ClReq*> batch;
-        const int64_t tn = ctx->cl_q.front()->three_n;
-        for (auto it = ctx->cl_q.begin(); it != ctx->cl_q.end() && (int)batch.size() < kClBatch;) {
-            if ((*it)->three_n == tn) {
-                batch.push_back(*it);
-                it = ctx->cl_q.erase(it);
-            } else {
-                ++it;
+        if (r.state.load(std::memory_order_relaxed) == 0) {
+            std::lock_guard<std::mutex> lk(ctx->cl_mu);
+            if (r.state.load(std::memory_order_relaxed) == 0 && ctx->cl_busy < kClLeaders && !ctx->cl_q.empty()) {
+                ++ctx->cl_busy;
+                ++ctx->cl_batches;
+                const int64_t tn = ctx->cl_q.front()->three_n;
+                for (auto it = ctx->cl_q.begin(); it != ctx->cl_q.end() && (int)batch.size() < kClBatch;) {
+                    if ((*it)->three_n == tn) {
+                        (*it)->state.store(1, std::memory_order_relaxed);
+                        batch.push_back(*it);
+                        ++ctx->cl_reqs;
+                        it = ctx->cl_q.erase(it);
+                    } else {
+                        ++it;
+                    }
+                }
             }
         }
-        lk.unlock();
+        if (batch.empty()) {
+            const int seen = r.state.load(std::memory_order_acquire);
+            if (seen != 2) cl_wait(&r.state, seen, spin);
+            continue;
+        }
         int32_t brc = MAC_OK;
         std::string msg;
         try {
@@ -2590,7 +2635,11 @@ int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, doubl
                 cs[q] = batch[q]->c;
                 os[q] = batch[q]->out;
             }
-            closure_batch(ctx, tn, cs.data(), os.data(), (int)batch.size());
+            const auto tb0 = std::chrono::steady_clock::now();
+            closure_batch(ctx, batch[0]->three_n, cs.data(), os.data(), (int)batch.size());
+            const double dtb = std::chrono::duration<double>(std::chrono::steady_clock::now() - tb0).count();
+            std::lock_guard<std::mutex> lk(ctx->cl_mu);
+            ctx->cl_batch_s += dtb;
         } catch (const HipError& he) {
             brc = he.e == hipErrorOutOfMemory ? MAC_E_NOMEM : MAC_E_HIP;
             char buf[512];
@@ -2604,16 +2653,25 @@ int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, doubl
             brc = MAC_E_HIP;
             msg = "unexpected exception";
         }
-        lk.lock();
-        for (ClReq* q : batch) {
+        ClReq* next = nullptr;   // a queued request whose thread may lead the freed slot
+        {
+            std::lock_guard<std::mutex> lk(ctx->cl_mu);
+            --ctx->cl_busy;
+            for (ClReq* q : ctx->cl_q)
+                if (q != &r) {
+                    next = q;
+                    break;
+                }
+            if (next) cl_wake(&next->state);   // (under the lock: the request still exists)
+        }
+        for (ClReq* q : batch) {   // (a request object lives until its state reads 2)
             q->rc = brc;
             q->err = msg;
-            q->done = true;
+            q->state.store(2, std::memory_order_release);
+            if (q != &r) cl_wake(&q->state);
         }
-        ctx->cl_busy = false;
-        ctx->cl_cv.notify_all();
+        spin = 0;
     }
-    lk.unlock();
     if (r.rc) return fail(r.rc, r.err);
     return MAC_OK;
     ABI_END
