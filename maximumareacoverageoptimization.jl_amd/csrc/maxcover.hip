@@ -180,6 +180,8 @@ struct mac_ctx {
     std::mutex cl_mu;
     std::deque<struct ClReq*> cl_q;
     int cl_busy = 0;   // batches in flight
+    std::atomic<int> cl_active{0};   // callers inside mac_area_f64's combiner
+    int cl_taken = 0;                // requests in batches in flight (under cl_mu)
     int64_t cl_batches = 0, cl_reqs = 0;   // (MAXCOVER_CL_STATS=1: printed at destroy)
     double cl_batch_s = 0.0;               // time inside the batches' evaluations
     std::vector<Lane*> lanes_free;
@@ -2551,6 +2553,8 @@ static void closure_batch(mac_ctx* ctx, int64_t three_n, const double* const* ca
 // frees. A lone caller runs its own request at once. Results per call are exactly the
 // single-candidate kernel's (the batch dimension only selects the candidate).
 static constexpr int kClLeaders = 2;   // batches in flight at once (two lanes, two streams)
+static constexpr int kClSpin = 64;        // pause iterations before a waiter sleeps on its futex
+static constexpr int kClGather = 0;        // pauses a would-be leader waits for every caller to queue (0: none)
 
 struct ClReq {
     const double* c;
@@ -2566,7 +2570,8 @@ struct ClReq {
 // that frees a batch slot while the request is still queued (it may then lead), or after 1 ms.
 static void cl_wait(std::atomic<int>* w, int seen, int spin)
 {
-    if (spin < 64) {
+    // a short spin, then sleep (spinning waiters take CPU from the threads that lead batches)
+    if (spin < kClSpin) {
         __builtin_ia32_pause();
         return;
     }
@@ -2597,6 +2602,7 @@ int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, doubl
     r.c = circles;
     r.three_n = three_n;
     r.out = area_out;
+    ctx->cl_active.fetch_add(1);
     {
         std::lock_guard<std::mutex> lk(ctx->cl_mu);
         ctx->cl_q.push_back(&r);
@@ -2605,7 +2611,12 @@ int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, doubl
         std::vector<ClReq*> batch;
         if (r.state.load(std::memory_order_relaxed) == 0) {
             std::lock_guard<std::mutex> lk(ctx->cl_mu);
-            if (r.state.load(std::memory_order_relaxed) == 0 && ctx->cl_busy < kClLeaders && !ctx->cl_q.empty()) {
+            // lead once every caller in the combiner has queued (the whole convoy in one launch),
+            // or after a short wait
+            const bool all_in = (int)ctx->cl_q.size() + ctx->cl_taken >= ctx->cl_active.load() ||
+                                spin >= kClGather;
+            if (r.state.load(std::memory_order_relaxed) == 0 && ctx->cl_busy < kClLeaders && all_in &&
+                !ctx->cl_q.empty()) {
                 ++ctx->cl_busy;
                 ++ctx->cl_batches;
                 const int64_t tn = ctx->cl_q.front()->three_n;
@@ -2614,6 +2625,7 @@ int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, doubl
                         (*it)->state.store(1, std::memory_order_relaxed);
                         batch.push_back(*it);
                         ++ctx->cl_reqs;
+                        ++ctx->cl_taken;
                         it = ctx->cl_q.erase(it);
                     } else {
                         ++it;
@@ -2657,6 +2669,7 @@ int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, doubl
         {
             std::lock_guard<std::mutex> lk(ctx->cl_mu);
             --ctx->cl_busy;
+            ctx->cl_taken -= (int)batch.size();
             for (ClReq* q : ctx->cl_q)
                 if (q != &r) {
                     next = q;
@@ -2672,6 +2685,7 @@ int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, doubl
         }
         spin = 0;
     }
+    ctx->cl_active.fetch_sub(1);
     if (r.rc) return fail(r.rc, r.err);
     return MAC_OK;
     ABI_END
