@@ -48,9 +48,11 @@ def main():
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("--config", type=int, default=4)
-    ap.add_argument("--chain", default="mac::prep_kernel;mac::disk_index_kernel<true, 3>;"
-                    "mac::walk_setup_kernel;mac::coverage_poll_kernel;mac::finalize_kernel",
-                    help="semicolon-separated kernels of one poll")
+    ap.add_argument("--chain", default="mac::prep_kernel;mac::fiw_kernel<true>;mac::fin2_kernel<true>",
+                    help="semicolon-separated kernels of one poll (default: the fused chain "
+                         "config 4 takes; the five-launch chain: mac::prep_kernel;"
+                         "mac::disk_index_kernel<true, 3>;mac::walk_setup_kernel;"
+                         "mac::coverage_poll_kernel;mac::finalize_kernel)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     fetch = load(a.fetch_dir, "FETCH_SIZE")
