@@ -366,10 +366,20 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
     # the evaluations the reference makes: poll candidates that pass cons3 (the extreme barrier
     # never calls the objective on the others), over every rank's shard
     feas = sum(r["feasible_evaluations"] for r in recs)
-    if world > 1:
+    if world > 1 and spec:
+        # speculation: every rank applies the same polls; the useful evaluations are the applied
+        # polls' (the sequential loop's), the discarded branches' are reported beside them
+        work = torch.tensor([feas], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(work)
+        spec_work = int(work.item())
+        feas = sum(r["useful_feasible_evaluations"] for r in recs)
+    elif world > 1:
         ft = torch.tensor([feas], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(ft)
         feas = int(ft.item())
+        spec_work = None
+    else:
+        spec_work = None
     if rank != 0:
         D.close()
         ctx.close()
@@ -431,6 +441,7 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
                            "iteration)",
             "mads_iterations": iters,
             "exchange_rounds": sum(r["rounds"] for r in recs),
+            "speculative_feasible_evaluations_all_ranks": spec_work,
             "mads_successes": succ,
             "failure_fraction": (1.0 - succ / iters) if iters else None,
             "rejected_polls": rejected,

@@ -220,11 +220,13 @@ int32_t mac_mads_result(mac_mads* m, double* x_out, mac_mads_stats* stats);
  * order up to the first success, so a run of failures advances up to P iterations per round:
  *   mac_mads_poll_ahead  evaluates (this stepper's shard of) the poll of the iteration `ahead`
  *                        failures past the current one, without advancing; done = 1 when that
- *                        poll does not exist (iteration limit or ell - ahead < 0);
+ *                        poll does not exist (iteration limit or ell - ahead < 0); feasible (may be
+ *                        NULL): its candidates that passed cons3 (evaluated);
  *   mac_mads_advance     applies one iteration's result (the poll at ahead = 0) as
  *                        mac_mads_update does, without a prior mac_mads_poll; moved = 1 when the
  *                        incumbent moved (success). Same iterates as the sequential loop. */
-int32_t mac_mads_poll_ahead(mac_mads* m, int32_t ahead, int32_t* done, double* best_obj, int64_t* best_idx);
+int32_t mac_mads_poll_ahead(mac_mads* m, int32_t ahead, int32_t* done, double* best_obj, int64_t* best_idx,
+                            int64_t* feasible);
 int32_t mac_mads_advance(mac_mads* m, double best_obj, int64_t best_idx, int32_t* moved);
 void mac_mads_destroy(mac_mads* m);
 /* Every later poll of the stepper also writes its 16-byte shard best {objective, index as

@@ -145,6 +145,8 @@ class Simulation:
                    rejected_polls=int(st.get("rejected_polls", 0)),
                    successes=int(st.get("successes", 0)),
                    rounds=int(st.get("rounds", st["iterations"])),
+                   useful_feasible_evaluations=int(st.get("useful_feasible_evaluations",
+                                                          st.get("feasible_evaluations", 0))),
                    fire_s=t1 - t0, remove_s=t2 - t1, mads_s=t3 - t2, step_s=t3 - t0,
                    mads_host_s={k: float(st.get(k, 0.0)) for k in
                                 ("host_enqueue_s", "host_perm_s", "wait_s", "host_post_s")},

@@ -208,13 +208,14 @@ class PollStepper:
         return np.concatenate([self.x[None, :] + B.T, self.x[None, :] - B.T], axis=0)
 
     def poll_ahead(self, ahead: int):
+        """(done, best_obj, best_idx, feasible): feasible is not tracked here (0)."""
         if self.it + ahead >= self.N_iter or self.ell - ahead < 0:
-            return True, np.inf, -1
+            return True, np.inf, -1, 0
         Xs = self._poll_matrix(ahead)[self.lo:self.hi]
         if Xs.shape[0] == 0:
-            return False, np.inf, -1
+            return False, np.inf, -1, 0
         bo, bi = self.poll_fn(Xs)
-        return False, float(bo), (self.lo + int(bi) if bi >= 0 else -1)
+        return False, float(bo), (self.lo + int(bi) if bi >= 0 else -1), 0
 
     def advance(self, best_obj: float, best_idx: int) -> bool:
         X = self._poll_matrix(0)

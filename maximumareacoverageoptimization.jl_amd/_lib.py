@@ -171,7 +171,7 @@ def _declare(L: ctypes.CDLL) -> None:
                             ctypes.POINTER(MadsParams), _i64, _i64, ctypes.POINTER(_vp)], _i32),
         "mac_mads_poll": ([_vp, ctypes.POINTER(_i32), _dp, _i64p], _i32),
         "mac_mads_update": ([_vp, ctypes.c_double, _i64], _i32),
-        "mac_mads_poll_ahead": ([_vp, _i32, ctypes.POINTER(_i32), _dp, _i64p], _i32),
+        "mac_mads_poll_ahead": ([_vp, _i32, ctypes.POINTER(_i32), _dp, _i64p, _i64p], _i32),
         "mac_mads_advance": ([_vp, ctypes.c_double, _i64, ctypes.POINTER(_i32)], _i32),
         "mac_mads_result": ([_vp, _dp, ctypes.POINTER(MadsStats)], _i32),
         "mac_mads_destroy": ([_vp], None),
@@ -726,11 +726,14 @@ class MadsStepper:
         _check(self._L.mac_mads_update(self._h, float(best_obj), int(best_idx)))
 
     def poll_ahead(self, ahead: int):
-        """mac_mads_poll_ahead: (done, best_obj, best_idx) of the poll that follows `ahead`
-        failures of the current iteration, the stepper unchanged."""
+        """mac_mads_poll_ahead: (done, best_obj, best_idx, feasible) of the poll that follows
+        `ahead` failures of the current iteration, the stepper unchanged; feasible = its
+        candidates that passed cons3."""
+        fe = _i64()
         _check(self._L.mac_mads_poll_ahead(self._h, int(ahead), ctypes.byref(self._done),
-                                           ctypes.byref(self._bo), ctypes.byref(self._bi)))
-        return bool(self._done.value), self._bo.value, int(self._bi.value)
+                                           ctypes.byref(self._bo), ctypes.byref(self._bi),
+                                           ctypes.byref(fe)))
+        return bool(self._done.value), self._bo.value, int(self._bi.value), int(fe.value)
 
     def advance(self, best_obj: float, best_idx: int) -> bool:
         """mac_mads_advance: apply one iteration's result; True when the incumbent moved."""

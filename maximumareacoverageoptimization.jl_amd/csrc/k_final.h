@@ -60,15 +60,19 @@ struct FinBest {
     int* hint;
     int* hint_host;
     int nhint;
+    // a stepper's cumulative count of candidates that passed cons3 (k_prep.h PrepArgs.feas; null:
+    // none): the last block also writes it to the mirror's word 4 (a 64-B slot), under the check
+    const unsigned long long* feas;
 };
 
 // Check word of a mirrored result (host: mirror_check in maxcover.hip): the host accepts the slot
 // only when seq is the one it waits for AND the check word matches the three words it read, so a
 // slot read while its stores are still landing (no fence orders them: a system-scope release
 // would write back the XCD's L2) is read again, never accepted torn.
-__host__ __device__ __forceinline__ uint64_t mirror_check(uint64_t o, uint64_t i, uint64_t q)
+__host__ __device__ __forceinline__ uint64_t mirror_check(uint64_t o, uint64_t i, uint64_t q, uint64_t f = 0)
 {
-    uint64_t z = o ^ (i * 0x9E3779B97F4A7C15ull) ^ (q * 0xC2B2AE3D27D4EB4Full) ^ 0x5851F42D4C957F2Dull;
+    uint64_t z = o ^ (i * 0x9E3779B97F4A7C15ull) ^ (q * 0xC2B2AE3D27D4EB4Full) ^ (f * 0xD6E8FEB86659FD93ull) ^
+                 0x5851F42D4C957F2Dull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
@@ -179,7 +183,8 @@ __device__ __forceinline__ bool finalize_argmin(const FinBest& fb, double o, int
         ix[r] = q < gridDim.x ? __hip_atomic_load(fb.blk + 2 * q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                               : ~0ull;
     }
-    // the hint words, in the same round trip
+    // the hint words and the feasible count, in the same round trip
+    const uint64_t fe = fb.feas ? __hip_atomic_load(fb.feas, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
     const bool hl = fb.hint && lane < fb.nhint;
     const int hv = hl ? __hip_atomic_load(fb.hint + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
 #pragma unroll
@@ -224,7 +229,8 @@ __device__ __forceinline__ bool finalize_argmin(const FinBest& fb, double o, int
             fb.mirror[0] = o;
             fb.mirror[1] = ix;
             fb.mirror[2] = fb.seq;
-            fb.mirror[3] = mirror_check(o, ix, fb.seq);
+            if (fb.feas) fb.mirror[4] = fe;
+            fb.mirror[3] = mirror_check(o, ix, fb.seq, fe);
             // a pipelined loop that has just stopped: polls after this one write no slot, so the
             // seq word jumps past every seq the host may wait for
             if (fb.st && !(gidx >= 0 && bo < fcur) && ell == 0) fb.mirror[2] = fb.done_seq;

@@ -338,24 +338,27 @@ struct LaneGuard {
 // A mapped result slot {obj bits, index, seq, check} (k_final.h) read once: true when it holds
 // seq `want` and its check word matches (else its stores are still landing, or it is another
 // poll's).
-static bool mirror_read(const uint64_t* h, uint64_t want, double* obj, int64_t* idx)
+static bool mirror_read(const uint64_t* h, uint64_t want, double* obj, int64_t* idx, uint64_t* feas = nullptr)
 {
     if (__atomic_load_n(h + 2, __ATOMIC_ACQUIRE) != want) return false;
     const uint64_t o = __atomic_load_n(h + 0, __ATOMIC_ACQUIRE);
     const uint64_t i = __atomic_load_n(h + 1, __ATOMIC_ACQUIRE);
     const uint64_t c = __atomic_load_n(h + 3, __ATOMIC_ACQUIRE);
-    if (c != mirror_check(o, i, want) || __atomic_load_n(h + 2, __ATOMIC_ACQUIRE) != want) return false;
+    const uint64_t f = feas ? __atomic_load_n(h + 4, __ATOMIC_ACQUIRE) : 0;
+    if (c != mirror_check(o, i, want, f) || __atomic_load_n(h + 2, __ATOMIC_ACQUIRE) != want) return false;
     *obj = __builtin_bit_cast(double, o);
     *idx = (int64_t)i;
+    if (feas) *feas = f;
     return true;
 }
 
 // Spin on a slot for up to `ms` milliseconds.
-static bool mirror_wait(const uint64_t* h, uint64_t want, double ms, double* obj, int64_t* idx)
+static bool mirror_wait(const uint64_t* h, uint64_t want, double ms, double* obj, int64_t* idx,
+                        uint64_t* feas = nullptr)
 {
     const auto t0 = std::chrono::steady_clock::now();
     for (int spin = 0;; ++spin) {
-        if (mirror_read(h, want, obj, idx)) return true;
+        if (mirror_read(h, want, obj, idx, feas)) return true;
         if ((spin & 1023) == 1023 &&
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > ms)
             return false;
@@ -752,6 +755,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                 fb.hint = L->fwhint.as<int>();   // (read and cleared by the argmin's last block)
                 fb.hint_host = L->d_dc + 8;
                 fb.nhint = kFwHints;
+                fb.feas = d_mirror ? d_feas : nullptr;
             }
             uint64_t* tsf = take_ts(nfin, ts_f, ts_nf);
             if (counts)
@@ -1044,6 +1048,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         fb.idx_base = idx_base;
         fb.blk = L->finblk.as<unsigned long long>();
         fb.arrive = L->finarrive.as<unsigned>();
+        fb.feas = d_mirror ? d_feas : nullptr;
     }
     uint64_t* tsf = ts_c >= 0 ? take_ts(nfin, ts_f, ts_nf) : nullptr;
     hipLaunchKernelGGL(finalize_kernel, dim3(nfin), dim3(kFinThreads), 0, s,
@@ -1871,6 +1876,7 @@ struct mac_mads {
     int ell = 0;
     std::vector<double> h_prev;   // cons3's prev (host copy: whole-poll rejection, poll_rejected)
     DevBuf d_feas;                // candidates that passed cons3 (the prep launches count them)
+    uint64_t feas_seen = 0;       // d_feas as the last mac_mads_poll_ahead read it
     uint64_t state = 0, T = 0, per_iter = 0;
     std::vector<int> rp, cp, rp_next, cp_next;
     double* hb = nullptr;
@@ -1946,15 +1952,20 @@ static void mads_best_of(mac_mads* m, const CandSrc& src, int Kc, int64_t idx_ba
 // The best {objective, global index} of the poll mads_best_of enqueued: from the mapped slot once
 // it holds this poll's seq and a matching check word, or, after 50 ms (a failed launch) or
 // without a slot, the stream synchronised and the copy.
-static void mads_wait_best(mac_mads* m, double* obj, int64_t* idx)
+static void mads_wait_best(mac_mads* m, double* obj, int64_t* idx, uint64_t* feas_cum = nullptr)
 {
     if (m->slotted) {
-        if (mirror_wait((const uint64_t*)m->hslot.p, m->seq, 50.0, obj, idx)) return;
+        if (mirror_wait((const uint64_t*)m->hslot.p, m->seq, 50.0, obj, idx, feas_cum)) return;
         HCK(hipMemcpyAsync(m->hb, mads_best_ptr(m), 16, hipMemcpyDeviceToHost, m->s));
     }
     HCK(hipStreamSynchronize(m->s));
     *obj = m->hb[0];
     *idx = __builtin_bit_cast(int64_t, m->hb[1]);
+    if (feas_cum) {
+        unsigned long long fe = 0;
+        HCK(hipMemcpy(&fe, m->d_feas.p, sizeof(fe), hipMemcpyDeviceToHost));
+        *feas_cum = fe;
+    }
 }
 
 static void mads_free(mac_mads* m)
@@ -2160,10 +2171,12 @@ int32_t mac_mads_update(mac_mads* m, double best_obj, int64_t best_idx)
 // consecutive failures. mac_mads_poll_ahead evaluates it (the whole poll, this stepper's shard)
 // without advancing the stepper; mac_mads_advance then applies the gathered results in order, one
 // iteration each, up to the first success. Same iterates as the sequential loop.
-int32_t mac_mads_poll_ahead(mac_mads* m, int32_t ahead, int32_t* done, double* best_obj, int64_t* best_idx)
+int32_t mac_mads_poll_ahead(mac_mads* m, int32_t ahead, int32_t* done, double* best_obj, int64_t* best_idx,
+                            int64_t* feasible)
 {
     ABI_BEGIN
     if (!m || !done || !best_obj || !best_idx) return fail(MAC_E_INVAL, "null argument");
+    if (feasible) *feasible = 0;
     if (ahead < 0) return fail(MAC_E_INVAL, "negative ahead");
     if (m->polled_b) return fail(MAC_E_INVAL, "mac_mads_poll_ahead with a mac_mads_poll pending");
     *done = 0;
@@ -2206,7 +2219,10 @@ int32_t mac_mads_poll_ahead(mac_mads* m, int32_t ahead, int32_t* done, double* b
     src.b = b;
     src.k0 = (int)m->lo;
     mads_best_of(m, src, Kc, m->lo, true);
-    mads_wait_best(m, best_obj, best_idx);
+    uint64_t fe = 0;
+    mads_wait_best(m, best_obj, best_idx, &fe);
+    if (feasible) *feasible = (int64_t)(fe - m->feas_seen);
+    m->feas_seen = fe;
     return MAC_OK;
     ABI_END
 }

@@ -220,9 +220,9 @@ def make_gather(device="cpu", group=None):
 
 
 class SpecGather:
-    """The speculative loop's exchange: every rank's (done, best objective, best index) in rank
-    order — one all-gather of a 24-B record per rank (RCCL on a GPU device, gloo on CPU) and one
-    host read."""
+    """The speculative loop's exchange: every rank's (done, best objective, best index, feasible
+    candidates of its poll) in rank order — one all-gather of a 32-B record per rank (RCCL on a GPU
+    device, gloo on CPU) and one host read."""
 
     def __init__(self, device="cpu", group=None):
         import torch
@@ -236,27 +236,28 @@ class SpecGather:
         if self.on_device:
             check_one_runtime()
         pin = self.on_device
-        self.stage = torch.zeros(3, dtype=torch.float64, pin_memory=pin)
-        self.rec = torch.zeros(3, dtype=torch.float64, device=self.device)
-        self.out = torch.empty((self.world, 3), dtype=torch.float64, device=self.device)
-        self.host = (torch.empty((self.world, 3), dtype=torch.float64, pin_memory=True)
+        self.stage = torch.zeros(4, dtype=torch.float64, pin_memory=pin)
+        self.rec = torch.zeros(4, dtype=torch.float64, device=self.device)
+        self.out = torch.empty((self.world, 4), dtype=torch.float64, device=self.device)
+        self.host = (torch.empty((self.world, 4), dtype=torch.float64, pin_memory=True)
                      if self.on_device else self.out)
 
-    def __call__(self, done, obj, idx):
+    def __call__(self, done, obj, idx, feasible=0):
         import torch
         import torch.distributed as dist
 
         self.stage[0] = 1.0 if done else 0.0
         self.stage[1] = float(obj)
         self.stage.view(torch.int64)[2] = int(idx)
+        self.stage.view(torch.int64)[3] = int(feasible)
         self.rec.copy_(self.stage)
-        dist.all_gather_into_tensor(self.out, self.rec.reshape(1, 3), group=self.group)
+        dist.all_gather_into_tensor(self.out, self.rec.reshape(1, 4), group=self.group)
         if self.on_device:
             self.host.copy_(self.out)
         h = self.host
         hi = h.view(torch.int64)
-        return [(bool(h[j, 0].item() != 0.0), float(h[j, 1].item()), int(hi[j, 2].item()))
-                for j in range(self.world)]
+        return [(bool(h[j, 0].item() != 0.0), float(h[j, 1].item()), int(hi[j, 2].item()),
+                 int(hi[j, 3].item())) for j in range(self.world)]
 
 
 def mads_loop_speculative(stepper, gather=None):
@@ -270,16 +271,18 @@ def mads_loop_speculative(stepper, gather=None):
     rank = gather.rank if gather is not None else 0
     world = gather.world if gather is not None else 1
     rounds = 0
+    useful = 0   # the applied polls' feasible candidates (the sequential loop's evaluations)
     while True:
         mine = stepper.poll_ahead(rank)
         recs = gather(*mine) if gather is not None else [mine]
         rounds += 1
         finished = False
         for j in range(world):
-            done, obj, idx = recs[j]
+            done, obj, idx, feas = recs[j]
             if done:
                 finished = True
                 break
+            useful += feas
             if stepper.advance(obj, idx):
                 break
         if finished:
@@ -287,6 +290,7 @@ def mads_loop_speculative(stepper, gather=None):
     x, st = stepper.result()
     st = dict(st)
     st["rounds"] = rounds
+    st["useful_feasible_evaluations"] = useful
     return x, st
 
 

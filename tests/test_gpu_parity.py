@@ -1067,15 +1067,17 @@ def test_native_mads_speculative_steppers(ctx, pkg, world):
     want_x, want = ctx.mads_run(x0, r_max, 1e5, **kw)
     steppers = [ctx.mads_stepper(x0, r_max, 1e5, **kw) for _ in range(world)]
     rounds = 0
+    useful = 0
     while True:
         res = [s_.poll_ahead(j) for j, s_ in enumerate(steppers)]
         rounds += 1
         finished = False
         for j in range(world):
-            done, bo, bi = res[j]
+            done, bo, bi, fe = res[j]
             if done:
                 finished = True
                 break
+            useful += fe
             moved = [s_.advance(bo, bi) for s_ in steppers]
             assert len(set(moved)) == 1
             if moved[0]:
@@ -1083,6 +1085,7 @@ def test_native_mads_speculative_steppers(ctx, pkg, world):
         if finished:
             break
     assert rounds < want["iterations"]
+    assert useful == want["feasible_evaluations"]   # the applied polls' evaluations = the loop's
     for s_ in steppers:
         xs, st = s_.result()
         s_.close()
