@@ -307,18 +307,31 @@ __device__ __forceinline__ void lds_barrier()
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <bool kMat>
-__device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
+// the workgroup's LDS (one block for both source kinds: their instantiations would each
+// declare their own)
+template <int PC>
+struct PrepLds {
+    double term[PC][kPrepU + 2];   // [candidate][UAV]; rows 16-B aligned (the fold reads pairs),
+                                   // 4 banks apart (+2)
+    int wbad[kPrepU / kWave][PC];  // per wave: a term of the candidate is negative
+    uint32_t wbadm[kPrepU / kWave];   // ... wbad as a mask over the candidates
+    int wrej[kPrepU / kWave];         // per wave: every UAV's diagonal steps fail (mst_w)
+    double dred[kPrepU / kWave][4];   // per wave: its share of the displacement bound
+};
+
+template <bool kMat, int PC>
+__device__ __forceinline__ void prep_block(const PrepArgs& a, int cw, unsigned char* lds)
 {
     // [candidate][UAV]; rows 16-B aligned (the fold reads pairs) and 4 banks apart (+2)
-    __shared__ __attribute__((aligned(16))) double term[kPrepC][kPrepU + 2];
-    __shared__ int wbad[kPrepU / kWave][kPrepC];  // per wave: a term of the candidate is negative
-    __shared__ uint32_t wbadm[kPrepU / kWave];       // ... wbad as a mask over the candidates
-    __shared__ int wrej[kPrepU / kWave];             // per wave: every UAV's diagonal steps fail (mst_w)
-    __shared__ double dred[kPrepU / kWave][4];       // per wave: its share of the displacement bound
+    PrepLds<PC>& L = *reinterpret_cast<PrepLds<PC>*>(lds);
+    auto& term = L.term;
+    auto& wbad = L.wbad;
+    auto& wbadm = L.wbadm;
+    auto& wrej = L.wrej;
+    auto& dred = L.dred;
     const int N = a.N, K = a.K;
     const int u = threadIdx.x, lane = u & (kWave - 1), wid = u / kWave;
-    const int k0 = cw * kPrepC;
+    const int k0 = cw * PC;
     const int n3 = 3 * N;
     // candidate c of the workgroup: k0 + c, or (pairs) the plus / minus candidates of B's columns
     // [4cw, 4cw + 4): c < 4 -> 4cw + c, c >= 4 -> n + 4cw + c - 4
@@ -342,9 +355,9 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
         const int i = ib + u;
         const bool iv = u < nb;
         const int ii = min(i, N - 1);
-        double v[kPrepC][3];
-        if (!kMat && a.pair) {
-            // x +- B[v][col]: each draw once for the candidate pair (kPrepC == 8: four columns)
+        double v[PC][3];
+        if (!kMat && PC == 8 && a.pair) {
+            // x +- B[v][col]: each draw once for the candidate pair (PC == 8: four columns)
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 const int col = 4 * cw + c;
@@ -358,7 +371,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
             }
         } else {
 #pragma unroll
-            for (int c = 0; c < kPrepC; ++c) {
+            for (int c = 0; c < PC; ++c) {
                 const int k = min(cand(c), K - 1);
 #pragma unroll
                 for (int q = 0; q < 3; ++q) {
@@ -383,7 +396,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
             const double T3 = pen_threshold(pa, ii);
             uint32_t wdead = 0u;   // this wave's part of the failures
 #pragma unroll
-            for (int c = 0; c < kPrepC; ++c) {
+            for (int c = 0; c < PC; ++c) {
                 const double R2 = v[c][2];
                 double t = pa.rmax ? __builtin_fabs(R2 - rm) : 0.0;
                 if (pa.prev) {
@@ -428,7 +441,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
             // the fused chain's displacement bound (k_fiw.h sup_box): over this workgroup's live
             // candidates (the ones the records below would take), a NaN difference counts as +inf
 #pragma unroll
-            for (int c = 0; c < kPrepC; ++c) {
+            for (int c = 0; c < PC; ++c) {
                 const double x = v[c][0], y = v[c][1], r = v[c][2];
                 if (cand(c) < K && !((dead >> c) & 1u) && r > 0.0 && __builtin_isfinite(x) &&
                     __builtin_isfinite(y)) {
@@ -466,7 +479,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
             double xm = 0.0, ym = 0.0, est = 0.0;
             bool any = false;
 #pragma unroll
-            for (int c = 0; c < kPrepC; ++c) {
+            for (int c = 0; c < PC; ++c) {
                 if (!a.prec) break;   // (the fused chain: keys only, no region records)
                 const double x = v[c][0], y = v[c][1], r = v[c][2];
                 // span_of's cases: r <= 0 or NaN, or a non-finite centre, covers nothing
@@ -485,9 +498,9 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
             }
             bool kb = false;   // a key of this disk is inexact (k_index.h "Keys")
             if (a.keysP) {     // the keys: packed words (two 16-B stores), escapes in fp32
-                uint32_t pk[kPrepC];
+                uint32_t pk[PC];
 #pragma unroll
-                for (int c = 0; c < kPrepC; ++c) {
+                for (int c = 0; c < PC; ++c) {
                     int dx = 0, dy = 0, dr = 0;
                     const bool packs = key_int(v[c][0], base[0], 1023.0, dx) &&
                                        key_int(v[c][1], base[1], 1023.0, dy) &&
@@ -503,7 +516,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
                     }
                 }
 #pragma unroll
-                for (int h = 0; h < kPrepC / 4; ++h)   // candidates cand(4h) .. cand(4h) + 3
+                for (int h = 0; h < PC / 4; ++h)   // candidates cand(4h) .. cand(4h) + 3
                     *reinterpret_cast<uint4*>(a.keysP + (int64_t)i * a.ldk + cand(4 * h)) =
                         make_uint4(pk[4 * h], pk[4 * h + 1], pk[4 * h + 2], pk[4 * h + 3]);
             }
@@ -522,7 +535,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
             // the chains, after every wave's other work (the adds are the critical path: the
             // folding wave then has its SIMD to itself), sequential in UAV order
             if (!excl) lds_barrier();   // (excl: passed above)
-            if (u < kPrepC) {
+            if (u < PC) {
 #pragma unroll
                 for (int w = 0; w < kPrepU / kWave; ++w) bad |= wbad[w][u] != 0;
                 if (!bad) {   // (a cons3 failure's vp is +inf: no chain to fold)
@@ -566,12 +579,12 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
         MAC_PREP_STAMP(3 + 3 * (ib / kPrepU));
         if (obj && ib + kPrepU < N) lds_barrier();   // the fold has read the terms
     }
-    if (obj && u < kPrepC && cand(u) < K) {
+    if (obj && u < PC && cand(u) < K) {
         a.vp[cand(u)] = bad ? __builtin_inf() : acc * a.penalty;
         if (a.dead8) a.dead8[cand(u)] = excl && bad ? 1 : 0;
     }
     if (obj && a.feas && wid == 0) {   // the evaluations: candidates that pass cons3
-        const uint64_t ok = __ballot(u < kPrepC && cand(u) < K && !bad);
+        const uint64_t ok = __ballot(u < PC && cand(u) < K && !bad);
         if (lane == 0 && ok) atomicAdd(a.feas, (unsigned long long)__popcll(ok));
     }
     if (a.pd) {   // the workgroup's displacement bound: the waves' shares in order
@@ -589,7 +602,8 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw)
     }
 }
 
-__global__ __launch_bounds__(kPrepU) __attribute__((amdgpu_waves_per_eu(4))) void prep_kernel(uint64_t* ts, PrepArgs a)
+template <int PC>
+__device__ __forceinline__ void prep_body(uint64_t* ts, PrepArgs& a)
 {
     ts_begin(ts);   // profiling only (the chain's first launch: k_common.h)
     if (a.lreset && blockIdx.x == 0 && threadIdx.x == 0) *a.lreset = 0;   // (read by fin2 after fiw)
@@ -601,9 +615,16 @@ __global__ __launch_bounds__(kPrepU) __attribute__((amdgpu_waves_per_eu(4))) voi
     // candidate groups — which fill the same lines of keysP and of the records — go to one XCD
     const int per = (int)((gridDim.x + 7) / 8), b = (int)blockIdx.x;
     const int cw = (int)(gridDim.x % 8) == 0 ? (b % 8) * per + b / 8 : b;
-    if (a.src.cands) prep_block<true>(a, cw);
-    else prep_block<false>(a, cw);
+    __shared__ __attribute__((aligned(16))) unsigned char lds[sizeof(PrepLds<PC>)];
+    if (a.src.cands) prep_block<true, PC>(a, cw, lds);
+    else prep_block<false, PC>(a, cw, lds);
     ts_end(ts);
+}
+
+// kPrepC candidates per workgroup, two workgroups per CU
+__global__ __launch_bounds__(kPrepU) __attribute__((amdgpu_waves_per_eu(4))) void prep_kernel(uint64_t* ts, PrepArgs a)
+{
+    prep_body<kPrepC>(ts, a);
 }
 
 // cands: see CandSrc. Writes disks[k*N + i] (the streaming scan's records).

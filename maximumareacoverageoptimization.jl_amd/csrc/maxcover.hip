@@ -706,8 +706,9 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             pr.mst_w = excl && fb_mads ? fb_mads->st : nullptr;
             pr.feas = d_feas;
             pr.lreset = L->fwcount.as<int>();
-            uint64_t* tsk = take_ts(nchain, ts_c, ts_nc);
-            hipLaunchKernelGGL(prep_kernel, dim3((unsigned)nchain), dim3(kPrepU), 0, s, tsk, pr);
+            const int nprep = nchain;
+            uint64_t* tsk = take_ts(nprep, ts_c, ts_nc);
+            hipLaunchKernelGGL(prep_kernel, dim3((unsigned)nprep), dim3(kPrepU), 0, s, tsk, pr);
             HCK(hipGetLastError());
             FwArgs fa{};
             fa.src = src;
@@ -719,7 +720,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             fa.g = ctx->grid;
             fa.dead = pr.dead8;
             fa.pd = pr.pd;
-            fa.npd = nchain;
+            fa.npd = nprep;
             fa.xy = ctx->xys.as<double2>();
             fa.w = ctx->ws.as<double>();
             fa.off = ctx->off.as<int32_t>();
