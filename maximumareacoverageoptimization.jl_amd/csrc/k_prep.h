@@ -228,7 +228,14 @@ struct PrepArgs {
     MadsState* mst_w;
     unsigned long long* feas;  // += the candidates that pass cons3 (null: not counted)
     int* lreset;               // the fused chain's hand-off list count, zeroed for this poll (null: none)
+    int xbase;                 // (prep_x_kernel) workgroup cw also takes candidate xbase + cw when < K
 };
+
+// The fused chain's prep over a matrix source (prep_x_kernel): kPrepCX candidates per workgroup
+// and floor(K / kPrepCX) workgroups, the remainder (fewer than the workgroups) one more each to
+// the first. At config 4 (K = 3073) that is 512 workgroups, two on every CU; kPrepC = 8 gives 385,
+// two on 129 CUs and one on the rest, and the doubled CUs set the launch's length.
+constexpr int kPrepCX = 6;
 
 // Packed keys. Disk i of candidate k is keyed by its offsets (dx, dy, dr) from candidate 0's
 // disk. When all three are integers that reproduce the doubles exactly (v0 + (double)d == v bit
@@ -309,7 +316,7 @@ __device__ __forceinline__ void lds_barrier()
 
 // the workgroup's LDS (one block for both source kinds: their instantiations would each
 // declare their own)
-template <int PC>
+template <int PC>   // (PC: candidate slots per workgroup)
 struct PrepLds {
     double term[PC][kPrepU + 2];   // [candidate][UAV]; rows 16-B aligned (the fold reads pairs),
                                    // 4 banks apart (+2)
@@ -319,11 +326,12 @@ struct PrepLds {
     double dred[kPrepU / kWave][4];   // per wave: its share of the displacement bound
 };
 
-template <bool kMat, int PC>
+// kX: slot PC holds the workgroup's extra candidate (prep_x_kernel; absent: >= K)
+template <bool kMat, int PC, bool kX = false>
 __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw, unsigned char* lds)
 {
-    // [candidate][UAV]; rows 16-B aligned (the fold reads pairs) and 4 banks apart (+2)
-    PrepLds<PC>& L = *reinterpret_cast<PrepLds<PC>*>(lds);
+    constexpr int NC = kX ? PC + 1 : PC;   // candidate slots
+    PrepLds<NC>& L = *reinterpret_cast<PrepLds<NC>*>(lds);
     auto& term = L.term;
     auto& wbad = L.wbad;
     auto& wbadm = L.wbadm;
@@ -335,7 +343,10 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw, unsigned c
     const int n3 = 3 * N;
     // candidate c of the workgroup: k0 + c, or (pairs) the plus / minus candidates of B's columns
     // [4cw, 4cw + 4): c < 4 -> 4cw + c, c >= 4 -> n + 4cw + c - 4
-    auto cand = [&](int c) { return a.pair ? (c < 4 ? 4 * cw + c : n3 + 4 * cw + c - 4) : k0 + c; };
+    auto cand = [&](int c) {
+        if (kX && c == PC) return a.xbase + cw;
+        return a.pair ? (c < 4 ? 4 * cw + c : n3 + 4 * cw + c - 4) : k0 + c;
+    };
     const bool obj = a.vp != nullptr;
     const PenArgs& pa = a.pa;
     MAC_PREP_STAMP(0);
@@ -355,7 +366,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw, unsigned c
         const int i = ib + u;
         const bool iv = u < nb;
         const int ii = min(i, N - 1);
-        double v[PC][3];
+        double v[NC][3];
         if (!kMat && PC == 8 && a.pair) {
             // x +- B[v][col]: each draw once for the candidate pair (PC == 8: four columns)
 #pragma unroll
@@ -371,7 +382,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw, unsigned c
             }
         } else {
 #pragma unroll
-            for (int c = 0; c < PC; ++c) {
+            for (int c = 0; c < NC; ++c) {
                 const int k = min(cand(c), K - 1);
 #pragma unroll
                 for (int q = 0; q < 3; ++q) {
@@ -396,7 +407,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw, unsigned c
             const double T3 = pen_threshold(pa, ii);
             uint32_t wdead = 0u;   // this wave's part of the failures
 #pragma unroll
-            for (int c = 0; c < PC; ++c) {
+            for (int c = 0; c < NC; ++c) {
                 const double R2 = v[c][2];
                 double t = pa.rmax ? __builtin_fabs(R2 - rm) : 0.0;
                 if (pa.prev) {
@@ -423,125 +434,32 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw, unsigned c
                 if (lane == 0) wrej[wid] = keep == 0;
             }
             MAC_PREP_STAMP(1 + 3 * (ib / kPrepU));
-        }
-        if (excl) {   // every wave's failures (the fold below needs no further barrier)
-            lds_barrier();
-            dead = 0u;
+            lds_barrier();   // every wave's terms and failures
+            if (excl) {   // (the records below leave the failures out)
+                dead = 0u;
 #pragma unroll
-            for (int w = 0; w < kPrepU / kWave; ++w) dead |= wbadm[w];
-            if (a.mst_w) {
-                bool rej = true;
+                for (int w = 0; w < kPrepU / kWave; ++w) dead |= wbadm[w];
+                if (a.mst_w) {
+                    bool rej = true;
 #pragma unroll
-                for (int w = 0; w < kPrepU / kWave; ++w) rej = rej && wrej[w] != 0;
-                if (cw == 0 && u == 0) a.mst_w->skip = rej ? 1 : 0;
-                if (rej) return;   // (uniform) the later launches see skip and return
-            }
-        }
-        if (a.pd && a.keysP && iv) {
-            // the fused chain's displacement bound (k_fiw.h sup_box): over this workgroup's live
-            // candidates (the ones the records below would take), a NaN difference counts as +inf
-#pragma unroll
-            for (int c = 0; c < PC; ++c) {
-                const double x = v[c][0], y = v[c][1], r = v[c][2];
-                if (cand(c) < K && !((dead >> c) & 1u) && r > 0.0 && __builtin_isfinite(x) &&
-                    __builtin_isfinite(y)) {
-                    double ex = __builtin_fabs(x - base[0]), ey = __builtin_fabs(y - base[1]), er = r - base[2];
-                    double el = base[2] - r;
-                    if (!(ex <= kDblMax)) ex = __builtin_inf();
-                    if (!(ey <= kDblMax)) ey = __builtin_inf();
-                    if (!(er == er)) er = __builtin_inf();
-                    if (!(el == el)) el = __builtin_inf();
-                    dmx = fmax(dmx, ex);
-                    dmy = fmax(dmy, ey);
-                    dmr = fmax(dmr, er);
-                    dml = fmax(dml, el);
+                    for (int w = 0; w < kPrepU / kWave; ++w) rej = rej && wrej[w] != 0;
+                    if (cw == 0 && u == 0) a.mst_w->skip = rej ? 1 : 0;
+                    if (rej) return;   // (uniform) the later launches see skip and return
                 }
             }
-        }
-        if (a.pd && ib + kPrepU >= N) {   // (uniform) this wave's share of the bound, into LDS now:
-            // its registers are free before the fold (thread 0 combines the waves at the end)
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) {
-                dmx = fmax(dmx, __shfl_xor(dmx, o, kWave));
-                dmy = fmax(dmy, __shfl_xor(dmy, o, kWave));
-                dmr = fmax(dmr, __shfl_xor(dmr, o, kWave));
-                dml = fmax(dml, __shfl_xor(dml, o, kWave));
-            }
-            if (lane == 0) {
-                dred[wid][0] = dmx;
-                dred[wid][1] = dmy;
-                dred[wid][2] = dmr;
-                dred[wid][3] = dml;
-            }
-        }
-        if ((a.prec || a.keysP) && iv) {
-            double xa = __builtin_inf(), xb = -__builtin_inf(), ya = __builtin_inf(), yb = -__builtin_inf();
-            double xm = 0.0, ym = 0.0, est = 0.0;
-            bool any = false;
-#pragma unroll
-            for (int c = 0; c < PC; ++c) {
-                if (!a.prec) break;   // (the fused chain: keys only, no region records)
-                const double x = v[c][0], y = v[c][1], r = v[c][2];
-                // span_of's cases: r <= 0 or NaN, or a non-finite centre, covers nothing
-                if (cand(c) < K && !((dead >> c) & 1u) && r > 0.0 && __builtin_isfinite(x) &&
-                    __builtin_isfinite(y)) {
-                    any = true;
-                    xa = fmin(xa, x - r);
-                    xb = fmax(xb, x + r);
-                    ya = fmin(ya, y - r);
-                    yb = fmax(yb, y + r);
-                    xm = fmax(xm, __builtin_fabs(x) + r);
-                    ym = fmax(ym, __builtin_fabs(y) + r);
-                    const double e = 2.0 * r * a.g.invS + 1.0;
-                    est += e * e;
-                }
-            }
-            bool kb = false;   // a key of this disk is inexact (k_index.h "Keys")
-            if (a.keysP) {     // the keys: packed words (two 16-B stores), escapes in fp32
-                uint32_t pk[PC];
-#pragma unroll
-                for (int c = 0; c < PC; ++c) {
-                    int dx = 0, dy = 0, dr = 0;
-                    const bool packs = key_int(v[c][0], base[0], 1023.0, dx) &&
-                                       key_int(v[c][1], base[1], 1023.0, dy) &&
-                                       key_int(v[c][2], base[2], 511.0, dr);
-                    pk[c] = packs ? key_pack(dx, dy, dr) : kKeyEsc;
-                    if (!packs) {
-#pragma unroll
-                        for (int q = 0; q < 3; ++q) {
-                            const float f = (float)(v[c][q] - base[q]);
-                            kb |= !((dead >> c) & 1u) && __builtin_bit_cast(uint64_t, base[q] + (double)f) != __builtin_bit_cast(uint64_t, v[c][q]);
-                            a.keysT[(int64_t)(q * N + i) * a.ldk + cand(c)] = f;
-                        }
-                    }
-                }
-#pragma unroll
-                for (int h = 0; h < PC / 4; ++h)   // candidates cand(4h) .. cand(4h) + 3
-                    *reinterpret_cast<uint4*>(a.keysP + (int64_t)i * a.ldk + cand(4 * h)) =
-                        make_uint4(pk[4 * h], pk[4 * h + 1], pk[4 * h + 2], pk[4 * h + 3]);
-            }
-            if (a.prec) {
-                int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
-                any = any && partial_range(xa, xb, xm, a.g.gx0, a.g.invS, a.g.nTx, x0, x1) &&
-                      partial_range(ya, yb, ym, a.g.gy0, a.g.invS, a.g.nTy, y0, y1);
-                a.prec[(int64_t)cw * N + i] =
-                    make_int4((int)range_pack(any, x0, x1, range_shift(a.g.nTx)),
-                              (int)range_pack(any, y0, y1, range_shift(a.g.nTy)),
-                              __builtin_bit_cast(int, (float)est), kb ? 1 : 0);
-            }
-        }
-        MAC_PREP_STAMP(2 + 3 * (ib / kPrepU));
-        if (obj) {
-            // the chains, after every wave's other work (the adds are the critical path: the
-            // folding wave then has its SIMD to itself), sequential in UAV order
-            if (!excl) lds_barrier();   // (excl: passed above)
-            if (u < PC) {
+            if (u < NC) {
+                // the chain, sequential in UAV order: lane c of wave 0 folds candidate slot c
+                // while the other waves go on to the bound and the keys below (wave 0 does its own
+                // share of them after the fold, which sets the launch's length)
 #pragma unroll
                 for (int w = 0; w < kPrepU / kWave; ++w) bad |= wbad[w][u] != 0;
                 if (!bad) {   // (a cons3 failure's vp is +inf: no chain to fold)
+                    // the chain's wave first at issue: the dependent adds are the launch's
+                    // critical path, the other waves on its SIMD have slack
+                    __builtin_amdgcn_s_setprio(3);
                     // batches of 2 kB terms (pair reads), the next batch's reads in flight while
                     // this batch's adds run: the dependent adds, not the LDS latency, set the pace
-                    constexpr int kB = 6;
+                    constexpr int kB = kX ? 4 : 3;   // (the most that fits 128 VGPRs beside v)
                     const double2* row2 = reinterpret_cast<const double2*>(&term[u][0]);
                     const int nfull = nb / (2 * kB);
                     // ping-pong buffers (no register moves between batches); the reads past the
@@ -573,18 +491,122 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw, unsigned c
                         }
                     }
                     for (int q = nfull * 2 * kB; q < nb; ++q) acc += term[u][q];
+                    __builtin_amdgcn_s_setprio(0);
                 }
+            }
+            MAC_PREP_STAMP(2 + 3 * (ib / kPrepU));
+        }
+        if (a.pd && a.keysP && iv) {
+            // the fused chain's displacement bound (k_fiw.h sup_box): over this workgroup's live
+            // candidates (the ones the records below would take), a NaN difference counts as +inf
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const double x = v[c][0], y = v[c][1], r = v[c][2];
+                if (cand(c) < K && !((dead >> c) & 1u) && r > 0.0 && __builtin_isfinite(x) &&
+                    __builtin_isfinite(y)) {
+                    double ex = __builtin_fabs(x - base[0]), ey = __builtin_fabs(y - base[1]), er = r - base[2];
+                    double el = base[2] - r;
+                    if (!(ex <= kDblMax)) ex = __builtin_inf();
+                    if (!(ey <= kDblMax)) ey = __builtin_inf();
+                    if (!(er == er)) er = __builtin_inf();
+                    if (!(el == el)) el = __builtin_inf();
+                    dmx = fmax(dmx, ex);
+                    dmy = fmax(dmy, ey);
+                    dmr = fmax(dmr, er);
+                    dml = fmax(dml, el);
+                }
+            }
+        }
+        if (a.pd && ib + kPrepU >= N) {   // (uniform) this wave's share of the bound, into LDS
+            // (thread 0 combines the waves at the end)
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+                dmx = fmax(dmx, __shfl_xor(dmx, o, kWave));
+                dmy = fmax(dmy, __shfl_xor(dmy, o, kWave));
+                dmr = fmax(dmr, __shfl_xor(dmr, o, kWave));
+                dml = fmax(dml, __shfl_xor(dml, o, kWave));
+            }
+            if (lane == 0) {
+                dred[wid][0] = dmx;
+                dred[wid][1] = dmy;
+                dred[wid][2] = dmr;
+                dred[wid][3] = dml;
+            }
+        }
+        if ((a.prec || a.keysP) && iv) {
+            double xa = __builtin_inf(), xb = -__builtin_inf(), ya = __builtin_inf(), yb = -__builtin_inf();
+            double xm = 0.0, ym = 0.0, est = 0.0;
+            bool any = false;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                if (!a.prec) break;   // (the fused chain: keys only, no region records)
+                const double x = v[c][0], y = v[c][1], r = v[c][2];
+                // span_of's cases: r <= 0 or NaN, or a non-finite centre, covers nothing
+                if (cand(c) < K && !((dead >> c) & 1u) && r > 0.0 && __builtin_isfinite(x) &&
+                    __builtin_isfinite(y)) {
+                    any = true;
+                    xa = fmin(xa, x - r);
+                    xb = fmax(xb, x + r);
+                    ya = fmin(ya, y - r);
+                    yb = fmax(yb, y + r);
+                    xm = fmax(xm, __builtin_fabs(x) + r);
+                    ym = fmax(ym, __builtin_fabs(y) + r);
+                    const double e = 2.0 * r * a.g.invS + 1.0;
+                    est += e * e;
+                }
+            }
+            bool kb = false;   // a key of this disk is inexact (k_index.h "Keys")
+            if (a.keysP) {     // the keys: packed words (two 16-B stores), escapes in fp32
+                uint32_t pk[NC];
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    int dx = 0, dy = 0, dr = 0;
+                    const bool packs = key_int(v[c][0], base[0], 1023.0, dx) &&
+                                       key_int(v[c][1], base[1], 1023.0, dy) &&
+                                       key_int(v[c][2], base[2], 511.0, dr);
+                    pk[c] = packs ? key_pack(dx, dy, dr) : kKeyEsc;
+                    if (!packs) {
+#pragma unroll
+                        for (int q = 0; q < 3; ++q) {
+                            const float f = (float)(v[c][q] - base[q]);
+                            kb |= !((dead >> c) & 1u) && __builtin_bit_cast(uint64_t, base[q] + (double)f) != __builtin_bit_cast(uint64_t, v[c][q]);
+                            a.keysT[(int64_t)(q * N + i) * a.ldk + cand(c)] = f;
+                        }
+                    }
+                }
+                uint32_t* const krow = a.keysP + (int64_t)i * a.ldk;
+                if constexpr (kX) {   // (k0 = PC * cw: even) 8-B stores, the extra word alone
+                    static_assert(PC % 2 == 0, "kX: an even candidate count");
+#pragma unroll
+                    for (int h = 0; h < PC / 2; ++h)
+                        *reinterpret_cast<uint2*>(krow + k0 + 2 * h) = make_uint2(pk[2 * h], pk[2 * h + 1]);
+                    if (cand(PC) < K) krow[cand(PC)] = pk[PC];
+                } else {
+#pragma unroll
+                    for (int h = 0; h < PC / 4; ++h)   // candidates cand(4h) .. cand(4h) + 3
+                        *reinterpret_cast<uint4*>(krow + cand(4 * h)) =
+                            make_uint4(pk[4 * h], pk[4 * h + 1], pk[4 * h + 2], pk[4 * h + 3]);
+                }
+            }
+            if (a.prec) {
+                int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
+                any = any && partial_range(xa, xb, xm, a.g.gx0, a.g.invS, a.g.nTx, x0, x1) &&
+                      partial_range(ya, yb, ym, a.g.gy0, a.g.invS, a.g.nTy, y0, y1);
+                a.prec[(int64_t)cw * N + i] =
+                    make_int4((int)range_pack(any, x0, x1, range_shift(a.g.nTx)),
+                              (int)range_pack(any, y0, y1, range_shift(a.g.nTy)),
+                              __builtin_bit_cast(int, (float)est), kb ? 1 : 0);
             }
         }
         MAC_PREP_STAMP(3 + 3 * (ib / kPrepU));
         if (obj && ib + kPrepU < N) lds_barrier();   // the fold has read the terms
     }
-    if (obj && u < PC && cand(u) < K) {
+    if (obj && u < NC && cand(u) < K) {
         a.vp[cand(u)] = bad ? __builtin_inf() : acc * a.penalty;
         if (a.dead8) a.dead8[cand(u)] = excl && bad ? 1 : 0;
     }
     if (obj && a.feas && wid == 0) {   // the evaluations: candidates that pass cons3
-        const uint64_t ok = __ballot(u < PC && cand(u) < K && !bad);
+        const uint64_t ok = __ballot(u < NC && cand(u) < K && !bad);
         if (lane == 0 && ok) atomicAdd(a.feas, (unsigned long long)__popcll(ok));
     }
     if (a.pd) {   // the workgroup's displacement bound: the waves' shares in order
@@ -602,7 +624,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw, unsigned c
     }
 }
 
-template <int PC>
+template <int PC, bool kX = false>
 __device__ __forceinline__ void prep_body(uint64_t* ts, PrepArgs& a)
 {
     ts_begin(ts);   // profiling only (the chain's first launch: k_common.h)
@@ -615,8 +637,9 @@ __device__ __forceinline__ void prep_body(uint64_t* ts, PrepArgs& a)
     // candidate groups — which fill the same lines of keysP and of the records — go to one XCD
     const int per = (int)((gridDim.x + 7) / 8), b = (int)blockIdx.x;
     const int cw = (int)(gridDim.x % 8) == 0 ? (b % 8) * per + b / 8 : b;
-    __shared__ __attribute__((aligned(16))) unsigned char lds[sizeof(PrepLds<PC>)];
-    if (a.src.cands) prep_block<true, PC>(a, cw, lds);
+    __shared__ __attribute__((aligned(16))) unsigned char lds[sizeof(PrepLds<kX ? PC + 1 : PC>)];
+    if constexpr (kX) prep_block<true, PC, true>(a, cw, lds);   // (matrix sources only)
+    else if (a.src.cands) prep_block<true, PC>(a, cw, lds);
     else prep_block<false, PC>(a, cw, lds);
     ts_end(ts);
 }
@@ -625,6 +648,12 @@ __device__ __forceinline__ void prep_body(uint64_t* ts, PrepArgs& a)
 __global__ __launch_bounds__(kPrepU) __attribute__((amdgpu_waves_per_eu(4))) void prep_kernel(uint64_t* ts, PrepArgs a)
 {
     prep_body<kPrepC>(ts, a);
+}
+
+// the fused chain's prep over a matrix source: kPrepCX (+1) candidates per workgroup (xbase)
+__global__ __launch_bounds__(kPrepU) __attribute__((amdgpu_waves_per_eu(4))) void prep_x_kernel(uint64_t* ts, PrepArgs a)
+{
+    prep_body<kPrepCX, true>(ts, a);
 }
 
 // cands: see CandSrc. Writes disks[k*N + i] (the streaming scan's records).

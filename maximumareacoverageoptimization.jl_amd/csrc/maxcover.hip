@@ -677,7 +677,11 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             const int ldk = keys_ld(K);
             counts = ctx->w_uniform ? 1 : 0;
             L->keysT.reserve(sizeof(float) * (size_t)4 * N * ldk);
-            L->pd.reserve(sizeof(double4) * (size_t)nchain);
+            // a matrix source: kPrepCX (+1) candidates per workgroup (k_prep.h prep_x_kernel)
+            const int gx = K / kPrepCX;
+            const bool xk = src.cands && !pair && gx >= 1 && K - gx * kPrepCX <= gx;
+            const int nprep = xk ? gx : nchain;
+            L->pd.reserve(sizeof(double4) * (size_t)nprep);
             L->frows.reserve((counts ? sizeof(unsigned) : sizeof(double)) * (size_t)N * ldk);
             if (L->fwhint.grow(sizeof(int) * kFwHints)) HCK(hipMemsetAsync(L->fwhint.p, 0, L->fwhint.cap, s));
             // cons3 failures are left out of the walk when only objectives are asked for
@@ -694,7 +698,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             pr.pa = pa;
             pr.penalty = penalty;
             pr.vp = d_vp;
-            pr.nchain = nchain;
+            pr.nchain = nprep;
+            pr.xbase = gx * kPrepCX;
             pr.skip_failed = d_area ? 0 : 1;
             pr.pair = pair ? 1 : 0;
             pr.g = ctx->grid;
@@ -706,9 +711,9 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             pr.mst_w = excl && fb_mads ? fb_mads->st : nullptr;
             pr.feas = d_feas;
             pr.lreset = L->fwcount.as<int>();
-            const int nprep = nchain;
             uint64_t* tsk = take_ts(nprep, ts_c, ts_nc);
-            hipLaunchKernelGGL(prep_kernel, dim3((unsigned)nprep), dim3(kPrepU), 0, s, tsk, pr);
+            if (xk) hipLaunchKernelGGL(prep_x_kernel, dim3((unsigned)nprep), dim3(kPrepU), 0, s, tsk, pr);
+            else hipLaunchKernelGGL(prep_kernel, dim3((unsigned)nprep), dim3(kPrepU), 0, s, tsk, pr);
             HCK(hipGetLastError());
             FwArgs fa{};
             fa.src = src;

@@ -21,12 +21,14 @@ for rep in range(3):
     ctx.profile_read(reset=True)
     ctx.poll_best(C, rmax)
     K, n3 = C.shape[0], C.shape[1]
-    nchain = (K + 7) // 8
-    nwg = nchain
-    buf = (ctypes.c_uint64 * (2 * nwg))()
+    cap = 2 * K
+    buf = (ctypes.c_uint64 * cap)()
     used = ctypes.c_int64()
-    assert L.mac_diag_stamps(ctx._h, buf, 2 * nwg, ctypes.byref(used)) == 0
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(nwg, 2).astype(np.int64)
+    assert L.mac_diag_stamps(ctx._h, buf, cap, ctypes.byref(used)) == 0
+    # the prep launch's workgroups: prep_x_kernel (K // 6 of them) for a matrix source
+    nchain = K // 6 if K // 6 >= K - 6 * (K // 6) else (K + 7) // 8
+    nwg = nchain
+    a = np.frombuffer(buf, dtype=np.uint64)[:2 * nwg].reshape(nwg, 2).astype(np.int64)
     base = a[:, 0].min()
     s = (a[:, 0] - base) / 100.0
     e = (a[:, 1] - base) / 100.0
@@ -46,5 +48,5 @@ if hasattr(L, "mac_diag_prep_read"):
     ph = np.diff(p[:, :cols], axis=1) / 100.0
     out["chain_phases_us_median"] = [float(v) for v in np.median(ph, axis=0)]
     out["chain_phases_us_max"] = [float(v) for v in ph.max(axis=0)]
-    out["chain_phase_names"] = "per block: loads+terms, regions+keys, fold"
+    out["chain_phase_names"] = "per block (thread 0 = wave 0): loads+terms+cons3, fold, bound+keys+regions"
 print(json.dumps(out, indent=1))
