@@ -853,7 +853,7 @@ def main():
                 "dominant_basis": ("in-kernel stamps: first workgroup start to last workgroup end; "
                                    "rocprof's dispatch-to-completion durations add the dispatch "
                                    "ramp and the end-of-kernel release, which weigh most on the "
-                                   "prep launch (385 x 512-thread workgroups, 10 MB of stores), "
+                                   "prep launch (512 x 512-thread workgroups, 10 MB of stores), "
                                    "and can rank it first (profiles/*rocprof*config4.csv)"),
                 "avg_launch_ms": (kernels[dominant]["avg_us"] * 1e-3 if dominant else avg_launch_ms),
                 "kernels": kernels,

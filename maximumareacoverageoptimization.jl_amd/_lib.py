@@ -42,7 +42,8 @@ MAC_STORE_F32 = 1
 # mac_profile_kernels launch roles (include/maxcover.h MAC_PROF_ROLES). Role 5 is one stamp slot
 # for the crowded-poll shared-entry pass: the union pass (shared_or_kernel) on equal weights — every
 # reference data set — else the bit-word kernel (shared_bits_kernel)
-PROF_ROLES = ("prep_kernel", "disk_index_kernel", "walk_setup_kernel", "coverage_tiled_poll_kernel",
+PROF_ROLES = ("prep_kernel",  # (role 0: the prep launch, prep_kernel or prep_x_kernel)
+              "disk_index_kernel", "walk_setup_kernel", "coverage_tiled_poll_kernel",
               "coverage_poll_kernel", "shared_or_kernel", "finalize_kernel", "fiw_kernel",
               "fin2_kernel")
 
