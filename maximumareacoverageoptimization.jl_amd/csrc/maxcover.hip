@@ -184,6 +184,7 @@ struct mac_ctx {
     int cl_taken = 0;                // requests in batches in flight (under cl_mu)
     int64_t cl_batches = 0, cl_reqs = 0;   // (MAXCOVER_CL_STATS=1: printed at destroy)
     double cl_batch_s = 0.0;               // time inside the batches' evaluations
+    double cl_phase_s[4] = {0, 0, 0, 0};   // ... split: staging, copy + launch enqueued, results
     std::vector<Lane*> lanes_free;
     std::vector<Lane*> lanes_all;
     hipStream_t setup_stream = nullptr;
@@ -1450,6 +1451,10 @@ void mac_ctx_destroy(mac_ctx* ctx)
         std::fprintf(stderr, "maxcover: closure batches %lld, requests %lld (%.2f per batch), %.1f us per batch\n",
                      (long long)ctx->cl_batches, (long long)ctx->cl_reqs,
                      (double)ctx->cl_reqs / (double)ctx->cl_batches, ctx->cl_batch_s / ctx->cl_batches * 1e6);
+    if (const char* e = std::getenv("MAXCOVER_CL_STATS"); e && *e == '1' && ctx->cl_batches)
+        std::fprintf(stderr, "maxcover: closure batch split (us): staging %.1f, copy+launch %.1f, results %.1f\n",
+                     ctx->cl_phase_s[0] / ctx->cl_batches * 1e6, ctx->cl_phase_s[1] / ctx->cl_batches * 1e6,
+                     ctx->cl_phase_s[2] / ctx->cl_batches * 1e6);
     (void)hipSetDevice(ctx->device);
     if (ctx->doorbell) {   // every armed poll released first (else the synchronisation would wait)
         __atomic_store_n(ctx->doorbell, ~(uint64_t)0 >> 1, __ATOMIC_RELEASE);
@@ -2508,8 +2513,10 @@ static void closure_batch(mac_ctx* ctx, int64_t three_n, const double* const* ca
     Lane* L = lg.lane;
     hipStream_t s = L->stream;
     const size_t one = sizeof(double) * (size_t)three_n;
+    const auto t0 = std::chrono::steady_clock::now();
     L->h_io.reserve(std::max<size_t>(one * B, 64));
     for (int b = 0; b < B; ++b) std::memcpy((char*)L->h_io.p + one * b, cands[b], one);
+    const auto t1 = std::chrono::steady_clock::now();
     L->cands.reserve(one * B);
     L->area.reserve(sizeof(double) * B);
     L->cpart.reserve(sizeof(unsigned long long) * (size_t)N * B);
@@ -2547,6 +2554,7 @@ static void closure_batch(mac_ctx* ctx, int64_t three_n, const double* const* ca
         std::lock_guard<std::mutex> lk(ctx->mu);
         ctx->prof.push_back({ts_a, (int64_t)nwg * B, -1, 0, (int64_t)B, nullptr, MAC_ALGO_TILED});
     }
+    const auto t2 = std::chrono::steady_clock::now();
     bool synced = false;
     for (int b = 0; b < B; ++b) {
         const uint64_t* slot = (const uint64_t*)L->h_cl.p + 4 * b;
@@ -2564,6 +2572,11 @@ static void closure_batch(mac_ctx* ctx, int64_t three_n, const double* const* ca
             HCK(hipMemcpy(&a, L->area.as<double>() + b, sizeof(double), hipMemcpyDeviceToHost));
         *outs[b] = a;
     }
+    const auto t3 = std::chrono::steady_clock::now();
+    std::lock_guard<std::mutex> lk(ctx->cl_mu);
+    ctx->cl_phase_s[0] += std::chrono::duration<double>(t1 - t0).count();
+    ctx->cl_phase_s[1] += std::chrono::duration<double>(t2 - t1).count();
+    ctx->cl_phase_s[2] += std::chrono::duration<double>(t3 - t2).count();
 }
 
 // Concurrent callers (DirectSearch's threaded poll, src/TDM_STATIC_opt.jl:129: one objective call
@@ -2574,7 +2587,10 @@ static void closure_batch(mac_ctx* ctx, int64_t three_n, const double* const* ca
 // condition-variable wake-up chain) and lead a later batch if theirs is still queued when a slot
 // frees. A lone caller runs its own request at once. Results per call are exactly the
 // single-candidate kernel's (the batch dimension only selects the candidate).
-static constexpr int kClLeaders = 2;   // batches in flight at once (two lanes, two streams)
+#ifndef MAC_CL_LEADERS
+#define MAC_CL_LEADERS 2
+#endif
+static constexpr int kClLeaders = MAC_CL_LEADERS;   // batches in flight at once (a lane, a stream each)
 static constexpr int kClSpin = 64;        // pause iterations before a waiter sleeps on its futex
 static constexpr int kClGather = 0;        // pauses a would-be leader waits for every caller to queue (0: none)
 
