@@ -302,10 +302,11 @@ __device__ __forceinline__ void range_unpack(uint32_t lo16, uint32_t hi16, int s
 
 #ifdef MAC_DIAG
 __device__ uint64_t g_diag_prep[64 * 16];   // diagnostic build only: workgroup phase stamps
-#define MAC_PREP_STAMP(q) if (threadIdx.x == 0 && cw < 64 && (q) < 16) g_diag_prep[16 * cw + (q)] = __builtin_amdgcn_s_memrealtime()
+#define MAC_PREP_STAMP_T(q, t) if (threadIdx.x == (t) && cw < 64 && (q) < 16) g_diag_prep[16 * cw + (q)] = __builtin_amdgcn_s_memrealtime()
 #else
-#define MAC_PREP_STAMP(q)
+#define MAC_PREP_STAMP_T(q, t)
 #endif
+#define MAC_PREP_STAMP(q) MAC_PREP_STAMP_T(q, 0)
 
 // A workgroup barrier for LDS only: global stores still in flight are not waited for
 // (__syncthreads would drain them first)
@@ -326,11 +327,10 @@ struct PrepLds {
     double dred[kPrepU / kWave][4];   // per wave: its share of the displacement bound
 };
 
-// kX: slot PC holds the workgroup's extra candidate (prep_x_kernel; absent: >= K)
-template <bool kMat, int PC, bool kX = false>
+template <bool kMat, int PC>
 __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw, unsigned char* lds)
 {
-    constexpr int NC = kX ? PC + 1 : PC;   // candidate slots
+    constexpr int NC = PC;   // candidate slots
     PrepLds<NC>& L = *reinterpret_cast<PrepLds<NC>*>(lds);
     auto& term = L.term;
     auto& wbad = L.wbad;
@@ -343,10 +343,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw, unsigned c
     const int n3 = 3 * N;
     // candidate c of the workgroup: k0 + c, or (pairs) the plus / minus candidates of B's columns
     // [4cw, 4cw + 4): c < 4 -> 4cw + c, c >= 4 -> n + 4cw + c - 4
-    auto cand = [&](int c) {
-        if (kX && c == PC) return a.xbase + cw;
-        return a.pair ? (c < 4 ? 4 * cw + c : n3 + 4 * cw + c - 4) : k0 + c;
-    };
+    auto cand = [&](int c) { return a.pair ? (c < 4 ? 4 * cw + c : n3 + 4 * cw + c - 4) : k0 + c; };
     const bool obj = a.vp != nullptr;
     const PenArgs& pa = a.pa;
     MAC_PREP_STAMP(0);
@@ -459,7 +456,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw, unsigned c
                     __builtin_amdgcn_s_setprio(3);
                     // batches of 2 kB terms (pair reads), the next batch's reads in flight while
                     // this batch's adds run: the dependent adds, not the LDS latency, set the pace
-                    constexpr int kB = kX ? 4 : 3;   // (the most that fits 128 VGPRs beside v)
+                    constexpr int kB = 3;   // (the most that fits 128 VGPRs beside v)
                     const double2* row2 = reinterpret_cast<const double2*>(&term[u][0]);
                     const int nfull = nb / (2 * kB);
                     // ping-pong buffers (no register moves between batches); the reads past the
@@ -575,18 +572,10 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw, unsigned c
                     }
                 }
                 uint32_t* const krow = a.keysP + (int64_t)i * a.ldk;
-                if constexpr (kX) {   // (k0 = PC * cw: even) 8-B stores, the extra word alone
-                    static_assert(PC % 2 == 0, "kX: an even candidate count");
 #pragma unroll
-                    for (int h = 0; h < PC / 2; ++h)
-                        *reinterpret_cast<uint2*>(krow + k0 + 2 * h) = make_uint2(pk[2 * h], pk[2 * h + 1]);
-                    if (cand(PC) < K) krow[cand(PC)] = pk[PC];
-                } else {
-#pragma unroll
-                    for (int h = 0; h < PC / 4; ++h)   // candidates cand(4h) .. cand(4h) + 3
-                        *reinterpret_cast<uint4*>(krow + cand(4 * h)) =
-                            make_uint4(pk[4 * h], pk[4 * h + 1], pk[4 * h + 2], pk[4 * h + 3]);
-                }
+                for (int h = 0; h < PC / 4; ++h)   // candidates cand(4h) .. cand(4h) + 3
+                    *reinterpret_cast<uint4*>(krow + cand(4 * h)) =
+                        make_uint4(pk[4 * h], pk[4 * h + 1], pk[4 * h + 2], pk[4 * h + 3]);
             }
             if (a.prec) {
                 int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
@@ -624,6 +613,222 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw, unsigned c
     }
 }
 
+// The fused chain's prep over a matrix source with one block of UAVs (N <= kPrepU; k_fiw.h):
+// kPrepCX candidates per workgroup plus, for the first K - xbase workgroups, candidate xbase + cw
+// (slot kPrepCX). Waves 0..7 hold a UAV per thread: loads, penalty terms and cons3 ballots, one
+// barrier, then per candidate slot the packed key and the share of the displacement bound, while
+// a ninth wave that holds no UAV folds the chains (lane c: slot c's, sequential in UAV order). The
+// fold and the keys are exclusive branches, so the candidate values are dead on the folding
+// wave's path (80 VGPRs: two workgroups, 18 waves, fit a CU). Results are prep_block's bit for bit
+// (the same terms in the same order, the same keys and bound).
+__device__ __forceinline__ void prep_block_x(const PrepArgs& a, int cw, unsigned char* lds)
+{
+    constexpr int PC = kPrepCX, NC = kPrepCX + 1, NW = kPrepU / kWave;
+    PrepLds<NC>& L = *reinterpret_cast<PrepLds<NC>*>(lds);
+    auto& term = L.term;
+    auto& wbad = L.wbad;
+    auto& wbadm = L.wbadm;
+    auto& wrej = L.wrej;
+    auto& dred = L.dred;
+    const int N = a.N, K = a.K;
+    const int u = threadIdx.x, lane = u & (kWave - 1), wid = u / kWave;
+    const bool fw = wid == NW;   // the folding wave
+    const int k0 = cw * PC;
+    auto cand = [&](int c) { return c < PC ? k0 + c : a.xbase + cw; };   // (>= K: absent)
+    const bool obj = a.vp != nullptr;
+    const PenArgs& pa = a.pa;
+    const bool excl = obj && pa.prev && a.skip_failed;
+    const bool iv = !fw && u < N;
+    const int ii = min(u, N - 1);
+    MAC_PREP_STAMP(0);
+    double v[NC][3];
+    double base[3] = {0.0, 0.0, 0.0};   // candidate 0's values: the keys' base
+    if (!fw) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int k = min(cand(c), K - 1);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) v[c][q] = a.src.cands[(int64_t)k * a.src.ldc + q * N + ii];
+        }
+#pragma unroll
+        for (int q = 0; q < 3; ++q) base[q] = a.src.cands[q * N + ii];
+        if (obj) {
+            // pen_term (above), the same operations in the same order
+            const double x1 = pa.prev ? pa.prev[ii] : 0.0, y1 = pa.prev ? pa.prev[N + ii] : 0.0;
+            const double z1 = pa.prev ? pa.prev[2 * N + ii] / pa.tan_half_fov : 0.0;
+            const double rm = pa.rmax ? pa.rmax[ii] : 0.0;
+            const double T3 = pen_threshold(pa, ii);
+            uint32_t wdead = 0u;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const double R2 = v[c][2];
+                double t = pa.rmax ? __builtin_fabs(R2 - rm) : 0.0;
+                if (pa.prev) {
+                    const double z2 = R2 / pa.tan_half_fov;
+                    const double ddx = x1 - v[c][0], ddy = y1 - v[c][1], ddz = z1 - z2;
+                    const double sq = ddx * ddx + ddy * ddy + ddz * ddz;
+                    if (sq > T3) t = -1.0;
+                }
+                term[c][u] = t;
+                const uint64_t neg = __ballot(iv && t < 0.0);
+                if (lane == 0) wbad[wid][c] = neg != 0;
+                wdead |= (neg != 0 ? 1u : 0u) << c;
+            }
+            if (lane == 0) wbadm[wid] = wdead;
+            if (a.mst_w) {   // the whole-poll rejection (uniform)
+                bool rej = true;
+                if (iv) {
+                    const double bb = (double)a.src.b;
+                    rej = diag_rejects(a.src.xinc[ii], bb, x1, 0, pa.tan_half_fov, T3) &&
+                          diag_rejects(a.src.xinc[N + ii], bb, y1, 1, pa.tan_half_fov, T3) &&
+                          diag_rejects(a.src.xinc[2 * N + ii], bb, pa.prev[2 * N + ii], 2, pa.tan_half_fov, T3);
+                }
+                const uint64_t keep = __ballot(!rej);
+                if (lane == 0) wrej[wid] = keep == 0;
+            }
+        }
+    }
+    MAC_PREP_STAMP(1);
+    uint32_t dead = 0u;
+    if (obj) {
+        lds_barrier();   // every wave's terms and failures
+        if (excl) {
+#pragma unroll
+            for (int w = 0; w < NW; ++w) dead |= wbadm[w];
+            if (a.mst_w) {
+                bool rej = true;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) rej = rej && wrej[w] != 0;
+                if (cw == 0 && u == 0) a.mst_w->skip = rej ? 1 : 0;
+                if (rej) return;   // (uniform) the later launches see skip and return
+            }
+        }
+    }
+    MAC_PREP_STAMP(2);
+    if (fw) {   // the chains
+        bool bad = false;
+        double acc = 0.0;
+        if (obj && lane < NC) {
+#pragma unroll
+            for (int w = 0; w < NW; ++w) bad |= wbad[w][lane] != 0;
+            if (!bad) {   // (a cons3 failure's vp is +inf: no chain to fold)
+                // batches of 2 kB terms (pair reads), the next batch's reads in flight while this
+                // batch's adds run; ping-pong buffers, the reads past the last batch re-read it
+                // (clamped) and are never added
+                constexpr int kB = 6;
+                const double2* row2 = reinterpret_cast<const double2*>(&term[lane][0]);
+                const int nfull = N / (2 * kB);
+                __builtin_amdgcn_s_setprio(3);   // the launch's critical path: first at issue
+                auto batch = [&](double2 (&buf)[kB], int bt) {
+                    const int at = (bt < nfull ? bt : nfull - 1) * kB;
+#pragma unroll
+                    for (int j = 0; j < kB; ++j) buf[j] = row2[at + j];
+                };
+                auto add = [&](const double2 (&buf)[kB]) {
+#pragma unroll
+                    for (int j = 0; j < kB; ++j) {
+                        acc += buf[j].x;
+                        acc += buf[j].y;
+                    }
+                };
+                if (nfull > 0) {
+                    double2 A[kB], B[kB];
+                    batch(A, 0);
+#pragma unroll 1
+                    for (int bt = 0; bt < nfull; bt += 2) {
+                        batch(B, bt + 1);
+                        __builtin_amdgcn_sched_barrier(0);   // (the reads stay ahead of the adds)
+                        add(A);
+                        if (bt + 1 >= nfull) break;
+                        batch(A, bt + 2);
+                        __builtin_amdgcn_sched_barrier(0);
+                        add(B);
+                    }
+                }
+                for (int q = nfull * 2 * kB; q < N; ++q) acc += term[lane][q];
+                __builtin_amdgcn_s_setprio(0);
+            }
+            MAC_PREP_STAMP_T(3, kPrepU);
+            if (cand(lane) < K) {
+                a.vp[cand(lane)] = bad ? __builtin_inf() : acc * a.penalty;
+                if (a.dead8) a.dead8[cand(lane)] = excl && bad ? 1 : 0;
+            }
+        }
+        if (obj && a.feas) {   // the evaluations: candidates that pass cons3
+            const uint64_t ok = __ballot(lane < NC && cand(lane) < K && !bad);
+            if (lane == 0 && ok) atomicAdd(a.feas, (unsigned long long)__popcll(ok));
+        }
+    } else {
+        // per candidate slot its key word (escapes: the fp32 offsets, k_index.h "Keys") and its
+        // share of the displacement bound (k_fiw.h sup_box: live candidates only — r > 0, a finite
+        // centre, not a cons3 failure; a NaN difference counts as +inf)
+        double dmx = -__builtin_inf(), dmy = -__builtin_inf(), dmr = -__builtin_inf(), dml = -__builtin_inf();
+        uint32_t pk[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const double x = v[c][0], y = v[c][1], r = v[c][2];
+            int dx = 0, dy = 0, dr = 0;
+            const bool packs = key_int(x, base[0], 1023.0, dx) && key_int(y, base[1], 1023.0, dy) &&
+                               key_int(r, base[2], 511.0, dr);
+            pk[c] = packs ? key_pack(dx, dy, dr) : kKeyEsc;
+            if (!packs && iv && cand(c) < K) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    a.keysT[(int64_t)(q * N + u) * a.ldk + cand(c)] = (float)(v[c][q] - base[q]);
+            }
+            if (a.pd && iv && cand(c) < K && !((dead >> c) & 1u) && r > 0.0 && __builtin_isfinite(x) &&
+                __builtin_isfinite(y)) {
+                double ex = __builtin_fabs(x - base[0]), ey = __builtin_fabs(y - base[1]), er = r - base[2];
+                double el = base[2] - r;
+                if (!(ex <= kDblMax)) ex = __builtin_inf();
+                if (!(ey <= kDblMax)) ey = __builtin_inf();
+                if (!(er == er)) er = __builtin_inf();
+                if (!(el == el)) el = __builtin_inf();
+                dmx = fmax(dmx, ex);
+                dmy = fmax(dmy, ey);
+                dmr = fmax(dmr, er);
+                dml = fmax(dml, el);
+            }
+        }
+        if (iv) {   // (k0 = PC * cw: even) 8-B stores, the extra word alone
+            static_assert(PC % 2 == 0, "an even candidate count");
+            uint32_t* const krow = a.keysP + (int64_t)u * a.ldk;
+#pragma unroll
+            for (int h = 0; h < PC / 2; ++h)
+                *reinterpret_cast<uint2*>(krow + k0 + 2 * h) = make_uint2(pk[2 * h], pk[2 * h + 1]);
+            if (cand(PC) < K) krow[cand(PC)] = pk[PC];
+        }
+        if (a.pd) {
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+                dmx = fmax(dmx, __shfl_xor(dmx, o, kWave));
+                dmy = fmax(dmy, __shfl_xor(dmy, o, kWave));
+                dmr = fmax(dmr, __shfl_xor(dmr, o, kWave));
+                dml = fmax(dml, __shfl_xor(dml, o, kWave));
+            }
+            if (lane == 0) {
+                dred[wid][0] = dmx;
+                dred[wid][1] = dmy;
+                dred[wid][2] = dmr;
+                dred[wid][3] = dml;
+            }
+        }
+    }
+    if (a.pd) {   // the workgroup's displacement bound: the waves' shares in order
+        lds_barrier();
+        if (u == 0) {
+            double4 m = make_double4(dred[0][0], dred[0][1], dred[0][2], dred[0][3]);
+            for (int q = 1; q < NW; ++q) {
+                m.x = fmax(m.x, dred[q][0]);
+                m.y = fmax(m.y, dred[q][1]);
+                m.z = fmax(m.z, dred[q][2]);
+                m.w = fmax(m.w, dred[q][3]);
+            }
+            a.pd[cw] = m;
+        }
+    }
+}
+
 template <int PC, bool kX = false>
 __device__ __forceinline__ void prep_body(uint64_t* ts, PrepArgs& a)
 {
@@ -638,7 +843,7 @@ __device__ __forceinline__ void prep_body(uint64_t* ts, PrepArgs& a)
     const int per = (int)((gridDim.x + 7) / 8), b = (int)blockIdx.x;
     const int cw = (int)(gridDim.x % 8) == 0 ? (b % 8) * per + b / 8 : b;
     __shared__ __attribute__((aligned(16))) unsigned char lds[sizeof(PrepLds<kX ? PC + 1 : PC>)];
-    if constexpr (kX) prep_block<true, PC, true>(a, cw, lds);   // (matrix sources only)
+    if constexpr (kX) prep_block_x(a, cw, lds);   // (matrix sources, N <= kPrepU)
     else if (a.src.cands) prep_block<true, PC>(a, cw, lds);
     else prep_block<false, PC>(a, cw, lds);
     ts_end(ts);
@@ -650,8 +855,9 @@ __global__ __launch_bounds__(kPrepU) __attribute__((amdgpu_waves_per_eu(4))) voi
     prep_body<kPrepC>(ts, a);
 }
 
-// the fused chain's prep over a matrix source: kPrepCX (+1) candidates per workgroup (xbase)
-__global__ __launch_bounds__(kPrepU) __attribute__((amdgpu_waves_per_eu(4))) void prep_x_kernel(uint64_t* ts, PrepArgs a)
+// the fused chain's prep over a matrix source: kPrepCX (+1) candidates per workgroup (xbase), a
+// ninth wave folding the chains; two workgroups (18 waves) per CU
+__global__ __launch_bounds__(kPrepU + kWave) __attribute__((amdgpu_waves_per_eu(6))) void prep_x_kernel(uint64_t* ts, PrepArgs a)
 {
     prep_body<kPrepCX, true>(ts, a);
 }

@@ -680,7 +680,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             L->keysT.reserve(sizeof(float) * (size_t)4 * N * ldk);
             // a matrix source: kPrepCX (+1) candidates per workgroup (k_prep.h prep_x_kernel)
             const int gx = K / kPrepCX;
-            const bool xk = src.cands && !pair && gx >= 1 && K - gx * kPrepCX <= gx;
+            const bool xk = src.cands && !pair && N <= kPrepU && gx >= 1 && K - gx * kPrepCX <= gx;
             const int nprep = xk ? gx : nchain;
             L->pd.reserve(sizeof(double4) * (size_t)nprep);
             L->frows.reserve((counts ? sizeof(unsigned) : sizeof(double)) * (size_t)N * ldk);
@@ -713,7 +713,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             pr.feas = d_feas;
             pr.lreset = L->fwcount.as<int>();
             uint64_t* tsk = take_ts(nprep, ts_c, ts_nc);
-            if (xk) hipLaunchKernelGGL(prep_x_kernel, dim3((unsigned)nprep), dim3(kPrepU), 0, s, tsk, pr);
+            if (xk) hipLaunchKernelGGL(prep_x_kernel, dim3((unsigned)nprep), dim3(kPrepU + kWave), 0, s, tsk, pr);
             else hipLaunchKernelGGL(prep_kernel, dim3((unsigned)nprep), dim3(kPrepU), 0, s, tsk, pr);
             HCK(hipGetLastError());
             FwArgs fa{};

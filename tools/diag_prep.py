@@ -48,5 +48,5 @@ if hasattr(L, "mac_diag_prep_read"):
     ph = np.diff(p[:, :cols], axis=1) / 100.0
     out["chain_phases_us_median"] = [float(v) for v in np.median(ph, axis=0)]
     out["chain_phases_us_max"] = [float(v) for v in ph.max(axis=0)]
-    out["chain_phase_names"] = "per block (thread 0 = wave 0): loads+terms+cons3, fold, bound+keys+regions"
+    out["chain_phase_names"] = "per block: loads+terms (wave 0), barrier (wave 0), fold after the barrier (the folding wave)"
 print(json.dumps(out, indent=1))
