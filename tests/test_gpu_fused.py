@@ -146,3 +146,34 @@ def test_fused_nan_and_inf_candidates(ctx, pkg, orc):
     assert np.array_equal(got, want), np.flatnonzero(got != want)[:5]
     assert np.array_equal(objs, want_obj, equal_nan=True)
     assert K >= 64
+
+
+@pytest.mark.parametrize("extra", [-1, 0, 4, 11])
+def test_fused_prep_candidate_remainders(ctx, pkg, orc, extra):
+    """The fused chain's matrix-source prep takes 6 candidates per workgroup and hands the remainder
+    K mod 6 to the first workgroups one each (k_prep.h prep_x_kernel): polls of K = 6N + 1 + extra
+    candidates (extra < 0: the last dropped; > 0: shifted copies of the first appended), against
+    the exact lattice counts, with and without cons3."""
+    wl = pkg.workloads
+    rng = wl.SplitMix64(4242 + extra)
+    G, N = 600, 40
+    x, y, w = wl.grid_points(G)
+    ctx.set_points(x, y, w)
+    x0 = wl.uniform_disks(N, G, rng)
+    C = wl.poll_candidates(x0, rng)
+    if extra < 0:
+        C = C[:extra]
+    elif extra > 0:
+        add = C[1:1 + extra].copy()
+        add[:, :N] += 1.0   # (integer shifts: still on the lattice's mesh)
+        C = np.concatenate([C, add])
+    K = C.shape[0]
+    assert K == 6 * N + 1 + extra
+    rmax = np.full(N, 30.0 * TAN50)
+    ctx.set_chain("fused")
+    try:
+        _full_poll_check(ctx, orc, C, rmax, G, ["poll"], f"remainder{extra}")
+        _, kern = _walks(ctx, C)
+    finally:
+        ctx.set_chain("auto")
+    assert "fiw_kernel" in kern, kern
