@@ -510,7 +510,9 @@ def main():
                     help="config 5 on P GPUs: shard every poll's candidates, or speculate over "
                          "failure branches (rank j polls the poll after j failures)")
     ap.add_argument("--algo", default="auto", choices=("auto", "tiled", "scan", "poll"))
-    ap.add_argument("--polls", type=int, default=4, help="distinct poll sets cycled over steps")
+    ap.add_argument("--polls", type=int, default=8,
+                    help="distinct poll sets cycled over steps (8 x 37.8 MB at config 4: more than the "
+                         "256-MB Infinity Cache holds, so every poll reads its matrix from HBM)")
     ap.add_argument("--tile-points", type=int, default=None,
                     help="points per spatial tile of the index (library default when omitted)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -838,6 +840,8 @@ def main():
                                 f"16-B argmin all-gather"),
                 "algo": args.algo, "chain": args.chain,
                 "step_mode": "armed" if armed else "plain",
+                "poll_sets": args.polls,
+                "poll_sets_bytes": int(args.polls * K * 3 * N * 8),
             },
             "roofline": {
                 "bound": "hbm",
