@@ -63,7 +63,7 @@ extern "C" {
 
 #define MAC_OPT_CHAIN        6  /* the poll chain: MAC_CHAIN_AUTO (default) | _FIVE | _FUSED */
 
-#define MAC_CHAIN_AUTO   0  /* the fused three-launch chain unless one of the lane's last 8 polls was crowded,
+#define MAC_CHAIN_AUTO   0  /* the fused three-launch chain unless one of the context's last 64 polls was crowded,
                                scattered or off the packed-key grid (then the five-launch chain)  */
 #define MAC_CHAIN_FIVE   1  /* always the five-launch chain (prep, index, set-up, walk, finalize)   */
 #define MAC_CHAIN_FUSED  2  /* the fused chain whenever it applies (K <= 3073, packed keys possible) */

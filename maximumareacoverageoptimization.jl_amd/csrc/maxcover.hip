@@ -168,7 +168,6 @@ struct Lane {
     // the fused chain (k_fiw.h): displacement partials, failure bytes, credit rows, hint words,
     // the shared entries handed to fin2_kernel
     DevBuf pd, dead8, frows, fwhint, fwlist, fwcount, fwsxy, fwsw;
-    int fused_bad[8] = {};                     // 1: a recent poll did not suit the fused chain
     int last_chain = 0;                        // the chain of the lane's last poll: 1 five-launch, 2 fused
 };
 
@@ -176,6 +175,10 @@ struct mac_ctx {
     int device = 0;
     int cus = 256;
     std::mutex mu;
+    // the fused chain's routing history over every lane's polls (enqueue_eval): bit q set when the
+    // q-th last reported poll did not suit it (a workload property: a MADS stepper or a new lane
+    // takes it over from the lanes before it)
+    std::atomic<uint64_t> fused_bad{0};
     // mac_area_f64's combiner: queued single-candidate requests, one batch launch at a time
     std::mutex cl_mu;
     std::deque<struct ClReq*> cl_q;
@@ -656,11 +659,20 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
     const int nchain = pair ? (3 * N) / 4 : (K + kPrepC - 1) / kPrepC;
 
     // The fused chain (k_fiw.h: prep -> fiw -> fin2) whenever the poll walk runs on packed keys of at
-    // most kFwMaxK + 1 candidates, unless one of the lane's last 8 polls did not suit it: a crowded
+    // most kFwMaxK + 1 candidates, unless one of the context's last 64 polls did not suit it: a crowded
     // poll (many shared entries: the five-launch chain's union pass), a scattered batch (the
-    // per-candidate walk) or escaped keys (fp32 keys). Either chain gives the same results.
+    // per-candidate walk) or escaped keys (fp32 keys). Either chain gives the same results. The
+    // history is long because a wrong choice costs asymmetrically: a crowded poll in the fused
+    // chain decides its shared entries per candidate in place (0.4-2 ms at configs 5 and 4
+    // clustered), an uncrowded one in the five-launch chain costs ~20 us more.
+    // A generated poll whose step the host knows (a stepper's, not the pipelined loop's) at
+    // 2^ell > 8 goes to the five-launch chain under AUTO: its disks spread over more than the
+    // index's direct-mapped box (ell <= 3) and its superset boxes overlap widely (config 5's first
+    // poll of an MPC step: 0.5 ms fused against ~0.11 ms).
+    const bool wide_gen = !src.cands && !src.mst && src.b > 8;
     if (poll_possible && want_keys && N > 0 && M > 0 && K > 0 && K <= kFwMaxK + 1 &&
-        ctx->chain != MAC_CHAIN_FIVE && walk_forced != kModeTiled) {
+        ctx->chain != MAC_CHAIN_FIVE && walk_forced != kModeTiled &&
+        (ctx->chain == MAC_CHAIN_FUSED || !wide_gen)) {
         ensure_hints(L);
         volatile int* hw = (volatile int*)L->h_dc.p;
         int bad_now = -1;   // the lane's last poll's report (a hint: it may be an older poll's)
@@ -669,11 +681,12 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         else if (L->last_chain == 1 && hw[0] < (1 << 30))
             bad_now = hw[0] > kBitsMinDisks || hw[4] == kModeTiled ? 1 : 0;
         if (bad_now >= 0) {
-            for (int q = 7; q > 0; --q) L->fused_bad[q] = L->fused_bad[q - 1];
-            L->fused_bad[0] = bad_now;
+            uint64_t o = ctx->fused_bad.load(std::memory_order_relaxed);
+            while (!ctx->fused_bad.compare_exchange_weak(o, (o << 1) | (uint64_t)bad_now,
+                                                         std::memory_order_relaxed)) {
+            }
         }
-        bool fused = true;
-        for (int q = 0; q < 8; ++q) fused = fused && !L->fused_bad[q];
+        const bool fused = ctx->fused_bad.load(std::memory_order_relaxed) == 0;
         if (fused || ctx->chain == MAC_CHAIN_FUSED) {
             const int ldk = keys_ld(K);
             counts = ctx->w_uniform ? 1 : 0;
