@@ -369,7 +369,8 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
     if world > 1 and spec:
         # speculation: every rank applies the same polls; the useful evaluations are the applied
         # polls' (the sequential loop's), the discarded branches' are reported beside them
-        work = torch.tensor([feas], dtype=torch.float64, device=coll_dev)
+        work = torch.tensor([sum(r["speculative_feasible_evaluations"] for r in recs)],
+                            dtype=torch.float64, device=coll_dev)
         dist.all_reduce(work)
         spec_work = int(work.item())
         feas = sum(r["useful_feasible_evaluations"] for r in recs)
@@ -452,6 +453,7 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
                              for k in ("fire_s", "remove_s", "mads_s")},
             "mads_host_split_s": {k: float(np.sum([r.get("mads_host_s", {}).get(k, 0.0) for r in recs]))
                                   for k in ("host_enqueue_s", "host_perm_s", "wait_s", "host_post_s")},
+            "slot_fallbacks": int(sum(r.get("slot_fallbacks", 0) for r in recs)),
             "parallelism": ("1 GPU" if world == 1 else
                             (f"{world} GPUs: speculation over failure branches (rank j polls the "
                              f"poll after j failures), one 24-B all-gather per round; fire stream "
@@ -463,9 +465,8 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
-            "kernel": (f"poll chain (prep, disk_index, walk_setup, coverage_{k_walk}, "
-                       f"shared bit-words when crowded, finalize + argmin); dominant kernel "
-                       f"{dominant}"),
+            "kernel": (f"poll chains ({', '.join(k for k, v in kernels.items() if v.get('launches'))}); "
+                       f"dominant kernel {dominant}"),
             "chain_ms": chain_ms, "polls": split[3],
             "split_ms_per_poll": ({"prep": split[0] / split[3], "walk": split[1] / split[3],
                                    "after_walk": split[2] / split[3]} if split[3] else None),
@@ -506,9 +507,10 @@ def main():
     ap.add_argument("--chain", choices=["auto", "five", "fused"], default="auto",
                     help="poll chain: the device's choice (auto), the five-launch chain or the "
                          "fused three-launch chain (MAC_OPT_CHAIN)")
-    ap.add_argument("--mads-mode", choices=["shard", "speculate"], default="shard",
-                    help="config 5 on P GPUs: shard every poll's candidates, or speculate over "
-                         "failure branches (rank j polls the poll after j failures)")
+    ap.add_argument("--mads-mode", choices=["shard", "speculate"], default="speculate",
+                    help="config 5 on P GPUs: speculate (default) over failure branches (rank j "
+                         "polls the poll after j failures: fewer dependent rounds), or shard "
+                         "every poll's candidates (the per-poll chain does not shrink)")
     ap.add_argument("--algo", default="auto", choices=("auto", "tiled", "scan", "poll"))
     ap.add_argument("--polls", type=int, default=8,
                     help="distinct poll sets cycled over steps (8 x 37.8 MB at config 4: more than the "
@@ -521,10 +523,11 @@ def main():
                     help="skip the parity guard and the closure timing (profiler passes: only "
                          "the warmup and timed polls launch kernels after set-up)")
     ap.add_argument("--seed", type=int, default=20250216)
-    ap.add_argument("--scaling", default="strong", choices=("strong", "weak"),
-                    help="N>1: strong (default, the north star's split) = the single poll's "
-                         "candidates sharded over the GPUs; weak = one full poll set per GPU "
-                         "(P*K candidates per step, a wider poll)")
+    ap.add_argument("--scaling", default="weak", choices=("strong", "weak"),
+                    help="N>1: weak (default) = one full poll set per GPU (P*K candidates per "
+                         "step: a P-fold wider poll, one 16-B argmin all-gather); strong = the "
+                         "single poll's candidates sharded over the GPUs (its latency-bound chain "
+                         "barely shrinks per rank: DESIGN.md section 6)")
     ap.add_argument("--shard-of", type=int, default=1,
                     help="time rank 0's shard of a P-way strong split alone on one GPU (no "
                          "collective; value = shard candidates / time)")
@@ -655,7 +658,8 @@ def main():
 
     # N > 1: the 16-B all-gather straight from d_best, ordered after the poll on its stream,
     # and one pinned host read of the world x 16-B result (dist.PollGather)
-    gat = pdist.PollGather(coll_dev) if distributed else None
+    gat = (pdist.PollGather(coll_dev, ctx=ctx if coll_dev.type == "cuda" else None)
+           if distributed else None)
     # one GPU, armed: poll j + 1 is enqueued behind the doorbell while poll j runs (its inputs are
     # resident; a MADS driver fills them once poll j's result is known) and released right after
     # that result is read, so no launch sits between dependent polls. Consecutive polls alternate
@@ -797,6 +801,38 @@ def main():
                    "copy-out, synchronous (what a Julia ccall per trial point costs)",
                    "threads": closure_threads(ctx, polls[0], (1, 4, 16))}
 
+    # the host-pointer poll (a DirectSearch-owned poll handed over through the C ABI from host
+    # memory, src/TDM_STATIC_opt.jl:162): the whole 3N x 2n matrix (mac_poll_best_f64) against
+    # the basis form (mac_poll_best_basis: incumbent + L's packed triangle + permutations + delta,
+    # mac_poll_basis_f64), both with cons3, timed per call on the same poll (results must agree)
+    host_poll = None
+    if rank == 0 and not args.no_extras and K > 1 and args.disk_shard_of == 1:
+        n = 3 * N
+        Lm, rp_, cp_ = wl.ltmads_basis_parts(n, 2, wl.SplitMix64(args.seed + 11))
+        Bm = Lm[rp_][:, cp_].astype(np.float64)
+        Cm = np.ascontiguousarray(np.concatenate([x0[None, :] + Bm.T, x0[None, :] - Bm.T]))
+        tri = np.ascontiguousarray(Lm[np.tril_indices(n)], dtype=np.int16)
+        kw3 = dict(prev=x0, d_lim=dlim, tan_half_fov=tan_half)
+        res_m = ctx.poll_best(Cm, r_max, 1e5, **kw3)
+        res_b = ctx.poll_basis(x0, tri, rp_, cp_, 1.0, r_max, 1e5, **kw3)
+        reps = 20
+        t_m = time.perf_counter()
+        for _ in range(reps):
+            ctx.poll_best(Cm, r_max, 1e5, **kw3)
+        t_m = (time.perf_counter() - t_m) / reps
+        t_b = time.perf_counter()
+        for _ in range(reps):
+            ctx.poll_basis(x0, tri, rp_, cp_, 1.0, r_max, 1e5, **kw3)
+        t_b = (time.perf_counter() - t_b) / reps
+        host_poll = {
+            "matrix_ms": t_m * 1e3, "basis_ms": t_b * 1e3, "candidates": int(Cm.shape[0]),
+            "matrix_bytes": int(Cm.nbytes), "basis_bytes": int(8 * n + 8 * n + tri.nbytes),
+            "agree": bool(res_m == res_b), "calls": reps,
+            "note": "host memory in, (objective, index) out, synchronous, with cons3: "
+                    "mac_poll_best_f64 ships the 3N x 2n matrix; mac_poll_basis_f64 ships the "
+                    "incumbent, L's packed lower triangle (int16), rp, cp and delta and expands "
+                    "the candidates on the device"}
+
     out = None
     if rank == 0:
         cpu = None
@@ -850,8 +886,8 @@ def main():
                 "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "traffic": traffic,
-                "kernel": (f"poll chain (prep, disk_index, walk_setup, coverage_{k_walk}, "
-                           f"finalize + argmin); dominant kernel {dominant}"),
+                "kernel": (f"poll chain ({', '.join(k for k, v in kernels.items() if v.get('launches'))}); "
+                           f"dominant kernel {dominant}"),
                 "chain_ms": chain_ms,
                 "dominant_kernel": dominant,
                 "dominant_basis": ("in-kernel stamps: first workgroup start to last workgroup end; "
@@ -886,6 +922,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "closure": closure,
+            "host_poll_ms": host_poll,
             "best": {"objective": result[0], "index": result[1]},
             "check_timed_poll_vs_scan": check,
             "setup_s": t_set,

@@ -154,6 +154,20 @@ int32_t mac_poll_best_f64(mac_ctx* ctx, const double* cands, int64_t three_n, in
                           const double* prev, const double* d_lim, double tan_half_fov,
                           double* obj_out, double* best_obj, int64_t* best_idx);
 
+/* Basis form of a caller-owned poll (DirectSearch's poll, src/TDM_STATIC_opt.jl:22-44 CustomPoll
+ * b / i / maximal_basis; :162): the 2n candidates (n = three_n) x_inc + delta * B[:, k] (index k)
+ * and x_inc - delta * B[:, k] (index n + k), k < n, with B = L[rp][:, cp]: B[v][k] =
+ * L[rp[v]][cp[k]], L lower triangular, passed as its lower triangle packed by rows (int16, entry
+ * (r, c <= r) at r(r+1)/2 + c; n(n+1)/2 entries), rp / cp permutations of [0, n) (any values in
+ * [0, n) are accepted). B's entry is delta * L exactly as the double product, so the candidates
+ * equal the matrix a caller would build with the same arithmetic, and the results equal
+ * mac_poll_best_f64 on that 3N x 2n matrix bit for bit. Ships 16n + n(n+1) bytes instead of 16n^2
+ * (config 4: 2.4 MB instead of 37.7 MB). obj_out nullable (2n doubles). */
+int32_t mac_poll_basis_f64(mac_ctx* ctx, const double* x_inc, int64_t three_n, const int16_t* ltri,
+                           const int32_t* rp, const int32_t* cp, double delta, const double* r_max,
+                           double penalty, const double* prev, const double* d_lim, double tan_half_fov,
+                           double* obj_out, double* best_obj, int64_t* best_idx);
+
 /* ---- native MADS driver ------------------------------------------ */
 /* A granular MADS with a complete LTMADS poll, the restatement of DirectSearch's Optimize!
  * (src/TDM_STATIC_opt.jl:118-169; the third-party algorithm is not vendored, so this is the
@@ -188,6 +202,9 @@ typedef struct mac_mads_stats {
                                      (src/TDM_Constraints.jl:67), so no candidate passes — a
                                      failure (ell - 1), as the extreme barrier makes it         */
     int64_t successes;            /* iterations whose poll moved the incumbent (the rest failed) */
+    int64_t slot_fallbacks;       /* polls whose result did not arrive through the mapped slot within
+                                     50 ms (read by a copy after a stream synchronisation instead):
+                                     0 in a healthy run                                           */
 } mac_mads_stats;
 int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const double* r_max,
                      double penalty, const double* prev, const double* d_lim, double tan_half_fov,
@@ -279,6 +296,15 @@ int32_t mac_poll_best_dev_f32(mac_ctx* ctx, const float* d_cands, int64_t three_
 int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* best_obj,
                        int64_t* best_idx);
 
+/* The multi-GPU poll's exchange, reduced on the device: d_records holds n_records 16-B records
+ * {objective, index as int64 bits} (the ranks' d_best, e.g. one RCCL all-gather into one buffer
+ * ordered on `stream`); one wave writes their lexicographic minimum to d_best (a record with
+ * index < 0 or an objective not < +inf never wins; ties to the lowest index; none: {+inf, -1})
+ * and to d_best's mapped result slot, so mac_best_fetch(d_best) returns the node's argmin without
+ * a copy or a stream synchronisation. Stream-ordered; returns after enqueueing. */
+int32_t mac_best_reduce_dev(mac_ctx* ctx, const void* d_records, int32_t n_records, void* d_best,
+                            void* stream);
+
 /* Armed device polls: the host turnaround between dependent polls of a MADS loop (the next poll
  * is known only after the previous one's result) taken off the device's critical path. The
  * chain of mac_poll_best_dev_f64 is enqueued ahead of time behind a stream wait on the context's
@@ -291,7 +317,9 @@ int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* b
  * (or the device) while an armed poll on it is not fired — mac_best_fetch of a fired poll never
  * does, and mac_ctx_destroy fires every outstanding ticket first. Argument errors are reported
  * before anything is enqueued; a poll that fails after its wait went in voids only its own ticket
- * (released together with the earlier tickets, never ahead of them). Buffers an armed poll grows
+ * (released together with the earlier tickets, never ahead of them). `stream` must be a created
+ * stream, not NULL (MAC_E_INVAL): an unfired wait on HIP's null stream would block every
+ * blocking-stream operation of the process. Buffers an armed poll grows
  * are released at the next device synchronisation (point-list changes, mac_ctx_destroy), since
  * freeing them would wait for the unfired poll. MAC_E_HIP when the device cannot wait on stream
  * values (hipDeviceAttributeCanUseStreamWaitValue). */

@@ -16,7 +16,7 @@ is what the parity tests exercise. See INTEGRATION.md.
 module MaxCoverAMD
 
 export MacContext, set_points!, calculateArea, createObjective, objective_batch, poll_best,
-       rmvCoveredPOI!, area_batch, mads_run
+       poll_basis, rmvCoveredPOI!, area_batch, mads_run
 
 const libmaxcover = get(ENV, "MAXCOVER_LIB",
     joinpath(@__DIR__, "..", "maximumareacoverageoptimization.jl_amd", "libmaxcover.so"))
@@ -155,6 +155,44 @@ function poll_best(cands::Matrix{Float64}, r_max::Vector{Float64}, ctx::MacConte
     return bo[], bi[] + 1, objs
 end
 
+"""
+poll_basis(x_inc, L, rp, cp, delta, r_max, ctx; prev, d_lim, tan_half_fov) — a DirectSearch-owned
+poll in basis form (src/TDM_STATIC_opt.jl:22-44 CustomPoll's b / i / maximal_basis; :162): the 2n
+candidates x_inc ± delta * B[:, k], B = L[rp, cp] (L lower triangular, rp / cp permutations,
+1-based here as in Julia), expanded on the GPU — 2.4 MB shipped at n = 1536 instead of the 37.7-MB
+matrix. Returns (best_obj, best_idx (1-based over [plus directions; minus directions], 0 if none
+feasible), objs).
+"""
+function poll_basis(x_inc::Vector{Float64}, L::AbstractMatrix{<:Integer}, rp::AbstractVector{<:Integer},
+                    cp::AbstractVector{<:Integer}, delta::Float64, r_max::Vector{Float64},
+                    ctx::MacContext; penalty::Float64 = 1e5,
+                    prev::Union{Nothing,Vector{Float64}} = nothing,
+                    d_lim::Union{Nothing,Vector{Float64}} = nothing, tan_half_fov::Float64 = 1.0)
+    n = length(x_inc)
+    tri = Vector{Int16}(undef, n * (n + 1) ÷ 2)
+    q = 1
+    @inbounds for r in 1:n, c in 1:r      # lower triangle packed by rows
+        tri[q] = Int16(L[r, c])
+        q += 1
+    end
+    rp0 = Int32.(rp .- 1)
+    cp0 = Int32.(cp .- 1)
+    objs = Vector{Float64}(undef, 2n)
+    bo = Ref{Float64}(Inf)
+    bi = Ref{Int64}(-1)
+    pprev = prev === nothing ? Ptr{Float64}(C_NULL) : pointer(prev)
+    pdlim = d_lim === nothing ? Ptr{Float64}(C_NULL) : pointer(d_lim)
+    GC.@preserve prev d_lim begin
+        check(ccall((:mac_poll_basis_f64, libmaxcover), Int32,
+                    (Ptr{Cvoid}, Ptr{Float64}, Int64, Ptr{Int16}, Ptr{Int32}, Ptr{Int32}, Float64,
+                     Ptr{Float64}, Float64, Ptr{Float64}, Ptr{Float64}, Float64, Ptr{Float64},
+                     Ref{Float64}, Ref{Int64}),
+                    ctx, x_inc, n, tri, rp0, cp0, delta, r_max, penalty, pprev, pdlim, tan_half_fov,
+                    objs, bo, bi))
+    end
+    return bo[], bi[] + 1, objs
+end
+
 struct MadsParams
     n_iter::Int64
     ell0::Int32
@@ -172,6 +210,10 @@ struct MadsStats
     host_perm_s::Float64
     wait_s::Float64
     host_post_s::Float64
+    feasible_evaluations::Int64
+    rejected_polls::Int64
+    successes::Int64
+    slot_fallbacks::Int64
 end
 
 """

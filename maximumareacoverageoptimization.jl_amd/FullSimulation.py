@@ -67,7 +67,7 @@ class Simulation:
     def __init__(self, ctx: Context, starting_circles, *, fire: DynamicArea | None = None,
                  firepoints=None, initial_points=None, N_iter: int = N_iter, d_lim=None,
                  r_max=None, seed: int = 20250216, ell0: int = 2, ell_max: int = 6,
-                 shard=None, gather=None, speculate: bool = False):
+                 shard=None, gather=None, speculate: bool | None = None, device=None):
         self.ctx = ctx
         self.x_prev = np.asarray(starting_circles, dtype=np.float64).copy()
         self.N = N = self.x_prev.size // 3
@@ -78,10 +78,21 @@ class Simulation:
         self.fire, self.firepoints = fire, firepoints
         self.N_iter, self.seed, self.ell0, self.ell_max = N_iter, seed, ell0, ell_max
         self.shard = shard          # (rank, world) or None: the whole poll on this GPU
+        # P GPUs: speculate over failure branches, rank j polling the poll after j failures
+        # (gather: dist.SpecGather) — the default, since sharding one poll cannot shorten its
+        # latency-bound chain — or shard every poll's candidates (speculate=False,
+        # gather: dist.make_gather). With no gather given, the default one is made on `device`
+        # (the collective's device: the rank's GPU under RCCL, "cpu" under gloo).
+        multi = shard is not None and shard[1] > 1
+        if speculate is None:
+            from .dist import SpecGather
+            speculate = multi and (gather is None or isinstance(gather, SpecGather))
+        if multi and gather is None:
+            from .dist import SpecGather, make_gather
+            dev = device if device is not None else "cpu"
+            gather = SpecGather(dev) if speculate else make_gather(dev)
         self.gather = gather
-        # P GPUs: shard every poll's candidates (gather: dist.make_gather), or speculate over
-        # failure branches, rank j polling the poll after j failures (gather: dist.SpecGather)
-        self.speculate = speculate
+        self.speculate = bool(speculate)
         if fire is not None:
             ctx.set_points_records(fire.initial_points())
         elif firepoints is not None:
@@ -147,6 +158,9 @@ class Simulation:
                    rounds=int(st.get("rounds", st["iterations"])),
                    useful_feasible_evaluations=int(st.get("useful_feasible_evaluations",
                                                           st.get("feasible_evaluations", 0))),
+                   speculative_feasible_evaluations=int(st.get("speculative_feasible_evaluations",
+                                                               st.get("feasible_evaluations", 0))),
+                   slot_fallbacks=int(st.get("slot_fallbacks", 0)),
                    fire_s=t1 - t0, remove_s=t2 - t1, mads_s=t3 - t2, step_s=t3 - t0,
                    mads_host_s={k: float(st.get(k, 0.0)) for k in
                                 ("host_enqueue_s", "host_perm_s", "wait_s", "host_post_s")},

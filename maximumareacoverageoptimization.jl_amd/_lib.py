@@ -68,7 +68,7 @@ EXPORTS = (
     "mac_poll_best_f32", "mac_poll_best_dev_f32",
     "mac_mads_begin", "mac_mads_poll", "mac_mads_update", "mac_mads_result", "mac_mads_destroy",
     "mac_mads_poll_ahead", "mac_mads_advance",
-    "mac_mads_best_buffer",
+    "mac_mads_best_buffer", "mac_best_reduce_dev", "mac_poll_basis_f64",
 )
 
 
@@ -86,7 +86,7 @@ class MadsStats(ctypes.Structure):
                 ("host_enqueue_s", ctypes.c_double), ("host_perm_s", ctypes.c_double),
                 ("wait_s", ctypes.c_double), ("host_post_s", ctypes.c_double),
                 ("feasible_evaluations", ctypes.c_int64), ("rejected_polls", ctypes.c_int64),
-                ("successes", ctypes.c_int64)]
+                ("successes", ctypes.c_int64), ("slot_fallbacks", ctypes.c_int64)]
 
 
 class FireParams(ctypes.Structure):
@@ -147,6 +147,11 @@ def _declare(L: ctypes.CDLL) -> None:
         "mac_poll_best_dev_f64": ([_vp, _vp, _i64, _i64, _vp, ctypes.c_double, _vp, _vp,
                                    ctypes.c_double, _i64, _vp, _vp, _vp], _i32),
         "mac_best_fetch": ([_vp, _vp, _vp, _dp, _i64p], _i32),
+        "mac_best_reduce_dev": ([_vp, _vp, _i32, _vp, _vp], _i32),
+        "mac_poll_basis_f64": ([_vp, _dp, _i64, ctypes.POINTER(ctypes.c_int16),
+                                ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                                ctypes.c_double, _dp, ctypes.c_double, _dp, _dp, ctypes.c_double,
+                                _dp, _dp, _i64p], _i32),
         "mac_poll_arm_dev_f64": ([_vp, _vp, _i64, _i64, _vp, ctypes.c_double, _vp, _vp,
                                   ctypes.c_double, _i64, _vp, _vp, _vp,
                                   ctypes.POINTER(ctypes.c_uint64)], _i32),
@@ -511,6 +516,43 @@ class Context:
             return bo.value, int(bi.value), objs
         return bo.value, int(bi.value)
 
+    def poll_basis(self, x_inc, L, rp, cp, delta: float, r_max, penalty: float = 1e5, prev=None,
+                   d_lim=None, tan_half_fov: float = 1.0, want_all: bool = False):
+        """mac_poll_basis_f64: the 2n-candidate poll x +- delta * B[:, k], B = L[rp][:, cp],
+        expanded on the device. L: n x n lower-triangular integers (|L| < 2^15; its lower triangle
+        is packed here) or the packed int16 triangle itself. Returns (best_obj, best_idx[, objs])."""
+        x = _f64(x_inc)
+        n = x.size
+        Lp = np.asarray(L)
+        if Lp.ndim == 2:
+            if Lp.shape != (n, n):
+                raise ValueError("L must be n x n")
+            if np.abs(Lp).max(initial=0) > 32767:
+                raise ValueError("|L| must fit int16")
+            Lp = Lp[np.tril_indices(n)]
+        tri = np.ascontiguousarray(Lp, dtype=np.int16)
+        if tri.size != n * (n + 1) // 2:
+            raise ValueError("packed L must hold n(n+1)/2 entries")
+        r = np.ascontiguousarray(rp, dtype=np.int32)
+        c = np.ascontiguousarray(cp, dtype=np.int32)
+        if r.size != n or c.size != n:
+            raise ValueError("rp / cp must hold n entries")
+        rm = _f64(r_max)
+        pv = _f64(prev) if prev is not None else None
+        dl = _f64(d_lim) if d_lim is not None else None
+        objs = np.empty(2 * n) if want_all else None
+        bo = ctypes.c_double()
+        bi = _i64()
+        _check(self._L.mac_poll_basis_f64(
+            self._h, _ptr(x), n, tri.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)),
+            r.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), c.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+            float(delta), _ptr(rm), float(penalty), _ptr(pv) if pv is not None else None,
+            _ptr(dl) if dl is not None else None, float(tan_half_fov),
+            _ptr(objs) if objs is not None else None, ctypes.byref(bo), ctypes.byref(bi)))
+        if want_all:
+            return bo.value, int(bi.value), objs
+        return bo.value, int(bi.value)
+
     # -- fp32 candidates (*_f32: widened exactly on the device, fp64 decisions)
     def area_f32(self, circles) -> float:
         c = _f32(circles)
@@ -678,6 +720,33 @@ class Context:
             return bo.value, bi.value
 
         return arm, fire, fetch
+
+    def best_reduce_dev(self, d_records, n_records: int, d_best, stream=None) -> None:
+        """mac_best_reduce_dev: the lexicographic minimum of n_records 16-B {objective, index}
+        records (device) into d_best and its mapped slot, on ``stream`` (read it with best_fetch)."""
+        _check(self._L.mac_best_reduce_dev(self._h, _devptr(d_records), int(n_records), _devptr(d_best),
+                                           _stream(stream, self.device)))
+
+    def reduce_step(self, d_records, n_records: int, d_best, stream=None):
+        """A bound mac_best_reduce_dev + mac_best_fetch (prebuilt ctypes arguments): returns a
+        zero-argument callable giving the reduced (objective, index)."""
+        h = _vp(self._h.value if isinstance(self._h, _vp) else self._h)
+        sv = _vp(_stream(stream, self.device))
+        red_args = (h, _vp(_devptr(d_records)), _i32(int(n_records)), _vp(_devptr(d_best)), sv)
+        bo, bi = ctypes.c_double(), ctypes.c_int64()
+        fetch_args = (h, _vp(_devptr(d_best)), sv, ctypes.byref(bo), ctypes.byref(bi))
+        red, fetch = self._L.mac_best_reduce_dev, self._L.mac_best_fetch
+
+        def step():
+            rc = red(*red_args)
+            if rc != MAC_OK:
+                _check(rc)
+            rc = fetch(*fetch_args)
+            if rc != MAC_OK:
+                _check(rc)
+            return bo.value, bi.value
+
+        return step
 
     def best_fetch(self, d_best, stream=None):
         """The (objective, index) the latest device poll on d_best wrote (mac_best_fetch).

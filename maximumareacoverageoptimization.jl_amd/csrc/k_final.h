@@ -376,4 +376,50 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
     ts_end(ts);
 }
 
+// The multi-GPU poll's exchange on the device (mac_best_reduce_dev): n 16-B records {objective,
+// index as int64 bits} — the ranks' poll bests, all-gathered by RCCL into one buffer on this
+// stream — reduced by one wave to their lexicographic minimum (dist.reduce_best's rule: a record
+// with index < 0 or an objective that is not < +inf never wins, ties to the lowest index), written
+// to best and to its mapped host slot exactly as finalize's last block writes a poll's result
+// (d_best with agent-scope stores, acknowledged, then the slot words under seq + check), so the
+// host reads the node's argmin with mac_best_fetch and no copy or stream synchronisation.
+__global__ __launch_bounds__(kWave) void best_reduce_kernel(const unsigned long long* __restrict__ rec, int n,
+                                                          unsigned long long* best, uint64_t* mirror,
+                                                          uint64_t seq)
+{
+    const int lane = threadIdx.x;
+    double bv = __builtin_inf();
+    long long bi = -1;
+    for (int q = lane; q < n; q += kWave) {
+        const double o = __builtin_bit_cast(double, rec[2 * q]);
+        const long long i = (long long)rec[2 * q + 1];
+        if (i >= 0 && o < __builtin_inf() && (bi < 0 || o < bv || (o == bv && i < bi))) {
+            bv = o;
+            bi = i;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const double o = __shfl_xor(bv, off, kWave);
+        const long long i = __shfl_xor(bi, off, kWave);
+        if (i >= 0 && (bi < 0 || o < bv || (o == bv && i < bi))) {
+            bv = o;
+            bi = i;
+        }
+    }
+    if (lane == 0) {
+        const uint64_t o = __builtin_bit_cast(uint64_t, bv);
+        const uint64_t ix = (uint64_t)bi;
+        __hip_atomic_store(best, (unsigned long long)o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(best + 1, (unsigned long long)ix, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (mirror) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            mirror[0] = o;
+            mirror[1] = ix;
+            mirror[2] = seq;
+            mirror[3] = mirror_check(o, ix, seq);
+        }
+    }
+}
+
 }  // namespace mac

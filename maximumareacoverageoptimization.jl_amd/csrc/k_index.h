@@ -278,18 +278,22 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
         get3(0, bx, by, br);
         load_partials();
         const int n = 3 * N;
-        if (!src.cands && 3 * n <= 2 * kIndexSlots && src.b <= 16384) {
+        if (!src.cands && 3 * n <= 2 * kIndexSlots && (src.ltri || src.b <= 16384)) {
             // the generator: candidates k and k + n are x + d and x - d of the same LTMADS entry
             // d = L[rp[v]][cp[k mod n]] (k_prep.h CandSrc), so disk i's 3 x n entries are drawn
             // once into the table's LDS (integers |d| <= b, as int16) and both signs built from
-            // them: the same doubles as src.get, half the stream draws, spread over all threads
+            // them: the same doubles as src.get, half the stream draws, spread over all threads.
+            // The basis form's table holds L itself and d = (double)L * delta (src.entry's product)
             int16_t* const dtab = reinterpret_cast<int16_t*>(table);
             const int r3[3] = {src.rp[i], src.rp[N + i], src.rp[2 * N + i]};
             for (int t = tid; t < 3 * n; t += kIdxThreads) {
                 const int a = t / n, kk = t - a * n;
-                dtab[t] = (int16_t)ltmads_entry(src.state, n, src.b, r3[a], src.cp[kk]);
+                const int r = r3[a], c = src.cp[kk];
+                dtab[t] = src.ltri ? (r < c ? (int16_t)0 : src.ltri[(int64_t)r * (r + 1) / 2 + c])
+                                   : (int16_t)ltmads_entry(src.state, n, src.b, r, c);
             }
             __syncthreads();
+            const double sc = src.ltri ? src.delta : 1.0;
             const double xi = src.xinc[i], yi = src.xinc[N + i], ri = src.xinc[2 * N + i];
 #pragma unroll
             for (int j = 0; j < P; ++j) {
@@ -297,7 +301,8 @@ __global__ __launch_bounds__(kIdxThreads) __attribute__((amdgpu_waves_per_eu(kPe
                 const int kg = kl + src.k0;
                 const bool plus = kg < n;
                 const int kk = plus ? kg : kg - n;
-                const double dx = (double)dtab[kk], dy = (double)dtab[n + kk], dr = (double)dtab[2 * n + kk];
+                const double dx = sc * (double)dtab[kk], dy = sc * (double)dtab[n + kk],
+                             dr = sc * (double)dtab[2 * n + kk];
                 cx[j] = plus ? xi + dx : xi - dx;
                 cy[j] = plus ? yi + dy : yi - dy;
                 cr[j] = plus ? ri + dr : ri - dr;

@@ -142,6 +142,12 @@ struct CandSrc {
     int k0;                // generator: candidate k of this source is candidate k0 + k of the poll
                            // (a rank's shard of it)
     const MadsState* mst;  // generator, pipelined MADS loop: b from the device state (else null)
+    // the basis form (mac_poll_basis_f64: a caller-owned poll, DirectSearch's B = L[rp][:, cp] and
+    // mesh size delta, src/TDM_STATIC_opt.jl:22-44): L's lower triangle packed by rows (int16,
+    // entry (r, c <= r) at r(r+1)/2 + c) and B's entries delta * L instead of the stream's draws
+    // (null: the stream). b is then a bound on |L| (the index's int16 table) and delta scales it.
+    const int16_t* ltri;
+    double delta;
     // Called at the top of every launch that reads the source: b = 2^ell from the device state;
     // false once the loop has stopped, or (launches after the prep: any_poll false) when the
     // prep rejected the poll whole (the launch returns at once). Uniform per workgroup.
@@ -153,13 +159,19 @@ struct CandSrc {
         b = (int64_t)1 << e;
         return true;
     }
+    // B's entry (r, c) of a generated poll (n = 3N): the stream's LTMADS draw, or delta * L[r][c]
+    __device__ __forceinline__ double entry(int n, int r, int c) const
+    {
+        if (ltri) return r < c ? 0.0 : delta * (double)ltri[(int64_t)r * (r + 1) / 2 + c];
+        return ltmads_entry(state, n, b, r, c);
+    }
     __device__ __forceinline__ double get(int kl, int v, int N) const
     {
         if (cands) return cands[(int64_t)kl * ldc + v];
         const int n = 3 * N;
         const int k = kl + k0;
         const int kk = k < n ? k : k - n;
-        const double d = ltmads_entry(state, n, b, rp[v], cp[kk]);
+        const double d = entry(n, rp[v], cp[kk]);
         return k < n ? xinc[v] + d : xinc[v] - d;
     }
 };
@@ -372,7 +384,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw, unsigned c
 #pragma unroll
                 for (int q = 0; q < 3; ++q) {
                     const int vv = q * N + ii;
-                    const double d = ltmads_entry(a.src.state, n3, a.src.b, a.src.rp[vv], a.src.cp[col]);
+                    const double d = a.src.entry(n3, a.src.rp[vv], a.src.cp[col]);
                     v[c][q] = a.src.xinc[vv] + d;
                     v[c + 4][q] = a.src.xinc[vv] - d;
                 }

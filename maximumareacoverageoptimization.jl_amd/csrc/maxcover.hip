@@ -669,7 +669,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
     // 2^ell > 8 goes to the five-launch chain under AUTO: its disks spread over more than the
     // index's direct-mapped box (ell <= 3) and its superset boxes overlap widely (config 5's first
     // poll of an MPC step: 0.5 ms fused against ~0.11 ms).
-    const bool wide_gen = !src.cands && !src.mst && src.b > 8;
+    const bool wide_gen = !src.cands && !src.mst &&
+                          (src.ltri ? (double)src.b * __builtin_fabs(src.delta) > 8.0 : src.b > 8);
     if (poll_possible && want_keys && N > 0 && M > 0 && K > 0 && K <= kFwMaxK + 1 &&
         ctx->chain != MAC_CHAIN_FIVE && walk_forced != kModeTiled &&
         (ctx->chain == MAC_CHAIN_FUSED || !wide_gen)) {
@@ -1181,6 +1182,92 @@ static int32_t host_eval(mac_ctx* ctx, const T* cands, int64_t three_n, int64_t 
     HCK(hipStreamSynchronize(s));
     if (staged && area_out) std::memcpy(area_out, h_area, sizeof(double) * K);
     if (staged && obj_out) std::memcpy(obj_out, h_obj, sizeof(double) * K);
+    if (best_obj) *best_obj = hb[0];
+    if (best_idx) *best_idx = __builtin_bit_cast(int64_t, hb[1]);
+    return MAC_OK;
+}
+
+// The basis form of a caller-owned poll (mac_poll_basis_f64): the incumbent, B = L[rp][:, cp] as L's
+// packed lower triangle (int16) with the two permutations, and delta; the 2n candidates
+// x + delta B[:, k], x - delta B[:, k] are expanded on the device (k_prep.h CandSrc.entry), so the
+// host ships n(n+1) + 16n bytes instead of the 3N x 2n matrix's 16 n^2.
+static int32_t host_eval_basis(mac_ctx* ctx, const double* x_inc, int64_t three_n, const int16_t* ltri,
+                               const int32_t* rp, const int32_t* cp, double delta, const double* r_max,
+                               double penalty, const double* prev, const double* d_lim,
+                               double tan_half_fov, double* obj_out, double* best_obj, int64_t* best_idx)
+{
+    const int64_t n = three_n;
+    const int64_t K = 2 * n;
+    int32_t rc = check_common(ctx, three_n, K);
+    if (rc) return rc;
+    if (n == 0) {
+        if (best_idx) *best_idx = -1;
+        if (best_obj) *best_obj = INFINITY;
+        return MAC_OK;
+    }
+    if (!x_inc || !ltri || !rp || !cp || !r_max) return fail(MAC_E_INVAL, "null argument");
+    if (!std::isfinite(delta)) return fail(MAC_E_INVAL, "delta not finite");
+    // the permutations index L on the device: every value must lie in [0, n)
+    for (int64_t v = 0; v < n; ++v)
+        if (rp[v] < 0 || rp[v] >= n || cp[v] < 0 || cp[v] >= n)
+            return fail(MAC_E_INVAL, "rp / cp entry outside [0, n)");
+    if (prev && !d_lim) return fail(MAC_E_INVAL, "prev given without d_lim");
+    const int N = (int)(three_n / 3);
+    int64_t bmax = 1;   // the largest |diagonal| (LTMADS: the step 2^ell): the chain's routing hint
+    for (int64_t r = 0; r < n; ++r) bmax = std::max<int64_t>(bmax, std::abs((int)ltri[r * (r + 1) / 2 + r]));
+    set_device(ctx);
+    LaneGuard lg(ctx);
+    Lane* L = lg.lane;
+    hipStream_t s = L->stream;
+    const size_t tri = (size_t)n * (size_t)(n + 1) / 2;
+    const size_t in_bytes = sizeof(double) * n + sizeof(int32_t) * 2 * n + sizeof(int16_t) * tri;
+    const size_t out_bytes = (obj_out ? sizeof(double) * K : 0) + 16;
+    L->cands.reserve(in_bytes);
+    L->obj.reserve(sizeof(double) * K);
+    L->best.reserve(16);
+    // one pinned staging area and one copy: [x 8n][rp 4n][cp 4n][L 2 tri]
+    L->h_io.reserve(std::max(in_bytes, out_bytes));
+    unsigned char* h = (unsigned char*)L->h_io.p;
+    std::memcpy(h, x_inc, sizeof(double) * n);
+    std::memcpy(h + 8 * n, rp, sizeof(int32_t) * n);
+    std::memcpy(h + 12 * n, cp, sizeof(int32_t) * n);
+    std::memcpy(h + 16 * n, ltri, sizeof(int16_t) * tri);
+    HCK(hipMemcpyAsync(L->cands.p, h, in_bytes, hipMemcpyHostToDevice, s));
+    L->rmax.reserve(sizeof(double) * N);
+    HCK(hipMemcpyAsync(L->rmax.p, r_max, sizeof(double) * N, hipMemcpyHostToDevice, s));
+    double* d_prev = nullptr;
+    double* d_dlimT = nullptr;
+    if (prev) {
+        L->prev.reserve(sizeof(double) * three_n);
+        L->dlim.reserve(sizeof(double) * N);
+        L->dlimraw.reserve(sizeof(double) * N);
+        L->h_dlim.resize(N);
+        for (int i = 0; i < N; ++i) L->h_dlim[i] = dlim_threshold(d_lim[i]);
+        HCK(hipMemcpyAsync(L->prev.p, prev, sizeof(double) * three_n, hipMemcpyHostToDevice, s));
+        HCK(hipMemcpyAsync(L->dlim.p, L->h_dlim.data(), sizeof(double) * N, hipMemcpyHostToDevice, s));
+        HCK(hipMemcpyAsync(L->dlimraw.p, d_lim, sizeof(double) * N, hipMemcpyHostToDevice, s));
+        d_prev = L->prev.as<double>();
+        d_dlimT = L->dlim.as<double>();
+    }
+    unsigned char* d = (unsigned char*)L->cands.p;
+    CandSrc src{};
+    src.xinc = (const double*)d;
+    src.rp = (const int*)(d + 8 * n);
+    src.cp = (const int*)(d + 12 * n);
+    src.ltri = (const int16_t*)(d + 16 * n);
+    src.delta = delta;
+    src.b = bmax;
+    src.k0 = 0;
+    enqueue_eval(ctx, L, s, src, N, (int)K, use_tiled(ctx, N, nullptr, three_n), L->rmax.as<double>(),
+                 penalty, d_prev, d_dlimT, d_prev ? L->dlimraw.as<double>() : nullptr, tan_half_fov,
+                 nullptr, L->obj.as<double>(), L->best.as<double>(), 0);
+    // (the upload completed before the kernels ran: the staging takes the results)
+    double* ho = (double*)L->h_io.p;
+    double* hb = ho + (obj_out ? K : 0);
+    if (obj_out) HCK(hipMemcpyAsync(ho, L->obj.p, sizeof(double) * K, hipMemcpyDeviceToHost, s));
+    HCK(hipMemcpyAsync(hb, L->best.p, 16, hipMemcpyDeviceToHost, s));
+    HCK(hipStreamSynchronize(s));
+    if (obj_out) std::memcpy(obj_out, ho, sizeof(double) * K);
     if (best_obj) *best_obj = hb[0];
     if (best_idx) *best_idx = __builtin_bit_cast(int64_t, hb[1]);
     return MAC_OK;
@@ -1912,6 +1999,7 @@ struct mac_mads {
     uint64_t* d_slot = nullptr;
     uint64_t seq = 0;
     bool slotted = false;
+    int64_t slot_fallbacks = 0;   // slot waits that timed out (copy + sync instead)
     double* ext_best = nullptr;   // mac_mads_best_buffer: the polls' best goes here
     int64_t polled_b = 0;        // 2^ell of the poll awaiting its update (0: none)
     double h_enq = 0, h_perm = 0, h_wait = 0, h_post = 0;
@@ -1979,7 +2067,16 @@ static void mads_best_of(mac_mads* m, const CandSrc& src, int Kc, int64_t idx_ba
 static void mads_wait_best(mac_mads* m, double* obj, int64_t* idx, uint64_t* feas_cum = nullptr)
 {
     if (m->slotted) {
-        if (mirror_wait((const uint64_t*)m->hslot.p, m->seq, 50.0, obj, idx, feas_cum)) return;
+        // a slotted poll always hands finalize the stepper's d_feas (mads_best_of), so the check
+        // word folds in the feasible count of word 4: read it whether or not the caller wants it
+        // (with f = 0 the check never matched once a candidate had passed cons3, and every wait
+        // ran into the 50-ms limit: round 5's sharded-loop stall)
+        uint64_t fe = 0;
+        if (mirror_wait((const uint64_t*)m->hslot.p, m->seq, 50.0, obj, idx, &fe)) {
+            if (feas_cum) *feas_cum = fe;
+            return;
+        }
+        ++m->slot_fallbacks;
         HCK(hipMemcpyAsync(m->hb, mads_best_ptr(m), 16, hipMemcpyDeviceToHost, m->s));
     }
     HCK(hipStreamSynchronize(m->s));
@@ -2217,10 +2314,7 @@ int32_t mac_mads_poll_ahead(mac_mads* m, int32_t ahead, int32_t* done, double* b
     const uint64_t state = m->state + (uint64_t)ahead * m->per_iter * 0x9E3779B97F4A7C15ull;
     const int Kc = (int)(m->hi - m->lo);
     if (Kc == 0) return MAC_OK;
-    if (poll_rejected(m, b)) {
-        ++m->rejected;
-        return MAC_OK;
-    }
+    if (poll_rejected(m, b)) return MAC_OK;   // (counted by mac_mads_advance once applied)
     if (ahead == 0) {   // the current iteration's permutations are computed already
         std::copy(m->rp_next.begin(), m->rp_next.end(), m->hperm);
         std::copy(m->cp_next.begin(), m->cp_next.end(), m->hperm + n);
@@ -2260,6 +2354,9 @@ int32_t mac_mads_advance(mac_mads* m, double best_obj, int64_t best_idx, int32_t
     if (m->it >= m->prm.n_iter || m->ell < 0) return fail(MAC_E_INVAL, "mac_mads_advance past the loop's end");
     const int n = m->n;
     const int64_t b = (int64_t)1 << m->ell;
+    // the applied poll's whole-poll rejection, decided as mac_mads_poll does (the speculating ranks'
+    // own polls ahead are not counted: they may never be applied)
+    if (m->hi > m->lo && poll_rejected(m, b)) ++m->rejected;
     ++m->it;
     m->evals += m->K;
     const bool better = best_idx >= 0 && best_obj < m->f;
@@ -2308,6 +2405,7 @@ int32_t mac_mads_result(mac_mads* m, double* x_out, mac_mads_stats* st)
         st->feasible_evaluations = (int64_t)fe;
         st->rejected_polls = m->rejected;
         st->successes = m->succ;
+        st->slot_fallbacks = m->slot_fallbacks;
     }
     return MAC_OK;
     ABI_END
@@ -2841,6 +2939,34 @@ static int32_t poll_dev_check(mac_ctx* ctx, const void* d_cands, int64_t three_n
     return MAC_OK;
 }
 
+// d_best's mapped result slot {obj, idx, seq, check} (k_final.h): its own, else the least recently
+// used one (a fetch still waiting on a reassigned slot sees another seq and falls back to the
+// stream + copy). Returns the slot's device address and the seq the next write carries.
+static uint64_t* assign_mirror(mac_ctx* ctx, const void* d_best, uint64_t* seq)
+{
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (!ctx->d_mirror) {
+        const size_t b = sizeof(uint64_t) * 4 * mac_ctx::kMirrorSlots;
+        ctx->h_mirror.reserve(b, hipHostMallocMapped | hipHostMallocCoherent);
+        std::memset(ctx->h_mirror.p, 0, b);
+        void* dp = nullptr;
+        HCK(hipHostGetDevicePointer(&dp, ctx->h_mirror.p, 0));
+        ctx->d_mirror = (uint64_t*)dp;
+    }
+    int q = 0;
+    for (int j = 0; j < mac_ctx::kMirrorSlots; ++j) {
+        if (ctx->mirror_key[j] == d_best) {
+            q = j;
+            break;
+        }
+        if (ctx->mirror_used[j] < ctx->mirror_used[q]) q = j;
+    }
+    ctx->mirror_key[q] = d_best;
+    ctx->mirror_used[q] = ++ctx->mirror_clock;
+    *seq = ctx->mirror_want[q] = ++ctx->mirror_seq;
+    return ctx->d_mirror + 4 * q;
+}
+
 template <class T>
 static int32_t poll_best_dev(mac_ctx* ctx, const T* d_cands_in, int64_t three_n, int64_t K,
                              const double* d_rmax, double penalty, const T* d_prev_in,
@@ -2891,33 +3017,8 @@ static int32_t poll_best_dev(mac_ctx* ctx, const T* d_cands_in, int64_t three_n,
         L->obj.reserve(sizeof(double) * K);
         d_o = L->obj.as<double>();
     }
-    uint64_t* d_mirror = nullptr;
     uint64_t seq = 0;
-    {
-        // d_best's result slot: its own, else the least recently used one (a fetch still waiting
-        // on a reassigned slot sees another seq and falls back to the stream + copy)
-        std::lock_guard<std::mutex> lk(ctx->mu);
-        if (!ctx->d_mirror) {
-            const size_t b = sizeof(uint64_t) * 4 * mac_ctx::kMirrorSlots;
-            ctx->h_mirror.reserve(b, hipHostMallocMapped | hipHostMallocCoherent);
-            std::memset(ctx->h_mirror.p, 0, b);
-            void* dp = nullptr;
-            HCK(hipHostGetDevicePointer(&dp, ctx->h_mirror.p, 0));
-            ctx->d_mirror = (uint64_t*)dp;
-        }
-        int q = 0;
-        for (int j = 0; j < mac_ctx::kMirrorSlots; ++j) {
-            if (ctx->mirror_key[j] == d_best) {
-                q = j;
-                break;
-            }
-            if (ctx->mirror_used[j] < ctx->mirror_used[q]) q = j;
-        }
-        ctx->mirror_key[q] = d_best;
-        ctx->mirror_used[q] = ++ctx->mirror_clock;
-        seq = ctx->mirror_want[q] = ++ctx->mirror_seq;
-        d_mirror = ctx->d_mirror + 4 * q;
-    }
+    uint64_t* d_mirror = assign_mirror(ctx, d_best, &seq);
     enqueue_eval(ctx, L, s, matrix_src(d_cands, N), N, (int)K, use_tiled(ctx, N, nullptr, three_n), d_rmax,
                  penalty, d_prev, d_dlimT, d_dlim, tan_half_fov, nullptr, d_o, (double*)d_best, idx_base,
                  d_mirror, seq);
@@ -2966,8 +3067,11 @@ int32_t mac_poll_arm_dev_f64(mac_ctx* ctx, const double* d_cands, int64_t three_
     // every argument failure is reported before the wait goes into the stream
     int32_t rc = poll_dev_check(ctx, d_cands, three_n, K, d_prev, d_dlim, d_best);
     if (rc) return rc;
+    // not on HIP's null stream: until the fire, a wait there would block every blocking-stream
+    // operation of the process (the library's own synchronous copies, torch's .item() / .cpu())
+    if (!stream) return fail(MAC_E_INVAL, "an armed poll needs a stream (not HIP's null stream)");
     set_device(ctx);
-    hipStream_t s = (hipStream_t)stream;   // NULL: HIP's null stream
+    hipStream_t s = (hipStream_t)stream;
     uint64_t t = 0;
     {
         std::lock_guard<std::mutex> lk(ctx->mu);
@@ -3039,6 +3143,37 @@ int32_t mac_poll_best_dev_f32(mac_ctx* ctx, const float* d_cands, int64_t three_
     ABI_BEGIN
     return poll_best_dev<float>(ctx, d_cands, three_n, K, d_rmax, penalty, d_prev, d_dlim,
                                 tan_half_fov, idx_base, d_obj, d_best, stream);
+    ABI_END
+}
+
+int32_t mac_poll_basis_f64(mac_ctx* ctx, const double* x_inc, int64_t three_n, const int16_t* ltri,
+                           const int32_t* rp, const int32_t* cp, double delta, const double* r_max,
+                           double penalty, const double* prev, const double* d_lim, double tan_half_fov,
+                           double* obj_out, double* best_obj, int64_t* best_idx)
+{
+    ABI_BEGIN
+    return host_eval_basis(ctx, x_inc, three_n, ltri, rp, cp, delta, r_max, penalty, prev, d_lim,
+                           tan_half_fov, obj_out, best_obj, best_idx);
+    ABI_END
+}
+
+int32_t mac_best_reduce_dev(mac_ctx* ctx, const void* d_records, int32_t n_records, void* d_best,
+                            void* stream)
+{
+    ABI_BEGIN
+    if (!ctx) return fail(MAC_E_INVAL, "null context");
+    if (!d_best || (!d_records && n_records > 0)) return fail(MAC_E_INVAL, "null d_best / d_records");
+    if (n_records < 0) return fail(MAC_E_INVAL, "negative record count");
+    if ((((uintptr_t)d_records) | ((uintptr_t)d_best)) & 7)
+        return fail(MAC_E_INVAL, "records / d_best not 8-byte aligned");
+    set_device(ctx);
+    uint64_t seq = 0;
+    uint64_t* d_mirror = assign_mirror(ctx, d_best, &seq);
+    hipLaunchKernelGGL(best_reduce_kernel, dim3(1), dim3(kWave), 0, (hipStream_t)stream,
+                       (const unsigned long long*)d_records, (int)n_records, (unsigned long long*)d_best,
+                       d_mirror, seq);
+    HCK(hipGetLastError());
+    return MAC_OK;
     ABI_END
 }
 

@@ -69,14 +69,19 @@ def gather_best(best16, group=None):
 
 
 class PollGather:
-    """The strong-split poll's exchange without per-poll allocations or pageable copies: the
-    poll's 16-B d_best (device) goes into ONE all-gather into a persistent (world x 2) buffer,
-    ordered after the poll on torch's current stream (the caller's poll stream), and ONE pinned
-    host read of the world x 16 B result follows (the next poll's candidates depend on it).
-    RCCL (device buffers) on a GPU backend; on gloo (CPU rehearsal) d_best is first copied into
-    a persistent pinned CPU record. ``seconds`` / ``calls``: host time spent here per poll."""
+    """The multi-GPU poll's exchange without per-poll allocations or pageable copies: the poll's
+    16-B d_best (device) goes into ONE all-gather into a persistent (world x 2) buffer, ordered
+    after the poll on torch's current stream (the caller's poll stream).
 
-    def __init__(self, device, group=None):
+    With ``ctx`` (a libmaxcover Context on this rank's GPU) the world records are reduced ON THE
+    DEVICE: mac_best_reduce_dev (one wave, ordered after the collective on the same stream) writes
+    the lexicographic minimum to a persistent 16-B buffer and its mapped host slot, and
+    mac_best_fetch reads that slot as soon as it lands — no device-to-host copy, event or stream
+    synchronisation, no host argmin. Without ``ctx``: one pinned host read of the world x 16 B
+    and the minimum on the host. On gloo (CPU rehearsal) d_best is first copied into a persistent
+    pinned CPU record. ``seconds`` / ``calls``: host time spent here per poll."""
+
+    def __init__(self, device, group=None, ctx=None):
         import torch
         import torch.distributed as dist
 
@@ -92,6 +97,10 @@ class PollGather:
                      if self.on_device else self.out)
         self.rec = None if self.on_device else torch.empty(2, dtype=torch.float64, pin_memory=pin)
         self.done = torch.cuda.Event() if self.on_device else None
+        self.ctx = ctx if self.on_device else None
+        self.res = (torch.empty(2, dtype=torch.float64, device=self.device)
+                    if self.ctx is not None else None)
+        self._reduce = {}   # stream handle -> bound reduce + fetch (Context.reduce_step)
         self.seconds = 0.0
         self.calls = 0
 
@@ -101,6 +110,18 @@ class PollGather:
         import torch.distributed as dist
 
         t0 = time.perf_counter()
+        if self.ctx is not None:
+            dist.all_gather_into_tensor(self.out, best16.reshape(1, 2), group=self.group)
+            # (the collective's completion is ordered before torch's current stream's next work)
+            sh = int(torch.cuda.current_stream(self.device).cuda_stream)
+            step = self._reduce.get(sh)
+            if step is None:
+                step = self._reduce[sh] = self.ctx.reduce_step(self.out, self.world, self.res,
+                                                                stream=sh)
+            r = step()
+            self.seconds += time.perf_counter() - t0
+            self.calls += 1
+            return r
         if self.on_device:
             dist.all_gather_into_tensor(self.out, best16.reshape(1, 2), group=self.group)
             self.host.copy_(self.out, non_blocking=True)
@@ -290,6 +311,10 @@ def mads_loop_speculative(stepper, gather=None):
     x, st = stepper.result()
     st = dict(st)
     st["rounds"] = rounds
+    # the stepper's own counter holds every poll this rank ran ahead, applied or not; the loop's
+    # evaluations are the applied polls' (gathered from whichever rank ran them)
+    st["speculative_feasible_evaluations"] = st.get("feasible_evaluations", useful)
+    st["feasible_evaluations"] = useful
     st["useful_feasible_evaluations"] = useful
     return x, st
 

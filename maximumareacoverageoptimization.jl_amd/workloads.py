@@ -106,6 +106,13 @@ def ltmads_basis(n: int, ell: int, rng: SplitMix64) -> np.ndarray:
     """n x n integer LTMADS-style basis: lower-triangular L with diagonal +-2^ell and strictly
     lower entries uniform in (-2^ell, 2^ell), rows and columns randomly permuted (Audet & Dennis
     2006, LTMADS). Column k is poll direction b_k."""
+    Lm, rp, cp = ltmads_basis_parts(n, ell, rng)
+    return Lm[rp][:, cp]
+
+
+def ltmads_basis_parts(n: int, ell: int, rng: SplitMix64):
+    """(L, rp, cp) with ltmads_basis's draws (the same rng stream): B = L[rp][:, cp] — the basis
+    form mac_poll_basis_f64 takes (L lower triangular, rp / cp permutations)."""
     b = 2 ** ell
     Lm = np.zeros((n, n), dtype=np.int64)
     signs = np.where(rng.uniform(n) < 0.5, -1, 1)
@@ -115,7 +122,7 @@ def ltmads_basis(n: int, ell: int, rng: SplitMix64) -> np.ndarray:
         Lm[il] = rng.integers(-b + 1, b - 1, il[0].size)
     rp = rng.permutation(n)
     cp = rng.permutation(n)
-    return Lm[rp][:, cp]
+    return Lm, rp, cp
 
 
 def poll_candidates(x0: np.ndarray, rng: SplitMix64, ell: int = 2, delta: float = 1.0,

@@ -38,9 +38,11 @@ def nccl1(ctx):
     dist.destroy_process_group()
 
 
-def test_poll_gather_over_rccl(nccl1, ctx, pkg):
-    """PollGather (bench.py's strong step): each device poll's d_best goes through the RCCL
-    all-gather and the pinned record; the result equals the poll's own (objective, index) from
+@pytest.mark.parametrize("reduce", ["host", "device"])
+def test_poll_gather_over_rccl(nccl1, ctx, pkg, reduce):
+    """PollGather (bench.py's multi-GPU step): each device poll's d_best goes through the RCCL
+    all-gather and either the pinned record + host argmin or the device argmin
+    (mac_best_reduce_dev) + mapped slot; the result equals the poll's own (objective, index) from
     mac_poll_best_f64, poll after poll, with no allocation in between."""
     import torch
 
@@ -53,7 +55,7 @@ def test_poll_gather_over_rccl(nccl1, ctx, pkg):
     rmax = np.full(N, 30.0 * TAN50)
     d_rmax = torch.from_numpy(rmax).to(nccl1)
     d_best = torch.empty(2, dtype=torch.float64, device=nccl1)
-    gather = d.PollGather(nccl1)
+    gather = d.PollGather(nccl1, ctx=ctx if reduce == "device" else None)
     out_ptr = gather.out.data_ptr()
     # the polls and the gather on one stream of the caller's (as bench.py's ranks do); the
     # default-stream variant is the next test
@@ -69,7 +71,8 @@ def test_poll_gather_over_rccl(nccl1, ctx, pkg):
     assert gather.calls == 5 and gather.out.data_ptr() == out_ptr
 
 
-def test_poll_gather_over_rccl_default_stream(nccl1, ctx, pkg):
+@pytest.mark.parametrize("reduce", ["host", "device"])
+def test_poll_gather_over_rccl_default_stream(nccl1, ctx, pkg, reduce):
     """The same exchange with no stream of the caller's: the candidates are copied, the poll
     enqueued (stream=None) and the all-gather issued on torch's default stream, with no
     synchronisation in between. stream=None is torch's current stream, which here is HIP's null
@@ -87,7 +90,7 @@ def test_poll_gather_over_rccl_default_stream(nccl1, ctx, pkg):
     rmax = np.full(N, 30.0 * TAN50)
     d_rmax = torch.from_numpy(rmax).to(nccl1)
     d_best = torch.empty(2, dtype=torch.float64, device=nccl1)
-    gather = d.PollGather(nccl1)
+    gather = d.PollGather(nccl1, ctx=ctx if reduce == "device" else None)
     assert torch.cuda.current_stream(nccl1).cuda_stream == 0
     for t in range(6):
         C = wl.poll_candidates(wl.uniform_disks(N, 256, rng), rng)
@@ -124,6 +127,7 @@ def test_sharded_mads_loop_over_rccl(nccl1, ctx, pkg):
     assert np.array_equal(xs, want_x)
     assert stats["f"] == want["f"] and stats["iterations"] == want["iterations"]
     assert gather.calls == want["iterations"]
+    assert stats["slot_fallbacks"] == 0   # every poll's best read through the mapped slot
 
 
 def test_broadcast_points_over_rccl(nccl1, pkg):
@@ -135,3 +139,34 @@ def test_broadcast_points_over_rccl(nccl1, pkg):
     assert gx.device.type == "cuda"
     for a, b in ((gx, x), (gy, y), (gw, w)):
         assert np.array_equal(a.cpu().numpy(), b)
+
+
+def test_best_reduce_dev_matches_reduce_best(ctx, pkg):
+    """mac_best_reduce_dev (the device side of the multi-GPU exchange) against dist.reduce_best on
+    record sets with ties (lowest index wins), empty shards (index -1), +inf / NaN objectives
+    (never selected), -inf, no record at all and more records than one wave (130)."""
+    import torch
+
+    d = import_module(pkg.__name__ + ".dist")
+    dev = torch.device("cuda", 0)
+    cases = [
+        [(3.0, 7), (1.0, 9), (1.0, 4), (2.0, 1)],
+        [(np.inf, -1), (np.inf, -1)],
+        [(np.inf, 3), (np.nan, 2), (5.0, -1)],
+        [(-np.inf, 8), (-1e300, 2), (-np.inf, 5)],
+        [],
+        [(float(v), int(i)) for v, i in zip(np.random.default_rng(3).integers(0, 4, 130),
+                                            np.random.default_rng(4).permutation(130))],
+    ]
+    res = torch.empty(2, dtype=torch.float64, device=dev)
+    for recs in cases:
+        rec = torch.zeros((max(len(recs), 1), 2), dtype=torch.float64)
+        for j, (o, i) in enumerate(recs):
+            rec[j, 0] = o
+            rec.view(torch.int64)[j, 1] = i
+        drec = rec.to(dev)
+        ctx.best_reduce_dev(drec, len(recs), res, stream=0)
+        got = ctx.best_fetch(res, stream=0)
+        want = d.reduce_best([o for o, _ in recs], [i for _, i in recs])
+        assert got[1] == want[1] and (got[0] == want[0] or (want[1] < 0 and got[0] == np.inf)), \
+            (recs[:6], got, want)

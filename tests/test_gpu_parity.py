@@ -1039,12 +1039,17 @@ def test_native_mads_sharded_steppers(ctx, pkg, world):
         for s_ in steppers:
             s_.update(bo, bi)
     assert polls == want["iterations"] > 5
+    polls_or_rounds = polls
     for s_ in steppers:
         xs, st = s_.result()
         s_.close()
         assert np.array_equal(xs, want_x)
         assert st["f"] == want["f"] and st["iterations"] == want["iterations"]
         assert st["evaluations"] == want["evaluations"]
+        # every poll's result came through the mapped slot (round 5's check-word mismatch made each
+        # wait run into its 50-ms limit and fall back to a copy): no fallback, and no long waits
+        assert st["slot_fallbacks"] == 0
+        assert st["wait_s"] < 0.005 * max(polls_or_rounds, 1) + 0.05
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -1086,12 +1091,17 @@ def test_native_mads_speculative_steppers(ctx, pkg, world):
             break
     assert rounds < want["iterations"]
     assert useful == want["feasible_evaluations"]   # the applied polls' evaluations = the loop's
+    polls_or_rounds = rounds
     for s_ in steppers:
         xs, st = s_.result()
         s_.close()
         assert np.array_equal(xs, want_x)
         assert st["f"] == want["f"] and st["iterations"] == want["iterations"]
         assert st["evaluations"] == want["evaluations"]
+        # every poll's result came through the mapped slot (round 5's check-word mismatch made each
+        # wait run into its 50-ms limit and fall back to a copy): no fallback, and no long waits
+        assert st["slot_fallbacks"] == 0
+        assert st["wait_s"] < 0.005 * max(polls_or_rounds, 1) + 0.05
 
 
 def test_mads_best_buffer_device_exchange(ctx, pkg):
@@ -1251,6 +1261,8 @@ def test_armed_polls_match_plain_polls(pkg):
         assert len({o for o, _ in want}) > 1   # (different polls, different bests)
         with pytest.raises(pkg.MaxCoverError):
             ctx.poll_fire(10 ** 6)              # never armed
+        with pytest.raises(pkg.MaxCoverError):  # HIP's null stream refused (nothing enqueued)
+            ctx.poll_arm(d_polls[0], 3 * N, K, d_rmax, bests[1], stream=0)
     with pkg.Context(0) as ctx2:                # destroyed with an armed poll never fired
         ctx2.set_points(x, y, w)
         ctx2.poll_arm(d_polls[0], 3 * N, K, d_rmax, bests[1], stream=stream.cuda_stream)
@@ -1300,3 +1312,74 @@ def test_armed_poll_grows_lane_buffers(pkg):
                           stream=s1.cuda_stream)
         assert ctx.best_fetch(bests[2], stream=s1.cuda_stream) == want[2]
     torch.cuda.synchronize(dev)
+
+
+@pytest.mark.parametrize("cons3", [False, True])
+def test_config4_basis_form_poll(ctx, pkg, orc, cons3):
+    """mac_poll_basis_f64 at config 4 (512 UAVs x 16.8M cells, n = 1536, 2n = 3072 candidates):
+    the incumbent, the LTMADS basis as L's packed lower triangle plus its row / column permutations
+    and delta (src/TDM_STATIC_opt.jl:22-44's b / i / maximal_basis) expanded on the device. Every
+    objective equals -25 x the exact lattice count + 1e5 x the oracle's sequential violation (or
+    +inf where the oracle's cons3 fails), bit for bit, and equals mac_poll_best_f64 on the 3N x 2n
+    matrix the same arithmetic builds; the argmin is the lowest minimiser."""
+    wl = pkg.workloads
+    rng = wl.SplitMix64(wl.SEED + 61)
+    x, y, w = wl.grid_points(4096)
+    ctx.set_points(x, y, w)
+    N = 512
+    x0 = wl.uniform_disks(N, 4096, rng)
+    n = 3 * N
+    # (cons3: mesh step 8 = ell 3, where some candidates move a UAV more than d_lim = 10 m; at the
+    # bench's ell = 2 every candidate passes)
+    Lm, rp, cp = wl.ltmads_basis_parts(n, 3 if cons3 else 2, rng)
+    B = Lm[rp][:, cp].astype(np.float64)
+    delta = 1.0
+    C = np.ascontiguousarray(np.concatenate([x0[None, :] + delta * B.T, x0[None, :] - delta * B.T]))
+    rmax = np.full(N, 30.0 * TAN50)
+    kw = dict(prev=x0, d_lim=np.full(N, 10.0), tan_half_fov=TAN50) if cons3 else {}
+    bo, bi, objs = ctx.poll_basis(x0, Lm, rp, cp, delta, rmax, 1e5, want_all=True, **kw)
+    mo, mi, mobjs = ctx.poll_best(C, rmax, 1e5, want_all=True, **kw)
+    assert np.array_equal(objs, mobjs) and (bo, bi) == (mo, mi)
+    want = -25.0 * orc.lattice_count_batch(C, 4096).astype(np.float64) + orc.violation_batch(C, rmax) * 1e5
+    if cons3:
+        feas = orc.cons3_batch(x0, C, np.full(N, 10.0), TAN50)
+        assert 0 < int(feas.sum()) < C.shape[0]
+        want = np.where(feas, want, np.inf)
+    assert np.array_equal(objs, want), np.flatnonzero(objs != want)[:5]
+    k = int(np.argmin(want))
+    assert bi == k and bo == want[k]
+
+
+def test_basis_form_scaled_and_rejected(ctx, pkg, orc):
+    """The basis form off the unit mesh: delta = 0.75 and 2.5 (B's entries delta * L as doubles,
+    matrix built with the same products), a small N through the generic walks; and argument
+    errors (a permutation entry outside [0, n), a packed triangle of the wrong size) refused
+    before anything runs."""
+    wl = pkg.workloads
+    rng = wl.SplitMix64(77)
+    x, y, w = wl.grid_points(256)
+    ctx.set_points(x, y, w)
+    N = 12
+    x0 = wl.uniform_disks(N, 256, rng)
+    n = 3 * N
+    rmax = np.full(N, 30.0 * TAN50)
+    for delta in (0.75, 2.5):
+        Lm, rp, cp = wl.ltmads_basis_parts(n, 3, rng)
+        Bd = delta * Lm[rp][:, cp].astype(np.float64)
+        C = np.ascontiguousarray(np.concatenate([x0[None, :] + Bd.T, x0[None, :] - Bd.T]))
+        for algo in ("auto", "poll", "tiled"):
+            ctx.set_algo(algo)
+            got = ctx.poll_basis(x0, Lm, rp, cp, delta, rmax, want_all=True)
+            want = ctx.poll_best(C, rmax, want_all=True)
+            assert got[:2] == want[:2] and np.array_equal(got[2], want[2]), (delta, algo)
+        ctx.set_algo("auto")
+        rec = np.stack([x, y, w, w, np.zeros_like(x)], axis=1)
+        viol = orc.violation_batch(C, rmax) * 1e5
+        for k in np.unique(np.floor(rng.uniform(6) * C.shape[0]).astype(np.int64)):
+            assert got[2][k] == -orc.ref_area(C[k], rec) + viol[k], (delta, k)
+    bad = rp.copy()
+    bad[3] = n
+    with pytest.raises(pkg.MaxCoverError):
+        ctx.poll_basis(x0, Lm, bad, cp, 1.0, rmax)
+    with pytest.raises(ValueError):
+        ctx.poll_basis(x0, Lm[np.tril_indices(n)][:-1], rp, cp, 1.0, rmax)

@@ -90,11 +90,13 @@ for s in $STEPS; do
     c5x2)    # rehearsal of the N=2 config-5 path (sharded MADS) on one GPU (gloo; both ranks on device 0)
         MAXCOVER_BENCH_DEVICE=0 run c5x2 400 python -m torch.distributed.run --nnodes=1 \
             --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 \
-            --config 5 --no-cpu --dist-backend gloo --steps 2 --warmup 1 ; rc=$? ;;
+            --config 5 --no-cpu --dist-backend gloo --steps 2 --warmup 1 --mads-mode shard ; rc=$?
+        grep '^{' gpurun_out/c5x2.log > gpurun_out/c5x2_${TAG}.json ;;
     c5x2s)   # the speculative N=2 config-5 loop on one GPU (gloo; both ranks on device 0)
         MAXCOVER_BENCH_DEVICE=0 run c5x2s 400 python -m torch.distributed.run --nnodes=1 \
             --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 2 \
-            --config 5 --no-cpu --dist-backend gloo --steps 2 --warmup 1 --mads-mode speculate ; rc=$? ;;
+            --config 5 --no-cpu --dist-backend gloo --steps 2 --warmup 1 --mads-mode speculate ; rc=$?
+        grep '^{' gpurun_out/c5x2s.log > gpurun_out/c5x2s_${TAG}.json ;;
     probe)
         { nproc; python3 -c "import os; print(os.cpu_count(), len(os.sched_getaffinity(0)))";
           cat /sys/fs/cgroup/cpu.max 2>/dev/null; lscpu | grep -E 'Model name|Socket|Core|Thread'; 

@@ -85,6 +85,32 @@ def main():
         torch.cuda.current_stream(dev).synchronize()
     out["poll_plus_sync_us"] = (time.perf_counter() - t0) / n * 1e6
 
+    # the device-reduced exchange: all-gather, one-wave argmin, mapped-slot read (no copy/sync)
+    pgd = pd.PollGather(dev, ctx=ctx)
+    for _ in range(50):
+        pgd(best)
+    pgd.seconds, pgd.calls = 0.0, 0
+    t0 = time.perf_counter()
+    for _ in range(args.calls):
+        pgd(best)
+    out["poll_gather_device_reduce_us"] = (time.perf_counter() - t0) / args.calls * 1e6
+    for _ in range(20):
+        ctx.poll_best_dev(tC, n3, K, tR, d_best, 1e5, stream=st)
+        pgd(d_best)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        ctx.poll_best_dev(tC, n3, K, tR, d_best, 1e5, stream=st)
+        pgd(d_best)
+    out["poll_plus_device_gather_us"] = (time.perf_counter() - t0) / n * 1e6
+    # the poll alone through its own mapped slot (the 1-GPU step)
+    step1 = ctx.poll_step(tC, n3, K, tR, d_best, 1e5, stream=st)
+    for _ in range(20):
+        step1()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        step1()
+    out["poll_step_us"] = (time.perf_counter() - t0) / n * 1e6
+
     dg = pd.DeviceGather(dev)
     for _ in range(50):
         dg(1.0, 0)
