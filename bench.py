@@ -545,6 +545,11 @@ def main():
                          "result is read (mac_poll_arm_dev_f64 / mac_poll_fire). Measured at "
                          "config 4: 0.0895 (plain) vs 0.0905 ms (armed): the stream's wait "
                          "releases the chain no sooner than a fresh launch starts it")
+    ap.add_argument("--exchange", default="rccl", choices=("rccl", "torch"),
+                    help="N>1 over RCCL: rccl (default) = libmaxcover's own communicator, the "
+                         "all-gather on the poll's stream and the device argmin in one C call "
+                         "(dist.RcclExchange); torch = torch.distributed's all-gather, then the "
+                         "device argmin (dist.PollGather)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL on ROCm) for the real multi-GPU run; gloo only to rehearse "
                          "N>1 with several ranks sharing one GPU (MAXCOVER_BENCH_DEVICE)")
@@ -658,8 +663,18 @@ def main():
 
     # N > 1: the 16-B all-gather straight from d_best, ordered after the poll on its stream,
     # and one pinned host read of the world x 16-B result (dist.PollGather)
-    gat = (pdist.PollGather(coll_dev, ctx=ctx if coll_dev.type == "cuda" else None)
-           if distributed else None)
+    # (RCCL: libmaxcover's own communicator, the all-gather on the poll's stream, dist.RcclExchange;
+    # --exchange torch: torch's collective + the device argmin; gloo rehearsals: PollGather's host path)
+    if distributed and coll_dev.type == "cuda" and args.exchange == "rccl":
+        gat = pdist.RcclExchange(ctx, coll_dev)
+    elif distributed:
+        gat = pdist.PollGather(coll_dev, ctx=ctx if coll_dev.type == "cuda" else None)
+    else:
+        gat = None
+    xsteps = ([ctx.poll_step(d, 3 * N, Kl, d_rmax, d_best, d_prev=pv, d_dlim=d_dlim,
+                             tan_half_fov=tan_half, idx_base=idx_base, stream=s_handle, fetch=False)
+               for d, pv in zip(d_polls, d_prevs)] if isinstance(gat, pdist.RcclExchange) else None)
+    xchg = gat.step_for(d_best, s_handle) if isinstance(gat, pdist.RcclExchange) else None
     # one GPU, armed: poll j + 1 is enqueued behind the doorbell while poll j runs (its inputs are
     # resident; a MADS driver fills them once poll j's result is known) and released right after
     # that result is read, so no launch sits between dependent polls. Consecutive polls alternate
@@ -688,6 +703,13 @@ def main():
     def step(i):
         """One MADS poll. It ends with the best (objective, index) on the host, because the
         next poll's candidates depend on it: polls never overlap."""
+        if xsteps is not None:   # two prebuilt C calls: the poll, then the exchange
+            xsteps[i % len(xsteps)]()
+            t_x = time.perf_counter()
+            r = xchg()
+            gat.seconds += time.perf_counter() - t_x
+            gat.calls += 1
+            return r
         if distributed:
             d = d_polls[i % len(d_polls)]
             ctx.poll_best_dev(d, 3 * N, Kl, d_rmax, d_best, d_prev=d_prevs[i % len(d_polls)],

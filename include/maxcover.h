@@ -305,6 +305,22 @@ int32_t mac_best_fetch(mac_ctx* ctx, const void* d_best, void* stream, double* b
 int32_t mac_best_reduce_dev(mac_ctx* ctx, const void* d_records, int32_t n_records, void* d_best,
                             void* stream);
 
+/* The multi-GPU poll exchange over RCCL (xGMI) on the poll's own stream. librccl is bound at run
+ * time from rccl_path (the copy the process already loaded when it is loaded, e.g. torch's; NULL:
+ * librccl.so.1 from the library path).
+ *   mac_comm_unique_id  rank 0 makes the communicator id (128 bytes) the ranks share out of band;
+ *   mac_comm_init       every rank (collective) joins with its rank and the world size;
+ *   mac_poll_exchange   all-gathers every rank's 16-B {objective, index} record d_best into the
+ *                       context's buffer (ncclAllGather on `stream`, ordered after the rank's poll),
+ *                       reduces it on the device as mac_best_reduce_dev into d_out and its mapped
+ *                       slot, and (best_obj / best_idx non-null) returns the node's argmin from the
+ *                       slot as mac_best_fetch does. Collective: every rank calls it per poll.
+ * The communicator is destroyed with the context. */
+int32_t mac_comm_unique_id(const char* rccl_path, void* id_out);
+int32_t mac_comm_init(mac_ctx* ctx, const char* rccl_path, const void* id, int32_t rank, int32_t world);
+int32_t mac_poll_exchange(mac_ctx* ctx, const void* d_best, void* d_out, void* stream, double* best_obj,
+                          int64_t* best_idx);
+
 /* Armed device polls: the host turnaround between dependent polls of a MADS loop (the next poll
  * is known only after the previous one's result) taken off the device's critical path. The
  * chain of mac_poll_best_dev_f64 is enqueued ahead of time behind a stream wait on the context's

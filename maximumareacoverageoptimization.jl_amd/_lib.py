@@ -69,6 +69,7 @@ EXPORTS = (
     "mac_mads_begin", "mac_mads_poll", "mac_mads_update", "mac_mads_result", "mac_mads_destroy",
     "mac_mads_poll_ahead", "mac_mads_advance",
     "mac_mads_best_buffer", "mac_best_reduce_dev", "mac_poll_basis_f64",
+    "mac_comm_unique_id", "mac_comm_init", "mac_poll_exchange",
 )
 
 
@@ -148,6 +149,9 @@ def _declare(L: ctypes.CDLL) -> None:
                                    ctypes.c_double, _i64, _vp, _vp, _vp], _i32),
         "mac_best_fetch": ([_vp, _vp, _vp, _dp, _i64p], _i32),
         "mac_best_reduce_dev": ([_vp, _vp, _i32, _vp, _vp], _i32),
+        "mac_comm_unique_id": ([ctypes.c_char_p, _vp], _i32),
+        "mac_comm_init": ([_vp, ctypes.c_char_p, _vp, _i32, _i32], _i32),
+        "mac_poll_exchange": ([_vp, _vp, _vp, _vp, _dp, _i64p], _i32),
         "mac_poll_basis_f64": ([_vp, _dp, _i64, ctypes.POINTER(ctypes.c_int16),
                                 ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                                 ctypes.c_double, _dp, ctypes.c_double, _dp, _dp, ctypes.c_double,
@@ -638,7 +642,7 @@ class Context:
 
     def poll_step(self, d_cands, three_n: int, K: int, d_rmax, d_best, penalty: float = 1e5,
                   d_prev=None, d_dlim=None, tan_half_fov: float = 1.0, idx_base: int = 0,
-                  d_obj=None, stream=None):
+                  d_obj=None, stream=None, fetch: bool = True):
         """A bound device poll: returns a zero-argument callable that enqueues the poll
         (mac_poll_best_dev_f64) and returns its (objective, index) (mac_best_fetch). The ctypes
         arguments are built once, so a step costs two foreign calls and nothing else on the
@@ -652,18 +656,23 @@ class Context:
         bo, bi = ctypes.c_double(), ctypes.c_int64()
         fetch_args = (h, _vp(_devptr(d_best)), _vp(_stream(stream, self.device)), ctypes.byref(bo),
                       ctypes.byref(bi))
-        poll, fetch = self._L.mac_poll_best_dev_f64, self._L.mac_best_fetch
+        poll, fetch_f = self._L.mac_poll_best_dev_f64, self._L.mac_best_fetch
 
         def step():
             rc = poll(*poll_args)
             if rc != MAC_OK:
                 _check(rc)
-            rc = fetch(*fetch_args)
+            rc = fetch_f(*fetch_args)
             if rc != MAC_OK:
                 _check(rc)
             return bo.value, bi.value
 
-        return step
+        def enqueue():
+            rc = poll(*poll_args)
+            if rc != MAC_OK:
+                _check(rc)
+
+        return step if fetch else enqueue
 
     def poll_arm(self, d_cands, three_n: int, K: int, d_rmax, d_best, penalty: float = 1e5,
                  d_prev=None, d_dlim=None, tan_half_fov: float = 1.0, idx_base: int = 0,
@@ -726,6 +735,39 @@ class Context:
         records (device) into d_best and its mapped slot, on ``stream`` (read it with best_fetch)."""
         _check(self._L.mac_best_reduce_dev(self._h, _devptr(d_records), int(n_records), _devptr(d_best),
                                            _stream(stream, self.device)))
+
+    # -- the multi-GPU poll exchange over RCCL on the poll's stream (mac_comm_*, mac_poll_exchange)
+    @staticmethod
+    def comm_unique_id(rccl_path: str | None = None) -> bytes:
+        """mac_comm_unique_id: a fresh 128-byte communicator id (rank 0 makes it)."""
+        buf = ctypes.create_string_buffer(128)
+        _check(load_library().mac_comm_unique_id(rccl_path.encode() if rccl_path else None, buf))
+        return buf.raw
+
+    def comm_init(self, uid: bytes, rank: int, world: int, rccl_path: str | None = None) -> None:
+        """mac_comm_init (collective over the ranks)."""
+        if len(uid) != 128:
+            raise ValueError("communicator id must be 128 bytes")
+        buf = ctypes.create_string_buffer(bytes(uid), 128)
+        _check(self._L.mac_comm_init(self._h, rccl_path.encode() if rccl_path else None, buf,
+                                     int(rank), int(world)))
+
+    def exchange_step(self, d_best, d_out, stream=None):
+        """A bound mac_poll_exchange (prebuilt ctypes arguments): returns a zero-argument callable
+        giving the node's (objective, index) over every rank's 16-B d_best."""
+        h = _vp(self._h.value if isinstance(self._h, _vp) else self._h)
+        bo, bi = ctypes.c_double(), ctypes.c_int64()
+        args = (h, _vp(_devptr(d_best)), _vp(_devptr(d_out)), _vp(_stream(stream, self.device)),
+                ctypes.byref(bo), ctypes.byref(bi))
+        f = self._L.mac_poll_exchange
+
+        def step():
+            rc = f(*args)
+            if rc != MAC_OK:
+                _check(rc)
+            return bo.value, bi.value
+
+        return step
 
     def reduce_step(self, d_records, n_records: int, d_best, stream=None):
         """A bound mac_best_reduce_dev + mac_best_fetch (prebuilt ctypes arguments): returns a

@@ -5,6 +5,7 @@
 // src/AreaCoverageCalculation.jl:63-110 (calculateArea). See DESIGN.md.
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
+#include <dlfcn.h>
 #include <linux/futex.h>
 #include <sys/syscall.h>
 #include <unistd.h>
@@ -171,10 +172,32 @@ struct Lane {
     int last_chain = 0;                        // the chain of the lane's last poll: 1 five-launch, 2 fused
 };
 
+// RCCL's C API, bound at run time from the librccl the process already uses (torch's, or the
+// system one): the multi-GPU poll exchange (mac_poll_exchange) issues its all-gather on the poll's
+// own stream. The few types it needs, by their published layout (rccl.h): ncclUniqueId is 128
+// opaque bytes, ncclComm_t a pointer, ncclUint8 = 1, ncclSuccess = 0.
+struct RcclUid {
+    char internal[128];
+};
+struct RcclApi {
+    void* lib = nullptr;
+    int (*get_unique_id)(RcclUid*) = nullptr;
+    int (*comm_init_rank)(void**, int, RcclUid, int) = nullptr;
+    int (*all_gather)(const void*, void*, size_t, int, void*, hipStream_t) = nullptr;
+    int (*comm_destroy)(void*) = nullptr;
+    const char* (*error_string)(int) = nullptr;
+};
+
 struct mac_ctx {
     int device = 0;
     int cus = 256;
     std::mutex mu;
+    // the multi-GPU poll exchange (mac_comm_init): an RCCL communicator over the node's ranks and
+    // the world x 16-B gather buffer
+    RcclApi* rccl = nullptr;
+    void* comm = nullptr;
+    int comm_rank = 0, comm_world = 0;
+    void* d_xrec = nullptr;
     // the fused chain's routing history over every lane's polls (enqueue_eval): bit q set when the
     // q-th last reported poll did not suit it (a workload property: a MADS stepper or a new lane
     // takes it over from the lanes before it)
@@ -1561,6 +1584,8 @@ void mac_ctx_destroy(mac_ctx* ctx)
         ctx->fired = ctx->armed;
     }
     (void)hipDeviceSynchronize();
+    if (ctx->comm) (void)ctx->rccl->comm_destroy(ctx->comm);
+    if (ctx->d_xrec) (void)hipFree(ctx->d_xrec);
     free_deferred(ctx);
     if (ctx->doorbell) (void)hipHostFree(ctx->doorbell);
     ctx->h_mirror.release();
@@ -3174,6 +3199,112 @@ int32_t mac_best_reduce_dev(mac_ctx* ctx, const void* d_records, int32_t n_recor
                        d_mirror, seq);
     HCK(hipGetLastError());
     return MAC_OK;
+    ABI_END
+}
+
+// librccl bound once per path (the process keeps it: RCCL is never unloaded under live comms)
+static RcclApi* rccl_api(const char* path)
+{
+    static std::mutex mu;
+    static std::vector<std::pair<std::string, RcclApi*>> apis;
+    std::lock_guard<std::mutex> lk(mu);
+    const std::string key = path ? path : "";
+    for (auto& a : apis)
+        if (a.first == key) return a.second;
+    void* h = nullptr;
+    if (path && *path) {
+        h = dlopen(path, RTLD_NOW | RTLD_LOCAL | RTLD_NOLOAD);   // the copy already loaded (torch's)
+        if (!h) h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+    } else {
+        h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    }
+    if (!h) return nullptr;
+    RcclApi* a = new RcclApi();
+    a->lib = h;
+    a->get_unique_id = (int (*)(RcclUid*))dlsym(h, "ncclGetUniqueId");
+    a->comm_init_rank = (int (*)(void**, int, RcclUid, int))dlsym(h, "ncclCommInitRank");
+    a->all_gather = (int (*)(const void*, void*, size_t, int, void*, hipStream_t))dlsym(h, "ncclAllGather");
+    a->comm_destroy = (int (*)(void*))dlsym(h, "ncclCommDestroy");
+    a->error_string = (const char* (*)(int))dlsym(h, "ncclGetErrorString");
+    if (!a->get_unique_id || !a->comm_init_rank || !a->all_gather || !a->comm_destroy) {
+        delete a;
+        return nullptr;
+    }
+    apis.push_back({key, a});
+    return a;
+}
+
+static int32_t rccl_fail(RcclApi* a, int r, const char* what)
+{
+    std::string m = std::string(what) + ": RCCL error " + std::to_string(r);
+    if (a && a->error_string) m += std::string(" (") + a->error_string(r) + ")";
+    return fail(MAC_E_HIP, m.c_str());
+}
+
+int32_t mac_comm_unique_id(const char* rccl_path, void* id_out)
+{
+    ABI_BEGIN
+    if (!id_out) return fail(MAC_E_INVAL, "null id");
+    RcclApi* a = rccl_api(rccl_path);
+    if (!a) return fail(MAC_E_HIP, "cannot load librccl");
+    RcclUid id{};
+    const int r = a->get_unique_id(&id);
+    if (r) return rccl_fail(a, r, "ncclGetUniqueId");
+    std::memcpy(id_out, &id, sizeof(id));
+    return MAC_OK;
+    ABI_END
+}
+
+int32_t mac_comm_init(mac_ctx* ctx, const char* rccl_path, const void* id, int32_t rank, int32_t world)
+{
+    ABI_BEGIN
+    if (!ctx || !id) return fail(MAC_E_INVAL, "null context / id");
+    if (world < 1 || rank < 0 || rank >= world) return fail(MAC_E_INVAL, "bad rank / world");
+    if (ctx->comm) return fail(MAC_E_INVAL, "communicator already set");
+    RcclApi* a = rccl_api(rccl_path);
+    if (!a) return fail(MAC_E_HIP, "cannot load librccl");
+    set_device(ctx);
+    RcclUid uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    void* comm = nullptr;
+    const int r = a->comm_init_rank(&comm, world, uid, rank);   // (collective: every rank calls it)
+    if (r) return rccl_fail(a, r, "ncclCommInitRank");
+    void* buf = nullptr;
+    if (hipMalloc(&buf, 16 * (size_t)world) != hipSuccess) {
+        (void)a->comm_destroy(comm);
+        return fail(MAC_E_NOMEM, "exchange buffer");
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->rccl = a;
+    ctx->comm = comm;
+    ctx->comm_rank = rank;
+    ctx->comm_world = world;
+    ctx->d_xrec = buf;
+    return MAC_OK;
+    ABI_END
+}
+
+int32_t mac_poll_exchange(mac_ctx* ctx, const void* d_best, void* d_out, void* stream, double* best_obj,
+                          int64_t* best_idx)
+{
+    ABI_BEGIN
+    if (!ctx || !d_best || !d_out) return fail(MAC_E_INVAL, "null argument");
+    if (!ctx->comm) return fail(MAC_E_INVAL, "no communicator (mac_comm_init)");
+    if ((((uintptr_t)d_best) | ((uintptr_t)d_out)) & 7) return fail(MAC_E_INVAL, "records not 8-byte aligned");
+    set_device(ctx);
+    hipStream_t s = (hipStream_t)stream;
+    // every rank's 16-B record into the gather buffer, on the poll's stream (RCCL over xGMI), then
+    // one wave's argmin into d_out and its mapped slot, then the slot read (mac_best_fetch)
+    const int r = ctx->rccl->all_gather(d_best, ctx->d_xrec, 16, 1 /* ncclUint8 */, ctx->comm, s);
+    if (r) return rccl_fail(ctx->rccl, r, "ncclAllGather");
+    uint64_t seq = 0;
+    uint64_t* d_mirror = assign_mirror(ctx, d_out, &seq);
+    hipLaunchKernelGGL(best_reduce_kernel, dim3(1), dim3(kWave), 0, s, (const unsigned long long*)ctx->d_xrec,
+                       ctx->comm_world, (unsigned long long*)d_out, d_mirror, seq);
+    HCK(hipGetLastError());
+    if (!best_obj && !best_idx) return MAC_OK;
+    return mac_best_fetch(ctx, d_out, stream, best_obj, best_idx);
     ABI_END
 }
 

@@ -137,6 +137,69 @@ class PollGather:
         return r
 
 
+def rccl_path():
+    """The librccl this process's torch uses (so libmaxcover binds the same RCCL), or None."""
+    import os
+    import torch
+
+    p = os.path.join(os.path.dirname(os.path.abspath(torch.__file__)), "lib", "librccl.so")
+    return p if os.path.exists(p) else None
+
+
+class RcclExchange:
+    """The multi-GPU poll's exchange inside libmaxcover (mac_poll_exchange): its own RCCL
+    communicator over the group's ranks (the id made by rank 0 and broadcast once), then per poll
+    ONE C call that enqueues the all-gather of the rank's 16-B d_best on the poll's stream (RCCL over
+    xGMI, no cross-stream event as torch's collectives need), the one-wave device argmin into a
+    persistent 16-B buffer and its mapped host slot, and reads the slot. ``seconds`` / ``calls``:
+    host time spent here per poll. Needs a GPU backend (the ranks' devices)."""
+
+    def __init__(self, ctx, device, group=None):
+        import time
+        import torch
+        import torch.distributed as dist
+
+        check_one_runtime()
+        t0 = time.perf_counter()
+        self.ctx = ctx
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.device = torch.device(device)
+        path = rccl_path()
+        uid = torch.zeros(128, dtype=torch.uint8, device=self.device)
+        if self.rank == 0:
+            uid.copy_(torch.tensor(list(ctx.comm_unique_id(path)), dtype=torch.uint8))
+        dist.broadcast(uid, 0, group=group)
+        ctx.comm_init(bytes(uid.cpu().tolist()), self.rank, self.world, path)
+        self.res = torch.empty(2, dtype=torch.float64, device=self.device)
+        self._steps = {}
+        self.init_s = time.perf_counter() - t0
+        self.seconds = 0.0
+        self.calls = 0
+
+    def step_for(self, best16, stream=None):
+        """The bound exchange of best16 on ``stream`` (a raw handle; None: torch's current stream):
+        a zero-argument callable returning the node's (objective, index)."""
+        import torch
+
+        sh = int(torch.cuda.current_stream(self.device).cuda_stream) if stream is None else int(stream)
+        key = (int(best16.data_ptr()), sh)
+        st = self._steps.get(key)
+        if st is None:
+            st = self._steps[key] = self.ctx.exchange_step(best16, self.res, stream=sh)
+        return st
+
+    def __call__(self, best16):
+        import time
+
+        t0 = time.perf_counter()
+        r = self.step_for(best16)()
+        self.seconds += time.perf_counter() - t0
+        self.calls += 1
+        return r
+
+
 class DeviceGather:
     """The per-iteration exchange of the sharded MADS loop without per-iteration allocations:
     on a GPU backend (RCCL) the stepper's polls write their 16-B shard best straight into a

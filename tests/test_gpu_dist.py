@@ -170,3 +170,44 @@ def test_best_reduce_dev_matches_reduce_best(ctx, pkg):
         want = d.reduce_best([o for o, _ in recs], [i for _, i in recs])
         assert got[1] == want[1] and (got[0] == want[0] or (want[1] < 0 and got[0] == np.inf)), \
             (recs[:6], got, want)
+
+
+def test_rccl_exchange_in_library(nccl1, ctx, pkg):
+    """dist.RcclExchange (bench.py's default multi-GPU step over RCCL): libmaxcover's own RCCL
+    communicator (id from rank 0, broadcast once), then per poll one C call — the all-gather of the
+    16-B d_best on the poll's stream, the device argmin and the mapped-slot read. Poll after poll
+    its (objective, index) equals mac_poll_best_f64's, on a caller's stream and on torch's default
+    (null) stream, with and without cons3."""
+    import torch
+
+    d = import_module(pkg.__name__ + ".dist")
+    wl = pkg.workloads
+    x, y, w = wl.grid_points(256)
+    with pkg.Context(0) as c2:   # (a context of its own: the communicator lives with it)
+        c2.set_points(x, y, w)
+        ex = d.RcclExchange(c2, nccl1)
+        rng = wl.SplitMix64(73)
+        N = 16
+        rmax = np.full(N, 30.0 * TAN50)
+        d_rmax = torch.from_numpy(rmax).to(nccl1)
+        d_best = torch.empty(2, dtype=torch.float64, device=nccl1)
+        s = torch.cuda.Stream(nccl1)
+        for t in range(6):
+            C = wl.poll_candidates(wl.uniform_disks(N, 256, rng), rng, ell=3)
+            kw = dict(prev=C[0], d_lim=np.full(N, 10.0), tan_half_fov=TAN50) if t % 2 else {}
+            want = c2.poll_best(C, rmax, 1e5, **kw)
+            d_c = torch.from_numpy(np.ascontiguousarray(C)).to(nccl1)
+            dkw = dict(d_prev=torch.from_numpy(C[0].copy()).to(nccl1),
+                       d_dlim=torch.full((N,), 10.0, dtype=torch.float64, device=nccl1),
+                       tan_half_fov=TAN50) if t % 2 else {}
+            if t < 3:
+                with torch.cuda.stream(s):
+                    c2.poll_best_dev(d_c, 3 * N, C.shape[0], d_rmax, d_best, stream=s.cuda_stream, **dkw)
+                    got = ex(d_best)
+            else:
+                torch.cuda.synchronize()
+                c2.poll_best_dev(d_c, 3 * N, C.shape[0], d_rmax, d_best, **dkw)   # torch's default stream
+                got = ex(d_best)
+            assert got == (want[0], want[1]), (t, got, want)
+        assert ex.calls == 6
+        torch.cuda.synchronize()

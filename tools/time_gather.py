@@ -111,6 +111,29 @@ def main():
         step1()
     out["poll_step_us"] = (time.perf_counter() - t0) / n * 1e6
 
+    # libmaxcover's own communicator: all-gather on the poll's stream + device argmin + slot, one C call
+    with pkg.Context(0) as cx:
+        cx.set_points(x, y, w)
+        rx = pd.RcclExchange(cx, dev)
+        xs = rx.step_for(best, st)
+        for _ in range(50):
+            xs()
+        t0 = time.perf_counter()
+        for _ in range(args.calls):
+            xs()
+        out["rccl_exchange_us"] = (time.perf_counter() - t0) / args.calls * 1e6
+        pstep = cx.poll_step(tC, n3, K, tR, d_best, 1e5, stream=st, fetch=False)
+        xs2 = rx.step_for(d_best, st)
+        for _ in range(20):
+            pstep()
+            xs2()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            pstep()
+            xs2()
+        out["poll_plus_rccl_exchange_us"] = (time.perf_counter() - t0) / n * 1e6
+        out["rccl_exchange_init_s"] = rx.init_s
+
     dg = pd.DeviceGather(dev)
     for _ in range(50):
         dg(1.0, 0)
