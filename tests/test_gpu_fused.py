@@ -177,3 +177,22 @@ def test_fused_prep_candidate_remainders(ctx, pkg, orc, extra):
     finally:
         ctx.set_chain("auto")
     assert "fiw_kernel" in kern, kern
+
+
+@pytest.mark.parametrize("chain", CHAINS, indirect=True)
+def test_large_counts_overflow_the_16bit_rows(ctx, pkg, orc, chain):
+    """Disks of R = 820 m on a 1024^2 grid at 5 m (about 84,000 entries each, more than a 16-bit
+    row holds): the fused chain's count rows carry 0xFFFF and the 32-bit overflow row (k_fiw.h),
+    and every area still equals 25 x the exact lattice count, with and without cons3, through
+    each chain."""
+    wl = pkg.workloads
+    rng = wl.SplitMix64(4242)
+    G, N = 1024, 16
+    x, y, w = wl.grid_points(G)
+    ctx.set_points(x, y, w)
+    x0 = wl.uniform_disks(N, G, rng, radius=820.0)
+    C = wl.poll_candidates(x0, rng, ell=2)
+    assert C.shape[0] >= 64
+    _full_poll_check(ctx, orc, C, np.full(N, 820.0), G, ["poll"], "r820-" + chain)
+    _, kern = _walks(ctx, C)
+    assert ("fiw_kernel" in kern) == (chain == "fused"), kern
