@@ -148,6 +148,9 @@ struct CandSrc {
     // (null: the stream). b is then a bound on |L| (the index's int16 table) and delta scales it.
     const int16_t* ltri;
     double delta;
+    // (host only) the chain a generated poll takes under MAC_CHAIN_AUTO: 1 = the five-launch chain
+    // (the host found the poll crowded: maxcover.hip host_crowded_disks), 0 = AUTO's history
+    int route_five;
     // Called at the top of every launch that reads the source: b = 2^ell from the device state;
     // false once the loop has stopped, or (launches after the prep: any_poll false) when the
     // prep rejected the poll whole (the launch returns at once). Uniform per workgroup.

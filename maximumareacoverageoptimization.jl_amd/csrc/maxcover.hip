@@ -696,7 +696,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                           (src.ltri ? (double)src.b * __builtin_fabs(src.delta) > 8.0 : src.b > 8);
     if (poll_possible && want_keys && N > 0 && M > 0 && K > 0 && K <= kFwMaxK + 1 &&
         ctx->chain != MAC_CHAIN_FIVE && walk_forced != kModeTiled &&
-        (ctx->chain == MAC_CHAIN_FUSED || !wide_gen)) {
+        (ctx->chain == MAC_CHAIN_FUSED || (!wide_gen && !src.route_five))) {
         ensure_hints(L);
         volatile int* hw = (volatile int*)L->h_dc.p;
         int bad_now = -1;   // the lane's last poll's report (a hint: it may be an older poll's)
@@ -1210,6 +1210,8 @@ static int32_t host_eval(mac_ctx* ctx, const T* cands, int64_t three_n, int64_t 
     return MAC_OK;
 }
 
+static int host_crowded_disks(const double* x, int N, double b, double S);
+
 // The basis form of a caller-owned poll (mac_poll_basis_f64): the incumbent, B = L[rp][:, cp] as L's
 // packed lower triangle (int16) with the two permutations, and delta; the 2n candidates
 // x + delta B[:, k], x - delta B[:, k] are expanded on the device (k_prep.h CandSrc.entry), so the
@@ -1281,6 +1283,7 @@ static int32_t host_eval_basis(mac_ctx* ctx, const double* x_inc, int64_t three_
     src.delta = delta;
     src.b = bmax;
     src.k0 = 0;
+    src.route_five = host_crowded_disks(x_inc, N, (double)bmax * std::fabs(delta), ctx->grid.S) > kBitsMinDisks;
     enqueue_eval(ctx, L, s, src, N, (int)K, use_tiled(ctx, N, nullptr, three_n), L->rmax.as<double>(),
                  penalty, d_prev, d_dlimT, d_prev ? L->dlimraw.as<double>() : nullptr, tan_half_fov,
                  nullptr, L->obj.as<double>(), L->best.as<double>(), 0);
@@ -2025,6 +2028,7 @@ struct mac_mads {
     uint64_t seq = 0;
     bool slotted = false;
     int64_t slot_fallbacks = 0;   // slot waits that timed out (copy + sync instead)
+    int route_five = 0;           // the polls are crowded (host_crowded_disks at begin): five-launch chain
     double* ext_best = nullptr;   // mac_mads_best_buffer: the polls' best goes here
     int64_t polled_b = 0;        // 2^ell of the poll awaiting its update (0: none)
     double h_enq = 0, h_perm = 0, h_wait = 0, h_post = 0;
@@ -2049,6 +2053,48 @@ static double* mads_best_ptr(mac_mads* m) { return m->ext_best ? m->ext_best : m
 // diag_rejects for each of the 3N variables: each is the diagonal of one column of B, so each
 // candidate carries one such step). Exact: the prep's cons3 would mark every candidate failed,
 // and the poll's result would be (+inf, -1).
+// Routing a generated poll from the poll itself (the native MADS driver knows its incumbent and mesh
+// step): the fused chain's superset boxes (k_fiw.h sup_box: every candidate's disk i lies within b of
+// the incumbent's per coordinate, so box i is within 2b + r_i of its centre, plus a tile of
+// rounding) overlap-tested by a sweep over the boxes sorted by their x start. More than
+// kBitsMinDisks disks with a lower-index neighbour is a crowded poll (the five-launch chain's
+// union pass decides its shared entries once; the fused chain would decide them per candidate in
+// place, 5-20x slower: tools/c5_route.py). Returns that count.
+static int host_crowded_disks(const double* x, int N, double b, double S)
+{
+    struct Bx {
+        double x0, x1, y0, y1;
+        int i;
+    };
+    std::vector<Bx> v;
+    v.reserve(N);
+    for (int i = 0; i < N; ++i) {
+        const double r = x[2 * N + i];
+        if (!(r + b > 0.0)) continue;   // covers nothing at any candidate
+        const double h = 2.0 * b + std::fabs(r) + S;
+        if (!std::isfinite(h) || !std::isfinite(x[i]) || !std::isfinite(x[N + i])) return N;   // (unknown)
+        v.push_back({x[i] - h, x[i] + h, x[N + i] - h, x[N + i] + h, i});
+    }
+    std::sort(v.begin(), v.end(), [](const Bx& a, const Bx& c) { return a.x0 < c.x0; });
+    std::vector<char> has(N, 0);
+    std::vector<int> act;   // boxes whose x range may still reach later starts
+    for (int q = 0; q < (int)v.size(); ++q) {
+        const Bx& c = v[q];
+        int w = 0;
+        for (int a : act) {
+            const Bx& o = v[a];
+            if (o.x1 < c.x0) continue;   // (dropped: no later box starts before it ends)
+            act[w++] = a;
+            if (o.y0 <= c.y1 && c.y0 <= o.y1) has[std::max(o.i, c.i)] = 1;
+        }
+        act.resize(w);
+        act.push_back(q);
+    }
+    int n = 0;
+    for (char h : has) n += h;
+    return n;
+}
+
 static bool poll_rejected(const mac_mads* m, int64_t b)
 {
     if (!m->d_prev) return false;
@@ -2195,6 +2241,9 @@ int32_t mac_mads_begin(mac_ctx* ctx, const double* x0, int64_t three_n, const do
         m->f = __builtin_bit_cast(int64_t, m->hb[1]) >= 0 ? m->hb[0] : INFINITY;
         m->evals = 1;
         m->ell = prm->ell0;
+        // the run's chain, from its first poll: x0 at mesh step 2^ell0 (the incumbent moves by a few
+        // steps over a run; crowding is a property of the UAVs' layout)
+        m->route_five = host_crowded_disks(x0, N, std::ldexp(1.0, prm->ell0), ctx->grid.S) > kBitsMinDisks ? 1 : 0;
         m->state = prm->seed;
         m->T = (uint64_t)n * (uint64_t)(n - 1) / 2;
         m->per_iter = (uint64_t)n + m->T + 2 * (uint64_t)n;   // ltmads_basis's draws
@@ -2258,6 +2307,7 @@ int32_t mac_mads_poll(mac_mads* m, int32_t* done, double* best_obj, int64_t* bes
         src.state = m->state;
         src.b = b;
         src.k0 = (int)m->lo;
+        src.route_five = m->route_five;
         mads_best_of(m, src, Kc, m->lo, true);
     }
     const auto tb = clk::now();
@@ -2361,6 +2411,7 @@ int32_t mac_mads_poll_ahead(mac_mads* m, int32_t ahead, int32_t* done, double* b
     src.state = state;
     src.b = b;
     src.k0 = (int)m->lo;
+    src.route_five = m->route_five;
     mads_best_of(m, src, Kc, m->lo, true);
     uint64_t fe = 0;
     mads_wait_best(m, best_obj, best_idx, &fe);
@@ -2552,6 +2603,7 @@ static void mads_run_pipelined(mac_mads* m)
         src.b = 0;   // from the device state
         src.k0 = 0;
         src.mst = dst;
+        src.route_five = m->route_five;
         FinBest fbm{};
         fbm.st = dst;
         fbm.x = src.xinc;
@@ -2735,6 +2787,8 @@ struct ClReq {
     int64_t three_n;
     double* out;
     std::atomic<int> state{0};   // 0 queued, 1 taken by a batch, 2 done
+    std::atomic<int> released{0};   // 1 once the leader no longer touches the request (after its
+                                    // futex wake): the owner's stack object may then go
     int32_t rc = MAC_OK;
     std::string err;
 };
@@ -2851,14 +2905,18 @@ int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, doubl
                 }
             if (next) cl_wake(&next->state);   // (under the lock: the request still exists)
         }
-        for (ClReq* q : batch) {   // (a request object lives until its state reads 2)
+        for (ClReq* q : batch) {   // (a request object lives until its released word reads 1)
             q->rc = brc;
             q->err = msg;
             q->state.store(2, std::memory_order_release);
             if (q != &r) cl_wake(&q->state);
+            q->released.store(1, std::memory_order_release);
         }
         spin = 0;
     }
+    // the leader that completed this request may still be between its state store and its wake
+    // (the futex word is this stack object): wait for its release, a few instructions away
+    while (r.released.load(std::memory_order_acquire) == 0) __builtin_ia32_pause();
     ctx->cl_active.fetch_sub(1);
     if (r.rc) return fail(r.rc, r.err);
     return MAC_OK;

@@ -196,3 +196,34 @@ def test_large_counts_overflow_the_16bit_rows(ctx, pkg, orc, chain):
     _full_poll_check(ctx, orc, C, np.full(N, 820.0), G, ["poll"], "r820-" + chain)
     _, kern = _walks(ctx, C)
     assert ("fiw_kernel" in kern) == (chain == "fused"), kern
+
+
+@pytest.mark.parametrize("disks", ["clustered", "uniform"])
+def test_native_mads_routes_from_the_poll(ctx, pkg, disks):
+    """The native MADS driver routes its generated polls from the poll (maxcover.hip
+    host_crowded_disks: the fused chain's superset boxes around the incumbent at the run's first
+    mesh step): a crowded layout (clustered disks, many disks with lower-index neighbours) runs
+    every poll through the five-launch chain from the first one — no fused launch, not even before
+    AUTO's history exists — and an uncrowded one (uniform disks) keeps the fused chain. Both end on
+    the same iterate as the same run forced through the five-launch chain."""
+    wl = pkg.workloads
+    G, N = 512, 64
+    x, y, w = wl.grid_points(G)
+    rng = wl.SplitMix64(515 if disks == "clustered" else 516)
+    x0 = (wl.clustered_disks if disks == "clustered" else wl.uniform_disks)(N, G, rng)
+    r_max = np.full(N, 30.0 * TAN50)
+    kw = dict(prev=x0, d_lim=np.full(N, 10.0), tan_half_fov=TAN50, n_iter=20, ell0=2, ell_max=5, seed=77)
+    with pkg.Context(0) as c2:   # (a fresh context: no routing history)
+        c2.set_points(x, y, w)
+        c2.profile(True)
+        c2.profile_read(reset=True)
+        xa, sa = c2.mads_run(x0, r_max, 1e5, **kw)
+        kern = {k: n for k, (ms, n) in c2.profile_kernels().items() if n}
+        c2.profile_read(reset=True)
+        c2.set_chain("five")
+        xb, sb = c2.mads_run(x0, r_max, 1e5, **kw)
+    assert np.array_equal(xa, xb) and sa["f"] == sb["f"]
+    if disks == "clustered":
+        assert "fiw_kernel" not in kern and kern.get("coverage_poll_kernel", 0) > 0, kern
+    else:
+        assert kern.get("fiw_kernel", 0) > 0, kern
