@@ -192,6 +192,11 @@ struct mac_ctx {
     int device = 0;
     int cus = 256;
     std::mutex mu;
+    // MAXCOVER_HOST_STATS=1: host time of a device poll call, split at its launches (printed at
+    // destroy): [0] entry -> prep launch call, [1] prep launch, [2] fiw launch, [3] fin2 launch
+    bool host_stats = false;
+    double hs_t[4] = {0, 0, 0, 0};
+    int64_t hs_n = 0;
     // the multi-GPU poll exchange (mac_comm_init): an RCCL communicator over the node's ranks and
     // the world x 16-B gather buffer
     RcclApi* rccl = nullptr;
@@ -605,6 +610,8 @@ static bool poll_walk_possible(const mac_ctx* ctx, int N, int K, bool tiled)
 // area_out/obj_out may be null; best may be null.
 // d_dlimT: cons3 thresholds per UAV (host calls), else d_dlim_raw: the raw d_lim, thresholded
 // where it is read (device calls).
+static thread_local std::chrono::steady_clock::time_point t_poll_entry;   // (MAXCOVER_HOST_STATS)
+
 static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& src, int N,
                          int K, bool tiled, const double* d_rmax, double penalty,
                          const double* d_prev, const double* d_dlimT, const double* d_dlim_raw,
@@ -750,9 +757,13 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             pr.feas = d_feas;
             pr.lreset = L->fwcount.as<int>();
             uint64_t* tsk = take_ts(nprep, ts_c, ts_nc);
+            using hclk = std::chrono::steady_clock;
+            hclk::time_point h1, h2, h3;
+            if (ctx->host_stats) h1 = hclk::now();
             if (xk) hipLaunchKernelGGL(prep_x_kernel, dim3((unsigned)nprep), dim3(kPrepU + kWave), 0, s, tsk, pr);
             else hipLaunchKernelGGL(prep_kernel, dim3((unsigned)nprep), dim3(kPrepU), 0, s, tsk, pr);
             HCK(hipGetLastError());
+            if (ctx->host_stats) h2 = hclk::now();
             FwArgs fa{};
             fa.src = src;
             fa.src.keysP = pr.keysP;
@@ -783,6 +794,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             if (counts) hipLaunchKernelGGL(fiw_kernel<true>, dim3(nfw), dim3(kFwThreads), 0, s, tsw, fa);
             else hipLaunchKernelGGL(fiw_kernel<false>, dim3(nfw), dim3(kFwThreads), 0, s, tsw, fa);
             HCK(hipGetLastError());
+            if (ctx->host_stats) h3 = hclk::now();
             const unsigned nfin = 8 * (unsigned)((K + 8 * kF2C - 1) / (8 * kF2C));
             FinBest fb{};
             if (d_best) {
@@ -809,6 +821,15 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
                 hipLaunchKernelGGL(fin2_kernel<false>, dim3(nfin), dim3(kF2Threads), 0, s, nullptr,
                                    L->frows.as<double>(), ldk, N, K, ctx->w0, d_vp, d_area, d_obj, fb, f2s, tsf);
             HCK(hipGetLastError());
+            if (ctx->host_stats) {
+                const auto h4 = hclk::now();
+                std::lock_guard<std::mutex> lk(ctx->mu);
+                ctx->hs_t[0] += std::chrono::duration<double>(h1 - t_poll_entry).count();
+                ctx->hs_t[1] += std::chrono::duration<double>(h2 - h1).count();
+                ctx->hs_t[2] += std::chrono::duration<double>(h3 - h2).count();
+                ctx->hs_t[3] += std::chrono::duration<double>(h4 - h3).count();
+                ++ctx->hs_n;
+            }
             L->last_chain = 2;
             prof_end();
             return;
@@ -1560,6 +1581,7 @@ int32_t mac_ctx_create(mac_ctx** out, int32_t device)
     if (device < 0 || device >= n) return fail(MAC_E_NODEVICE, "device index out of range");
     HCK(hipSetDevice(device));
     mac_ctx* ctx = new mac_ctx();
+    if (const char* e = std::getenv("MAXCOVER_HOST_STATS"); e && *e == '1') ctx->host_stats = true;
     ctx->device = device;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -1581,6 +1603,10 @@ void mac_ctx_destroy(mac_ctx* ctx)
         std::fprintf(stderr, "maxcover: closure batch split (us): staging %.1f, copy+launch %.1f, results %.1f\n",
                      ctx->cl_phase_s[0] / ctx->cl_batches * 1e6, ctx->cl_phase_s[1] / ctx->cl_batches * 1e6,
                      ctx->cl_phase_s[2] / ctx->cl_batches * 1e6);
+    if (ctx->host_stats && ctx->hs_n)
+        std::fprintf(stderr, "maxcover: fused polls %lld, host us per poll: to prep launch %.2f, prep launch %.2f, "
+                     "fiw launch %.2f, fin2 launch %.2f\n", (long long)ctx->hs_n, ctx->hs_t[0] / ctx->hs_n * 1e6,
+                     ctx->hs_t[1] / ctx->hs_n * 1e6, ctx->hs_t[2] / ctx->hs_n * 1e6, ctx->hs_t[3] / ctx->hs_n * 1e6);
     (void)hipSetDevice(ctx->device);
     if (ctx->doorbell) {   // every armed poll released first (else the synchronisation would wait)
         __atomic_store_n(ctx->doorbell, ~(uint64_t)0 >> 1, __ATOMIC_RELEASE);
@@ -3056,6 +3082,7 @@ static int32_t poll_best_dev(mac_ctx* ctx, const T* d_cands_in, int64_t three_n,
                              const double* d_dlim, double tan_half_fov, int64_t idx_base,
                              double* d_obj, void* d_best, void* stream)
 {
+    if (ctx && ctx->host_stats) t_poll_entry = std::chrono::steady_clock::now();
     constexpr bool f32 = std::is_same<T, float>::value;
     int32_t rc = poll_dev_check(ctx, d_cands_in, three_n, K, d_prev_in, d_dlim, d_best);
     if (rc) return rc;
