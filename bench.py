@@ -326,8 +326,12 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
     D = pkg.DynamicArea.DynamicArea(**fire_kw, seed=args.seed, device=dev_index)
     shard = (rank, world) if world > 1 else None
     spec = world > 1 and args.mads_mode == "speculate"
-    gather = ((pdist.SpecGather(coll_dev) if spec else pdist.make_gather(coll_dev))
-              if world > 1 else None)
+    gather = None
+    if world > 1 and coll_dev.type == "cuda" and args.exchange == "rccl":
+        # libmaxcover's own communicator: the per-round exchange in one C call
+        gather = (pdist.RcclSpecGather(ctx, coll_dev) if spec else pdist.RcclShardGather(ctx, coll_dev))
+    elif world > 1:
+        gather = pdist.SpecGather(coll_dev) if spec else pdist.make_gather(coll_dev)
     sim = pkg.FullSimulation.Simulation(ctx, x0, fire=D, N_iter=args.mads_iters, seed=args.seed,
                                         shard=shard, gather=gather, speculate=spec)
     t_set = time.perf_counter() - t_set
@@ -454,6 +458,7 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
             "mads_host_split_s": {k: float(np.sum([r.get("mads_host_s", {}).get(k, 0.0) for r in recs]))
                                   for k in ("host_enqueue_s", "host_perm_s", "wait_s", "host_post_s")},
             "slot_fallbacks": int(sum(r.get("slot_fallbacks", 0) for r in recs)),
+            "exchange": type(gather).__name__ if gather is not None else None,
             "parallelism": ("1 GPU" if world == 1 else
                             (f"{world} GPUs: speculation over failure branches (rank j polls the "
                              f"poll after j failures), one 24-B all-gather per round; fire stream "
@@ -665,12 +670,15 @@ def main():
     # and one pinned host read of the world x 16-B result (dist.PollGather)
     # (RCCL: libmaxcover's own communicator, the all-gather on the poll's stream, dist.RcclExchange;
     # --exchange torch: torch's collective + the device argmin; gloo rehearsals: PollGather's host path)
+    gat = None
     if distributed and coll_dev.type == "cuda" and args.exchange == "rccl":
-        gat = pdist.RcclExchange(ctx, coll_dev)
-    elif distributed:
+        try:
+            gat = pdist.RcclExchange(ctx, coll_dev)
+        except Exception as e:   # (reported; the exchange then runs through torch's collective)
+            log(f"bench.py: libmaxcover's RCCL exchange unavailable ({e}); torch.distributed's instead")
+            gat = None
+    if gat is None and distributed:
         gat = pdist.PollGather(coll_dev, ctx=ctx if coll_dev.type == "cuda" else None)
-    else:
-        gat = None
     xsteps = ([ctx.poll_step(d, 3 * N, Kl, d_rmax, d_best, d_prev=pv, d_dlim=d_dlim,
                              tan_half_fov=tan_half, idx_base=idx_base, stream=s_handle, fetch=False)
                for d, pv in zip(d_polls, d_prevs)] if isinstance(gat, pdist.RcclExchange) else None)
@@ -945,6 +953,7 @@ def main():
             "cpu_baseline": cpu,
             "closure": closure,
             "host_poll_ms": host_poll,
+            "exchange": (type(gat).__name__ if gat is not None else None),
             "best": {"objective": result[0], "index": result[1]},
             "check_timed_poll_vs_scan": check,
             "setup_s": t_set,

@@ -320,6 +320,11 @@ int32_t mac_comm_unique_id(const char* rccl_path, void* id_out);
 int32_t mac_comm_init(mac_ctx* ctx, const char* rccl_path, const void* id, int32_t rank, int32_t world);
 int32_t mac_poll_exchange(mac_ctx* ctx, const void* d_best, void* d_out, void* stream, double* best_obj,
                           int64_t* best_idx);
+/* Every rank's host record of `bytes` bytes (a multiple of 8, at most 256) gathered into `out`
+ * (world x bytes, rank order) over the context's communicator: one upload, the all-gather and one
+ * download on `stream`, then its synchronisation (the speculative MADS loop's per-round exchange:
+ * {done, objective, index, feasible} of every rank's poll). Collective. */
+int32_t mac_exchange_records(mac_ctx* ctx, const void* rec, int32_t bytes, void* out, void* stream);
 
 /* Armed device polls: the host turnaround between dependent polls of a MADS loop (the next poll
  * is known only after the previous one's result) taken off the device's critical path. The

@@ -88,9 +88,12 @@ class Simulation:
             from .dist import SpecGather
             speculate = multi and (gather is None or isinstance(gather, SpecGather))
         if multi and gather is None:
-            from .dist import SpecGather, make_gather
+            from .dist import RcclShardGather, RcclSpecGather, SpecGather, make_gather
             dev = device if device is not None else "cpu"
-            gather = SpecGather(dev) if speculate else make_gather(dev)
+            if str(dev).startswith("cuda"):   # libmaxcover's own RCCL communicator on ctx
+                gather = RcclSpecGather(ctx, dev) if speculate else RcclShardGather(ctx, dev)
+            else:
+                gather = SpecGather(dev) if speculate else make_gather(dev)
         self.gather = gather
         self.speculate = bool(speculate)
         if fire is not None:

@@ -9,6 +9,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+import weakref
 
 import numpy as np
 
@@ -69,7 +70,7 @@ EXPORTS = (
     "mac_mads_begin", "mac_mads_poll", "mac_mads_update", "mac_mads_result", "mac_mads_destroy",
     "mac_mads_poll_ahead", "mac_mads_advance",
     "mac_mads_best_buffer", "mac_best_reduce_dev", "mac_poll_basis_f64",
-    "mac_comm_unique_id", "mac_comm_init", "mac_poll_exchange",
+    "mac_comm_unique_id", "mac_comm_init", "mac_poll_exchange", "mac_exchange_records",
 )
 
 
@@ -152,6 +153,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mac_comm_unique_id": ([ctypes.c_char_p, _vp], _i32),
         "mac_comm_init": ([_vp, ctypes.c_char_p, _vp, _i32, _i32], _i32),
         "mac_poll_exchange": ([_vp, _vp, _vp, _vp, _dp, _i64p], _i32),
+        "mac_exchange_records": ([_vp, _vp, _i32, _vp, _vp], _i32),
         "mac_poll_basis_f64": ([_vp, _dp, _i64, ctypes.POINTER(ctypes.c_int16),
                                 ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                                 ctypes.c_double, _dp, ctypes.c_double, _dp, _dp, ctypes.c_double,
@@ -324,6 +326,7 @@ class Context:
         self._h = h
         self.device = int(device)
         self._L = L
+        self._steppers = weakref.WeakSet()   # closed before the context (they use its device state)
         self.set_algo(algo)
         if tile_points is not None:
             self.set_option(MAC_OPT_TILE_POINTS, int(tile_points))
@@ -331,6 +334,8 @@ class Context:
     # -- lifetime
     def close(self) -> None:
         if getattr(self, "_h", None):
+            for st in list(getattr(self, "_steppers", ())):
+                st.close()
             self._L.mac_ctx_destroy(self._h)
             self._h = None
 
@@ -624,8 +629,10 @@ class Context:
                      ell_max: int = 6, seed: int = 20250216, shard=None) -> "MadsStepper":
         """mac_mads_begin: the native loop one poll at a time over the candidate shard
         ``shard`` = (lo, hi) of each poll's 2n candidates (None: the whole poll)."""
-        return MadsStepper(self, x0, r_max, penalty, prev, d_lim, tan_half_fov, n_iter, ell0,
-                           ell_max, seed, shard)
+        st = MadsStepper(self, x0, r_max, penalty, prev, d_lim, tan_half_fov, n_iter, ell0,
+                         ell_max, seed, shard)
+        self._steppers.add(st)
+        return st
 
     # -- device-resident, stream-ordered
     def area_batch_dev(self, d_cands, three_n: int, K: int, d_area, stream=None) -> None:
@@ -768,6 +775,12 @@ class Context:
             return bo.value, bi.value
 
         return step
+
+    def exchange_records(self, rec: np.ndarray, out: np.ndarray, stream=None) -> None:
+        """mac_exchange_records: rec (this rank's record, a contiguous array of 8-B words) gathered
+        from every rank into out (world rows of the same size)."""
+        _check(self._L.mac_exchange_records(self._h, rec.ctypes.data, int(rec.nbytes), out.ctypes.data,
+                                            _stream(stream, self.device)))
 
     def reduce_step(self, d_records, n_records: int, d_best, stream=None):
         """A bound mac_best_reduce_dev + mac_best_fetch (prebuilt ctypes arguments): returns a

@@ -203,6 +203,9 @@ struct mac_ctx {
     void* comm = nullptr;
     int comm_rank = 0, comm_world = 0;
     void* d_xrec = nullptr;
+    std::mutex xmu;          // mac_exchange_records: its staging
+    PinnedBuf h_xrec;        // [own record 256 B][world records]
+    void* d_xrec2 = nullptr;
     // the fused chain's routing history over every lane's polls (enqueue_eval): bit q set when the
     // q-th last reported poll did not suit it (a workload property: a MADS stepper or a new lane
     // takes it over from the lanes before it)
@@ -1615,6 +1618,8 @@ void mac_ctx_destroy(mac_ctx* ctx)
     (void)hipDeviceSynchronize();
     if (ctx->comm) (void)ctx->rccl->comm_destroy(ctx->comm);
     if (ctx->d_xrec) (void)hipFree(ctx->d_xrec);
+    if (ctx->d_xrec2) (void)hipFree(ctx->d_xrec2);
+    ctx->h_xrec.release();
     free_deferred(ctx);
     if (ctx->doorbell) (void)hipHostFree(ctx->doorbell);
     ctx->h_mirror.release();
@@ -3366,6 +3371,34 @@ int32_t mac_comm_init(mac_ctx* ctx, const char* rccl_path, const void* id, int32
     ctx->comm_rank = rank;
     ctx->comm_world = world;
     ctx->d_xrec = buf;
+    return MAC_OK;
+    ABI_END
+}
+
+int32_t mac_exchange_records(mac_ctx* ctx, const void* rec, int32_t bytes, void* out, void* stream)
+{
+    ABI_BEGIN
+    if (!ctx || !rec || !out) return fail(MAC_E_INVAL, "null argument");
+    if (!ctx->comm) return fail(MAC_E_INVAL, "no communicator (mac_comm_init)");
+    if (bytes <= 0 || bytes > 256 || bytes % 8) return fail(MAC_E_INVAL, "record size: a multiple of 8 up to 256");
+    set_device(ctx);
+    hipStream_t s = (hipStream_t)stream;
+    const size_t W = (size_t)ctx->comm_world;
+    std::lock_guard<std::mutex> xl(ctx->xmu);   // (one exchange at a time: the buffers are the context's)
+    if (!ctx->h_xrec.p) {
+        ctx->h_xrec.reserve(256 * (W + 1));
+        HCK(hipMalloc(&ctx->d_xrec2, 256 * (W + 1)));
+    }
+    // this rank's record up, every rank's gathered on the stream, then down: one synchronisation
+    unsigned char* h = (unsigned char*)ctx->h_xrec.p;
+    unsigned char* d = (unsigned char*)ctx->d_xrec2;
+    std::memcpy(h, rec, (size_t)bytes);
+    HCK(hipMemcpyAsync(d, h, (size_t)bytes, hipMemcpyHostToDevice, s));
+    const int r = ctx->rccl->all_gather(d, d + 256, (size_t)bytes, 1 /* ncclUint8 */, ctx->comm, s);
+    if (r) return rccl_fail(ctx->rccl, r, "ncclAllGather");
+    HCK(hipMemcpyAsync(h + 256, d + 256, (size_t)bytes * W, hipMemcpyDeviceToHost, s));
+    HCK(hipStreamSynchronize(s));
+    std::memcpy(out, h + 256, (size_t)bytes * W);
     return MAC_OK;
     ABI_END
 }

@@ -159,19 +159,11 @@ class RcclExchange:
         import torch
         import torch.distributed as dist
 
-        check_one_runtime()
         t0 = time.perf_counter()
         self.ctx = ctx
         self.group = group
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
         self.device = torch.device(device)
-        path = rccl_path()
-        uid = torch.zeros(128, dtype=torch.uint8, device=self.device)
-        if self.rank == 0:
-            uid.copy_(torch.tensor(list(ctx.comm_unique_id(path)), dtype=torch.uint8))
-        dist.broadcast(uid, 0, group=group)
-        ctx.comm_init(bytes(uid.cpu().tolist()), self.rank, self.world, path)
+        self.rank, self.world = _lib_comm(ctx, device, group)
         self.res = torch.empty(2, dtype=torch.float64, device=self.device)
         self._steps = {}
         self.init_s = time.perf_counter() - t0
@@ -198,6 +190,83 @@ class RcclExchange:
         self.seconds += time.perf_counter() - t0
         self.calls += 1
         return r
+
+
+def _lib_comm(ctx, device, group=None):
+    """libmaxcover's own communicator on ctx (mac_comm_init over the group's ranks, the id made
+    by rank 0 and broadcast once); returns (rank, world)."""
+    import torch
+    import torch.distributed as dist
+
+    check_one_runtime()
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    path = rccl_path()
+    uid = torch.zeros(128, dtype=torch.uint8, device=torch.device(device))
+    if rank == 0:
+        uid.copy_(torch.tensor(list(ctx.comm_unique_id(path)), dtype=torch.uint8))
+    dist.broadcast(uid, 0, group=group)
+    ctx.comm_init(bytes(uid.cpu().tolist()), rank, world, path)
+    return rank, world
+
+
+class RcclShardGather:
+    """The sharded MADS loop's per-iteration exchange inside libmaxcover: the stepper's polls write
+    their shard best into a persistent 16-B device buffer (mac_mads_best_buffer, bound by
+    ``mads_loop``), and one C call (mac_poll_exchange) all-gathers every rank's buffer over the
+    context's RCCL communicator, reduces it on the device and reads the result from its mapped
+    slot. ``seconds`` / ``calls`` as DeviceGather's."""
+
+    def __init__(self, ctx, device, group=None):
+        import torch
+
+        self.device = torch.device(device)
+        self.rank, self.world = _lib_comm(ctx, device, group)
+        self.ctx = ctx
+        self.best = torch.zeros(2, dtype=torch.float64, device=self.device)
+        self.res = torch.empty(2, dtype=torch.float64, device=self.device)
+        self._step = None
+        self.seconds = 0.0
+        self.calls = 0
+
+    def bind(self, stepper) -> None:
+        import torch
+        torch.cuda.current_stream(self.device).synchronize()   # (the zero-fill lands first)
+        stepper.best_buffer(self.best)
+        self._step = self.ctx.exchange_step(self.best, self.res, stream=0)
+
+    def __call__(self, obj, idx):
+        import time
+
+        t0 = time.perf_counter()
+        r = self._step()
+        self.seconds += time.perf_counter() - t0
+        self.calls += 1
+        return r
+
+
+class RcclSpecGather:
+    """SpecGather's exchange inside libmaxcover (mac_exchange_records): every rank's {done,
+    objective, index, feasible} 32-B record through the context's RCCL communicator in one C call
+    (upload, all-gather, download, one synchronisation on a private stream)."""
+
+    def __init__(self, ctx, device, group=None):
+        import torch
+
+        self.rank, self.world = _lib_comm(ctx, device, group)
+        self.ctx = ctx
+        self.rec = np.zeros(4, dtype=np.float64)
+        self.out = np.zeros((self.world, 4), dtype=np.float64)
+        self.stream = torch.cuda.Stream(torch.device(device))
+
+    def __call__(self, done, obj, idx, feasible=0):
+        self.rec[0] = 1.0 if done else 0.0
+        self.rec[1] = float(obj)
+        self.rec.view(np.int64)[2] = int(idx)
+        self.rec.view(np.int64)[3] = int(feasible)
+        self.ctx.exchange_records(self.rec, self.out, stream=self.stream.cuda_stream)
+        hi = self.out.view(np.int64)
+        return [(bool(self.out[j, 0] != 0.0), float(self.out[j, 1]), int(hi[j, 2]), int(hi[j, 3]))
+                for j in range(self.world)]
 
 
 class DeviceGather:

@@ -211,3 +211,40 @@ def test_rccl_exchange_in_library(nccl1, ctx, pkg):
             assert got == (want[0], want[1]), (t, got, want)
         assert ex.calls == 6
         torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("mode", ["shard", "speculate"])
+def test_mads_loops_over_the_library_exchange(nccl1, pkg, mode):
+    """The config-5 multi-GPU loops over libmaxcover's own RCCL communicator: the sharded loop with
+    dist.RcclShardGather (the stepper's device best buffer all-gathered and reduced on the device,
+    mac_poll_exchange) and the speculative loop with dist.RcclSpecGather (every rank's 32-B record,
+    mac_exchange_records). Same iterate, objective and iteration count as mac_mads_run."""
+    d = import_module(pkg.__name__ + ".dist")
+    wl = pkg.workloads
+    x, y, w = wl.grid_points(200)
+    rng = wl.SplitMix64(505)
+    N = 9
+    x0 = np.concatenate([np.round(250 + rng.uniform(N) * 400), np.round(250 + rng.uniform(N) * 400),
+                         np.full(N, 30.0)])
+    r_max = np.full(N, 30.0 * TAN50)
+    kw = dict(prev=x0, d_lim=np.full(N, 10.0), tan_half_fov=TAN50, n_iter=30, ell0=2, ell_max=5,
+              seed=919)
+    with pkg.Context(0) as c2:
+        c2.set_points(x, y, w)
+        want_x, want = c2.mads_run(x0, r_max, 1e5, **kw)
+        st = c2.mads_stepper(x0, r_max, 1e5, **kw)
+        try:
+            if mode == "shard":
+                g = d.RcclShardGather(c2, nccl1)
+                xs, stats = d.mads_loop(st, g)
+                assert g.calls == want["iterations"] and stats["slot_fallbacks"] == 0
+            else:
+                g = d.RcclSpecGather(c2, nccl1)
+                xs, stats = d.mads_loop_speculative(st, g)
+                # (one rank: one iteration per round, and the round that finds the loop done)
+                assert stats["rounds"] == want["iterations"] + 1
+                assert stats["feasible_evaluations"] == want["feasible_evaluations"]
+        finally:
+            st.close()
+    assert np.array_equal(xs, want_x)
+    assert stats["f"] == want["f"] and stats["iterations"] == want["iterations"]
