@@ -198,7 +198,11 @@ def _declare(L: ctypes.CDLL) -> None:
                                    ctypes.c_double, _i64, _vp, _vp, _vp], _i32),
     }
     for name, (args, res) in sig.items():
-        f = getattr(L, name)
+        # (an older build lacks the newer symbols: bound as far as it has them, so A/B tools can
+        # load it; tests/test_abi.py checks that the in-tree library exports every one)
+        f = getattr(L, name, None)
+        if f is None:
+            continue
         f.argtypes = args
         f.restype = res
 

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <dlfcn.h>
+#include <sched.h>
 #include <linux/futex.h>
 #include <sys/syscall.h>
 #include <unistd.h>
@@ -217,8 +218,7 @@ struct mac_ctx {
     std::atomic<int> cl_active{0};   // callers inside mac_area_f64's combiner
     int cl_taken = 0;                // requests in batches in flight (under cl_mu)
     int64_t cl_batches = 0, cl_reqs = 0;   // (MAXCOVER_CL_STATS=1: printed at destroy)
-    double cl_batch_s = 0.0;               // time inside the batches' evaluations
-    double cl_phase_s[4] = {0, 0, 0, 0};   // ... split: staging, copy + launch enqueued, results
+    double cl_phase_s[2] = {0, 0};         // per batch: staging, copy + launch enqueued
     std::vector<Lane*> lanes_free;
     std::vector<Lane*> lanes_all;
     hipStream_t setup_stream = nullptr;
@@ -1599,13 +1599,10 @@ void mac_ctx_destroy(mac_ctx* ctx)
 {
     if (!ctx) return;
     if (const char* e = std::getenv("MAXCOVER_CL_STATS"); e && *e == '1' && ctx->cl_batches)
-        std::fprintf(stderr, "maxcover: closure batches %lld, requests %lld (%.2f per batch), %.1f us per batch\n",
-                     (long long)ctx->cl_batches, (long long)ctx->cl_reqs,
-                     (double)ctx->cl_reqs / (double)ctx->cl_batches, ctx->cl_batch_s / ctx->cl_batches * 1e6);
-    if (const char* e = std::getenv("MAXCOVER_CL_STATS"); e && *e == '1' && ctx->cl_batches)
-        std::fprintf(stderr, "maxcover: closure batch split (us): staging %.1f, copy+launch %.1f, results %.1f\n",
-                     ctx->cl_phase_s[0] / ctx->cl_batches * 1e6, ctx->cl_phase_s[1] / ctx->cl_batches * 1e6,
-                     ctx->cl_phase_s[2] / ctx->cl_batches * 1e6);
+        std::fprintf(stderr, "maxcover: closure batches %lld, requests %lld (%.2f per batch); per batch (us): "
+                     "staging %.1f, copy+launch %.1f\n",
+                     (long long)ctx->cl_batches, (long long)ctx->cl_reqs, (double)ctx->cl_reqs / (double)ctx->cl_batches,
+                     ctx->cl_phase_s[0] / ctx->cl_batches * 1e6, ctx->cl_phase_s[1] / ctx->cl_batches * 1e6);
     if (ctx->host_stats && ctx->hs_n)
         std::fprintf(stderr, "maxcover: fused polls %lld, host us per poll: to prep launch %.2f, prep launch %.2f, "
                      "fiw launch %.2f, fin2 launch %.2f\n", (long long)ctx->hs_n, ctx->hs_t[0] / ctx->hs_n * 1e6,
@@ -2718,18 +2715,32 @@ int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const doub
 // synchronisation). AUTO / TILED walks, N <= kClosureMaxN; if a slot has not landed within 2 ms (a
 // failed launch) a stream synchronisation reports it.
 static constexpr int kClBatch = 64;   // concurrent mac_area_f64 calls evaluated by one launch
+// slot reads spun with a pause before a reader starts yielding its CPU (MAXCOVER_CL_READSPIN overrides)
+static const int kClReadSpin = [] {
+    const char* e = std::getenv("MAXCOVER_CL_READSPIN");
+    return e ? std::max(0, std::atoi(e)) : 64;
+}();
 
 static bool closure_path(const mac_ctx* ctx, int64_t three_n)
 {
     return (ctx->algo == MAC_ALGO_AUTO || ctx->algo == MAC_ALGO_TILED) && three_n / 3 <= kClosureMaxN;
 }
 
-static void closure_batch(mac_ctx* ctx, int64_t three_n, const double* const* cands, double* const* outs, int B)
+// A launched batch of closure candidates: its lane (stream, staging, result slots) stays with the
+// batch until every one of its callers has read its slot (the last returns the lane to the pool),
+// so a later batch can neither overwrite a slot nor the staging before they are consumed.
+struct ClBatch {
+    Lane* L = nullptr;
+    uint64_t seq = 0;
+    std::atomic<int> readers{0};
+};
+
+// Stage the B candidates in the lane's pinned buffer, copy them up and launch one closure_kernel
+// (grid.y = B) whose candidate b writes its area into the lane's mapped slot b under `seq`. Returns
+// after enqueueing: the launching caller does not wait for the results.
+static uint64_t closure_launch(mac_ctx* ctx, Lane* L, int64_t three_n, const double* const* cands, int B)
 {
     const int N = (int)(three_n / 3);
-    set_device(ctx);
-    LaneGuard lg(ctx);
-    Lane* L = lg.lane;
     hipStream_t s = L->stream;
     const size_t one = sizeof(double) * (size_t)three_n;
     const auto t0 = std::chrono::steady_clock::now();
@@ -2774,42 +2785,71 @@ static void closure_batch(mac_ctx* ctx, int64_t three_n, const double* const* ca
         ctx->prof.push_back({ts_a, (int64_t)nwg * B, -1, 0, (int64_t)B, nullptr, MAC_ALGO_TILED});
     }
     const auto t2 = std::chrono::steady_clock::now();
-    bool synced = false;
-    for (int b = 0; b < B; ++b) {
-        const uint64_t* slot = (const uint64_t*)L->h_cl.p + 4 * b;
-        double a = 0.0;
-        int64_t unused = 0;
-        if (!synced && mirror_wait(slot, seq, 2.0, &a, &unused)) {
-            *outs[b] = a;
-            continue;
-        }
-        if (!synced) {
-            HCK(hipStreamSynchronize(s));
-            synced = true;
-        }
-        if (!mirror_read(slot, seq, &a, &unused))
-            HCK(hipMemcpy(&a, L->area.as<double>() + b, sizeof(double), hipMemcpyDeviceToHost));
-        *outs[b] = a;
-    }
-    const auto t3 = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> lk(ctx->cl_mu);
     ctx->cl_phase_s[0] += std::chrono::duration<double>(t1 - t0).count();
     ctx->cl_phase_s[1] += std::chrono::duration<double>(t2 - t1).count();
-    ctx->cl_phase_s[2] += std::chrono::duration<double>(t3 - t2).count();
+    return seq;
+}
+
+// Candidate b's area of a launched batch, from its mapped slot (spinning with pauses: the other
+// callers' threads lead batches meanwhile); after 2 ms (a failed launch) the lane's stream is
+// synchronised, which reports the error, then the slot or the device word is read.
+static double closure_read(mac_ctx* ctx, ClBatch* bt, int b)
+{
+    const uint64_t* slot = (const uint64_t*)bt->L->h_cl.p + 4 * b;
+    double a = 0.0;
+    int64_t unused = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int spin = 0;; ++spin) {
+        if (mirror_read(slot, bt->seq, &a, &unused)) return a;
+        // past a short spin, yield the CPU between reads: under many concurrent callers the
+        // threads launching the next batches need it more than the spinning readers (the call's
+        // HIP enqueue time doubles when every CPU of the share spins)
+        if (spin < kClReadSpin) __builtin_ia32_pause();
+        else sched_yield();
+        if ((spin & 255) == 255 &&
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > 2.0)
+            break;
+    }
+    set_device(ctx);
+    HCK(hipStreamSynchronize(bt->L->stream));
+    if (!mirror_read(slot, bt->seq, &a, &unused))
+        HCK(hipMemcpy(&a, bt->L->area.as<double>() + b, sizeof(double), hipMemcpyDeviceToHost));
+    return a;
+}
+
+// One caller is done with the batch; the last returns the lane (its stream holds nothing unread:
+// every slot has landed, so the kernel that wrote them is ending, and later work on the stream is
+// ordered after it).
+static void closure_done(mac_ctx* ctx, ClBatch* bt)
+{
+    if (bt->readers.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        bt->L->last = bt->L->stream;
+        ctx->lanes_free.push_back(bt->L);
+    }
+    delete bt;
 }
 
 // Concurrent callers (DirectSearch's threaded poll, src/TDM_STATIC_opt.jl:129: one objective call
 // per trial point per thread) are combined: a caller queues its request; while fewer than
-// kClLeaders batches are in flight, a caller whose request is still queued takes every queued
-// request of the same size (up to kClBatch) and evaluates them in one launch on its own lane
-// (stream), marking each done; the others spin on their own request's state word (no lock, no
-// condition-variable wake-up chain) and lead a later batch if theirs is still queued when a slot
-// frees. A lone caller runs its own request at once. Results per call are exactly the
-// single-candidate kernel's (the batch dimension only selects the candidate).
+// kClLeaders batches are being launched, a caller whose request is still queued takes every queued
+// request of the same size (up to kClBatch), launches them as one batch on a lane of its own and
+// goes back to waiting for its own result like every other caller: no thread waits for a batch's
+// results but the threads whose requests it holds, each on its own mapped slot, so the next batch
+// can be formed and launched while earlier ones run (round 5's leaders waited for their whole batch
+// before another could start). A lone caller launches its own request at once. Results per call are
+// exactly the single-candidate kernel's (the batch dimension only selects the candidate).
 #ifndef MAC_CL_LEADERS
 #define MAC_CL_LEADERS 2
 #endif
-static constexpr int kClLeaders = MAC_CL_LEADERS;   // batches in flight at once (a lane, a stream each)
+// batches being launched at once (MAXCOVER_CL_LEADERS overrides, for measurements)
+static const int kClLeaders = [] {
+    const char* e = std::getenv("MAXCOVER_CL_LEADERS");
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 1 && v <= 16 ? v : MAC_CL_LEADERS;
+}();
 static constexpr int kClSpin = 64;        // pause iterations before a waiter sleeps on its futex
 static constexpr int kClGather = 0;        // pauses a would-be leader waits for every caller to queue (0: none)
 
@@ -2817,19 +2857,20 @@ struct ClReq {
     const double* c;
     int64_t three_n;
     double* out;
-    std::atomic<int> state{0};   // 0 queued, 1 taken by a batch, 2 done
+    std::atomic<int> state{0};   // 0 queued, 1 taken by a batch, 2 failed, 3 launched (read the slot)
     std::atomic<int> released{0};   // 1 once the leader no longer touches the request (after its
                                     // futex wake): the owner's stack object may then go
+    ClBatch* bt = nullptr;       // (state 3) the batch and this request's slot in it
+    int b = 0;
     int32_t rc = MAC_OK;
     std::string err;
 };
 
 // Waiting on a request's state word: a short spin, then a futex sleep (no CPU taken from the
-// threads that lead batches); woken by the leader that completes the request, or by the leader
-// that frees a batch slot while the request is still queued (it may then lead), or after 1 ms.
+// threads that lead batches); woken by the leader that launches the request, or by the leader
+// that frees a launch slot while the request is still queued (it may then lead), or after 1 ms.
 static void cl_wait(std::atomic<int>* w, int seen, int spin)
 {
-    // a short spin, then sleep (spinning waiters take CPU from the threads that lead batches)
     if (spin < kClSpin) {
         __builtin_ia32_pause();
         return;
@@ -2866,9 +2907,11 @@ int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, doubl
         std::lock_guard<std::mutex> lk(ctx->cl_mu);
         ctx->cl_q.push_back(&r);
     }
-    for (int spin = 0; r.state.load(std::memory_order_acquire) != 2; ++spin) {
+    for (int spin = 0;; ++spin) {
+        const int st = r.state.load(std::memory_order_acquire);
+        if (st == 2 || st == 3) break;
         std::vector<ClReq*> batch;
-        if (r.state.load(std::memory_order_relaxed) == 0) {
+        if (st == 0) {
             std::lock_guard<std::mutex> lk(ctx->cl_mu);
             // lead once every caller in the combiner has queued (the whole convoy in one launch),
             // or after a short wait
@@ -2894,23 +2937,20 @@ int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, doubl
         }
         if (batch.empty()) {
             const int seen = r.state.load(std::memory_order_acquire);
-            if (seen != 2) cl_wait(&r.state, seen, spin);
+            if (seen != 2 && seen != 3) cl_wait(&r.state, seen, spin);
             continue;
         }
+        // lead: launch the batch, hand every request its slot, go back to waiting for our own
+        ClBatch* bt = new ClBatch();
+        bt->readers.store((int)batch.size(), std::memory_order_relaxed);
         int32_t brc = MAC_OK;
         std::string msg;
         try {
             std::vector<const double*> cs(batch.size());
-            std::vector<double*> os(batch.size());
-            for (size_t q = 0; q < batch.size(); ++q) {
-                cs[q] = batch[q]->c;
-                os[q] = batch[q]->out;
-            }
-            const auto tb0 = std::chrono::steady_clock::now();
-            closure_batch(ctx, batch[0]->three_n, cs.data(), os.data(), (int)batch.size());
-            const double dtb = std::chrono::duration<double>(std::chrono::steady_clock::now() - tb0).count();
-            std::lock_guard<std::mutex> lk(ctx->cl_mu);
-            ctx->cl_batch_s += dtb;
+            for (size_t q = 0; q < batch.size(); ++q) cs[q] = batch[q]->c;
+            set_device(ctx);
+            bt->L = acquire_lane(ctx, nullptr);
+            bt->seq = closure_launch(ctx, bt->L, batch[0]->three_n, cs.data(), (int)batch.size());
         } catch (const HipError& he) {
             brc = he.e == hipErrorOutOfMemory ? MAC_E_NOMEM : MAC_E_HIP;
             char buf[512];
@@ -2924,7 +2964,15 @@ int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, doubl
             brc = MAC_E_HIP;
             msg = "unexpected exception";
         }
-        ClReq* next = nullptr;   // a queued request whose thread may lead the freed slot
+        if (brc != MAC_OK) {   // nothing was launched: the lane back, the requests failed
+            if (bt->L) {
+                std::lock_guard<std::mutex> lk(ctx->mu);
+                ctx->lanes_free.push_back(bt->L);
+            }
+            delete bt;
+            bt = nullptr;
+        }
+        ClReq* next = nullptr;   // a queued request whose thread may lead the freed launch slot
         {
             std::lock_guard<std::mutex> lk(ctx->cl_mu);
             --ctx->cl_busy;
@@ -2936,18 +2984,31 @@ int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, doubl
                 }
             if (next) cl_wake(&next->state);   // (under the lock: the request still exists)
         }
-        for (ClReq* q : batch) {   // (a request object lives until its released word reads 1)
-            q->rc = brc;
-            q->err = msg;
-            q->state.store(2, std::memory_order_release);
-            if (q != &r) cl_wake(&q->state);
-            q->released.store(1, std::memory_order_release);
+        for (size_t q = 0; q < batch.size(); ++q) {   // (a request lives until its released word reads 1)
+            ClReq* rq = batch[q];
+            rq->bt = bt;
+            rq->b = (int)q;
+            rq->rc = brc;
+            rq->err = msg;
+            rq->state.store(bt ? 3 : 2, std::memory_order_release);
+            if (rq != &r) cl_wake(&rq->state);
+            rq->released.store(1, std::memory_order_release);
         }
         spin = 0;
     }
-    // the leader that completed this request may still be between its state store and its wake
-    // (the futex word is this stack object): wait for its release, a few instructions away
+    // the leader that launched this request may still be between its state store and its wake (the
+    // futex word is this stack object): wait for its release, a few instructions away
     while (r.released.load(std::memory_order_acquire) == 0) __builtin_ia32_pause();
+    if (r.state.load(std::memory_order_acquire) == 3) {
+        try {
+            *area_out = closure_read(ctx, r.bt, r.b);
+        } catch (...) {
+            closure_done(ctx, r.bt);
+            ctx->cl_active.fetch_sub(1);
+            throw;
+        }
+        closure_done(ctx, r.bt);
+    }
     ctx->cl_active.fetch_sub(1);
     if (r.rc) return fail(r.rc, r.err);
     return MAC_OK;
