@@ -636,10 +636,14 @@ __device__ __forceinline__ void prep_block(const PrepArgs& a, int cw, unsigned c
 // fold and the keys are exclusive branches, so the candidate values are dead on the folding
 // wave's path (80 VGPRs: two workgroups, 18 waves, fit a CU). Results are prep_block's bit for bit
 // (the same terms in the same order, the same keys and bound).
+template <bool kGen>
 __device__ __forceinline__ void prep_block_x(const PrepArgs& a, int cw, unsigned char* lds)
 {
-    constexpr int PC = kPrepCX, NC = kPrepCX + 1, NW = kPrepU / kWave;
-    PrepLds<NC>& L = *reinterpret_cast<PrepLds<NC>*>(lds);
+    // kGen: a generated complete poll (K = 2n, n = 3N): workgroup cw takes the columns 3cw .. 3cw + 2
+    // of B, slots 0-2 their plus candidates (k = col), slots 3-5 their minus candidates (k = n + col),
+    // each B entry drawn once for both; N workgroups
+    constexpr int PC = kPrepCX, NC = kGen ? kPrepCX : kPrepCX + 1, NW = kPrepU / kWave;
+    PrepLds<kPrepCX + 1>& L = *reinterpret_cast<PrepLds<kPrepCX + 1>*>(lds);
     auto& term = L.term;
     auto& wbad = L.wbad;
     auto& wbadm = L.wbadm;
@@ -649,7 +653,11 @@ __device__ __forceinline__ void prep_block_x(const PrepArgs& a, int cw, unsigned
     const int u = threadIdx.x, lane = u & (kWave - 1), wid = u / kWave;
     const bool fw = wid == NW;   // the folding wave
     const int k0 = cw * PC;
-    auto cand = [&](int c) { return c < PC ? k0 + c : a.xbase + cw; };   // (>= K: absent)
+    const int n3 = 3 * N;
+    auto cand = [&](int c) {   // (>= K: absent)
+        if constexpr (kGen) return c < 3 ? 3 * cw + c : n3 + 3 * cw + c - 3;
+        else return c < PC ? k0 + c : a.xbase + cw;
+    };
     const bool obj = a.vp != nullptr;
     const PenArgs& pa = a.pa;
     const bool excl = obj && pa.prev && a.skip_failed;
@@ -659,14 +667,30 @@ __device__ __forceinline__ void prep_block_x(const PrepArgs& a, int cw, unsigned
     double v[NC][3];
     double base[3] = {0.0, 0.0, 0.0};   // candidate 0's values: the keys' base
     if (!fw) {
+        if constexpr (kGen) {
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            const int k = min(cand(c), K - 1);
+            for (int q = 0; q < 3; ++q) {
+                const int vv = q * N + ii;
+                const int rv = a.src.rp[vv];
+                const double xv = a.src.xinc[vv];
 #pragma unroll
-            for (int q = 0; q < 3; ++q) v[c][q] = a.src.cands[(int64_t)k * a.src.ldc + q * N + ii];
+                for (int c = 0; c < 3; ++c) {
+                    const double d = a.src.entry(n3, rv, a.src.cp[3 * cw + c]);
+                    v[c][q] = xv + d;
+                    v[c + 3][q] = xv - d;
+                }
+                base[q] = xv + a.src.entry(n3, rv, a.src.cp[0]);
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int k = min(cand(c), K - 1);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) v[c][q] = a.src.cands[(int64_t)k * a.src.ldc + q * N + ii];
+            }
+#pragma unroll
+            for (int q = 0; q < 3; ++q) base[q] = a.src.cands[q * N + ii];
         }
-#pragma unroll
-        for (int q = 0; q < 3; ++q) base[q] = a.src.cands[q * N + ii];
         if (obj) {
             // pen_term (above), the same operations in the same order
             const double x1 = pa.prev ? pa.prev[ii] : 0.0, y1 = pa.prev ? pa.prev[N + ii] : 0.0;
@@ -779,6 +803,7 @@ __device__ __forceinline__ void prep_block_x(const PrepArgs& a, int cw, unsigned
         // centre, not a cons3 failure; a NaN difference counts as +inf)
         double dmx = -__builtin_inf(), dmy = -__builtin_inf(), dmr = -__builtin_inf(), dml = -__builtin_inf();
         uint32_t pk[NC];
+        bool kb = false;   // (records) a key of this disk is inexact (k_index.h "Keys")
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             const double x = v[c][0], y = v[c][1], r = v[c][2];
@@ -788,8 +813,12 @@ __device__ __forceinline__ void prep_block_x(const PrepArgs& a, int cw, unsigned
             pk[c] = packs ? key_pack(dx, dy, dr) : kKeyEsc;
             if (!packs && iv && cand(c) < K) {
 #pragma unroll
-                for (int q = 0; q < 3; ++q)
-                    a.keysT[(int64_t)(q * N + u) * a.ldk + cand(c)] = (float)(v[c][q] - base[q]);
+                for (int q = 0; q < 3; ++q) {
+                    const float f = (float)(v[c][q] - base[q]);
+                    kb |= !((dead >> c) & 1u) &&
+                          __builtin_bit_cast(uint64_t, base[q] + (double)f) != __builtin_bit_cast(uint64_t, v[c][q]);
+                    a.keysT[(int64_t)(q * N + u) * a.ldk + cand(c)] = f;
+                }
             }
             if (a.pd && iv && cand(c) < K && !((dead >> c) & 1u) && r > 0.0 && __builtin_isfinite(x) &&
                 __builtin_isfinite(y)) {
@@ -805,13 +834,48 @@ __device__ __forceinline__ void prep_block_x(const PrepArgs& a, int cw, unsigned
                 dml = fmax(dml, el);
             }
         }
-        if (iv) {   // (k0 = PC * cw: even) 8-B stores, the extra word alone
-            static_assert(PC % 2 == 0, "an even candidate count");
+        if (iv) {
             uint32_t* const krow = a.keysP + (int64_t)u * a.ldk;
+            if constexpr (kGen) {   // two runs of three words (plus and minus candidates)
 #pragma unroll
-            for (int h = 0; h < PC / 2; ++h)
-                *reinterpret_cast<uint2*>(krow + k0 + 2 * h) = make_uint2(pk[2 * h], pk[2 * h + 1]);
-            if (cand(PC) < K) krow[cand(PC)] = pk[PC];
+                for (int c = 0; c < NC; ++c) krow[cand(c)] = pk[c];
+            } else {   // (k0 = PC * cw: even) 8-B stores, the extra word alone
+                static_assert(PC % 2 == 0, "an even candidate count");
+#pragma unroll
+                for (int h = 0; h < PC / 2; ++h)
+                    *reinterpret_cast<uint2*>(krow + k0 + 2 * h) = make_uint2(pk[2 * h], pk[2 * h + 1]);
+                if (cand(PC) < K) krow[cand(PC)] = pk[PC];
+            }
+        }
+        if (a.prec && iv) {
+            // the five-launch chain's partial region record (prep_block's): a tile box holding the
+            // spans of the live candidates' disks, the span-area estimate and the key flag
+            double xa = __builtin_inf(), xb = -__builtin_inf(), ya = __builtin_inf(), yb = -__builtin_inf();
+            double xm = 0.0, ym = 0.0, est = 0.0;
+            bool any = false;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const double x = v[c][0], y = v[c][1], r = v[c][2];
+                if (cand(c) < K && !((dead >> c) & 1u) && r > 0.0 && __builtin_isfinite(x) &&
+                    __builtin_isfinite(y)) {
+                    any = true;
+                    xa = fmin(xa, x - r);
+                    xb = fmax(xb, x + r);
+                    ya = fmin(ya, y - r);
+                    yb = fmax(yb, y + r);
+                    xm = fmax(xm, __builtin_fabs(x) + r);
+                    ym = fmax(ym, __builtin_fabs(y) + r);
+                    const double e = 2.0 * r * a.g.invS + 1.0;
+                    est += e * e;
+                }
+            }
+            int x0 = 0, x1 = -1, y0 = 0, y1 = -1;
+            any = any && partial_range(xa, xb, xm, a.g.gx0, a.g.invS, a.g.nTx, x0, x1) &&
+                  partial_range(ya, yb, ym, a.g.gy0, a.g.invS, a.g.nTy, y0, y1);
+            a.prec[(int64_t)cw * N + u] =
+                make_int4((int)range_pack(any, x0, x1, range_shift(a.g.nTx)),
+                          (int)range_pack(any, y0, y1, range_shift(a.g.nTy)),
+                          __builtin_bit_cast(int, (float)est), kb ? 1 : 0);
         }
         if (a.pd) {
 #pragma unroll
@@ -858,9 +922,14 @@ __device__ __forceinline__ void prep_body(uint64_t* ts, PrepArgs& a)
     const int per = (int)((gridDim.x + 7) / 8), b = (int)blockIdx.x;
     const int cw = (int)(gridDim.x % 8) == 0 ? (b % 8) * per + b / 8 : b;
     __shared__ __attribute__((aligned(16))) unsigned char lds[sizeof(PrepLds<kX ? PC + 1 : PC>)];
-    if constexpr (kX) prep_block_x(a, cw, lds);   // (matrix sources, N <= kPrepU)
-    else if (a.src.cands) prep_block<true, PC>(a, cw, lds);
-    else prep_block<false, PC>(a, cw, lds);
+    if constexpr (kX) {   // (N <= kPrepU) a matrix, or a generated complete poll in column triples
+        if (a.src.cands) prep_block_x<false>(a, cw, lds);
+        else prep_block_x<true>(a, cw, lds);
+    } else if (a.src.cands) {
+        prep_block<true, PC>(a, cw, lds);
+    } else {
+        prep_block<false, PC>(a, cw, lds);
+    }
     ts_end(ts);
 }
 

@@ -689,6 +689,10 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
     // generated complete polls (the native MADS loop: K = 2n): the prep draws each B entry once
     // for its plus and minus candidates (k_prep.h PrepArgs.pair)
     const bool pair = !src.cands && src.k0 == 0 && K == 6 * N && (3 * N) % 4 == 0 && kPrepC == 8;
+    // ... or, with one block of UAVs, prep_x_kernel's layout (k_prep.h prep_block_x<true>): a column
+    // triple of B per workgroup (its plus and minus candidates: 6), N workgroups, a ninth wave
+    // folding the penalty chains beside the keys and the records
+    const bool gen_x = !src.cands && src.k0 == 0 && K == 6 * N && N >= 1 && N <= kPrepU;
     const int nchain = pair ? (3 * N) / 4 : (K + kPrepC - 1) / kPrepC;
 
     // The fused chain (k_fiw.h: prep -> fiw -> fin2) whenever the poll walk runs on packed keys of at
@@ -727,8 +731,8 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             L->keysT.reserve(sizeof(float) * (size_t)4 * N * ldk);
             // a matrix source: kPrepCX (+1) candidates per workgroup (k_prep.h prep_x_kernel)
             const int gx = K / kPrepCX;
-            const bool xk = src.cands && !pair && N <= kPrepU && gx >= 1 && K - gx * kPrepCX <= gx;
-            const int nprep = xk ? gx : nchain;
+            const bool xk = (src.cands && !pair && N <= kPrepU && gx >= 1 && K - gx * kPrepCX <= gx) || gen_x;
+            const int nprep = gen_x ? N : xk ? gx : nchain;
             L->pd.reserve(sizeof(double4) * (size_t)nprep);
             L->frows.reserve((counts ? sizeof(unsigned) : sizeof(double)) * (size_t)N * ldk);
             if (L->fwhint.grow(sizeof(int) * kFwHints)) HCK(hipMemsetAsync(L->fwhint.p, 0, L->fwhint.cap, s));
@@ -839,10 +843,14 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         }
     }
     if (poll_possible) L->last_chain = 1;
+    int nrec = nchain;   // the prep's records per disk (workgroups of the prep launch)
 
     if ((d_obj || poll_possible) && K > 0) {
         // the prep launch (k_prep.h): penalty chains + cons3 into vp, the poll walk's partial
         // regions, and the index's fp32 keys
+        // a generated complete poll with the index's keys: prep_x_kernel's column-triple layout
+        const bool gx5 = gen_x && poll_possible && want_keys;
+        nrec = gx5 ? N : nchain;
         PrepArgs pr{};
         pr.src = src;
         pr.N = N;
@@ -850,7 +858,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         pr.pa = pa;
         pr.penalty = penalty;
         pr.vp = d_vp;
-        pr.nchain = nchain;
+        pr.nchain = nrec;
         pr.skip_failed = d_area ? 0 : 1;   // (the index maps them to an inert position likewise)
         pr.pair = pair ? 1 : 0;
         pr.g = ctx->grid;
@@ -860,7 +868,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
         pr.mst_w = fb_mads && poll_possible && d_obj && d_prev && !d_area && N <= kPrepU ? fb_mads->st
                                                                                            : nullptr;
         if (poll_possible) {
-            L->prec.reserve(sizeof(int4) * (size_t)nchain * N);
+            L->prec.reserve(sizeof(int4) * (size_t)nrec * N);
             pr.prec = L->prec.as<int4>();
         }
         if (want_keys) {
@@ -874,8 +882,9 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             isrc.keysT = pr.keysT;
             isrc.ldk = ldk;
         }
-        uint64_t* tsk = poll_possible ? take_ts(nchain, ts_c, ts_nc) : nullptr;
-        hipLaunchKernelGGL(prep_kernel, dim3((unsigned)nchain), dim3(kPrepU), 0, s, tsk, pr);
+        uint64_t* tsk = poll_possible ? take_ts(nrec, ts_c, ts_nc) : nullptr;
+        if (gx5) hipLaunchKernelGGL(prep_x_kernel, dim3((unsigned)nrec), dim3(kPrepU + kWave), 0, s, tsk, pr);
+        else hipLaunchKernelGGL(prep_kernel, dim3((unsigned)nchain), dim3(kPrepU), 0, s, tsk, pr);
         HCK(hipGetLastError());
     }
 
@@ -938,7 +947,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             L->mode.reserve((1 + kDcCount) * sizeof(int));  // [0] walk, [1..kDcCount] the poll walk's counters (k_common.h)
             const IndexOut io{L->disks.as<DiskRec>(), L->umap.as<int>(), L->ucount.as<int>(),
                               L->region.as<int4>(), L->cost.as<double2>(), L->mode.as<int>() + 1,
-                              L->prec.as<int4>(), nchain,
+                              L->prec.as<int4>(), nrec,
                               L->lane4.as<float4>(), L->lanexp.as<float>(), L->rows.as<int2>(),
                               ctx->off.as<int32_t>(),
                               // cons3 failures are not evaluated (objective +inf) unless the caller

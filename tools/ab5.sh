@@ -12,7 +12,8 @@ for r in $(seq 1 "$R"); do
     python3 - "$v" "gpurun_out/ab5/$v$r.log" <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][0])
-print(sys.argv[1], "ms_per_step %.2f" % d["ms_per_step"], "chain_us %.1f" % (d["roofline"]["chain_ms"] * 1e3))
+print(sys.argv[1], "ms_per_step %.2f" % d["ms_per_step"], "chain_us %.1f" % (d["roofline"]["chain_ms"] * 1e3),
+      {k: round(v["avg_us"], 1) for k, v in d["roofline"]["kernels"].items()})
 PY
   done
 done
