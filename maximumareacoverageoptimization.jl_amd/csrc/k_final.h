@@ -268,9 +268,13 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
     // poll walk's map and neighbour counts are read speculatively: both are valid memory for
     // either walk), so it costs no round trip of its own
     const int mv = mode ? *mode : 0;
-    // the candidate's penalty, loaded with the first batch of rows (one round trip fewer)
-    const double vpk = (vp && sg == 0 && k < K) ? vp[k] : 0.0;
-    if (counts && spart && map) {  // equal weights: integer rows, exact in any order
+    // the candidate's penalty, loaded with the first batch of rows (one round trip fewer); every
+    // lane of the poll walk's counts path takes it: a candidate that failed cons3 (vp = +inf, no area
+    // asked for) has objective +inf whatever it covers, so its count gathers — the second, dependent
+    // round trip — are left out (config 5: most of a poll's candidates at l >= 2)
+    const bool cnt_path = counts && spart && map;
+    const double vpk = (vp && (sg == 0 || cnt_path) && k < K) ? vp[k] : 0.0;
+    if (cnt_path) {  // equal weights: integer rows, exact in any order
         constexpr int B = 8;
         int pos0[B];
         bool sh0[B];
@@ -281,13 +285,14 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(
             pos0[b] = in ? map[(int64_t)gb * K + k] : -1;
             sh0[b] = in && ncount[gb] > 0;
         }
+        const bool skip = vp && !area_out && !(vpk < __builtin_inf());   // (+inf or NaN: no area needed)
         if (mv == kModePoll) {
             const unsigned* const crow = reinterpret_cast<const unsigned*>(partial);
             const unsigned* const srow = reinterpret_cast<const unsigned*>(spart);
             __shared__ uint64_t ired[kFinThreads / kFinC][kFinC];
             const int G = n_poll;
             uint64_t a = 0;
-            if (k < K) {
+            if (k < K && !skip) {
                 // per row: the count at candidate k's position (the poll walk writes one per
                 // position, the map gives candidate k's), plus its shared-entry count when the
                 // disk has neighbours
