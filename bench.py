@@ -555,6 +555,10 @@ def main():
                          "all-gather on the poll's stream and the device argmin in one C call "
                          "(dist.RcclExchange); torch = torch.distributed's all-gather, then the "
                          "device argmin (dist.PollGather)")
+    ap.add_argument("--stamps", default="separate", choices=("separate", "timed"),
+                    help="config 2-4: in-kernel stamps (roofline.kernels, chain) from a second pass "
+                         "over the same steps after the timed region (separate, default) or from "
+                         "the timed steps themselves (timed)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL on ROCm) for the real multi-GPU run; gloo only to rehearse "
                          "N>1 with several ranks sharing one GPU (MAXCOVER_BENCH_DEVICE)")
@@ -758,8 +762,26 @@ def main():
         if not check:
             log("WARNING: timed poll vs scan disagree", pick, o_scan, objs[pick], got_best)
 
-    ctx.profile(True)
-    ctx.profile_read(reset=True)
+    def run_steps(first):
+        res = None
+        if armed:
+            for i in range(first, first + args.steps):
+                fire(i % nb)
+                if i + 1 < first + args.steps:
+                    arm((i + 1) % nb)
+                res = fetch(i % nb)
+        else:
+            for i in range(args.steps):
+                res = step(first + i)
+        return res
+
+    # the timed region; the in-kernel stamps (roofline, kernels) come from the same steps run once
+    # more right after it with stamping on (--stamps separate, the default: the stamps' host
+    # bookkeeping stays out of the timed polls), or from the timed steps themselves (--stamps timed)
+    stamp_timed = args.stamps == "timed"
+    if stamp_timed:
+        ctx.profile(True)
+        ctx.profile_read(reset=True)
     if gat is not None:
         gat.seconds, gat.calls = 0.0, 0
     if distributed:
@@ -769,20 +791,18 @@ def main():
                 # later poll's is enqueued while its predecessor runs)
         arm(args.warmup % nb)
     t0 = time.perf_counter()
-    result = None
-    if armed:
-        for i in range(args.warmup, args.warmup + args.steps):
-            fire(i % nb)
-            if i + 1 < args.warmup + args.steps:
-                arm((i + 1) % nb)
-            result = fetch(i % nb)
-    else:
-        for i in range(args.steps):
-            result = step(args.warmup + i)
+    result = run_steps(args.warmup)
     if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    if not stamp_timed:   # the stamped pass: the same polls (the same poll sets, in order)
+        ctx.profile(True)
+        ctx.profile_read(reset=True)
+        if armed:
+            arm(args.warmup % nb)
+        run_steps(args.warmup)
+        torch.cuda.synchronize(dev)
     split = ctx.profile_split()
     kern = ctx.profile_kernels()
     k_ms, k_launches, k_cands, k_walk = ctx.profile_read(reset=True)
@@ -941,7 +961,10 @@ def main():
                     if k_launches else None,
                     "note": "SURVEY 8(d)'s full-scan bytes per evaluation: what a brute-force "
                             "scan would have to stream, not a roofline of this algorithm"},
-                "timing": "in-kernel workgroup stamps (s_memrealtime) over the timed steps",
+                "timing": ("in-kernel workgroup stamps (s_memrealtime) over the timed steps"
+                           if args.stamps == "timed" else
+                           "in-kernel workgroup stamps (s_memrealtime) over a second pass of the "
+                           "timed steps (the same polls), run right after the timed region"),
                 "note": "achieved = floor.bytes / chain_ms (first workgroup start of the chain's "
                         "first launch to the last workgroup end of its last); avg_launch_ms = the "
                         "dominant (longest) kernel alone, kernels = every launch of the chain "
