@@ -11,6 +11,7 @@
 #include <sys/syscall.h>
 #include <unistd.h>
 #include <hipcub/hipcub.hpp>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <chrono>
@@ -90,7 +91,9 @@ static thread_local std::vector<std::pair<void*, bool>>* t_defer_free = nullptr;
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
-    void reserve(size_t bytes)
+    // fine: fine-grained device memory (host-writable through a large BAR: the closure's
+    // candidates, closure_launch)
+    void reserve(size_t bytes, bool fine = false)
     {
         if (bytes <= cap) return;
         if (p && t_defer_free)
@@ -101,7 +104,10 @@ struct DevBuf {
         cap = 0;
         size_t b = bytes < 256 ? 256 : bytes;
         b = (b + 255) & ~(size_t)255;
-        HCK(hipMalloc(&p, b));
+        if (fine)
+            HCK(hipExtMallocWithFlags(&p, b, hipDeviceMallocFinegrained));
+        else
+            HCK(hipMalloc(&p, b));
         cap = b;
     }
     // reserve(); true when the buffer was (re)allocated (its contents are then undefined)
@@ -164,6 +170,7 @@ struct Lane {
     uint64_t* d_cl = nullptr;                  // ... its device address
     uint64_t cl_seq = 0;
     DevBuf cpart, carrive, ctot;               // closure_kernel: credits, arrivals, packed count
+    DevBuf clv;                                // closure candidates written by the host (BAR)
     DevBuf prec, cost;                         // prep launch: per-disk records; walk costs
     int um_hist[8] = {};                       // most distinct positions of a disk, last 8 polls
     int walk_hist[8] = {};                     // the walk AUTO would have chosen, last 8 polls
@@ -214,11 +221,19 @@ struct mac_ctx {
     // mac_area_f64's combiner: queued single-candidate requests, one batch launch at a time
     std::mutex cl_mu;
     std::deque<struct ClReq*> cl_q;
-    int cl_busy = 0;   // batches in flight
+    std::atomic<int> cl_busy{0};   // batches being launched (changed under cl_mu; read as a hint)
     std::atomic<int> cl_active{0};   // callers inside mac_area_f64's combiner
     int cl_taken = 0;                // requests in batches in flight (under cl_mu)
+    // queued callers sleep on the futex word of their generation (the batches taken since the
+    // context began, cl_gen: every request queued between two takes is in the second's batch)
+    std::atomic<uint32_t> cl_gen{0};     // (changed under cl_mu)
+    std::atomic<int> cl_genw[64] = {};
     int64_t cl_batches = 0, cl_reqs = 0;   // (MAXCOVER_CL_STATS=1: printed at destroy)
-    double cl_phase_s[2] = {0, 0};         // per batch: staging, copy + launch enqueued
+    // MAXCOVER_CL_STATS=1 (nanoseconds, relaxed adds: no lock on the combiner's path)
+    std::atomic<int64_t> cl_phase_ns[4] = {};   // per batch: staging, copy + launch enqueued, hand-out, lane
+    std::atomic<int64_t> cl_req_ns[5] = {};     // per request: queued -> taken -> handed out -> seen ->
+                                                // slot read; the call
+    std::atomic<int64_t> cl_led{0};             // requests whose own thread led their batch
     std::vector<Lane*> lanes_free;
     std::vector<Lane*> lanes_all;
     hipStream_t setup_stream = nullptr;
@@ -272,6 +287,9 @@ struct mac_ctx {
     Grid grid{};
     int64_t nTiles = 1;
     bool w_uniform = false;   // every entry's weight is bit-identical to w0 (build_index)
+    // the host writes closure candidates straight into fine-grained device memory (a large-BAR
+    // device: no host-to-device copy per closure batch); MAXCOVER_CL_BAR=0 turns it off
+    bool cl_bar = false;
     double w0 = 0.0;
     // setup scratch
     DevBuf keys_in, keys_out, idx_in, tmp, bbox, flags_s, flags_o, keep, sel_count, cx, cy, cw,
@@ -1598,6 +1616,10 @@ int32_t mac_ctx_create(mac_ctx** out, int32_t device)
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         ctx->cus = prop.multiProcessorCount;
+    int bar = 0;
+    const char* eb = std::getenv("MAXCOVER_CL_BAR");
+    ctx->cl_bar = hipDeviceGetAttribute(&bar, hipDeviceAttributeIsLargeBar, device) == hipSuccess && bar == 1 &&
+                  !(eb && *eb == '0');
     HCK(hipStreamCreateWithFlags(&ctx->setup_stream, hipStreamNonBlocking));
     *out = ctx;
     return MAC_OK;
@@ -1607,11 +1629,18 @@ int32_t mac_ctx_create(mac_ctx** out, int32_t device)
 void mac_ctx_destroy(mac_ctx* ctx)
 {
     if (!ctx) return;
-    if (const char* e = std::getenv("MAXCOVER_CL_STATS"); e && *e == '1' && ctx->cl_batches)
+    if (const char* e = std::getenv("MAXCOVER_CL_STATS"); e && *e == '1' && ctx->cl_batches) {
         std::fprintf(stderr, "maxcover: closure batches %lld, requests %lld (%.2f per batch); per batch (us): "
-                     "staging %.1f, copy+launch %.1f\n",
+                     "lane %.1f, staging %.1f, copy+launch %.1f, hand-out %.1f\n",
                      (long long)ctx->cl_batches, (long long)ctx->cl_reqs, (double)ctx->cl_reqs / (double)ctx->cl_batches,
-                     ctx->cl_phase_s[0] / ctx->cl_batches * 1e6, ctx->cl_phase_s[1] / ctx->cl_batches * 1e6);
+                     ctx->cl_phase_ns[3] * 1e-3 / ctx->cl_batches, ctx->cl_phase_ns[0] * 1e-3 / ctx->cl_batches,
+                     ctx->cl_phase_ns[1] * 1e-3 / ctx->cl_batches, ctx->cl_phase_ns[2] * 1e-3 / ctx->cl_batches);
+        const double u = 1e-3 / (double)ctx->cl_reqs;
+        std::fprintf(stderr, "maxcover: closure per request (us): queued %.1f, taken -> handed out %.1f, "
+                     "-> seen %.1f, -> slot read %.1f; call %.1f; led by own thread %.0f%%\n",
+                     ctx->cl_req_ns[0] * u, ctx->cl_req_ns[1] * u, ctx->cl_req_ns[2] * u, ctx->cl_req_ns[3] * u,
+                     ctx->cl_req_ns[4] * u, 100.0 * ctx->cl_led / ctx->cl_reqs);
+    }
     if (ctx->host_stats && ctx->hs_n)
         std::fprintf(stderr, "maxcover: fused polls %lld, host us per poll: to prep launch %.2f, prep launch %.2f, "
                      "fiw launch %.2f, fin2 launch %.2f\n", (long long)ctx->hs_n, ctx->hs_t[0] / ctx->hs_n * 1e6,
@@ -1639,7 +1668,7 @@ void mac_ctx_destroy(mac_ctx* ctx)
                           &l->ncount, &l->dlist, &l->qual, &l->spart, &l->vp, &l->xinc,
                           &l->perm, &l->ucount, &l->umap, &l->keysT, &l->lane4,
                           &l->lanexp, &l->rows, &l->nboxT, &l->cnt, &l->dlimraw, &l->finblk, &l->finarrive, &l->c32, &l->p32,
-                          &l->cpart, &l->carrive, &l->ctot, &l->prec, &l->cost, &l->nboxU,
+                          &l->cpart, &l->carrive, &l->ctot, &l->clv, &l->prec, &l->cost, &l->nboxU,
                           &l->ncountU, &l->orjobs, &l->pd, &l->dead8, &l->frows, &l->fwhint, &l->fwlist, &l->fwcount,
                           &l->fwsxy, &l->fwsw})
             b->release();
@@ -2719,9 +2748,10 @@ int32_t mac_mads_run(mac_ctx* ctx, const double* x0, int64_t three_n, const doub
     ABI_END
 }
 
-// The single-candidate closure (k_closure.h): the candidates through the lane's pinned staging, one
-// kernel (grid.y = the batch), each area from its own mapped slot (no copy back, no stream
-// synchronisation). AUTO / TILED walks, N <= kClosureMaxN; if a slot has not landed within 2 ms (a
+// The single-candidate closure (k_closure.h): the candidates written by the host straight into the
+// lane's fine-grained device buffer through the BAR (a large-BAR device; else pinned staging and a
+// copy), one kernel (grid.y = the batch), each area from its own mapped slot (no copy either way,
+// no stream synchronisation). AUTO / TILED walks, N <= kClosureMaxN; if a slot has not landed within 2 ms (a
 // failed launch) a stream synchronisation reports it.
 static constexpr int kClBatch = 64;   // concurrent mac_area_f64 calls evaluated by one launch
 // slot reads spun with a pause before a reader starts yielding its CPU (MAXCOVER_CL_READSPIN overrides)
@@ -2735,6 +2765,14 @@ static bool closure_path(const mac_ctx* ctx, int64_t three_n)
     return (ctx->algo == MAC_ALGO_AUTO || ctx->algo == MAC_ALGO_TILED) && three_n / 3 <= kClosureMaxN;
 }
 
+static const bool kClStats = [] {
+    const char* e = std::getenv("MAXCOVER_CL_STATS");
+    return e && *e == '1';
+}();static void cl_add(std::atomic<int64_t>& a, std::chrono::steady_clock::duration d)
+{
+    a.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(d).count(), std::memory_order_relaxed);
+}
+
 // A launched batch of closure candidates: its lane (stream, staging, result slots) stays with the
 // batch until every one of its callers has read its slot (the last returns the lane to the pool),
 // so a later batch can neither overwrite a slot nor the staging before they are consumed.
@@ -2744,8 +2782,8 @@ struct ClBatch {
     std::atomic<int> readers{0};
 };
 
-// Stage the B candidates in the lane's pinned buffer, copy them up and launch one closure_kernel
-// (grid.y = B) whose candidate b writes its area into the lane's mapped slot b under `seq`. Returns
+// Write the B candidates into the lane's device buffer (through the BAR, or pinned staging and a
+// copy) and launch one closure_kernel (grid.y = B) whose candidate b writes its area into the lane's mapped slot b under `seq`. Returns
 // after enqueueing: the launching caller does not wait for the results.
 static uint64_t closure_launch(mac_ctx* ctx, Lane* L, int64_t three_n, const double* const* cands, int B)
 {
@@ -2753,10 +2791,20 @@ static uint64_t closure_launch(mac_ctx* ctx, Lane* L, int64_t three_n, const dou
     hipStream_t s = L->stream;
     const size_t one = sizeof(double) * (size_t)three_n;
     const auto t0 = std::chrono::steady_clock::now();
-    L->h_io.reserve(std::max<size_t>(one * B, 64));
-    for (int b = 0; b < B; ++b) std::memcpy((char*)L->h_io.p + one * b, cands[b], one);
+    const double* dc;
+    if (ctx->cl_bar) {   // straight into device memory through the BAR; the fence drains the
+                         // write-combining buffers before the launch's doorbell
+        L->clv.reserve(one * kClBatch, true);
+        for (int b = 0; b < B; ++b) std::memcpy((char*)L->clv.p + one * b, cands[b], one);
+        _mm_sfence();
+        dc = L->clv.as<double>();
+    } else {
+        L->h_io.reserve(std::max<size_t>(one * B, 64));
+        for (int b = 0; b < B; ++b) std::memcpy((char*)L->h_io.p + one * b, cands[b], one);
+        L->cands.reserve(one * B);
+        dc = L->cands.as<double>();
+    }
     const auto t1 = std::chrono::steady_clock::now();
-    L->cands.reserve(one * B);
     L->area.reserve(sizeof(double) * B);
     L->cpart.reserve(sizeof(unsigned long long) * (size_t)N * B);
     // zero once; the last block of each candidate resets its words
@@ -2770,7 +2818,7 @@ static uint64_t closure_launch(mac_ctx* ctx, Lane* L, int64_t three_n, const dou
         L->d_cl = (uint64_t*)dp;
     }
     const uint64_t seq = ++L->cl_seq;
-    HCK(hipMemcpyAsync(L->cands.p, L->h_io.p, one * B, hipMemcpyHostToDevice, s));
+    if (!ctx->cl_bar) HCK(hipMemcpyAsync(L->cands.p, L->h_io.p, one * B, hipMemcpyHostToDevice, s));
     const int nwg = (N + kClosureDisksPerWG - 1) / kClosureDisksPerWG;   // a wave per disk
     int64_t ts_a = -1;
     uint64_t* ts = nullptr;
@@ -2785,7 +2833,7 @@ static uint64_t closure_launch(mac_ctx* ctx, Lane* L, int64_t three_n, const dou
     const ClosureOut co{L->cpart.as<unsigned long long>(), L->ctot.as<unsigned long long>(),
                         L->carrive.as<unsigned>(), L->area.as<double>(), L->d_cl, seq};
     hipLaunchKernelGGL(closure_kernel, dim3((unsigned)nwg, (unsigned)B), dim3(kBlock),
-                       (uint32_t)closure_lds_bytes(N), s, ts, L->cands.as<double>(), N, ctx->grid,
+                       (uint32_t)closure_lds_bytes(N), s, ts, dc, N, ctx->grid,
                        ctx->xys.as<double2>(), ctx->ws.as<double>(), ctx->off.as<int32_t>(),
                        ctx->w_uniform ? 1 : 0, ctx->w0, co);
     HCK(hipGetLastError());
@@ -2793,10 +2841,11 @@ static uint64_t closure_launch(mac_ctx* ctx, Lane* L, int64_t three_n, const dou
         std::lock_guard<std::mutex> lk(ctx->mu);
         ctx->prof.push_back({ts_a, (int64_t)nwg * B, -1, 0, (int64_t)B, nullptr, MAC_ALGO_TILED});
     }
-    const auto t2 = std::chrono::steady_clock::now();
-    std::lock_guard<std::mutex> lk(ctx->cl_mu);
-    ctx->cl_phase_s[0] += std::chrono::duration<double>(t1 - t0).count();
-    ctx->cl_phase_s[1] += std::chrono::duration<double>(t2 - t1).count();
+    if (kClStats) {
+        const auto t2 = std::chrono::steady_clock::now();
+        cl_add(ctx->cl_phase_ns[0], t1 - t0);
+        cl_add(ctx->cl_phase_ns[1], t2 - t1);
+    }
     return seq;
 }
 
@@ -2859,8 +2908,35 @@ static const int kClLeaders = [] {
     const int v = e ? std::atoi(e) : 0;
     return v >= 1 && v <= 16 ? v : MAC_CL_LEADERS;
 }();
-static constexpr int kClSpin = 64;        // pause iterations before a waiter sleeps on its futex
+// pause iterations before a waiter sleeps on its futex (MAXCOVER_CL_SPIN overrides, for measurements)
+static const int kClSpin = [] {
+    const char* e = std::getenv("MAXCOVER_CL_SPIN");
+    return e ? std::max(0, std::atoi(e)) : 64;
+}();
+
 static constexpr int kClGather = 0;        // pauses a would-be leader waits for every caller to queue (0: none)
+// batches one thread launches in a row while requests are queued (MAXCOVER_CL_LEAD overrides): the
+// launching thread is awake on a CPU, a queued caller woken to lead instead takes tens of
+// microseconds to run; the cap bounds how long the leader's own call waits behind others' batches
+static const int kClLead = [] {
+    const char* e = std::getenv("MAXCOVER_CL_LEAD");
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 1 ? v : 16;
+}();
+
+// Waiting while queued: a short spin, then a futex sleep (no CPU taken from the threads that lead
+// batches) on the word of the request's generation, or 1 ms. A leader that launches generation g's
+// batch bumps g's word and wakes ONE sleeper (a futex wake costs the waker microseconds per thread;
+// the launching thread is the combiner's bottleneck); a thread woken with its request launched
+// passes the wake on to the rest of its generation. A leader that frees a launch slot with requests
+// still queued wakes one of them to lead.
+static std::atomic<int>& cl_word(mac_ctx* ctx, uint32_t gen) { return ctx->cl_genw[gen & 63]; }
+
+static void cl_wake(std::atomic<int>& w, int n)
+{
+    w.fetch_add(1, std::memory_order_seq_cst);
+    syscall(SYS_futex, reinterpret_cast<int*>(&w), FUTEX_WAKE_PRIVATE, n, nullptr, nullptr, 0);
+}
 
 struct ClReq {
     const double* c;
@@ -2869,28 +2945,35 @@ struct ClReq {
     std::atomic<int> state{0};   // 0 queued, 1 taken by a batch, 2 failed, 3 launched (read the slot)
     std::atomic<int> released{0};   // 1 once the leader no longer touches the request (after its
                                     // futex wake): the owner's stack object may then go
+    uint32_t gen = 0;            // the generation whose futex word this request sleeps on (cl_mu)
+    std::chrono::steady_clock::time_point t_taken, t_handed;   // (MAXCOVER_CL_STATS=1)
     ClBatch* bt = nullptr;       // (state 3) the batch and this request's slot in it
     int b = 0;
     int32_t rc = MAC_OK;
     std::string err;
 };
 
-// Waiting on a request's state word: a short spin, then a futex sleep (no CPU taken from the
-// threads that lead batches); woken by the leader that launches the request, or by the leader
-// that frees a launch slot while the request is still queued (it may then lead), or after 1 ms.
-static void cl_wait(std::atomic<int>* w, int seen, int spin)
+static void cl_wait(mac_ctx* ctx, ClReq& r, int spin)
 {
     if (spin < kClSpin) {
         __builtin_ia32_pause();
         return;
     }
+    uint32_t g = r.gen;   // (written by this thread only)
+    if (r.state.load(std::memory_order_relaxed) == 0 && g != ctx->cl_gen.load(std::memory_order_relaxed)) {
+        // still queued past an earlier take (a batch of another size): join the current generation
+        std::lock_guard<std::mutex> lk(ctx->cl_mu);
+        if (r.state.load(std::memory_order_relaxed) == 0) r.gen = ctx->cl_gen.load(std::memory_order_relaxed);
+        g = r.gen;
+    }
+    std::atomic<int>& w = cl_word(ctx, g);
+    const int v = w.load(std::memory_order_seq_cst);
+    const int st = r.state.load(std::memory_order_seq_cst);
+    if (st == 2 || st == 3) return;
     struct timespec ts{0, 1000000};
-    syscall(SYS_futex, reinterpret_cast<int*>(w), FUTEX_WAIT_PRIVATE, seen, &ts, nullptr, 0);
-}
-
-static void cl_wake(std::atomic<int>* w)
-{
-    syscall(SYS_futex, reinterpret_cast<int*>(w), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+    syscall(SYS_futex, reinterpret_cast<int*>(&w), FUTEX_WAIT_PRIVATE, v, &ts, nullptr, 0);
+    const int now = r.state.load(std::memory_order_acquire);
+    if (now == 2 || now == 3) cl_wake(w, INT_MAX);   // the rest of the generation's sleepers
 }
 
 int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, double* area_out)
@@ -2911,45 +2994,67 @@ int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, doubl
     r.c = circles;
     r.three_n = three_n;
     r.out = area_out;
+    using clk = std::chrono::steady_clock;
+    const auto tq = kClStats ? clk::now() : clk::time_point{};
+    bool led = false;
     ctx->cl_active.fetch_add(1);
     {
         std::lock_guard<std::mutex> lk(ctx->cl_mu);
+        r.gen = ctx->cl_gen.load(std::memory_order_relaxed);
         ctx->cl_q.push_back(&r);
     }
-    for (int spin = 0;; ++spin) {
+    // take every queued request of the front request's size (up to kClBatch) as a batch, if a
+    // launch slot is free (under cl_mu)
+    auto take = [&](std::vector<ClReq*>& batch, bool& mixed) {
+        if (ctx->cl_busy >= kClLeaders || ctx->cl_q.empty()) return;
+        ++ctx->cl_busy;
+        ++ctx->cl_batches;
+        const uint32_t g = ctx->cl_gen.fetch_add(1, std::memory_order_relaxed);   // requests queued from
+                                                                                  // now on: the next batch's
+        const int64_t tn = ctx->cl_q.front()->three_n;
+        for (auto it = ctx->cl_q.begin(); it != ctx->cl_q.end() && (int)batch.size() < kClBatch;) {
+            if ((*it)->three_n == tn) {
+                if (kClStats) (*it)->t_taken = clk::now();
+                (*it)->state.store(1, std::memory_order_relaxed);
+                batch.push_back(*it);
+                ++ctx->cl_reqs;
+                ++ctx->cl_taken;
+                it = ctx->cl_q.erase(it);
+            } else {
+                ++it;
+            }
+        }
+        // a request of this generation left queued (another size, or past kClBatch) sleeps on the
+        // same word: the batch's wake must then reach every sleeper, not one
+        mixed = false;
+        for (ClReq* q : ctx->cl_q) mixed |= q->gen == g;
+    };
+    std::vector<ClReq*> batch;
+    bool mixed = false;
+    for (int spin = 0, led_batches = 0;; ++spin) {
         const int st = r.state.load(std::memory_order_acquire);
-        if (st == 2 || st == 3) break;
-        std::vector<ClReq*> batch;
-        if (st == 0) {
+        const bool mine = st == 2 || st == 3;   // this request is launched (or failed)
+        if (mine && (batch.empty() || led_batches >= kClLead)) break;
+        if (!mine && batch.empty() && ctx->cl_busy.load(std::memory_order_relaxed) < kClLeaders) {
             std::lock_guard<std::mutex> lk(ctx->cl_mu);
             // lead once every caller in the combiner has queued (the whole convoy in one launch),
             // or after a short wait
             const bool all_in = (int)ctx->cl_q.size() + ctx->cl_taken >= ctx->cl_active.load() ||
                                 spin >= kClGather;
-            if (r.state.load(std::memory_order_relaxed) == 0 && ctx->cl_busy < kClLeaders && all_in &&
-                !ctx->cl_q.empty()) {
-                ++ctx->cl_busy;
-                ++ctx->cl_batches;
-                const int64_t tn = ctx->cl_q.front()->three_n;
-                for (auto it = ctx->cl_q.begin(); it != ctx->cl_q.end() && (int)batch.size() < kClBatch;) {
-                    if ((*it)->three_n == tn) {
-                        (*it)->state.store(1, std::memory_order_relaxed);
-                        batch.push_back(*it);
-                        ++ctx->cl_reqs;
-                        ++ctx->cl_taken;
-                        it = ctx->cl_q.erase(it);
-                    } else {
-                        ++it;
-                    }
-                }
-            }
+            if (r.state.load(std::memory_order_relaxed) == 0 && all_in) take(batch, mixed);
         }
         if (batch.empty()) {
             const int seen = r.state.load(std::memory_order_acquire);
-            if (seen != 2 && seen != 3) cl_wait(&r.state, seen, spin);
+            if (seen != 2 && seen != 3) cl_wait(ctx, r, spin);
             continue;
         }
-        // lead: launch the batch, hand every request its slot, go back to waiting for our own
+        // lead: launch the batch, hand every request its slot; then, while requests are queued and
+        // up to kClLead batches, lead again (this thread is awake on a CPU: a queued caller woken
+        // to lead takes tens of microseconds to run under load), else wait for our own slot
+        for (ClReq* q : batch) led |= q == &r;
+        ++led_batches;
+        const bool again = led_batches < kClLead;
+        const auto tp = kClStats ? clk::now() : clk::time_point{};
         ClBatch* bt = new ClBatch();
         bt->readers.store((int)batch.size(), std::memory_order_relaxed);
         int32_t brc = MAC_OK;
@@ -2959,6 +3064,7 @@ int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, doubl
             for (size_t q = 0; q < batch.size(); ++q) cs[q] = batch[q]->c;
             set_device(ctx);
             bt->L = acquire_lane(ctx, nullptr);
+            if (kClStats) cl_add(ctx->cl_phase_ns[3], clk::now() - tp);
             bt->seq = closure_launch(ctx, bt->L, batch[0]->three_n, cs.data(), (int)batch.size());
         } catch (const HipError& he) {
             brc = he.e == hipErrorOutOfMemory ? MAC_E_NOMEM : MAC_E_HIP;
@@ -2981,33 +3087,50 @@ int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, doubl
             delete bt;
             bt = nullptr;
         }
-        ClReq* next = nullptr;   // a queued request whose thread may lead the freed launch slot
+        const auto th = kClStats ? clk::now() : clk::time_point{};
+        std::vector<uint32_t> wake_gens;
+        std::vector<ClReq*> handed;
+        handed.swap(batch);
+        const int wake_n = mixed ? INT_MAX : 1;
         {
             std::lock_guard<std::mutex> lk(ctx->cl_mu);
             --ctx->cl_busy;
-            ctx->cl_taken -= (int)batch.size();
-            for (ClReq* q : ctx->cl_q)
-                if (q != &r) {
-                    next = q;
-                    break;
-                }
-            if (next) cl_wake(&next->state);   // (under the lock: the request still exists)
+            ctx->cl_taken -= (int)handed.size();
+            if (again && brc == MAC_OK) {
+                take(batch, mixed);   // the next batch, taken before this one's callers run
+            } else {   // a queued request whose thread may lead the freed launch slot
+                for (ClReq* q : ctx->cl_q)
+                    if (q != &r) {
+                        cl_wake(cl_word(ctx, q->gen), 1);
+                        break;
+                    }
+            }
+            // the generations of the handed-out requests (one, but for requests of another size
+            // queued past an earlier take)
+            for (ClReq* q : handed) wake_gens.push_back(q->gen);
         }
-        for (size_t q = 0; q < batch.size(); ++q) {   // (a request lives until its released word reads 1)
-            ClReq* rq = batch[q];
+        for (size_t q = 0; q < handed.size(); ++q) {   // (a request lives until its released word reads 1)
+            ClReq* rq = handed[q];
             rq->bt = bt;
             rq->b = (int)q;
             rq->rc = brc;
             rq->err = msg;
-            rq->state.store(bt ? 3 : 2, std::memory_order_release);
-            if (rq != &r) cl_wake(&rq->state);
+            if (kClStats) rq->t_handed = clk::now();
+            rq->state.store(bt ? 3 : 2, std::memory_order_seq_cst);
             rq->released.store(1, std::memory_order_release);
         }
+        // one sleeper per generation woken here; it wakes the others (cl_wait)
+        std::sort(wake_gens.begin(), wake_gens.end());
+        for (size_t q = 0; q < wake_gens.size(); ++q)
+            if (q == 0 || wake_gens[q] != wake_gens[q - 1])
+                cl_wake(cl_word(ctx, wake_gens[q]), wake_gens.front() == wake_gens.back() ? wake_n : INT_MAX);
+        if (kClStats) cl_add(ctx->cl_phase_ns[2], clk::now() - th);
         spin = 0;
     }
     // the leader that launched this request may still be between its state store and its wake (the
     // futex word is this stack object): wait for its release, a few instructions away
     while (r.released.load(std::memory_order_acquire) == 0) __builtin_ia32_pause();
+    const auto tl = kClStats ? clk::now() : clk::time_point{};
     if (r.state.load(std::memory_order_acquire) == 3) {
         try {
             *area_out = closure_read(ctx, r.bt, r.b);
@@ -3017,6 +3140,15 @@ int32_t mac_area_f64(mac_ctx* ctx, const double* circles, int64_t three_n, doubl
             throw;
         }
         closure_done(ctx, r.bt);
+    }
+    if (kClStats) {
+        const auto te = clk::now();
+        cl_add(ctx->cl_req_ns[0], r.t_taken - tq);
+        cl_add(ctx->cl_req_ns[1], r.t_handed - r.t_taken);
+        cl_add(ctx->cl_req_ns[2], tl - r.t_handed);
+        cl_add(ctx->cl_req_ns[3], te - tl);
+        cl_add(ctx->cl_req_ns[4], te - tq);
+        ctx->cl_led.fetch_add(led, std::memory_order_relaxed);
     }
     ctx->cl_active.fetch_sub(1);
     if (r.rc) return fail(r.rc, r.err);

@@ -11,12 +11,32 @@ import bench  # noqa: E402
 
 pkg = ge.load_package()
 x, y, w, C, rmax = pkg.workloads.make_config(4)
-for T in (1, 4, 16):
+
+
+def cpu_stat():
+    """The cgroup's CPU accounting (cgroup v2 cpu.stat: usage and throttling), {} if absent."""
+    try:
+        return {k: int(v) for k, v in (ln.split() for ln in open("/sys/fs/cgroup/cpu.stat"))}
+    except OSError:
+        return {}
+
+
+try:
+    print("cpu.max", open("/sys/fs/cgroup/cpu.max").read().strip(), "affinity", len(os.sched_getaffinity(0)),
+          flush=True)
+except OSError:
+    pass
+for T in [int(t) for t in os.environ.get("CL_PROBE_THREADS", "1,4,16").split(",")]:
     ctx = pkg.Context(0)
     ctx.set_points(x, y, w)
-    ctx.profile(True)
+    prof = os.environ.get("CL_PROBE_PROFILE", "1") == "1"   # in-kernel stamps (as bench.py: off)
+    ctx.profile(prof)
     ctx.profile_read(reset=True)
+    c0 = cpu_stat()
     r = bench.closure_threads(ctx, C, (T,), seconds=0.5)
+    c1 = cpu_stat()
+    if c0 and c1:   # CPU-seconds per wall second (includes the probe's setup), throttled periods
+        r["cgroup"] = {k: c1.get(k, 0) - c0.get(k, 0) for k in ("usage_usec", "nr_throttled", "throttled_usec")}
     k_ms, k_launches, k_cands, _ = ctx.profile_read(reset=True)
     ctx.profile(False)
     r["kernel_us_per_launch"] = k_ms / max(k_launches, 1) * 1e3
