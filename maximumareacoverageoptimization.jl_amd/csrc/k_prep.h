@@ -815,8 +815,9 @@ __device__ __forceinline__ void prep_block_x(const PrepArgs& a, int cw, unsigned
 #pragma unroll
                 for (int q = 0; q < 3; ++q) {
                     const float f = (float)(v[c][q] - base[q]);
-                    kb |= !((dead >> c) & 1u) &&
-                          __builtin_bit_cast(uint64_t, base[q] + (double)f) != __builtin_bit_cast(uint64_t, v[c][q]);
+                    if constexpr (kGen)
+                        kb |= !((dead >> c) & 1u) &&
+                              __builtin_bit_cast(uint64_t, base[q] + (double)f) != __builtin_bit_cast(uint64_t, v[c][q]);
                     a.keysT[(int64_t)(q * N + u) * a.ldk + cand(c)] = f;
                 }
             }
@@ -847,7 +848,8 @@ __device__ __forceinline__ void prep_block_x(const PrepArgs& a, int cw, unsigned
                 if (cand(PC) < K) krow[cand(PC)] = pk[PC];
             }
         }
-        if (a.prec && iv) {
+        if (kGen && a.prec && iv) {
+            // (generated polls only: a matrix source takes this kernel in the fused chain alone)
             // the five-launch chain's partial region record (prep_block's): a tile box holding the
             // spans of the live candidates' disks, the span-area estimate and the key flag
             double xa = __builtin_inf(), xb = -__builtin_inf(), ya = __builtin_inf(), yb = -__builtin_inf();
@@ -908,7 +910,7 @@ __device__ __forceinline__ void prep_block_x(const PrepArgs& a, int cw, unsigned
     }
 }
 
-template <int PC, bool kX = false>
+template <int PC, bool kX = false, bool kGen = false>
 __device__ __forceinline__ void prep_body(uint64_t* ts, PrepArgs& a)
 {
     ts_begin(ts);   // profiling only (the chain's first launch: k_common.h)
@@ -923,8 +925,7 @@ __device__ __forceinline__ void prep_body(uint64_t* ts, PrepArgs& a)
     const int cw = (int)(gridDim.x % 8) == 0 ? (b % 8) * per + b / 8 : b;
     __shared__ __attribute__((aligned(16))) unsigned char lds[sizeof(PrepLds<kX ? PC + 1 : PC>)];
     if constexpr (kX) {   // (N <= kPrepU) a matrix, or a generated complete poll in column triples
-        if (a.src.cands) prep_block_x<false>(a, cw, lds);
-        else prep_block_x<true>(a, cw, lds);
+        prep_block_x<kGen>(a, cw, lds);
     } else if (a.src.cands) {
         prep_block<true, PC>(a, cw, lds);
     } else {
@@ -940,10 +941,15 @@ __global__ __launch_bounds__(kPrepU) __attribute__((amdgpu_waves_per_eu(4))) voi
 }
 
 // the fused chain's prep over a matrix source: kPrepCX (+1) candidates per workgroup (xbase), a
-// ninth wave folding the chains; two workgroups (18 waves) per CU
+// ninth wave folding the chains; two workgroups (18 waves) per CU. kGen: a generated complete poll
+// in column triples, its own kernel: one code path per register allocation (80 VGPRs each; the
+// matrix path spill-free, where one kernel holding both paths spilled 13 VGPRs: config 4's prep
+// 20.7 -> 26.1 us). 6 waves per EU beat 5 for the generated path too (prep 17.9 vs 23.7 us with
+// 82 VGPRs and no spill: the two it spills here are off the hot path)
+template <bool kGen>
 __global__ __launch_bounds__(kPrepU + kWave) __attribute__((amdgpu_waves_per_eu(6))) void prep_x_kernel(uint64_t* ts, PrepArgs a)
 {
-    prep_body<kPrepCX, true>(ts, a);
+    prep_body<kPrepCX, true, kGen>(ts, a);
 }
 
 // cands: see CandSrc. Writes disks[k*N + i] (the streaming scan's records).

@@ -785,7 +785,10 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             using hclk = std::chrono::steady_clock;
             hclk::time_point h1, h2, h3;
             if (ctx->host_stats) h1 = hclk::now();
-            if (xk) hipLaunchKernelGGL(prep_x_kernel, dim3((unsigned)nprep), dim3(kPrepU + kWave), 0, s, tsk, pr);
+            if (xk && gen_x)
+                hipLaunchKernelGGL(prep_x_kernel<true>, dim3((unsigned)nprep), dim3(kPrepU + kWave), 0, s, tsk, pr);
+            else if (xk)
+                hipLaunchKernelGGL(prep_x_kernel<false>, dim3((unsigned)nprep), dim3(kPrepU + kWave), 0, s, tsk, pr);
             else hipLaunchKernelGGL(prep_kernel, dim3((unsigned)nprep), dim3(kPrepU), 0, s, tsk, pr);
             HCK(hipGetLastError());
             if (ctx->host_stats) h2 = hclk::now();
@@ -901,7 +904,7 @@ static void enqueue_eval(mac_ctx* ctx, Lane* L, hipStream_t s, const CandSrc& sr
             isrc.ldk = ldk;
         }
         uint64_t* tsk = poll_possible ? take_ts(nrec, ts_c, ts_nc) : nullptr;
-        if (gx5) hipLaunchKernelGGL(prep_x_kernel, dim3((unsigned)nrec), dim3(kPrepU + kWave), 0, s, tsk, pr);
+        if (gx5) hipLaunchKernelGGL(prep_x_kernel<true>, dim3((unsigned)nrec), dim3(kPrepU + kWave), 0, s, tsk, pr);
         else hipLaunchKernelGGL(prep_kernel, dim3((unsigned)nchain), dim3(kPrepU), 0, s, tsk, pr);
         HCK(hipGetLastError());
     }

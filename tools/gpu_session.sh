@@ -154,7 +154,7 @@ for s in $STEPS; do
                 -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-extras ; rc=$?
         fi
         fatal $rc || python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write --config 4 \
-            --chain 'mac::prep_x_kernel;mac::fiw_kernel<true>;mac::fin2_kernel<true>' \
+            --chain 'mac::prep_x_kernel<false>;mac::fiw_kernel<true>;mac::fin2_kernel<true>' \
             --out gpurun_out/pmc_traffic_config4.json ;;
     diagprep)   # prep launch: per-workgroup spans; phases of the first 64 (diagnostic build)
         MAXCOVER_LIB=$PWD/maximumareacoverageoptimization.jl_amd/libmaxcover_diag.so \

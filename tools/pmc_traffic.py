@@ -48,7 +48,7 @@ def main():
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("--config", type=int, default=4)
-    ap.add_argument("--chain", default="mac::prep_x_kernel;mac::fiw_kernel<true>;mac::fin2_kernel<true>",
+    ap.add_argument("--chain", default="mac::prep_x_kernel<false>;mac::fiw_kernel<true>;mac::fin2_kernel<true>",
                     help="semicolon-separated kernels of one poll (default: the fused chain "
                          "config 4 takes; the five-launch chain: mac::prep_kernel;"
                          "mac::disk_index_kernel<true, 3>;mac::walk_setup_kernel;"
