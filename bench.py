@@ -223,6 +223,20 @@ def cpu_baseline(x, y, w, cands, seconds_target: float, threads: int):
     return n / dt, desc
 
 
+def stamp_setup(ctx, stamp_timed):
+    """Before the timed region: the stamp slots allocated and zeroed (ctx.profile(True): a device
+    synchronisation, 32 MB of slots, a memset), stamping then left on (--stamps timed) or off until
+    the stamped pass after the timed region. Ranks sharing one GPU (the gloo rehearsals) ran the
+    config-5 loop at 35.6 ms per MPC step with this set-up first done after the timed region, 22.6-24.4
+    with it before (same box; cause not identified; single-GPU runs: profiles/r06_stamp_setup_ab.json).
+    MAXCOVER_BENCH_NO_STAMP_SETUP=1 skips it (for that A/B)."""
+    if stamp_timed or os.environ.get("MAXCOVER_BENCH_NO_STAMP_SETUP") != "1":
+        ctx.profile(True)
+        ctx.profile_read(reset=True)
+        if not stamp_timed:
+            ctx.profile(False)
+
+
 def closure_threads(ctx, cands, sweep, seconds=0.25):
     """Aggregate mac_area_f64 calls/s with T native host threads calling at once (DirectSearch's
     SetMaxEvals threaded poll, src/TDM_STATIC_opt.jl:129: one objective call per trial point per
@@ -341,9 +355,7 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
     # the in-kernel stamps: from the timed MPC steps (--stamps timed) or, by default, from as many
     # MPC steps run right after them (the loop's state moves on, so the same steps cannot be rerun)
     stamp_timed = args.stamps == "timed"
-    if stamp_timed:
-        ctx.profile(True)
-        ctx.profile_read(reset=True)
+    stamp_setup(ctx, stamp_timed)
     recs = []
     if world > 1:
         dist.barrier()
@@ -791,9 +803,7 @@ def main():
     # more right after it with stamping on (--stamps separate, the default: the stamps' host
     # bookkeeping stays out of the timed polls), or from the timed steps themselves (--stamps timed)
     stamp_timed = args.stamps == "timed"
-    if stamp_timed:
-        ctx.profile(True)
-        ctx.profile_read(reset=True)
+    stamp_setup(ctx, stamp_timed)
     if gat is not None:
         gat.seconds, gat.calls = 0.0, 0
     if distributed:
