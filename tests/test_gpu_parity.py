@@ -307,6 +307,58 @@ def test_concurrent_closure_calls(ctx, pkg, orc, threads):
     assert not errs, errs[:5]
 
 
+def test_closure_bar_and_copy_paths_agree(pkg, orc):
+    """The closure's two ways in (maxcover.hip closure_launch): candidates written by the host
+    straight into fine-grained device memory through the BAR (the default on a large-BAR device)
+    and pinned staging + a copy (MAXCOVER_CL_BAR=0, read at context creation). Same areas, equal to
+    the C oracle's, for several disk counts and weighted entries, from one thread and from eight at
+    once (combined batches)."""
+    import os
+    import threading
+    wl = pkg.workloads
+    rng = wl.SplitMix64(4242)
+    x, y, w = wl.grid_points(180)
+    w = w * (1.0 + (np.arange(w.size) % 7) / 8.0)   # weighted: the fp64 credit path
+    rec = recs(x, y, w)
+    pl = orc.PointerList(rec)
+    polls = [wl.poll_candidates(wl.uniform_disks(N, 180, rng), rng)[:16] for N in (5, 17, 40)]
+    want = [pl.area_batch(C) for C in polls]
+    got = {}
+    for bar in ("1", "0"):
+        old = os.environ.get("MAXCOVER_CL_BAR")
+        os.environ["MAXCOVER_CL_BAR"] = bar
+        try:
+            c = pkg.Context(0)
+        finally:
+            if old is None:
+                del os.environ["MAXCOVER_CL_BAR"]
+            else:
+                os.environ["MAXCOVER_CL_BAR"] = old
+        try:
+            c.set_points(x, y, w)
+            single = [np.array([c.area(np.ascontiguousarray(C[k])) for k in range(C.shape[0])])
+                      for C in polls]
+            res = {}
+
+            def run(t):
+                C = polls[t % 3]
+                res[t] = [c.area(np.ascontiguousarray(C[k])) for k in range(t % 2, C.shape[0], 2)]
+
+            th = [threading.Thread(target=run, args=(t,)) for t in range(8)]
+            for h in th:
+                h.start()
+            for h in th:
+                h.join()
+            got[bar] = (single, res)
+        finally:
+            c.close()
+    for bar, (single, res) in got.items():
+        for j, C in enumerate(polls):
+            assert np.array_equal(single[j], want[j]), (bar, j)
+        for t, vals in res.items():
+            assert np.array_equal(np.array(vals), want[t % 3][t % 2::2]), (bar, t)
+
+
 # ---------------------------------------------------------------------------- device API
 
 def test_device_pointer_api(ctx, pkg, orc):
