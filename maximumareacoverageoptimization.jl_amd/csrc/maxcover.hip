@@ -218,6 +218,7 @@ struct mac_ctx {
     // q-th last reported poll did not suit it (a workload property: a MADS stepper or a new lane
     // takes it over from the lanes before it)
     std::atomic<uint64_t> fused_bad{0};
+    std::atomic<bool> route_seeded{false};   // the first matrix poll's routing from the poll (seed_route)
     // mac_area_f64's combiner: queued single-candidate requests, one batch launch at a time
     std::mutex cl_mu;
     std::deque<struct ClReq*> cl_q;
@@ -1171,6 +1172,21 @@ static int32_t check_common(mac_ctx* ctx, int64_t three_n, int64_t K)
 }
 
 // Host-pointer batch: upload, evaluate, download.
+static int host_crowded_disks(const double* x, int N, double b, double S);
+
+// A context's first matrix poll routes from the poll, before any chain has reported to the history
+// above: its candidate 0 (a DirectSearch poll's incumbent) overlap-tested as host_crowded_disks
+// does for generated polls, with no displacement (the matrix's spread is unknown here). A crowded
+// incumbent starts the history all "unsuited" (the five-launch chain; the fused chain again after
+// 64 polls that suit it), so a crowded poll does not pay the fused chain's in-place shared
+// decisions on its first call (clustered config 4: 2.7 ms against 0.17). Not from an arming call
+// (its stream waits on the doorbell: no synchronous copy there).
+static void seed_route(mac_ctx* ctx, const double* x0, int N)
+{
+    if (N > 0 && host_crowded_disks(x0, N, 0.0, ctx->grid.S) > kBitsMinDisks)
+        ctx->fused_bad.store(~(uint64_t)0, std::memory_order_relaxed);
+}
+
 template <class T>
 static int32_t host_eval(mac_ctx* ctx, const T* cands, int64_t three_n, int64_t K,
                          const double* r_max, double penalty, const T* prev,
@@ -1240,6 +1256,14 @@ static int32_t host_eval(mac_ctx* ctx, const T* cands, int64_t three_n, int64_t 
     }
     const double* hc = nullptr;
     if constexpr (!f32) hc = cands;   // (AUTO's host-side walk estimate reads fp64 candidates)
+    if (K > 1 && !t_defer_free && !ctx->route_seeded.exchange(true)) {
+        if constexpr (f32) {
+            std::vector<double> x0(cands, cands + three_n);
+            seed_route(ctx, x0.data(), N);
+        } else {
+            seed_route(ctx, cands, N);
+        }
+    }
     const bool tiled = use_tiled(ctx, N, hc, three_n);
     enqueue_eval(ctx, L, s, matrix_src(L->cands.as<double>(), N), N, (int)K, tiled, d_rmax, penalty, d_prev,
                  d_dlimT, d_prev ? L->dlimraw.as<double>() : nullptr, tan_half_fov,
@@ -1264,7 +1288,6 @@ static int32_t host_eval(mac_ctx* ctx, const T* cands, int64_t three_n, int64_t 
     return MAC_OK;
 }
 
-static int host_crowded_disks(const double* x, int N, double b, double S);
 
 // The basis form of a caller-owned poll (mac_poll_basis_f64): the incumbent, B = L[rp][:, cp] as L's
 // packed lower triangle (int16) with the two permutations, and delta; the 2n candidates
@@ -3336,6 +3359,12 @@ static int32_t poll_best_dev(mac_ctx* ctx, const T* d_cands_in, int64_t three_n,
     if (!d_o) {
         L->obj.reserve(sizeof(double) * K);
         d_o = L->obj.as<double>();
+    }
+    if (K > 1 && !t_defer_free && !ctx->route_seeded.exchange(true)) {   // (seed_route)
+        std::vector<double> x0((size_t)three_n);
+        HCK(hipMemcpyAsync(x0.data(), d_cands, sizeof(double) * (size_t)three_n, hipMemcpyDeviceToHost, s));
+        HCK(hipStreamSynchronize(s));
+        seed_route(ctx, x0.data(), N);
     }
     uint64_t seq = 0;
     uint64_t* d_mirror = assign_mirror(ctx, d_best, &seq);

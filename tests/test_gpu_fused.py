@@ -199,6 +199,46 @@ def test_large_counts_overflow_the_16bit_rows(ctx, pkg, orc, chain):
 
 
 @pytest.mark.parametrize("disks", ["clustered", "uniform"])
+@pytest.mark.parametrize("where", ["device", "host"])
+def test_first_matrix_poll_routes_from_the_poll(pkg, orc, disks, where):
+    """A context's first matrix poll (DirectSearch's, handed over as a candidate matrix) routes
+    from the poll before any chain has reported (maxcover.hip seed_route: candidate 0's disks
+    overlap-tested on the host): a crowded incumbent (clustered disks) runs the five-launch chain
+    from the first poll on — no fused launch — and an uncrowded one keeps the fused chain. The
+    objectives equal the C oracle's either way."""
+    import torch
+    wl = pkg.workloads
+    G, N = 512, 64
+    x, y, w = wl.grid_points(G)
+    rng = wl.SplitMix64(617 if disks == "clustered" else 618)
+    x0 = (wl.clustered_disks if disks == "clustered" else wl.uniform_disks)(N, G, rng)
+    C = wl.poll_candidates(x0, rng)
+    r_max = np.full(N, 30.0 * TAN50)
+    want = -orc.PointerList(recs(x, y, w)).area_batch(C) + orc.violation_batch(C, r_max) * 1e5
+    with pkg.Context(0) as c2:   # (a fresh context: no routing history)
+        c2.set_points(x, y, w)
+        c2.profile(True)
+        c2.profile_read(reset=True)
+        if where == "host":
+            _, _, obj = c2.poll_best(C, r_max, 1e5, want_all=True)
+        else:
+            dev = torch.device("cuda", 0)
+            dC = torch.from_numpy(np.ascontiguousarray(C)).to(dev)
+            dR = torch.from_numpy(r_max).to(dev)
+            dB = torch.empty(2, dtype=torch.float64, device=dev)
+            dO = torch.empty(C.shape[0], dtype=torch.float64, device=dev)
+            c2.poll_best_dev(dC, 3 * N, C.shape[0], dR, dB, d_obj=dO)
+            torch.cuda.synchronize()
+            obj = dO.cpu().numpy()
+        kern = {k: n for k, (ms, n) in c2.profile_kernels().items() if n}
+    assert np.array_equal(obj, want)
+    if disks == "clustered":
+        assert "fiw_kernel" not in kern and kern.get("coverage_poll_kernel", 0) > 0, kern
+    else:
+        assert kern.get("fiw_kernel", 0) > 0, kern
+
+
+@pytest.mark.parametrize("disks", ["clustered", "uniform"])
 def test_native_mads_routes_from_the_poll(ctx, pkg, disks):
     """The native MADS driver routes its generated polls from the poll (maxcover.hip
     host_crowded_disks: the fused chain's superset boxes around the incumbent at the run's first
