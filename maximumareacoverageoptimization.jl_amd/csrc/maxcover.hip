@@ -290,7 +290,7 @@ struct mac_ctx {
     bool w_uniform = false;   // every entry's weight is bit-identical to w0 (build_index)
     // the host writes closure candidates straight into fine-grained device memory (a large-BAR
     // device: no host-to-device copy per closure batch); MAXCOVER_CL_BAR=0 turns it off
-    bool cl_bar = false;
+    std::atomic<bool> cl_bar{false};
     double w0 = 0.0;
     // setup scratch
     DevBuf keys_in, keys_out, idx_in, tmp, bbox, flags_s, flags_o, keep, sel_count, cx, cy, cw,
@@ -2818,9 +2818,18 @@ static uint64_t closure_launch(mac_ctx* ctx, Lane* L, int64_t three_n, const dou
     const size_t one = sizeof(double) * (size_t)three_n;
     const auto t0 = std::chrono::steady_clock::now();
     const double* dc;
-    if (ctx->cl_bar) {   // straight into device memory through the BAR; the fence drains the
-                         // write-combining buffers before the launch's doorbell
-        L->clv.reserve(one * kClBatch, true);
+    bool bar = ctx->cl_bar.load(std::memory_order_relaxed);
+    if (bar) {
+        try {
+            L->clv.reserve(one * kClBatch, true);
+        } catch (const HipError&) {   // no fine-grained device memory to spare: the copy path from now on
+            (void)hipGetLastError();
+            ctx->cl_bar.store(false, std::memory_order_relaxed);
+            bar = false;
+        }
+    }
+    if (bar) {   // straight into device memory through the BAR; the fence drains the
+                 // write-combining buffers before the launch's doorbell
         for (int b = 0; b < B; ++b) std::memcpy((char*)L->clv.p + one * b, cands[b], one);
         _mm_sfence();
         dc = L->clv.as<double>();
@@ -2844,7 +2853,7 @@ static uint64_t closure_launch(mac_ctx* ctx, Lane* L, int64_t three_n, const dou
         L->d_cl = (uint64_t*)dp;
     }
     const uint64_t seq = ++L->cl_seq;
-    if (!ctx->cl_bar) HCK(hipMemcpyAsync(L->cands.p, L->h_io.p, one * B, hipMemcpyHostToDevice, s));
+    if (!bar) HCK(hipMemcpyAsync(L->cands.p, L->h_io.p, one * B, hipMemcpyHostToDevice, s));
     const int nwg = (N + kClosureDisksPerWG - 1) / kClosureDisksPerWG;   // a wave per disk
     int64_t ts_a = -1;
     uint64_t* ts = nullptr;
