@@ -224,9 +224,10 @@ def cpu_baseline(x, y, w, cands, seconds_target: float, threads: int):
 
 
 def stamp_setup(ctx, stamp_timed):
-    """Before the timed region: the stamp slots allocated and zeroed (ctx.profile(True): a device
-    synchronisation, 32 MB of slots, a memset), stamping then left on (--stamps timed) or off until
-    the stamped pass after the timed region. Ranks sharing one GPU (the gloo rehearsals) ran the
+    """Before the warmup (so that nothing stands between it and the timed region): the stamp slots
+    allocated and zeroed (ctx.profile(True): a device synchronisation, 32 MB of slots, a memset),
+    stamping then left on (--stamps timed; the warmup's stamps are reset before the timed steps) or
+    off until the stamped pass after the timed region. Ranks sharing one GPU (the gloo rehearsals) ran the
     config-5 loop at 35.6 ms per MPC step with this set-up first done after the timed region, 22.6-24.4
     with it before (same box; cause not identified; single-GPU runs: profiles/r06_stamp_setup_ab.json).
     MAXCOVER_BENCH_NO_STAMP_SETUP=1 skips it (for that A/B)."""
@@ -349,13 +350,16 @@ def bench_config5(args, pkg, dev_index, rank=0, world=1, coll_dev=None):
     sim = pkg.FullSimulation.Simulation(ctx, x0, fire=D, N_iter=args.mads_iters, seed=args.seed,
                                         shard=shard, gather=gather, speculate=spec)
     t_set = time.perf_counter() - t_set
+    # the in-kernel stamps: from the timed MPC steps (--stamps timed) or, by default, from as many
+    # MPC steps run right after them (the loop's state moves on, so the same steps cannot be rerun);
+    # the slots are set up before the warmup
+    stamp_timed = args.stamps == "timed"
+    stamp_setup(ctx, stamp_timed)
     for _ in range(args.warmup):
         sim.step()
     torch.cuda.synchronize()
-    # the in-kernel stamps: from the timed MPC steps (--stamps timed) or, by default, from as many
-    # MPC steps run right after them (the loop's state moves on, so the same steps cannot be rerun)
-    stamp_timed = args.stamps == "timed"
-    stamp_setup(ctx, stamp_timed)
+    if stamp_timed:
+        ctx.profile_read(reset=True)   # (the warmup steps' stamps out)
     recs = []
     if world > 1:
         dist.barrier()
@@ -755,36 +759,15 @@ def main():
                 return gat(d_best)
         return steps[i % len(steps)]()   # poll + the 16-B result from pinned host memory
 
+    # the stamp slots before the warmup, so that the warmup polls lead straight into the timed ones
+    stamp_timed = args.stamps == "timed"
+    stamp_setup(ctx, stamp_timed)
     if armed:
         run_armed(0, args.warmup)
     else:
         for i in range(args.warmup):
             step(i)
     torch.cuda.synchronize(dev)
-
-    # correctness guard on the timed workload: the timed poll (this rank's shard, the device's
-    # walk choice, cons3) writes every objective; 16 sampled candidates plus its argmin are
-    # re-evaluated by the streaming scan (an independent kernel) and must agree bit for bit
-    check = None
-    if K > 1 and not args.no_extras:
-        d_obj = torch.empty(Kl, dtype=torch.float64, device=dev)
-        ctx.poll_best_dev(d_polls[0], 3 * N, Kl, d_rmax, d_best, d_prev=d_prevs[0], d_dlim=d_dlim,
-                          tan_half_fov=tan_half, idx_base=idx_base, d_obj=d_obj, stream=s_handle)
-        got_best = ctx.best_fetch(d_best, stream=s_handle)
-        torch.cuda.synchronize(dev)
-        objs = d_obj.cpu().numpy()
-        pick = np.unique(np.concatenate([
-            np.floor(wl.SplitMix64(args.seed + 7).uniform(16) * Kl).astype(np.int64),
-            [int(np.argmin(objs))]]))
-        ctx.set_algo("scan")
-        _, _, o_scan = ctx.poll_best(polls[0][lo:hi][pick], r_max, 1e5, prev=polls[0][0],
-                                     d_lim=dlim, tan_half_fov=tan_half, want_all=True)
-        ctx.set_algo(args.algo)
-        kmin = int(np.argmin(objs))
-        check = bool(np.array_equal(o_scan, objs[pick]) and got_best[1] == idx_base + kmin
-                     and got_best[0] == objs[kmin])
-        if not check:
-            log("WARNING: timed poll vs scan disagree", pick, o_scan, objs[pick], got_best)
 
     def run_steps(first):
         res = None
@@ -802,8 +785,8 @@ def main():
     # the timed region; the in-kernel stamps (roofline, kernels) come from the same steps run once
     # more right after it with stamping on (--stamps separate, the default: the stamps' host
     # bookkeeping stays out of the timed polls), or from the timed steps themselves (--stamps timed)
-    stamp_timed = args.stamps == "timed"
-    stamp_setup(ctx, stamp_timed)
+    if stamp_timed:
+        ctx.profile_read(reset=True)   # (the warmup polls' stamps out)
     if gat is not None:
         gat.seconds, gat.calls = 0.0, 0
     if distributed:
@@ -836,6 +819,31 @@ def main():
     if result is None:
         b = d_best.cpu()
         result = (float(b[0]), int(b.view(torch.int64)[1]))
+
+    # (after the timed region, which follows the warmup directly) correctness guard on the timed workload: the timed poll (this rank's shard, the device's
+    # walk choice, cons3) writes every objective; 16 sampled candidates plus its argmin are
+    # re-evaluated by the streaming scan (an independent kernel) and must agree bit for bit
+    check = None
+    if K > 1 and not args.no_extras:
+        d_obj = torch.empty(Kl, dtype=torch.float64, device=dev)
+        ctx.poll_best_dev(d_polls[0], 3 * N, Kl, d_rmax, d_best, d_prev=d_prevs[0], d_dlim=d_dlim,
+                          tan_half_fov=tan_half, idx_base=idx_base, d_obj=d_obj, stream=s_handle)
+        got_best = ctx.best_fetch(d_best, stream=s_handle)
+        torch.cuda.synchronize(dev)
+        objs = d_obj.cpu().numpy()
+        pick = np.unique(np.concatenate([
+            np.floor(wl.SplitMix64(args.seed + 7).uniform(16) * Kl).astype(np.int64),
+            [int(np.argmin(objs))]]))
+        ctx.set_algo("scan")
+        _, _, o_scan = ctx.poll_best(polls[0][lo:hi][pick], r_max, 1e5, prev=polls[0][0],
+                                     d_lim=dlim, tan_half_fov=tan_half, want_all=True)
+        ctx.set_algo(args.algo)
+        kmin = int(np.argmin(objs))
+        check = bool(np.array_equal(o_scan, objs[pick]) and got_best[1] == idx_base + kmin
+                     and got_best[0] == objs[kmin])
+        if not check:
+            log("WARNING: timed poll vs scan disagree", pick, o_scan, objs[pick], got_best)
+
 
     total_evals = K_step * args.steps
     value = total_evals / elapsed
