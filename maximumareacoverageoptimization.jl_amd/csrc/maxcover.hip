@@ -1187,6 +1187,58 @@ static void seed_route(mac_ctx* ctx, const double* x0, int N)
         ctx->fused_bad.store(~(uint64_t)0, std::memory_order_relaxed);
 }
 
+// A large host buffer into device memory through the lane's pinned staging: host threads copy
+// chunks into the staging while this thread enqueues each chunk's async copy as soon as it has
+// landed (a single-threaded memcpy of config 4's 37.7-MB matrix took ~3 ms before the first byte
+// moved; MAXCOVER_STAGE_THREADS sets the threads, 1 = the plain copy). Returns once every copy is
+// enqueued and every host thread has finished (the staging may then be reused after the stream).
+static const int kStageThreads = [] {
+    const char* e = std::getenv("MAXCOVER_STAGE_THREADS");
+    const int v = e ? std::atoi(e) : 8;
+    return std::max(1, std::min(v, 32));
+}();
+
+static void staged_upload(const void* src, void* pinned, void* dev, size_t bytes, hipStream_t s)
+{
+    constexpr size_t kChunk = (size_t)4 << 20;
+    const int T = (int)std::min<size_t>((size_t)kStageThreads, (bytes + kChunk - 1) / kChunk);
+    if (T <= 1 || bytes < 2 * kChunk) {
+        std::memcpy(pinned, src, bytes);
+        HCK(hipMemcpyAsync(dev, pinned, bytes, hipMemcpyHostToDevice, s));
+        return;
+    }
+    const size_t nc = (bytes + kChunk - 1) / kChunk;
+    std::vector<std::atomic<int>> done(nc);
+    for (auto& d : done) d.store(0, std::memory_order_relaxed);
+    auto work = [&](int t) {   // chunks t, t + T, ...: the early chunks land first
+        for (size_t c = (size_t)t; c < nc; c += (size_t)T) {
+            const size_t o = c * kChunk, n = std::min(kChunk, bytes - o);
+            std::memcpy((char*)pinned + o, (const char*)src + o, n);
+            done[c].store(1, std::memory_order_release);
+        }
+    };
+    std::vector<std::thread> th;
+    int started = 1;   // workers 1 .. started-1 run on their own threads; the rest on this one
+    try {
+        th.reserve((size_t)T - 1);
+        for (int t = 1; t < T; ++t, ++started) th.emplace_back(work, t);
+    } catch (...) {   // (no thread to spare: this thread copies their chunks too)
+    }
+    for (int t = started; t < T; ++t) work(t);
+    work(0);
+    HipError err{hipSuccess, "", 0};
+    for (size_t c = 0; c < nc; ++c) {   // (every thread is joined before an error leaves)
+        while (!done[c].load(std::memory_order_acquire)) std::this_thread::yield();
+        const size_t o = c * kChunk, n = std::min(kChunk, bytes - o);
+        if (err.e == hipSuccess) {
+            const hipError_t e = hipMemcpyAsync((char*)dev + o, (const char*)pinned + o, n, hipMemcpyHostToDevice, s);
+            if (e != hipSuccess) err = HipError{e, "hipMemcpyAsync (staged_upload)", __LINE__};
+        }
+    }
+    for (auto& t : th) t.join();
+    if (err.e != hipSuccess) throw err;
+}
+
 template <class T>
 static int32_t host_eval(mac_ctx* ctx, const T* cands, int64_t three_n, int64_t K,
                          const double* r_max, double penalty, const T* prev,
@@ -1218,15 +1270,17 @@ static int32_t host_eval(mac_ctx* ctx, const T* cands, int64_t three_n, int64_t 
     const bool staged = std::max(in_bytes, out_bytes) <= ((size_t)64 << 20);
     if (staged) L->h_io.reserve(std::max<size_t>(std::max(in_bytes, out_bytes), 64));
     const T* src_in = cands;
-    if (staged && in_bytes) {
-        std::memcpy(L->h_io.p, cands, in_bytes);
-        src_in = (const T*)L->h_io.p;
-    }
-    if (three_n * K > 0) {
-        if constexpr (f32)
-            upload_widen(src_in, three_n * K, L->c32, L->cands.as<double>(), s);
-        else
-            HCK(hipMemcpyAsync(L->cands.p, src_in, in_bytes, hipMemcpyHostToDevice, s));
+    if constexpr (!f32) {
+        if (staged && in_bytes)
+            staged_upload(cands, L->h_io.p, L->cands.p, in_bytes, s);
+        else if (in_bytes)
+            HCK(hipMemcpyAsync(L->cands.p, cands, in_bytes, hipMemcpyHostToDevice, s));
+    } else {
+        if (staged && in_bytes) {
+            std::memcpy(L->h_io.p, cands, in_bytes);
+            src_in = (const T*)L->h_io.p;
+        }
+        if (three_n * K > 0) upload_widen(src_in, three_n * K, L->c32, L->cands.as<double>(), s);
     }
     const bool want_obj = obj_out || best_obj || best_idx;
     double* d_rmax = nullptr;

@@ -729,16 +729,16 @@ def test_walk_choice_poll_batches(ctx, pkg, orc, disks):
     C = wl.poll_candidates(x0, rng)
     assert C.shape[0] == 6 * N + 1 >= 64
     want = 25.0 * orc.lattice_count_batch(C, G).astype(np.float64)
-    ctx.set_algo("auto")
-    area, walk = _walk_of(ctx, C)
-    assert walk == "poll", walk
-    assert np.array_equal(area, want)
-    ctx.set_algo("tiled")
-    area_t, walk_t = _walk_of(ctx, C[:64])
-    # the whole crowded poll through the forced per-candidate walk: its pairs come from the
-    # poll-level neighbour lists (k_walk.h), no unit rebuilds all N(N-1)/2 of them
-    area_f, walk_f = _walk_of(ctx, C)
-    ctx.set_algo("auto")
+    with pkg.Context(0) as c2:   # (a fresh context: AUTO's routing history is the context's)
+        c2.set_points(x, y, w)
+        area, walk = _walk_of(c2, C)
+        assert walk == "poll", walk
+        assert np.array_equal(area, want)
+        c2.set_algo("tiled")
+        area_t, walk_t = _walk_of(c2, C[:64])
+        # the whole crowded poll through the forced per-candidate walk: its pairs come from the
+        # poll-level neighbour lists (k_walk.h), no unit rebuilds all N(N-1)/2 of them
+        area_f, walk_f = _walk_of(c2, C)
     assert walk_t == walk_f == "tiled", (walk_t, walk_f)
     assert np.array_equal(area_t, want[:64])
     assert np.array_equal(area_f, want)
@@ -750,7 +750,8 @@ def test_walk_choice_scattered_batch(ctx, pkg, orc):
     The choice is made on the device once the neighbour lists exist; the host launches that
     walk's kernel when the lane's recent polls chose it (maxcover.hip enqueue_eval), so a lane
     that ran poll-walk polls runs this batch once through the poll walk (same areas), records
-    the choice, and takes the per-candidate walk from the next call on."""
+    the choice, and takes the per-candidate walk from the next call on (the five-launch chain on
+    a fresh context; AUTO there takes the fused chain, which has no walk choice: same areas)."""
     wl = pkg.workloads
     rng = wl.SplitMix64(4244)
     G, N, K = 512, 8, 64
@@ -758,12 +759,16 @@ def test_walk_choice_scattered_batch(ctx, pkg, orc):
     ctx.set_points(x, y, w)
     C = np.stack([wl.uniform_disks(N, G, rng) for _ in range(K)])
     want = 25.0 * orc.lattice_count_batch(C, G).astype(np.float64)
-    ctx.set_algo("auto")
-    area0, _ = _walk_of(ctx, C)
-    area, walk = _walk_of(ctx, C)
-    assert walk == "tiled", walk
-    assert np.array_equal(area0, want)
-    assert np.array_equal(area, want)
+    with pkg.Context(0) as c2:   # (a fresh context: AUTO's routing history is the context's)
+        c2.set_points(x, y, w)
+        fused = _walk_of(c2, C)   # AUTO on a fresh context: the fused chain (no walk choice)
+        c2.set_chain("five")      # the five-launch chain's walk choice
+        runs = [_walk_of(c2, C) for _ in range(2)]
+    # (a lane with no report launches the per-candidate walk's kernel at once; one that ran
+    # poll-walk polls records the choice on its first call) by the second call, that walk
+    assert runs[-1][1] == "tiled", [r[1] for r in runs]
+    for area, _ in [fused] + runs:
+        assert np.array_equal(area, want)
 
 
 @pytest.mark.parametrize("case", ["real_clustered", "big_radius", "mixed_weights", "pythagorean",
